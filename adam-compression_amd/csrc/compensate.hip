@@ -1,0 +1,285 @@
+// K1: momentum correction + velocity accumulation, with the strided sample of
+// |velocity| fused into the same streaming pass; K2: standalone sampling.
+//
+// Reference: DGCSGDMemory.compensate (dgc/memory.py:50-70) and the sampling of
+// DGCCompressor._sparsify (dgc/compression.py:113-121).
+//
+// Bit-exactness: the reference issues separate ATen ops (add_, mul_), so every
+// intermediate rounds to fp32. This file is built with -ffp-contract=off and uses
+// __fadd_rn / __fmul_rn so no multiply-add is ever fused:
+//   nesterov: mmt = (mmt + g) * m ;  vec = (vec + mmt) + g   [accumulate]
+//                                     out = mmt + g           [dense branch]
+//   plain:    mmt = mmt * m + g   ;  vec = vec + mmt         [accumulate]
+//                                     out = mmt               [dense branch]
+//
+// HBM: 20 B/element (read g, mmt, vec; write mmt, vec), 16-B vector accesses,
+// grid-stride over float4. The sample |vec[start + q*stride]| is written from
+// registers, saving a strided re-read of vec (which touches ~1/3 of its lines).
+#include "dgc_common.hpp"
+
+namespace dgc {
+
+struct SampleSpec {
+    float* out;        // nullptr: no sampling
+    int64_t start;
+    int64_t stride;    // >= 4 on the fused path
+    int64_t count;     // ceil((n - start) / stride)
+};
+
+template <bool NEST, bool ACC>
+__device__ __forceinline__ float comp1(float g, float& m, float& v, float mom) {
+    if (NEST) {
+        m = __fmul_rn(__fadd_rn(m, g), mom);
+        if (ACC) {
+            v = __fadd_rn(__fadd_rn(v, m), g);
+            return v;
+        }
+        return __fadd_rn(m, g);
+    }
+    m = __fadd_rn(__fmul_rn(m, mom), g);
+    if (ACC) {
+        v = __fadd_rn(v, m);
+        return v;
+    }
+    return m;
+}
+
+__device__ __forceinline__ void floor_divmod(int64_t d, int64_t s, int64_t& q, int64_t& r) {
+    q = d / s;
+    r = d - q * s;
+    if (r < 0) {
+        r += s;
+        q -= 1;
+    }
+}
+
+// Vector path: all four pointers 16-B aligned. Each thread walks float4 index v
+// with a grid stride; (q, r) track floor/mod of (4v - start) by the sample stride
+// incrementally (one real division per thread).
+template <bool NEST, bool ACC, bool SAMPLE>
+__global__ void __launch_bounds__(kBlock)
+k_compensate4(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __restrict__ vec,
+              float4* __restrict__ out, int64_t n4, float mom, SampleSpec sp, int64_t step_q,
+              int64_t step_r) {
+    int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t G = (int64_t)gridDim.x * kBlock;
+    int64_t q = 0, r = 0;
+    if (SAMPLE) floor_divmod(4 * v - sp.start, sp.stride, q, r);
+    for (; v < n4; v += G) {
+        const float4 gv = g[v];
+        float4 mv = mmt[v];
+        float4 vv = ACC ? vec[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 ov;
+        ov.x = comp1<NEST, ACC>(gv.x, mv.x, vv.x, mom);
+        ov.y = comp1<NEST, ACC>(gv.y, mv.y, vv.y, mom);
+        ov.z = comp1<NEST, ACC>(gv.z, mv.z, vv.z, mom);
+        ov.w = comp1<NEST, ACC>(gv.w, mv.w, vv.w, mom);
+        mmt[v] = mv;
+        if (ACC)
+            vec[v] = vv;
+        else
+            out[v] = ov;
+        if (SAMPLE) {
+            // element 4v+j is a sample iff (r + j) % stride == 0, i.e. r + j in {0, stride}
+            const int64_t j = (r == 0) ? 0 : sp.stride - r;
+            if (j < 4) {
+                const int64_t qi = (r == 0) ? q : q + 1;
+                if (qi >= 0 && qi < sp.count) {
+                    const float x = j == 0 ? ov.x : j == 1 ? ov.y : j == 2 ? ov.z : ov.w;
+                    sp.out[qi] = fabsf(x);
+                }
+            }
+            r += step_r;
+            q += step_q;
+            if (r >= sp.stride) {
+                r -= sp.stride;
+                q += 1;
+            }
+        }
+    }
+}
+
+// Scalar path: any alignment, any stride; also used for the < 4-element tail.
+template <bool NEST, bool ACC, bool SAMPLE>
+__global__ void __launch_bounds__(kBlock)
+k_compensate1(const float* __restrict__ g, float* __restrict__ mmt, float* __restrict__ vec,
+              float* __restrict__ out, int64_t begin, int64_t n, float mom, SampleSpec sp) {
+    for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        float mv = mmt[i];
+        float vv = ACC ? vec[i] : 0.f;
+        const float ov = comp1<NEST, ACC>(g[i], mv, vv, mom);
+        mmt[i] = mv;
+        if (ACC)
+            vec[i] = vv;
+        else
+            out[i] = ov;
+        if (SAMPLE && i >= sp.start) {
+            const int64_t d = i - sp.start;
+            if (d % sp.stride == 0 && d / sp.stride < sp.count) sp.out[d / sp.stride] = fabsf(ov);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_sample_strided(const float* __restrict__ vec, int64_t start, int64_t stride, int64_t count,
+                 float* __restrict__ out) {
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < count;
+         q += (int64_t)gridDim.x * kBlock)
+        out[q] = fabsf(vec[start + q * stride]);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_sample_gather(const float* __restrict__ vec, const int64_t* __restrict__ idx, int64_t count,
+                float* __restrict__ out) {
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < count;
+         q += (int64_t)gridDim.x * kBlock)
+        out[q] = fabsf(vec[idx[q]]);
+}
+
+// DGCSGDMemory.update (dgc/memory.py:72-77) on its own: zero the transmitted slots.
+template <typename I>
+__global__ void __launch_bounds__(kBlock)
+k_mask(float* __restrict__ mmt, float* __restrict__ vec, const I* __restrict__ idx, int64_t count,
+       int64_t n, int* bad) {
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < count;
+         q += (int64_t)gridDim.x * kBlock) {
+        int64_t i = (int64_t)idx[q];
+        if (i < 0) i += n;             // torch index_fill_ wraps negative indices
+        if (i < 0 || i >= n) {
+            atomicOr(bad, 1);
+            continue;
+        }
+        if (mmt) mmt[i] = 0.f;
+        vec[i] = 0.f;
+    }
+}
+
+template <bool NEST, bool ACC>
+static int launch_comp(const float* g, float* m, float* v, float* o, int64_t n, float mom,
+                       SampleSpec sp, hipStream_t st) {
+    const bool sample = sp.out != nullptr;
+    const bool vec_ok = aligned16(g) && aligned16(m) && (ACC ? aligned16(v) : aligned16(o)) &&
+                        (!sample || sp.stride >= 4);
+    int64_t done = 0;
+    if (vec_ok) {
+        const int64_t n4 = n / 4;
+        if (n4 > 0) {
+            const int grid = grid_for(n4);
+            const int64_t G = 4 * (int64_t)grid * kBlock;
+            const int64_t sq = sample ? G / sp.stride : 0, sr = sample ? G % sp.stride : 0;
+            auto g4 = reinterpret_cast<const float4*>(g);
+            auto m4 = reinterpret_cast<float4*>(m);
+            auto v4 = reinterpret_cast<float4*>(v);
+            auto o4 = reinterpret_cast<float4*>(o);
+            if (sample)
+                hipLaunchKernelGGL((k_compensate4<NEST, ACC, true>), dim3(grid), dim3(kBlock), 0, st,
+                                   g4, m4, v4, o4, n4, mom, sp, sq, sr);
+            else
+                hipLaunchKernelGGL((k_compensate4<NEST, ACC, false>), dim3(grid), dim3(kBlock), 0, st,
+                                   g4, m4, v4, o4, n4, mom, sp, sq, sr);
+            DGC_LAUNCHED();
+        }
+        done = n4 * 4;
+    }
+    if (done < n) {
+        const int grid = grid_for(n - done);
+        if (sample)
+            hipLaunchKernelGGL((k_compensate1<NEST, ACC, true>), dim3(grid), dim3(kBlock), 0, st,
+                               g, m, v, o, done, n, mom, sp);
+        else
+            hipLaunchKernelGGL((k_compensate1<NEST, ACC, false>), dim3(grid), dim3(kBlock), 0, st,
+                               g, m, v, o, done, n, mom, sp);
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
+}
+
+int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n, float momentum,
+               bool nesterov, bool accumulate, float* samples, int64_t s_start, int64_t s_stride,
+               int64_t s_count, hipStream_t st) {
+    if (n < 0) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: n < 0");
+    if (n == 0) return DGC_OK;
+    if (!grad || !mmt) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: null grad/mmt");
+    if (accumulate && !vec) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: accumulate needs vec");
+    if (accumulate && out && out != vec)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: accumulate writes vec (out must be NULL or vec)");
+    if (!accumulate && !out) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: dense branch needs out");
+    SampleSpec sp{nullptr, 0, 1, 0};
+    if (samples) {
+        if (!accumulate) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: sampling needs accumulate=1");
+        if (s_stride < 1 || s_start < 0 || s_start >= n)
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: bad sample start/stride");
+        if (s_count != ceil_div(n - s_start, s_stride))
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: num_samples must be ceil((n-start)/stride)");
+        sp = SampleSpec{samples, s_start, s_stride, s_count};
+        if (s_stride < 4) {
+            // tiny strides (sample_ratio >= 0.25): unfused, samples read back after the pass
+            DGC_TRY(compensate(grad, mmt, vec, out, n, momentum, nesterov, accumulate, nullptr, 0,
+                               1, 0, st));
+            const int grid = grid_for(s_count);
+            hipLaunchKernelGGL(k_sample_strided, dim3(grid), dim3(kBlock), 0, st, vec, s_start,
+                               s_stride, s_count, samples);
+            DGC_LAUNCHED();
+            return DGC_OK;
+        }
+    }
+    if (nesterov)
+        return accumulate ? launch_comp<true, true>(grad, mmt, vec, out, n, momentum, sp, st)
+                          : launch_comp<true, false>(grad, mmt, vec, out, n, momentum, sp, st);
+    return accumulate ? launch_comp<false, true>(grad, mmt, vec, out, n, momentum, sp, st)
+                      : launch_comp<false, false>(grad, mmt, vec, out, n, momentum, sp, st);
+}
+
+}  // namespace dgc
+
+extern "C" int dgc_compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n,
+                              float momentum, int32_t nesterov, int32_t accumulate, float* samples,
+                              int64_t sample_start, int64_t sample_stride, int64_t num_samples,
+                              void* stream) {
+    return dgc::compensate(grad, mmt, vec, out, n, momentum, nesterov != 0, accumulate != 0, samples,
+                           sample_start, sample_stride, num_samples,
+                           static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_sample_strided(const float* vec, int64_t n, int64_t start, int64_t stride,
+                                  float* samples, int64_t num_samples, void* stream) {
+    if (!vec || !samples || stride < 1 || start < 0 || (n > 0 && start >= n))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_sample_strided: bad arguments");
+    if (num_samples != dgc::ceil_div(n - start, stride))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_sample_strided: num_samples must be ceil((n-start)/stride)");
+    if (num_samples == 0) return DGC_OK;
+    hipLaunchKernelGGL(dgc::k_sample_strided, dim3(dgc::grid_for(num_samples)), dim3(dgc::kBlock), 0,
+                       static_cast<hipStream_t>(stream), vec, start, stride, num_samples, samples);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+extern "C" int dgc_sample_gather(const float* vec, const int64_t* sample_indices, int64_t num_samples,
+                                 float* samples, void* stream) {
+    if (!vec || !sample_indices || !samples || num_samples < 0)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_sample_gather: bad arguments");
+    if (num_samples == 0) return DGC_OK;
+    hipLaunchKernelGGL(dgc::k_sample_gather, dim3(dgc::grid_for(num_samples)), dim3(dgc::kBlock), 0,
+                       static_cast<hipStream_t>(stream), vec, sample_indices, num_samples, samples);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+extern "C" int dgc_mask_indices(float* mmt, float* vec, int64_t n, const void* indices, int32_t idtype,
+                                int64_t count, int32_t* bad_flag, void* stream) {
+    if (!vec || (count > 0 && !indices) || !bad_flag)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_mask_indices: null argument");
+    if (idtype != DGC_I64 && idtype != DGC_I32) DGC_FAIL(DGC_ERR_DTYPE, "dgc_mask_indices: index dtype");
+    if (count <= 0) return DGC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = dgc::grid_for(count);
+    if (idtype == DGC_I32)
+        hipLaunchKernelGGL(dgc::k_mask<int32_t>, dim3(grid), dim3(dgc::kBlock), 0, s, mmt, vec,
+                           static_cast<const int32_t*>(indices), count, n, bad_flag);
+    else
+        hipLaunchKernelGGL(dgc::k_mask<int64_t>, dim3(grid), dim3(dgc::kBlock), 0, s, mmt, vec,
+                           static_cast<const int64_t*>(indices), count, n, bad_flag);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}

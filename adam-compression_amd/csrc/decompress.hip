@@ -1,0 +1,349 @@
+// K6: deterministic decompress = grad.zero_().index_put_([idx], vals, accumulate=True)
+// followed by grad.mul_(1/W) (dgc/compression.py:179-194), over the rank-order
+// concatenation that the allgather produced (dgc/compression.py:200-212).
+//
+// The reference's single-threaded CPU index_put_ adds entries in input order. The
+// input is a sequence of RUNS (one per rank; our compress emits each rank's indices
+// ascending), so the dense result is reproduced bit-for-bit without atomics:
+//
+//   bounds  one thread per (run, chunk) binary-searches the first entry of the run
+//           whose index reaches the chunk (runs are non-decreasing);
+//   chunk   one workgroup per 4096-element chunk: zero a 16 KB LDS tile, add the
+//           runs' entries for the chunk IN RUN ORDER (a barrier between runs; inside
+//           a run an index appears once — or, for a non-decreasing run with
+//           repeats, its first occurrence sums the repeats in order), scale by
+//           1/W, and write the tile out with 16-B stores.
+//
+// HBM: the dense write (4 B/elem) plus the sparse reads W*k*(vb+ib). Untouched
+// slots come out +0.0 exactly as zero_() * (1/W).
+#include "dgc_common.hpp"
+
+namespace dgc {
+
+constexpr int kChunk = 4096;
+constexpr int kMaxRuns = 64;
+
+struct Run {
+    const void* vals;
+    const void* idx;
+    long long count;
+};
+
+struct DecWS {
+    Run* runs;
+    int32_t* nruns;
+    int32_t* status;      // bit 0: index out of range
+    int32_t* ndesc;       // detected descents
+    long long* desc;      // their positions (unsorted)
+    long long* bnd;       // [kMaxRuns][nchunks + 1]
+    int64_t nchunks;
+};
+
+static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, size_t* bytes = nullptr) {
+    Carver c(base);
+    DecWS w{};
+    w.nchunks = ceil_div(n, kChunk);
+    w.runs = c.take<Run>(kMaxRuns);
+    w.nruns = c.take<int32_t>(4);
+    w.status = w.nruns ? w.nruns + 1 : nullptr;
+    w.ndesc = w.nruns ? w.nruns + 2 : nullptr;
+    w.desc = c.take<long long>(kMaxRuns);
+    w.bnd = c.take<long long>((size_t)max_runs * (w.nchunks + 1));
+    if (bytes) *bytes = c.bytes();
+    return w;
+}
+
+template <int VD>
+__device__ __forceinline__ float load_val(const void* p, long long e) {
+    if (VD == DGC_F16) return __half2float(reinterpret_cast<const __half*>(p)[e]);
+    return reinterpret_cast<const float*>(p)[e];
+}
+
+template <int ID>
+__device__ __forceinline__ long long load_idx(const void* p, long long e) {
+    if (ID == DGC_I32) return reinterpret_cast<const int32_t*>(p)[e];
+    return reinterpret_cast<const int64_t*>(p)[e];
+}
+
+// ---------------------------------------------------------------- run tables
+struct HostRuns {
+    int32_t n;
+    long long off[kMaxRuns + 1];
+};
+
+__global__ void k_runs_host(DecWS w, HostRuns hr, const char* vals, const char* idx, int vb, int ib) {
+    const int r = threadIdx.x;
+    if (r < hr.n) w.runs[r] = Run{vals + hr.off[r] * vb, idx + hr.off[r] * ib, hr.off[r + 1] - hr.off[r]};
+    if (r == 0) *w.nruns = hr.n;
+}
+
+__global__ void k_runs_packed(DecWS w, const char* payload, int world, int64_t stride, int64_t voff,
+                              int64_t ioff, int64_t capacity) {
+    const int r = threadIdx.x;
+    if (r < world) {
+        const char* base = payload + (int64_t)r * stride;
+        long long c = *reinterpret_cast<const long long*>(base);
+        c = c < 0 ? 0 : (c > capacity ? capacity : c);
+        w.runs[r] = Run{base + voff, base + ioff, c};
+    }
+    if (r == 0) *w.nruns = world;
+}
+
+template <int ID>
+__global__ void __launch_bounds__(kBlock)
+k_find_descents(const void* idx, long long total, DecWS w) {
+    for (long long j = (long long)blockIdx.x * kBlock + threadIdx.x; j + 1 < total;
+         j += (long long)gridDim.x * kBlock) {
+        if (load_idx<ID>(idx, j + 1) < load_idx<ID>(idx, j)) {
+            const int slot = atomicAdd(w.ndesc, 1);
+            if (slot < kMaxRuns - 1) w.desc[slot] = j + 1;
+        }
+    }
+}
+
+__global__ void k_runs_from_descents(DecWS w, const char* vals, const char* idx, int vb, int ib,
+                                     long long total) {
+    if (threadIdx.x != 0) return;
+    int nd = *w.ndesc;
+    if (nd > kMaxRuns - 1) {
+        *w.nruns = 0;
+        return;
+    }
+    long long* d = w.desc;
+    for (int i = 1; i < nd; ++i) {   // insertion sort, <= 63 entries
+        const long long v = d[i];
+        int j = i - 1;
+        while (j >= 0 && d[j] > v) {
+            d[j + 1] = d[j];
+            --j;
+        }
+        d[j + 1] = v;
+    }
+    long long prev = 0;
+    for (int r = 0; r <= nd; ++r) {
+        const long long end = r < nd ? d[r] : total;
+        w.runs[r] = Run{vals + prev * vb, idx + prev * ib, end - prev};
+        prev = end;
+    }
+    *w.nruns = nd + 1;
+}
+
+// ---------------------------------------------------------------- bounds
+template <int ID>
+__global__ void __launch_bounds__(kBlock)
+k_bounds(DecWS w, int64_t n, int max_runs) {
+    const int nr = *w.nruns;
+    const int64_t stride = w.nchunks + 1;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < (int64_t)max_runs * stride;
+         t += (int64_t)gridDim.x * kBlock) {
+        const int r = (int)(t / stride);
+        if (r >= nr) break;
+        const int64_t c = t - (int64_t)r * stride;
+        const Run run = w.runs[r];
+        const long long key = c == w.nchunks ? n : c * (long long)kChunk;
+        long long lo = 0, hi = run.count;   // first entry with idx >= key
+        while (lo < hi) {
+            const long long mid = (lo + hi) >> 1;
+            if (load_idx<ID>(run.idx, mid) < key)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        w.bnd[t] = lo;
+        if ((c == 0 && lo > 0) || (c == w.nchunks && lo < run.count)) atomicOr(w.status, 1);
+    }
+}
+
+// ---------------------------------------------------------------- chunk scatter
+template <int VD, int ID>
+__global__ void __launch_bounds__(kBlock)
+k_scatter_chunks(DecWS w, float* __restrict__ grad, int64_t n, float scale) {
+    __shared__ __attribute__((aligned(16))) float acc[kChunk];
+    const int nr = *w.nruns;
+    const int64_t stride = w.nchunks + 1;
+    const bool vec_out = aligned16(grad);
+    for (int64_t c = blockIdx.x; c < w.nchunks; c += gridDim.x) {
+        const long long base = c * (long long)kChunk;
+        for (int j = threadIdx.x; j < kChunk; j += kBlock) acc[j] = 0.f;
+        __syncthreads();
+        for (int r = 0; r < nr; ++r) {
+            const Run run = w.runs[r];
+            const long long b0 = w.bnd[r * stride + c], b1 = w.bnd[r * stride + c + 1];
+            for (long long e = b0 + threadIdx.x; e < b1; e += kBlock) {
+                const long long i = load_idx<ID>(run.idx, e);
+                if (e > b0 && load_idx<ID>(run.idx, e - 1) == i) continue;   // not the first of a repeat
+                const long long off = i - base;
+                if (off < 0 || off >= kChunk) {   // only an unsorted run can land here
+                    atomicOr(w.status, 2);
+                    continue;
+                }
+                float a = acc[off];
+                long long f = e;
+                do {
+                    a = __fadd_rn(a, load_val<VD>(run.vals, f));
+                    ++f;
+                } while (f < b1 && load_idx<ID>(run.idx, f) == i);
+                acc[off] = a;
+            }
+            __syncthreads();
+        }
+        const long long len = n - base < kChunk ? n - base : kChunk;
+        if (vec_out && len == kChunk) {
+            float4* g4 = reinterpret_cast<float4*>(grad + base);
+            const float4* a4 = reinterpret_cast<const float4*>(acc);
+            for (int j = threadIdx.x; j < kChunk / 4; j += kBlock) {
+                float4 v = a4[j];
+                if (scale != 1.0f) {
+                    v.x = __fmul_rn(v.x, scale);
+                    v.y = __fmul_rn(v.y, scale);
+                    v.z = __fmul_rn(v.z, scale);
+                    v.w = __fmul_rn(v.w, scale);
+                }
+                g4[j] = v;
+            }
+        } else {
+            for (int j = threadIdx.x; j < len; j += kBlock)
+                grad[base + j] = scale != 1.0f ? __fmul_rn(acc[j], scale) : acc[j];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- host side
+static int vbytes(int vd) { return vd == DGC_F16 ? 2 : 4; }
+static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
+
+template <int VD, int ID>
+static int run_scatter(const DecWS& w, float* grad, int64_t n, float scale, int max_runs, hipStream_t s) {
+    const int64_t work = (int64_t)max_runs * (w.nchunks + 1);
+    hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, n, max_runs);
+    DGC_LAUNCHED();
+    hipLaunchKernelGGL((k_scatter_chunks<VD, ID>), dim3(grid_for(w.nchunks, 1)), dim3(kBlock), 0, s, w,
+                       grad, n, scale);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+static int dispatch_scatter(int vd, int id, const DecWS& w, float* grad, int64_t n, float scale,
+                            int max_runs, hipStream_t s) {
+    if (vd == DGC_F32 && id == DGC_I64) return run_scatter<DGC_F32, DGC_I64>(w, grad, n, scale, max_runs, s);
+    if (vd == DGC_F32 && id == DGC_I32) return run_scatter<DGC_F32, DGC_I32>(w, grad, n, scale, max_runs, s);
+    if (vd == DGC_F16 && id == DGC_I64) return run_scatter<DGC_F16, DGC_I64>(w, grad, n, scale, max_runs, s);
+    if (vd == DGC_F16 && id == DGC_I32) return run_scatter<DGC_F16, DGC_I32>(w, grad, n, scale, max_runs, s);
+    DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
+}
+
+static int check_common(int vd, int id, float* grad, int64_t n, void* ws, size_t ws_bytes, int runs) {
+    if ((vd != DGC_F32 && vd != DGC_F16) || (id != DGC_I64 && id != DGC_I32))
+        DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
+    if (!grad || n < 1) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: null grad or n < 1");
+    if (runs < 1 || runs > kMaxRuns) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: 1..%d runs supported", kMaxRuns);
+    size_t need = 0;
+    carve_dec(nullptr, n, runs, &need);
+    if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
+        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_decompress: workspace needs %zu bytes, 256-B aligned", need);
+    return DGC_OK;
+}
+
+int decompress(const void* values, int vd, const void* indices, int id, int64_t total,
+               const int64_t* run_offsets, int32_t nruns, float* grad, int64_t n, float scale, void* ws,
+               size_t ws_bytes, hipStream_t s) {
+    const int max_runs = run_offsets ? nruns : kMaxRuns;
+    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, max_runs));
+    if (total < 0 || (total > 0 && (!values || !indices)))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: null values/indices");
+    DecWS w = carve_dec(ws, n, max_runs);
+    DGC_HIP(hipMemsetAsync(w.nruns, 0, 4 * sizeof(int32_t), s));
+    const char* v = static_cast<const char*>(values);
+    const char* ix = static_cast<const char*>(indices);
+    if (run_offsets) {
+        HostRuns hr{};
+        hr.n = nruns;
+        for (int r = 0; r <= nruns; ++r) hr.off[r] = run_offsets[r];
+        if (hr.off[0] != 0 || hr.off[nruns] != total)
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: run_offsets must span [0, total]");
+        for (int r = 0; r < nruns; ++r)
+            if (hr.off[r + 1] < hr.off[r]) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: run_offsets decrease");
+        hipLaunchKernelGGL(k_runs_host, dim3(1), dim3(kMaxRuns), 0, s, w, hr, v, ix, vbytes(vd), ibytes(id));
+        DGC_LAUNCHED();
+    } else {
+        if (total > 1) {
+            if (id == DGC_I32)
+                hipLaunchKernelGGL(k_find_descents<DGC_I32>, dim3(grid_for(total)), dim3(kBlock), 0, s, ix, total, w);
+            else
+                hipLaunchKernelGGL(k_find_descents<DGC_I64>, dim3(grid_for(total)), dim3(kBlock), 0, s, ix, total, w);
+            DGC_LAUNCHED();
+        }
+        hipLaunchKernelGGL(k_runs_from_descents, dim3(1), dim3(64), 0, s, w, v, ix, vbytes(vd), ibytes(id), total);
+        DGC_LAUNCHED();
+        int32_t nr = 0;
+        DGC_HIP(hipMemcpyAsync(&nr, w.nruns, sizeof(nr), hipMemcpyDeviceToHost, s));
+        DGC_HIP(hipStreamSynchronize(s));
+        if (nr == 0)
+            DGC_FAIL(DGC_ERR_UNSORTED, "dgc_decompress: input has more than %d descending runs", kMaxRuns);
+    }
+    return dispatch_scatter(vd, id, w, grad, n, scale, max_runs, s);
+}
+
+int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff) {
+    const int64_t v = 16;
+    const int64_t i = (int64_t)align_up(v + capacity * vbytes(vd), 16);
+    if (voff) *voff = v;
+    if (ioff) *ioff = i;
+    return (int64_t)align_up(i + capacity * ibytes(id), 256);
+}
+
+int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity, int vd,
+                      int id, float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, hipStream_t s) {
+    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world));
+    int64_t voff, ioff;
+    const int64_t min_stride = payload_layout(capacity, vd, id, &voff, &ioff);
+    if (!payload || rank_stride < min_stride || capacity < 0)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed: rank_stride %lld < layout %lld",
+                 (long long)rank_stride, (long long)min_stride);
+    DecWS w = carve_dec(ws, n, world);
+    DGC_HIP(hipMemsetAsync(w.nruns, 0, 4 * sizeof(int32_t), s));
+    hipLaunchKernelGGL(k_runs_packed, dim3(1), dim3(kMaxRuns), 0, s, w, static_cast<const char*>(payload),
+                       world, rank_stride, voff, ioff, capacity);
+    DGC_LAUNCHED();
+    return dispatch_scatter(vd, id, w, grad, n, scale, world, s);
+}
+
+}  // namespace dgc
+
+extern "C" size_t dgc_decompress_workspace(int64_t n, int32_t max_runs) {
+    size_t b = 0;
+    if (max_runs < 1 || max_runs > dgc::kMaxRuns) max_runs = dgc::kMaxRuns;
+    dgc::carve_dec(nullptr, n, max_runs, &b);
+    return b;
+}
+
+extern "C" int dgc_decompress(const void* values, int32_t vdtype, const void* indices, int32_t idtype,
+                              int64_t total, const int64_t* run_offsets, int32_t nruns, float* grad,
+                              int64_t n, float scale, void* ws, size_t ws_bytes, void* stream) {
+    return dgc::decompress(values, vdtype, indices, idtype, total, run_offsets, nruns, grad, n, scale, ws,
+                           ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int64_t dgc_payload_layout(int64_t capacity, int32_t vdtype, int32_t idtype,
+                                      int64_t* values_offset, int64_t* indices_offset) {
+    return dgc::payload_layout(capacity, vdtype, idtype, values_offset, indices_offset);
+}
+
+extern "C" int dgc_decompress_packed(const void* payload, int32_t world, int64_t rank_stride,
+                                     int64_t capacity, int32_t vdtype, int32_t idtype, float* grad,
+                                     int64_t n, float scale, void* ws, size_t ws_bytes, void* stream) {
+    return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
+                                  ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_decompress_status(const void* ws, int32_t* status, void* stream) {
+    if (!ws || !status) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_status: null argument");
+    dgc::Carver c(const_cast<void*>(ws));
+    c.take<dgc::Run>(dgc::kMaxRuns);
+    int32_t* nr = c.take<int32_t>(4);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DGC_HIP(hipMemcpyAsync(status, nr + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    DGC_HIP(hipStreamSynchronize(s));
+    return DGC_OK;
+}

@@ -1,0 +1,120 @@
+// Shared device/host helpers for libdgc_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "dgc_hip.h"
+
+namespace dgc {
+
+// ------------------------------------------------------------------ errors
+void set_error(const char* fmt, ...);
+
+#define DGC_FAIL(code, ...)            \
+    do {                               \
+        ::dgc::set_error(__VA_ARGS__); \
+        return (code);                 \
+    } while (0)
+
+#define DGC_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (call);                                                        \
+        if (_e != hipSuccess)                                                          \
+            DGC_FAIL(DGC_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #call,           \
+                     hipGetErrorString(_e));                                           \
+    } while (0)
+
+#define DGC_LAUNCHED() DGC_HIP(hipGetLastError())
+
+#define DGC_TRY(call)              \
+    do {                           \
+        int _s = (call);           \
+        if (_s != DGC_OK) return _s; \
+    } while (0)
+
+// ------------------------------------------------------------------ constants
+constexpr int kWave = 64;                 // CDNA wavefront
+constexpr int kBlock = 256;               // 4 waves
+constexpr int kMaxGrid = 256 * 8;         // 256 CUs x 8 resident 256-thread blocks
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline int grid_for(int64_t work_items, int per_block = kBlock, int cap = kMaxGrid) {
+    int64_t g = ceil_div(work_items, per_block);
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+__host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Workspace carving: every region 256-B aligned.
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+    template <typename T>
+    T* take(size_t count) {
+        off = align_up(off, 256);
+        T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+        off += count * sizeof(T);
+        return p;
+    }
+    size_t bytes() const { return align_up(off, 256); }
+};
+
+// ------------------------------------------------------------------ device helpers
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const uint32_t lane = __lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__device__ __forceinline__ uint32_t abs_key(float x) {
+    return __float_as_uint(x) & 0x7FFFFFFFu;   // |x| bit pattern: uint order == float order
+}
+
+// Exclusive prefix over (lane, j) order of 4 predicate bits per lane (bit j of p),
+// i.e. element order 4*lane + j. Returns the lane's base and the wave total.
+__device__ __forceinline__ void wave_prefix4(uint32_t p, uint32_t& lane_base, uint32_t& total) {
+    const uint64_t m0 = __ballot(p & 1u), m1 = __ballot(p & 2u);
+    const uint64_t m2 = __ballot(p & 4u), m3 = __ballot(p & 8u);
+    const uint64_t lt = lanemask_lt();
+    lane_base = __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+    total = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+}
+
+__device__ __forceinline__ void wave_prefix1(bool p, uint32_t& lane_base, uint32_t& total) {
+    const uint64_t m = __ballot(p);
+    lane_base = __popcll(m & lanemask_lt());
+    total = __popcll(m);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Wire value store (fp32 / fp16 round-to-nearest-even, overflow -> inf like torch).
+__device__ __forceinline__ void store_value(void* out, int64_t pos, float x, int vdtype) {
+    if (vdtype == DGC_F16)
+        reinterpret_cast<__half*>(out)[pos] = __float2half_rn(x);
+    else
+        reinterpret_cast<float*>(out)[pos] = x;
+}
+
+__device__ __forceinline__ void store_index(void* out, int64_t pos, int64_t idx, int idtype) {
+    if (idtype == DGC_I32)
+        reinterpret_cast<int32_t*>(out)[pos] = (int32_t)idx;
+    else
+        reinterpret_cast<int64_t*>(out)[pos] = idx;
+}
+
+}  // namespace dgc

@@ -1,0 +1,141 @@
+"""ctypes binding of ``libdgc_hip.so`` (the C ABI declared in ``include/dgc_hip.h``).
+
+The product path has no CPU fallback: if the library cannot be loaded, or a tensor
+is not an fp32 tensor on an MI355X, every entry point raises.
+"""
+import ctypes
+import os
+
+import torch
+
+__all__ = ["lib", "check", "stream_of", "ptr", "SelectParams", "SelectInfo", "Workspace",
+           "VD", "ID", "BRANCHES", "LIB_PATH", "available"]
+
+LIB_PATH = os.environ.get(
+    "DGC_HIP_LIB",
+    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libdgc_hip.so"))
+
+DGC_OK = 0
+SYNC_DEVICE, SYNC_HOST = 0, 1
+VD = {torch.float32: 0, torch.float16: 1}
+ID = {torch.int64: 0, torch.int32: 1}
+BRANCHES = {0: "direct", 1: "ok", 2: "trunc", 3: "resample", 4: "exhausted"}
+
+
+class SelectParams(ctypes.Structure):
+    _fields_ = [("numel", ctypes.c_int64), ("num_selects", ctypes.c_int64),
+                ("num_samples", ctypes.c_int64), ("upper_count", ctypes.c_int64),
+                ("lower_count", ctypes.c_int64), ("upper", ctypes.c_float), ("lower", ctypes.c_float),
+                ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("masking", ctypes.c_int32),
+                ("vdtype", ctypes.c_int32), ("idtype", ctypes.c_int32), ("update_memory", ctypes.c_int32)]
+
+
+class SelectInfo(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int64), ("candidates", ctypes.c_int64),
+                ("threshold0", ctypes.c_float), ("threshold", ctypes.c_float),
+                ("branch", ctypes.c_int32), ("recounts", ctypes.c_int32),
+                ("overflow_segments", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+INFO_BYTES = ctypes.sizeof(SelectInfo)
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+_SIGNATURES = {
+    "dgc_last_error": (ctypes.c_char_p, []),
+    "dgc_version": (ctypes.c_char_p, []),
+    "dgc_compensate": (ctypes.c_int, [_P, _P, _P, _P, _I64, _F, _I32, _I32, _P, _I64, _I64, _I64, _P]),
+    "dgc_mask_indices": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _I64, _P, _P]),
+    "dgc_sample_strided": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P]),
+    "dgc_sample_gather": (ctypes.c_int, [_P, _P, _I64, _P, _P]),
+    "dgc_kth_largest_workspace": (_SZ, [_I64]),
+    "dgc_kth_largest": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _SZ, _P]),
+    "dgc_select_workspace": (_SZ, [_I64, _I64]),
+    "dgc_select": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(SelectParams), _P, _P, _P, _P, _P, _SZ,
+                                  _I32, _P]),
+    "dgc_compress_workspace": (_SZ, [_I64, _I64, _I64]),
+    "dgc_compress": (ctypes.c_int, [_P, _P, _P, _F, _I32, _I64, _I64, _I64, ctypes.POINTER(SelectParams),
+                                    _P, _P, _P, _P, _P, _SZ, _I32, _P]),
+    "dgc_decompress_workspace": (_SZ, [_I64, _I32]),
+    "dgc_decompress": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, ctypes.POINTER(ctypes.c_int64), _I32, _P,
+                                      _I64, _F, _P, _SZ, _P]),
+    "dgc_payload_layout": (_I64, [_I64, _I32, _I32, ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.POINTER(ctypes.c_int64)]),
+    "dgc_decompress_packed": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
+    "dgc_decompress_status": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
+}
+
+_lib = None
+_load_error = None
+
+
+def _load():
+    global _lib, _load_error
+    if _lib is not None or _load_error is not None:
+        return _lib
+    try:
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    except OSError as e:   # pragma: no cover - reported through lib()
+        _load_error = e
+    return _lib
+
+
+def available():
+    return _load() is not None
+
+
+def lib():
+    """The loaded library; raises if it is missing (there is no fallback path)."""
+    handle = _load()
+    if handle is None:
+        raise RuntimeError(f"libdgc_hip.so could not be loaded from {LIB_PATH}: {_load_error}. "
+                           "Build it with `make -C adam-compression_amd/csrc` (hipcc, gfx950).")
+    return handle
+
+
+def check(status, what="dgc"):
+    if status != DGC_OK:
+        msg = lib().dgc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def require_cuda_f32(t, what):
+    if not (torch.is_tensor(t) and t.is_cuda):
+        raise RuntimeError(f"{what}: the DGC hot path runs on the MI355X only (got a "
+                           f"{'CPU' if torch.is_tensor(t) else type(t).__name__} tensor)")
+    if t.dtype != torch.float32:
+        raise NotImplementedError(f"{what}: fp32 tensors only (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+
+
+class Workspace:
+    """Grow-only device scratch buffers keyed by (device, tag): the library never allocates."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, device, nbytes, tag="ws"):
+        key = (str(device), tag)
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self._bufs[key] = buf
+        return buf

@@ -1,0 +1,147 @@
+"""Flat-bucket DGC step with no host synchronisation (the padded fast path).
+
+One fp32 gradient bucket per rank goes through the whole DGC step of the
+reference — compensate -> sample -> threshold -> select/adapt/resample -> update
+(dgc/memory.py:50-77, dgc/compression.py:109-177) -> allgather
+(dgc/compression.py:200-212) -> decompress (dgc/compression.py:179-194) — with
+every decision kept on the device:
+
+* the payload is fixed-capacity: ``[count | values(k) | indices(k)]`` per rank
+  (``dgc_payload_layout``), so the RCCL allgather needs no size exchange and the
+  decompress reads each rank's count on the device;
+* the selection runs in ``DGC_SYNC_DEVICE`` mode (adaptation recounts and the
+  resample chain are launched and early-exit on a device flag).
+
+The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
+kernels); the sample start is drawn from a ``random.Random`` seeded identically on
+every rank, one draw per step, like the reference's global ``random`` call.
+"""
+import math
+import random
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+__all__ = ["DGCBucket", "algorithmic_bytes"]
+
+
+def algorithmic_bytes(numel, k, num_samples, world, vbytes=4, ibytes=8):
+    """Bytes one rank must move per step:
+    compensate 20N + select re-read 4N + dense decompress write 4N, the samples 4S,
+    masking 8k, payload written k(vb+ib) + gathered W*k(vb+ib) read, scatter RMW 8Wk."""
+    return (28 * numel + 4 * num_samples + 8 * k + (1 + world) * k * (vbytes + ibytes) + 8 * world * k)
+
+
+class DGCBucket:
+    def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
+                 sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
+                 max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
+                 device=None, world_size=None, seed=42):
+        from .compression import DGCCompressor, _layout
+        self.device = torch.device(device or "cuda")
+        self.numel = N = int(numel)
+        ratio = compress_ratio if compress_ratio <= 1.0 else 1.0 / compress_ratio
+        sample_ratio = min(max(sample_ratio, 0.01), 1.0)
+        self.stride, self.num_samples = DGCCompressor._stride_and_samples(N, ratio, sample_ratio)
+        self.top_k_samples = int(math.ceil(self.num_samples * ratio))
+        self.k = int(math.ceil(N * ratio))
+        self.momentum, self.nesterov = float(momentum), bool(nesterov)
+        self.world = world_size or (dist.get_world_size() if dist.is_initialized() else 1)
+        self.vdtype = torch.float16 if fp16_values else torch.float32
+        self.idtype = torch.int32 if int32_indices else torch.int64
+        self.rng = random.Random(seed)
+
+        p = _lib.SelectParams()
+        p.numel, p.num_selects, p.num_samples = N, self.k, self.num_samples
+        p.upper_count = math.floor(self.k * compress_upper_bound)
+        p.lower_count = math.ceil(compress_lower_bound * self.k)
+        p.upper, p.lower = float(compress_upper_bound), float(compress_lower_bound)
+        p.max_iters, p.resample, p.masking = int(max_adaptation_iters), int(bool(resample)), int(bool(momentum_masking))
+        p.vdtype, p.idtype, p.update_memory = _lib.VD[self.vdtype], _lib.ID[self.idtype], 1
+        self.params = p
+
+        dev = self.device
+        self.mmt = torch.zeros(N, dtype=torch.float32, device=dev)
+        self.vec = torch.zeros(N, dtype=torch.float32, device=dev)
+        L = _lib.lib()
+        self.sampled = N != self.num_samples
+        self.samples = torch.empty(self.num_samples + 2 if self.sampled else 1, dtype=torch.float32, device=dev)
+        self.thr = torch.empty(64, dtype=torch.float32, device=dev)
+        n_thr = self.num_samples + 1 if self.sampled else N
+        self.kth_ws = torch.empty(max(256, L.dgc_kth_largest_workspace(n_thr)), dtype=torch.uint8, device=dev)
+        self.sel_ws = torch.empty(L.dgc_select_workspace(N, self.k), dtype=torch.uint8, device=dev)
+        self.info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
+        self.rank_stride, self.voff, self.ioff = _layout(self.k, self.vdtype, self.idtype)
+        self.payload = torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev)
+        self.gathered = (torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=dev)
+                         if self.world > 1 else self.payload)
+        self.dec_ws = torch.empty(L.dgc_decompress_workspace(N, self.world), dtype=torch.uint8, device=dev)
+        self.scale = 1.0 / self.world
+        self._L = L
+
+    # ---------------------------------------------------------------- phases
+    def compensate(self, grad):
+        """K1 with the strided sample fused in; returns the sample count L."""
+        L = self._L
+        N = self.numel
+        if self.sampled:
+            self.start = self.rng.randint(0, self.stride - 1)
+            cnt = (N - self.start + self.stride - 1) // self.stride
+        else:
+            self.start, cnt = 0, 0
+        _lib.check(L.dgc_compensate(grad.data_ptr(), self.mmt.data_ptr(), self.vec.data_ptr(), None, N,
+                                    self.momentum, int(self.nesterov), 1,
+                                    self.samples.data_ptr() if self.sampled else None, self.start, self.stride,
+                                    cnt, _lib.stream_of(self.device)), "dgc_compensate")
+        self.cnt = cnt if self.sampled else N
+        return self.cnt
+
+    def threshold(self):
+        L = self._L
+        src = self.samples if self.sampled else self.vec
+        _lib.check(L.dgc_kth_largest(src.data_ptr(), self.cnt, self.top_k_samples, self.thr.data_ptr(),
+                                     self.kth_ws.data_ptr(), self.kth_ws.numel(), _lib.stream_of(self.device)),
+                   "dgc_kth_largest")
+
+    def select(self):
+        L = self._L
+        base = self.payload.data_ptr()
+        import ctypes
+        _lib.check(L.dgc_select(self.vec.data_ptr(), self.mmt.data_ptr(), self.thr.data_ptr(),
+                                ctypes.byref(self.params), base + self.voff, base + self.ioff, base,
+                                self.info.data_ptr(), self.sel_ws.data_ptr(), self.sel_ws.numel(),
+                                _lib.SYNC_DEVICE, _lib.stream_of(self.device)), "dgc_select")
+
+    def exchange(self):
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.gathered, self.payload)
+
+    def decompress(self, out):
+        L = self._L
+        _lib.check(L.dgc_decompress_packed(self.gathered.data_ptr(), self.world, self.rank_stride, self.k,
+                                           _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
+                                           self.numel, self.scale, self.dec_ws.data_ptr(), self.dec_ws.numel(),
+                                           _lib.stream_of(self.device)), "dgc_decompress_packed")
+
+    def step(self, grad, out, events=None):
+        """compensate -> threshold -> select -> allgather -> decompress; ``events`` maps a
+        phase name to a (start, end) pair of torch.cuda.Event recorded around it."""
+        ev = events or {}
+        for name, fn in (("compensate", lambda: self.compensate(grad)), ("threshold", self.threshold),
+                         ("select", self.select), ("allgather", self.exchange),
+                         ("decompress", lambda: self.decompress(out))):
+            pair = ev.get(name)
+            if pair:
+                pair[0].record()
+            fn()
+            if pair:
+                pair[1].record()
+
+    def last_info(self):
+        raw = self.info.cpu().numpy().tobytes()
+        i = _lib.SelectInfo.from_buffer_copy(raw)
+        return dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
+                    branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
+                    overflow_segments=i.overflow_segments)

@@ -1,0 +1,161 @@
+"""Data-parallel optimizer wrapper — drop-in for the reference's patched Horovod
+``DistributedOptimizer`` (dgc/horovod/optimizer.py:34-194, 370-417).
+
+Per parameter, an autograd grad-accumulator hook calls
+``compression.compress(p.grad, name)`` and then ``compression.communicate`` (found
+by ``getattr``, falling back to a plain allreduce); ``step()`` / ``synchronize()``
+wait on every handle, ``decompress`` the result and ``p.grad.set_`` it before the
+wrapped optimizer steps (dgc/horovod/optimizer.py:105-187). Hooks are registered
+only when the world has more than one rank (or ``HOROVOD_ELASTIC=1``), exactly as
+the reference does (dgc/horovod/optimizer.py:79-80).
+
+The transport is ``dgc.comm`` (torch.distributed; RCCL over xGMI on MI355X)
+instead of Horovod/MPI. The Adasum delta-model variant
+(dgc/horovod/optimizer.py:197-367) is not part of the DGC path and is refused.
+"""
+import os
+import warnings
+from contextlib import contextmanager
+
+import torch
+
+from dgc import comm
+from dgc.comm import Adasum, Average
+from dgc.horovod.compression import Compression
+
+__all__ = ["DistributedOptimizer"]
+
+
+class _DistributedOptimizer(torch.optim.Optimizer):
+    def __init__(self, params, named_parameters, compression, backward_passes_per_step=1, op=Average):
+        super(self.__class__, self).__init__(params)
+        self._compression = compression
+        self._communicate_ = getattr(compression, "communicate", None) or \
+            (lambda t, name, op: comm.allreduce_async_(t, name=name, op=op))
+        self._synchronize_ = getattr(compression, "synchronize", comm.synchronize)
+
+        if named_parameters is not None:
+            named_parameters = list(named_parameters)
+        else:
+            named_parameters = [(f"allreduce.noname.{i}", v)
+                                for group in self.param_groups for i, v in enumerate(group["params"])]
+        if any(not isinstance(p, tuple) for p in named_parameters):
+            raise ValueError("named_parameters should be a sequence of tuples (name, parameter), "
+                             "usually produced by model.named_parameters().")
+        names = [k for k, _ in named_parameters]
+        dups = {n for n in names if names.count(n) > 1}
+        if dups:
+            raise ValueError("Parameter names in named_parameters must be unique. Found duplicates: "
+                             + ", ".join(sorted(dups)))
+        all_ids = {id(v) for group in self.param_groups for v in group["params"]}
+        unnamed = all_ids - {id(v) for _, v in named_parameters}
+        if unnamed:
+            raise ValueError("named_parameters was specified, but one or more model parameters were "
+                             "not named. Python object ids: " + ", ".join(str(i) for i in unnamed))
+
+        self._parameter_names = {v: k for k, v in sorted(named_parameters, key=lambda kv: kv[0])}
+        self.backward_passes_per_step = backward_passes_per_step
+        self._allreduce_delay = {v: backward_passes_per_step for _, v in named_parameters}
+        self.op = op
+        self._handles = {}
+        self._grad_accs = []
+        self._requires_update = set()
+        self._synchronized = False
+        self._should_synchronize = True
+        if comm.size() > 1 or os.environ.get("HOROVOD_ELASTIC") == "1":
+            self._register_hooks()
+
+    def load_state_dict(self, *args, **kwargs):
+        self._handles = {}
+        self._synchronized = False
+        self._should_synchronize = True
+        for p in self._allreduce_delay:
+            self._allreduce_delay[p] = self.backward_passes_per_step
+        super(self.__class__, self).load_state_dict(*args, **kwargs)
+
+    def set_backward_passes_per_step(self, passes):
+        self.backward_passes_per_step = passes
+        for p in self._allreduce_delay:
+            self._allreduce_delay[p] = passes
+
+    def _register_hooks(self):
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.requires_grad:
+                    p.grad = p.data.new(p.size()).zero_()
+                    self._requires_update.add(p)
+                    grad_acc = p.expand_as(p).grad_fn.next_functions[0][0]
+                    grad_acc.register_hook(self._make_hook(p))
+                    self._grad_accs.append(grad_acc)
+
+    def _allreduce_grad_async(self, p):
+        name = self._parameter_names.get(p)
+        tensor_compressed, ctx = self._compression.compress(p.grad, name)
+        handle = self._communicate_(tensor_compressed, name=name, op=self.op)
+        return handle, ctx
+
+    def _make_hook(self, p):
+        def hook(*ignore):
+            if p in self._handles and self._handles[p][0] is not None:
+                if self._allreduce_delay[p] <= 0:
+                    raise AssertionError("Gradients were computed more than backward_passes_per_step times "
+                                         "before call to step(). Increase backward_passes_per_step to "
+                                         "accumulate gradients locally.")
+            assert not p.grad.requires_grad
+            assert self._allreduce_delay[p] > 0
+            handle, ctx = None, None
+            self._allreduce_delay[p] -= 1
+            if self._allreduce_delay[p] == 0:
+                handle, ctx = self._allreduce_grad_async(p)
+            self._handles[p] = (handle, ctx)
+        return hook
+
+    def synchronize(self):
+        for p in self._requires_update - set(self._handles.keys()):
+            self._handles[p] = self._allreduce_grad_async(p)
+        for p, (handle, ctx) in list(self._handles.items()):
+            if handle is None:
+                self._handles[p] = self._allreduce_grad_async(p)
+        for p, (handle, ctx) in self._handles.items():
+            output = self._synchronize_(handle)
+            self._allreduce_delay[p] = self.backward_passes_per_step
+            p.grad.set_(self._compression.decompress(output, ctx))
+        self._handles.clear()
+        self._synchronized = True
+
+    @contextmanager
+    def skip_synchronize(self):
+        """Use after an explicit ``optimizer.synchronize()`` so ``step()`` does not sync again."""
+        self._should_synchronize = False
+        try:
+            yield
+        finally:
+            self._should_synchronize = True
+
+    def step(self, closure=None):
+        if self._should_synchronize:
+            if self._synchronized:
+                warnings.warn("optimizer.step() called without optimizer.skip_synchronize() context after "
+                              "optimizer.synchronize(). This can cause training slowdown. You may want to "
+                              "consider using optimizer.skip_synchronize() context if you use "
+                              "optimizer.synchronize() in your code.")
+            self.synchronize()
+        self._synchronized = False
+        return super(self.__class__, self).step(closure)
+
+    def zero_grad(self, *args, **kwargs):
+        if self._handles:
+            raise AssertionError("optimizer.zero_grad() was called after loss.backward() but before "
+                                 "optimizer.step() or optimizer.synchronize(). This is prohibited as it "
+                                 "can cause a race condition.")
+        return super(self.__class__, self).zero_grad(*args, **kwargs)
+
+
+def DistributedOptimizer(optimizer, named_parameters=None, compression=Compression.none,
+                         backward_passes_per_step=1, op=Average):
+    """Wrap ``optimizer`` so gradients are compressed, exchanged across ranks and
+    decompressed before it steps (dgc/horovod/optimizer.py:370-417)."""
+    if op == Adasum and comm.size() > 1:
+        raise NotImplementedError("Adasum is not part of the DGC path (dgc/horovod/optimizer.py:197-367)")
+    cls = type(optimizer.__class__.__name__, (optimizer.__class__,), dict(_DistributedOptimizer.__dict__))
+    return cls(optimizer.param_groups, named_parameters, compression, backward_passes_per_step, op)

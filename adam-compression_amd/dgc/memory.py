@@ -1,0 +1,122 @@
+"""Momentum-correction memory for DGC — drop-in for the reference ``dgc/memory.py``.
+
+Same classes, constructor arguments, methods and state layout as the reference
+(``Memory`` static API, dgc/memory.py:9-28; ``DGCSGDMemory``, dgc/memory.py:31-88).
+The arithmetic runs in ``libdgc_hip.so`` on the MI355X:
+
+* ``compensate``  -> ``dgc_compensate`` (K1: one fused streaming pass, fp32 with the
+  reference's two separate roundings, no FMA contraction);
+* ``update``      -> ``dgc_mask_indices`` (the same masking that ``dgc_compress``
+  fuses into its emit kernel when the compressor drives this memory).
+
+``momentums`` / ``velocities`` stay plain param-shaped fp32 tensors keyed by name,
+so ``state_dict`` / ``load_state_dict`` and checkpoints are unchanged.
+"""
+import torch
+
+from . import _lib
+from . import comm
+
+__all__ = ["Memory", "DGCSGDMemory"]
+
+
+class Memory:
+    """No-op memory (dgc/memory.py:9-28)."""
+
+    @staticmethod
+    def initialize(*args, **kwargs):
+        pass
+
+    @staticmethod
+    def compensate(tensor, *args, **kwargs):
+        return tensor
+
+    @staticmethod
+    def update(*args, **kwargs):
+        pass
+
+    @staticmethod
+    def state_dict():
+        return None
+
+    @staticmethod
+    def load_state_dict(state_dict):
+        pass
+
+
+class DGCSGDMemory(Memory):
+    """Memory for momentum correction in DGC for momentum SGD (dgc/memory.py:31-88)."""
+
+    def __init__(self, momentum=0.9, nesterov=False, gradient_clipping=None, momentum_masking=True):
+        self.gradient_clipping = gradient_clipping
+        self.momentum_masking = momentum_masking
+        self.momentum = momentum
+        self.nesterov = nesterov
+        self.momentums = {}
+        self.velocities = {}
+        self._bad = {}
+
+    def initialize(self, named_parameters):
+        """zeros_like per parameter (dgc/memory.py:43-48)."""
+        if comm.rank() == 0:
+            print("=> initializing dgc sgd memory")
+        for name, param in named_parameters:
+            self.momentums[name] = torch.zeros_like(param.data)
+            self.velocities[name] = torch.zeros_like(param.data)
+
+    # ------------------------------------------------------------------ K1
+    def _clip(self, grad):
+        return self.gradient_clipping(grad) if self.gradient_clipping is not None else grad
+
+    def compensate(self, grad, name, accumulate=True):
+        """Momentum correction + local accumulation (dgc/memory.py:50-70).
+
+        accumulate=True returns ``velocities[name]`` itself (updated in place);
+        accumulate=False (dense tensors) returns a new tensor."""
+        grad = self._clip(grad)
+        mmt = self.momentums[name]
+        _lib.require_cuda_f32(grad, "DGCSGDMemory.compensate")
+        _lib.require_cuda_f32(mmt, "DGCSGDMemory.compensate")
+        g = grad.contiguous()
+        L = _lib.lib()
+        stream = _lib.stream_of(g.device)
+        if accumulate:
+            vec = self.velocities[name]
+            _lib.check(L.dgc_compensate(_lib.ptr(g), _lib.ptr(mmt), _lib.ptr(vec), None, mmt.numel(),
+                                        float(self.momentum), int(bool(self.nesterov)), 1, None, 0, 1, 0,
+                                        stream), "dgc_compensate")
+            return vec
+        out = torch.empty_like(mmt)
+        _lib.check(L.dgc_compensate(_lib.ptr(g), _lib.ptr(mmt), None, _lib.ptr(out), mmt.numel(),
+                                    float(self.momentum), int(bool(self.nesterov)), 0, None, 0, 1, 0,
+                                    stream), "dgc_compensate")
+        return out
+
+    def update(self, name, ctx):
+        """Zero the transmitted slots (dgc/memory.py:72-77)."""
+        indices = ctx[0]
+        vec = self.velocities[name]
+        mmt = self.momentums[name]
+        _lib.require_cuda_f32(vec, "DGCSGDMemory.update")
+        idx = indices.reshape(-1)
+        if idx.dtype not in _lib.ID:
+            idx = idx.to(torch.int64)
+        idx = idx.contiguous()
+        bad = self._bad.get(vec.device)
+        if bad is None:
+            bad = self._bad[vec.device] = torch.zeros(1, dtype=torch.int32, device=vec.device)
+        L = _lib.lib()
+        _lib.check(L.dgc_mask_indices(_lib.ptr(mmt) if self.momentum_masking else None, _lib.ptr(vec),
+                                      vec.numel(), _lib.ptr(idx), _lib.ID[idx.dtype], idx.numel(),
+                                      _lib.ptr(bad), _lib.stream_of(vec.device)), "dgc_mask_indices")
+
+    def state_dict(self):
+        return dict(momentums=self.momentums, velocities=self.velocities)
+
+    def load_state_dict(self, state_dict):
+        momentums = state_dict["momentums"]
+        velocities = state_dict["velocities"]
+        for name in self.momentums.keys():
+            if name in momentums:
+                self.momentums[name] = momentums[name]
+                self.velocities[name] = velocities[name]

@@ -1,0 +1,181 @@
+/*
+ * dgc_hip.h — C ABI of libdgc_hip.so, the MI355X (gfx950) DGC hot path.
+ *
+ * Every entry point replaces a piece of the reference's PyTorch/Horovod path
+ * (emma-mens/adam-compression, paths relative to the reference root):
+ *
+ *   dgc_compensate        DGCSGDMemory.compensate            dgc/memory.py:50-70
+ *                         (+ the strided sample of _sparsify  dgc/compression.py:113,119)
+ *   dgc_sample_strided    importance[start::stride]          dgc/compression.py:113,119
+ *   dgc_sample_gather     importance[randint(...)]           dgc/compression.py:120-121
+ *   dgc_kth_largest       min(topk(samples, k))              dgc/compression.py:123
+ *   dgc_mask_indices      DGCSGDMemory.update                dgc/memory.py:72-77
+ *   dgc_select            ge/nonzero + adaptation loop +     dgc/compression.py:124-153
+ *                         resample + truncate + gather,
+ *                         DGCSGDMemory.update,               dgc/memory.py:72-77
+ *                         wire casts                         dgc/compression.py:168-171
+ *   dgc_compress          compensate -> _sparsify -> update  dgc/compression.py:155-172
+ *   dgc_decompress        zero_ + index_put_(accumulate)     dgc/compression.py:179-194
+ *                         + mul_(1/W) over the rank-order
+ *                         concatenation of the allgather     dgc/compression.py:200-212
+ *   dgc_decompress_packed the same, straight from the padded RCCL allgather buffer
+ *
+ * Conventions
+ *   - All tensor pointers are DEVICE pointers owned by the caller (PyTorch's caching
+ *     allocator). The library never allocates; scratch comes from a caller-supplied
+ *     workspace whose size the *_workspace() queries return. Workspaces must be
+ *     256-byte aligned.
+ *   - Every call is stream-ordered on `stream` (a hipStream_t; NULL = legacy stream)
+ *     and returns immediately, except dgc_compress / dgc_select with
+ *     DGC_SYNC_HOST, which read a few bytes of device state back to skip kernels.
+ *   - Return value: DGC_OK or an error code; dgc_last_error() gives a thread-local
+ *     message. Kernel faults surface at the caller's next synchronisation.
+ *   - Element counts are int64: the 7B-element buckets exceed 2^32.
+ */
+#ifndef DGC_HIP_H
+#define DGC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum dgc_status {
+    DGC_OK = 0,
+    DGC_ERR_INVALID = 1,      /* bad argument (null pointer, k > n, ...) */
+    DGC_ERR_DTYPE = 2,        /* unsupported value / index dtype */
+    DGC_ERR_OVERFLOW = 3,     /* int32 indices requested for n > 2^31 - 1 */
+    DGC_ERR_HIP = 4,          /* a HIP runtime call failed */
+    DGC_ERR_WORKSPACE = 5,    /* workspace too small or misaligned */
+    DGC_ERR_UNSORTED = 6      /* decompress input has more descending runs than supported */
+};
+
+enum dgc_vdtype { DGC_F32 = 0, DGC_F16 = 1 };   /* wire value dtype  (fp16_values)   */
+enum dgc_idtype { DGC_I64 = 0, DGC_I32 = 1 };   /* wire index dtype  (int32_indices) */
+
+enum dgc_sync_mode {
+    DGC_SYNC_DEVICE = 0,      /* every decision on device; no host synchronisation      */
+    DGC_SYNC_HOST = 1         /* read decisions back to skip unneeded launches (drop-in) */
+};
+
+/* Branch taken by the selection (mirrors the reference's adaptation loop). */
+enum dgc_branch {
+    DGC_BRANCH_DIRECT = 0,    /* numel == num_samples: no adaptation loop */
+    DGC_BRANCH_OK = 1,        /* lower*k <= n <= k                        */
+    DGC_BRANCH_TRUNC = 2,     /* k < n <= upper*k: first k ascending      */
+    DGC_BRANCH_RESAMPLE = 3,  /* n > upper*k: top-k of the candidates     */
+    DGC_BRANCH_EXHAUSTED = 4  /* max_adaptation_iters recounts used up    */
+};
+
+/* Per-tensor selection parameters: DGCCompressor.attributes[name]
+ * (dgc/compression.py:85) plus the compressor's knobs (dgc/compression.py:18-54). */
+typedef struct dgc_select_params {
+    int64_t numel;            /* N                                          */
+    int64_t num_selects;      /* k = ceil(N * ratio)                        */
+    int64_t num_samples;      /* attributes num_samples (N == S: no loop)   */
+    int64_t upper_count;      /* floor(k * compress_upper_bound)  (n > U)   */
+    int64_t lower_count;      /* ceil(compress_lower_bound * k)   (n < L)   */
+    float upper;              /* fl32(compress_upper_bound), threshold *=   */
+    float lower;              /* fl32(compress_lower_bound), threshold *=   */
+    int32_t max_iters;        /* max_adaptation_iters                       */
+    int32_t resample;         /* resample flag                              */
+    int32_t masking;          /* DGCSGDMemory.momentum_masking               */
+    int32_t vdtype;           /* enum dgc_vdtype of values_out              */
+    int32_t idtype;           /* enum dgc_idtype of indices_out             */
+    int32_t update_memory;    /* 1: zero the emitted slots of vec (and of   */
+                              /*    mmt when masking) = DGCSGDMemory.update */
+                              /* 0: pure selection, vec/mmt untouched       */
+} dgc_select_params;
+
+/* Device-resident result record written by dgc_select / dgc_compress. */
+typedef struct dgc_select_info {
+    int64_t count;            /* n emitted (== *count_out)                  */
+    int64_t candidates;       /* count at the final threshold               */
+    float threshold0;         /* sampled threshold                          */
+    float threshold;          /* final threshold                            */
+    int32_t branch;           /* enum dgc_branch                            */
+    int32_t recounts;         /* adaptation recounts executed               */
+    int32_t overflow_segments;/* segments whose candidate list spilled      */
+    int32_t reserved;
+} dgc_select_info;
+
+const char* dgc_last_error(void);
+const char* dgc_version(void);
+
+/* ---- K1: momentum correction + velocity accumulation (+ fused strided sample) ----
+ * accumulate=1: mmt, vec updated in place, out must be NULL or == vec.
+ * accumulate=0: mmt updated, result written to out (vec unused).
+ * samples != NULL: samples[q] = |vec_new[sample_start + q*sample_stride]| for
+ *                  q < num_samples (num_samples = ceil((n - start) / stride)). */
+int dgc_compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n,
+                   float momentum, int32_t nesterov, int32_t accumulate,
+                   float* samples, int64_t sample_start, int64_t sample_stride,
+                   int64_t num_samples, void* stream);
+
+/* DGCSGDMemory.update (dgc/memory.py:72-77) as a standalone scatter: vec[i] = 0 and,
+ * when mmt != NULL (momentum_masking), mmt[i] = 0 for i in indices[0..count).
+ * Negative indices wrap like torch; out-of-range ones set *bad_flag (device int). */
+int dgc_mask_indices(float* mmt, float* vec, int64_t n, const void* indices, int32_t idtype,
+                     int64_t count, int32_t* bad_flag, void* stream);
+
+/* ---- K2: sampling ---- */
+int dgc_sample_strided(const float* vec, int64_t n, int64_t start, int64_t stride,
+                       float* samples, int64_t num_samples, void* stream);
+int dgc_sample_gather(const float* vec, const int64_t* sample_indices, int64_t num_samples,
+                      float* samples, void* stream);
+
+/* ---- K3: k-th largest of |x| (topk threshold); NaN if any |x| is NaN ---- */
+size_t dgc_kth_largest_workspace(int64_t n);
+int dgc_kth_largest(const float* x, int64_t n, int64_t k, float* thr_out,
+                    void* ws, size_t ws_bytes, void* stream);
+
+/* ---- K4: selection, adaptation loop, pack, masking ----
+ * vec (length numel) is read; with params.update_memory its emitted slots are
+ * zeroed, and mmt's too when params.masking (dgc_compress forces update_memory=1). thr0 is the device scalar from dgc_kth_largest. Writes
+ * values_out[0..n), indices_out[0..n) (ascending), *count_out = n (device int64)
+ * and *info_out (device, may be NULL). */
+size_t dgc_select_workspace(int64_t numel, int64_t num_selects);
+int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_params* params,
+               void* values_out, void* indices_out, int64_t* count_out,
+               dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
+               void* stream);
+
+/* ---- fused compress: compensate + sample + threshold + select ---- */
+size_t dgc_compress_workspace(int64_t numel, int64_t num_selects, int64_t num_samples);
+int dgc_compress(const float* grad, float* mmt, float* vec, float momentum, int32_t nesterov,
+                 int64_t sample_start, int64_t sample_stride, int64_t top_k_samples,
+                 const dgc_select_params* params, void* values_out, void* indices_out,
+                 int64_t* count_out, dgc_select_info* info_out, void* ws, size_t ws_bytes,
+                 int32_t sync_mode, void* stream);
+
+/* ---- K6: deterministic decompress ----
+ * grad[0..n) = scale * (rank-order sequential sum of the entries), every other
+ * slot +0.0. dgc_decompress takes the concatenated (values, indices) of the
+ * allgather; run_offsets (HOST array of nruns+1 entry offsets, e.g. the per-rank
+ * counts' prefix sums) may be NULL, in which case runs are detected on device. */
+size_t dgc_decompress_workspace(int64_t n, int32_t max_runs);
+int dgc_decompress(const void* values, int32_t vdtype, const void* indices, int32_t idtype,
+                   int64_t total, const int64_t* run_offsets, int32_t nruns,
+                   float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, void* stream);
+
+/* Packed per-rank payload (the RCCL allgather unit), byte offsets from the
+ * rank's base:  [0] int64 count | [values_offset] values | [indices_offset] indices;
+ * rank r starts at payload + r * rank_stride. */
+int64_t dgc_payload_layout(int64_t capacity, int32_t vdtype, int32_t idtype,
+                           int64_t* values_offset, int64_t* indices_offset);
+int dgc_decompress_packed(const void* payload, int32_t world, int64_t rank_stride,
+                          int64_t capacity, int32_t vdtype, int32_t idtype,
+                          float* grad, int64_t n, float scale, void* ws, size_t ws_bytes,
+                          void* stream);
+
+/* Status word written by the decompress kernels: bit 0 = an index was out of
+ * range [0, n) and was ignored; bit 1 = a run given by run_offsets was not
+ * non-decreasing (its stray entries were ignored). Reads 4 bytes from the workspace (synchronous). */
+int dgc_decompress_status(const void* ws, int32_t* status, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGC_HIP_H */

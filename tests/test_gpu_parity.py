@@ -1,0 +1,478 @@
+"""GPU parity: every kernel of libdgc_hip.so against the numpy oracle (bit-exact for
+indices, counts, thresholds, state and wire bytes), and the drop-in classes against
+the reference-generated golden fixtures. Runs through the C ABI on cuda:0."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dgc_oracle as O
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc import _lib
+    return _lib.lib()
+
+
+def stream():
+    from dgc import _lib
+    return _lib.stream_of(DEV)
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view({4: np.uint32, 2: np.uint16, 8: np.uint64}[a.dtype.itemsize])
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def check(L, rc):
+    assert rc == 0, L.dgc_last_error().decode()
+
+
+# ----------------------------------------------------------------------------- K1
+@pytest.mark.parametrize("nesterov", [True, False])
+@pytest.mark.parametrize("n", [1, 3, 4, 1000, 4099, (1 << 20) + 3])
+def test_compensate_accumulate_bitexact(L, nesterov, n):
+    g0, m0, v0 = synth.gradient(1, n), synth.gradient(2, n), synth.gradient(3, n)
+    m, v = m0.copy(), v0.copy()
+    tg, tm, tv = to_dev(g0), to_dev(m0), to_dev(v0)
+    for step in range(3):
+        O.compensate(g0, m, v, 0.9, nesterov, True)
+        check(L, L.dgc_compensate(P(tg), P(tm), P(tv), None, n, 0.9, int(nesterov), 1, None, 0, 1, 0, stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(tm.cpu().numpy()), bits(m))
+    assert np.array_equal(bits(tv.cpu().numpy()), bits(v))
+
+
+@pytest.mark.parametrize("nesterov", [True, False])
+def test_compensate_dense_branch_and_unaligned(L, nesterov):
+    n = 100003
+    g0, m0 = synth.gradient(4, n + 1), synth.gradient(5, n + 1)
+    m = m0[1:].copy()
+    want = O.compensate(g0[1:], m, None, 0.9, nesterov, accumulate=False)
+    tg, tm = to_dev(g0), to_dev(m0)
+    out = torch.empty(n + 1, device=DEV)
+    # element offset 1: 4-B aligned only -> scalar path
+    check(L, L.dgc_compensate(tg.data_ptr() + 4, tm.data_ptr() + 4, None, out.data_ptr() + 4, n, 0.9,
+                              int(nesterov), 0, None, 0, 1, 0, stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()[1:]), bits(want))
+    assert np.array_equal(bits(tm.cpu().numpy()[1:]), bits(m))
+
+
+@pytest.mark.parametrize("stride,start", [(97, 0), (97, 5), (97, 96), (9, 3), (33, 32), (2, 1), (3, 0)])
+@pytest.mark.parametrize("n", [1000003, 4096 * 3 + 1])
+def test_compensate_fused_sample(L, n, stride, start):
+    g0, m0, v0 = synth.gradient(6, n), synth.gradient(7, n), synth.gradient(8, n)
+    m, v = m0.copy(), v0.copy()
+    O.compensate(g0, m, v, 0.9, True, True)
+    want = O.strided_samples(v, start, stride)
+    tg, tm, tv = to_dev(g0), to_dev(m0), to_dev(v0)
+    cnt = (n - start + stride - 1) // stride
+    samples = torch.full((cnt + 1,), -1.0, device=DEV)
+    check(L, L.dgc_compensate(P(tg), P(tm), P(tv), None, n, 0.9, 1, 1, P(samples), start, stride, cnt, stream()))
+    torch.cuda.synchronize()
+    got = samples.cpu().numpy()
+    assert np.array_equal(bits(got[:cnt]), bits(want)) and got[cnt] == -1.0
+    assert np.array_equal(bits(tv.cpu().numpy()), bits(v))
+    # standalone K2 over the same velocity gives the same samples
+    s2 = torch.empty(cnt, device=DEV)
+    check(L, L.dgc_sample_strided(P(tv), n, start, stride, P(s2), cnt, stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(s2.cpu().numpy()), bits(want))
+
+
+def test_sample_gather(L):
+    n = 50000
+    v = synth.gradient(9, n)
+    idx = np.random.default_rng(0).integers(0, n, 777)
+    out = torch.empty(777, device=DEV)
+    check(L, L.dgc_sample_gather(P(to_dev(v)), P(to_dev(idx)), 777, P(out), stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(np.abs(v[idx])))
+
+
+# ----------------------------------------------------------------------------- K3
+def kth_dev(L, x_np, k):
+    x = to_dev(x_np)
+    out = torch.empty(1, device=DEV)
+    wsz = L.dgc_kth_largest_workspace(x_np.size)
+    ws = torch.empty(max(wsz, 256), dtype=torch.uint8, device=DEV)
+    check(L, L.dgc_kth_largest(P(x), x_np.size, k, P(out), P(ws), wsz, stream()))
+    torch.cuda.synchronize()
+    return out.cpu().numpy()[0]
+
+
+@pytest.mark.parametrize("n", [1, 100, 32768, 32769, 1000000, 10309279])
+def test_kth_largest_matches_topk_min(L, n):
+    x = synth.gradient(10 + n % 7, n)
+    for k in sorted({1, max(1, n // 1000), max(1, n // 97), n}):
+        want = O.kth_largest(np.abs(x), k)
+        got = kth_dev(L, x, k)
+        assert bits(np.float32(got)) == bits(want), (n, k)
+
+
+@pytest.mark.parametrize("kind", ["ties", "sparse", "bf16"])
+def test_kth_largest_ties(L, kind):
+    x = synth.gradient(11, 200000, kind)
+    for k in (1, 7, 2000, 150000, 200000):
+        assert bits(np.float32(kth_dev(L, x, k))) == bits(O.kth_largest(np.abs(x), k)), (kind, k)
+
+
+def test_kth_largest_specials(L):
+    x = synth.gradient(12, 50000)
+    x[[5, 77]] = np.inf
+    x[100] = -np.inf
+    assert kth_dev(L, x, 3) == np.inf and kth_dev(L, x, 4) == O.kth_largest(np.abs(x), 4)
+    x[9] = np.nan
+    assert np.isnan(kth_dev(L, x, 1000))          # topk ranks NaN first, min propagates it
+    small = x[:1000].copy()
+    assert np.isnan(kth_dev(L, small, 10))
+    z = np.zeros(5000, np.float32)
+    z[::2] = -0.0
+    assert bits(np.float32(kth_dev(L, z, 17))) == 0   # |-0| == +0
+
+
+# ----------------------------------------------------------------------------- K4
+def select_dev(L, vec_np, mmt_np, thr, attrs, *, upper=1.3, lower=0.8, max_iters=10, resample=True,
+               masking=True, fp16=False, int32=False, update_memory=True, sync=1):
+    from dgc import _lib
+    numel, k, S, ks, stride = attrs
+    p = _lib.SelectParams()
+    p.numel, p.num_selects, p.num_samples = numel, k, S
+    p.upper_count, p.lower_count = O.adapt_bounds(k, upper, lower)
+    p.upper, p.lower = upper, lower
+    p.max_iters, p.resample, p.masking = max_iters, int(resample), int(masking)
+    p.vdtype, p.idtype, p.update_memory = int(fp16), int(int32), int(update_memory)
+    tv, tm = to_dev(vec_np), to_dev(mmt_np)
+    t0 = torch.tensor([thr], dtype=torch.float32, device=DEV)
+    vals = torch.empty(k, dtype=torch.float16 if fp16 else torch.float32, device=DEV)
+    idx = torch.empty(k, dtype=torch.int32 if int32 else torch.int64, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=DEV)
+    wsz = L.dgc_select_workspace(numel, k)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    check(L, L.dgc_select(P(tv), P(tm), P(t0), ctypes.byref(p), P(vals), P(idx), P(cnt), P(info), P(ws), wsz,
+                          sync, stream()))
+    torch.cuda.synchronize()
+    n = int(cnt.item())
+    inf = _lib.SelectInfo.from_buffer_copy(info.cpu().numpy().tobytes())
+    return (vals.cpu().numpy()[:n], idx.cpu().numpy()[:n], tv.cpu().numpy(), tm.cpu().numpy(),
+            _lib.BRANCHES[inf.branch], inf)
+
+
+SELECT_CASES = [
+    # name, n, ratio, kind, scale, extra oracle kwargs
+    ("normal_1m", 1000000, 0.001, "normal", 1.0, {}),
+    ("normal_2m_r1e-2", 2000003, 0.01, "normal", 1.0, {}),
+    ("layered_resample", 300000, 0.001, "layered", 1.0, {}),
+    ("layered_overflow", 200000, 0.05, "layered", 1.0, {}),   # dense local candidates: list spill
+    ("ties_int", 100000, 0.01, "ties", 1.0, {}),
+    ("sparse_zeros", 100000, 0.01, "sparse", 1.0, {}),
+    ("bf16", 500000, 0.001, "bf16", 1.0, {}),
+    ("noresample", 50000, 0.01, "layered", 1.0, dict(resample=False)),
+    ("iters2", 300000, 0.001, "layered", 1.0, dict(max_iters=2)),
+    ("iters0", 300000, 0.001, "normal", 1.0, dict(max_iters=0)),
+    ("direct_small", 1500, 0.001, "normal", 1.0, {}),
+    ("tail_odd", 4096 * 5 + 3, 0.01, "normal", 1.0, {}),
+]
+
+
+@pytest.mark.parametrize("case", SELECT_CASES, ids=[c[0] for c in SELECT_CASES])
+@pytest.mark.parametrize("thr_scale", [1.0, 1.25, 0.85, 3.0])
+def test_select_matches_oracle(L, case, thr_scale):
+    name, n, ratio, kind, scale, kw = case
+    attrs = O.attributes(n, ratio)
+    vec = synth.gradient(hash(name) % 1000, n, kind, scale)
+    mmt = synth.gradient(hash(name) % 1000 + 1, n)
+    start = 3 % attrs[4]
+    samples = np.abs(vec[start::attrs[4]]) if attrs[0] != attrs[2] else np.abs(vec)
+    t0 = np.float32(O.kth_largest(samples, attrs[3]) * np.float32(thr_scale))
+    okw = dict(upper=1.3, lower=0.8, max_iters=kw.get("max_iters", 10), resample=kw.get("resample", True))
+    ov, oi, info = O.sparsify(vec, attrs, threshold=t0, **okw)
+    for sync in (1, 0):
+        gv, gi, gvec, gmmt, branch, inf = select_dev(L, vec, mmt, t0, attrs, sync=sync, **okw)
+        assert branch == info["branch"], (name, sync)
+        assert inf.recounts == len(info["counts"]) - 1
+        assert np.array_equal(gi, oi), (name, sync, branch)
+        assert np.array_equal(bits(gv), bits(ov))
+        assert bits(np.float32(inf.threshold)) == bits(info["threshold"])
+        ev, em = vec.copy(), mmt.copy()
+        O.update(em, ev, oi, True)
+        assert np.array_equal(bits(gvec), bits(ev)) and np.array_equal(bits(gmmt), bits(em))
+    if name == "layered_overflow" and thr_scale == 1.0:
+        assert inf.overflow_segments > 0      # the spill path really ran
+
+
+@pytest.mark.parametrize("fp16,int32,masking,update", [(True, True, True, True), (False, True, False, True),
+                                                        (True, False, True, False)])
+def test_select_wire_and_memory_flags(L, fp16, int32, masking, update):
+    n, ratio = 65537, 0.01
+    attrs = O.attributes(n, ratio)
+    vec = synth.gradient(31, n, "normal", 30000.0)      # fp16 overflow -> inf, like torch
+    mmt = synth.gradient(32, n)
+    t0 = O.kth_largest(np.abs(vec[::attrs[4]]), attrs[3])
+    ov, oi, info = O.sparsify(vec, attrs, threshold=t0)
+    wv, wi = O.wire_cast(ov, oi, fp16, int32)
+    gv, gi, gvec, gmmt, branch, _ = select_dev(L, vec, mmt, t0, attrs, fp16=fp16, int32=int32, masking=masking,
+                                               update_memory=update)
+    assert gi.dtype == wi.dtype and np.array_equal(gi, wi)
+    assert np.array_equal(bits(gv), bits(wv))
+    ev, em = vec.copy(), mmt.copy()
+    if update:
+        O.update(em, ev, oi, masking)
+    assert np.array_equal(bits(gvec), bits(ev)) and np.array_equal(bits(gmmt), bits(em))
+
+
+# ----------------------------------------------------------------------------- drop-in
+def quiet(fn, *a, **kw):
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a, **kw)
+
+
+def test_dropin_compress_against_goldens(L, golden_compress):
+    from dgc.compression import DGCCompressor
+    from dgc.memory import DGCSGDMemory
+    meta, arrays = golden_compress
+    for name, case in meta.items():
+        N = case["N"]
+        extra = case["extra"]
+        mem = DGCSGDMemory(momentum=0.9, nesterov=case["nesterov"], momentum_masking=case["masking"])
+        comp = quiet(DGCCompressor, case["ratio"], memory=mem, fp16_values=case["fp16"],
+                     int32_indices=case["int32"], resample=case["resample"], **extra)
+        param = torch.zeros(N, device=DEV)
+        quiet(mem.initialize, [("w", param)])
+        quiet(comp.initialize, [("w", param)])
+        attrs = tuple(case["attrs"])
+        m_o, v_o = np.zeros(N, np.float32), np.zeros(N, np.float32)
+        random.seed(42)
+        follow_golden = True
+        okw = dict(resample=case["resample"], max_iters=extra.get("max_adaptation_iters", 10))
+        for s, step in enumerate(case["per_step"]):
+            g = synth.gradient(step["seed"], N, case["kind"], case["scale"])
+            state = random.getstate()
+            start = random.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
+            random.setstate(state)
+            (vals, idx), ctx = comp.compress(to_dev(g), "w")
+            ov, oi, info = O.compress_step(g, m_o, v_o, attrs, start, nesterov=case["nesterov"],
+                                           momentum_masking=case["masking"], **okw)
+            wv, wi = O.wire_cast(ov, oi, case["fp16"], case["int32"])
+            gi = idx.view(-1).cpu().numpy()
+            gv = vals.view(-1).cpu().numpy()
+            key = f"{name}/s{s}"
+            assert comp.last_info()["branch"] == info["branch"], key
+            assert np.array_equal(gi, wi), key
+            assert np.array_equal(bits(gv), bits(wv)), key
+            assert np.array_equal(bits(mem.momentums["w"].cpu().numpy()), bits(m_o)), key
+            assert np.array_equal(bits(mem.velocities["w"].cpu().numpy()), bits(v_o)), key
+            if follow_golden:
+                ref_i = arrays[key + "/indices"]
+                if info["branch"] == "resample":
+                    ref_i = np.sort(ref_i)
+                if np.array_equal(gi, ref_i):
+                    assert synth.digest(mem.velocities["w"].cpu().numpy()) == step["vec_sha"], key
+                else:
+                    follow_golden = False      # reference tie pick differs (see oracle docstring)
+            # decompress at W = 1 back into the gradient buffer
+            out = comp.decompress(comp.synchronize(comp.communicate((vals, idx), "w", "Average")), ctx)
+            dense = out.view(-1).cpu().numpy()
+            want = O.decompress([wv], [wi], N, 1)
+            assert np.array_equal(bits(dense), bits(want)), key
+
+
+def test_dropin_decompress_against_goldens(L, golden_decompress):
+    from dgc.compression import DGCCompressor
+    meta, arrays = golden_decompress
+    for name, case in meta.items():
+        N, W = case["N"], case["W"]
+        for s in range(case["steps"]):
+            vals = [arrays[f"{name}/s{s}/r{q}/values"] for q in range(W)]
+            idxs = [arrays[f"{name}/s{s}/r{q}/indices"] for q in range(W)]
+            want = np.zeros(N, np.float32)
+            nz = arrays[f"{name}/s{s}/dec_nz_idx"]
+            want[nz] = arrays[f"{name}/s{s}/dec_nz_val"]
+            comp = quiet(DGCCompressor, case["ratio"], fp16_values=case["fp16"], int32_indices=case["int32"])
+            comp.world_size = W
+            quiet(comp.initialize, [("w", (N, [N]))])
+            grad = torch.full((N,), 7.0, device=DEV)
+            ctx = ("w", N, [N], torch.float32, torch.int64, grad)
+            cat_v, cat_i = to_dev(np.concatenate(vals)), to_dev(np.concatenate(idxs))
+            # (a) runs detected on device (reference-format input, resample order included)
+            out = comp.decompress([cat_v, cat_i], ctx)
+            assert np.array_equal(bits(out.cpu().numpy()), bits(want)), (name, s, "detect")
+            assert synth.digest(out.cpu().numpy()) == case["per_step"][s]["dense_sha"]
+            # (b) host-known run offsets, as our synchronize provides
+            from dgc.compression import _Gathered
+            g = _Gathered([cat_v.view(-1, 1), cat_i.view(-1, 1)])
+            g.run_offsets = list(np.cumsum([0] + [len(v) for v in vals]))
+            grad.fill_(3.0)
+            out = comp.decompress(g, ctx)
+            assert np.array_equal(bits(out.cpu().numpy()), bits(want)), (name, s, "offsets")
+
+
+def test_decompress_packed_and_repeats(L):
+    from dgc import _lib
+    N, W, cap = 100000, 4, 3000
+    rng = np.random.default_rng(5)
+    stride = L.dgc_payload_layout(cap, 0, 0, None, None)
+    voff, ioff = 16, 16 + 4 * cap
+    payload = np.zeros(W * stride, np.uint8)
+    vals, idxs = [], []
+    for r in range(W):
+        c = int(rng.integers(0, cap))
+        i = np.sort(rng.choice(N, c, replace=False)).astype(np.int64)
+        v = rng.standard_normal(c).astype(np.float32)
+        base = r * stride
+        payload[base: base + 8] = np.frombuffer(np.int64(c).tobytes(), np.uint8)
+        payload[base + voff: base + voff + 4 * c] = np.frombuffer(v.tobytes(), np.uint8)
+        payload[base + ioff: base + ioff + 8 * c] = np.frombuffer(i.tobytes(), np.uint8)
+        vals.append(v)
+        idxs.append(i)
+    want = O.decompress(vals, idxs, N, W)
+    grad = torch.empty(N, device=DEV)
+    wsz = L.dgc_decompress_workspace(N, W)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    check(L, L.dgc_decompress_packed(P(to_dev(payload)), W, stride, cap, 0, 0, P(grad), N, 1.0 / W, P(ws), wsz,
+                                     stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(grad.cpu().numpy()), bits(want))
+    # one non-decreasing run with repeated indices: sequential order within the repeats
+    i = np.sort(rng.integers(0, 5000, 20000)).astype(np.int64)
+    v = rng.standard_normal(20000).astype(np.float32)
+    want = O.decompress([v], [i], 5000, 1)
+    grad = torch.empty(5000, device=DEV)
+    offs = (ctypes.c_int64 * 2)(0, 20000)
+    wsz = L.dgc_decompress_workspace(5000, 1)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    check(L, L.dgc_decompress(P(to_dev(v)), 0, P(to_dev(i)), 0, 20000, offs, 1, P(grad), 5000, 1.0, P(ws), wsz,
+                              stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(grad.cpu().numpy()), bits(want))
+    # out-of-range indices are ignored and flagged
+    bad = np.array([-1, 3, 5000], np.int64)
+    offs = (ctypes.c_int64 * 2)(0, 3)
+    check(L, L.dgc_decompress(P(to_dev(np.ones(3, np.float32))), 0, P(to_dev(bad)), 0, 3, offs, 1, P(grad), 5000,
+                              1.0, P(ws), wsz, stream()))
+    st = ctypes.c_int32(0)
+    check(L, L.dgc_decompress_status(P(ws), ctypes.byref(st), stream()))
+    assert st.value == 1 and grad[3].item() == 1.0 and grad.sum().item() == 1.0
+
+
+def test_decompress_unsorted_falls_back_to_stable_order(L):
+    from dgc.compression import DGCCompressor
+    N = 3000
+    rng = np.random.default_rng(6)
+    i = rng.integers(0, N, 5000).astype(np.int64)          # thousands of descents, repeats
+    v = rng.standard_normal(5000).astype(np.float32)
+    want = O.decompress([v], [i], N, 2)
+    comp = quiet(DGCCompressor, 0.01)
+    comp.world_size = 2
+    quiet(comp.initialize, [("w", (N, [N]))])
+    grad = torch.zeros(N, device=DEV)
+    out = comp.decompress([to_dev(v), to_dev(i)], ("w", N, [N], torch.float32, torch.int64, grad))
+    assert np.array_equal(bits(out.cpu().numpy()), bits(want))
+
+
+def test_memory_update_and_dense_branch(L):
+    from dgc.compression import DGCCompressor
+    from dgc.memory import DGCSGDMemory
+    mem = DGCSGDMemory(momentum=0.9, nesterov=True)
+    comp = quiet(DGCCompressor, 0.01, memory=mem, fp16_values=True)
+    b = torch.zeros(1000, device=DEV)
+    quiet(mem.initialize, [("b", b)])
+    g = synth.gradient(40, 1000)
+    t, ctx = comp.compress(to_dev(g), "b")                  # dense: fp16 cast only
+    assert t.dtype == torch.float16
+    out = comp.decompress(t, ctx)                           # upcast + compensate(accumulate=False)
+    m = np.zeros(1000, np.float32)
+    want = O.compensate(g.astype(np.float16).astype(np.float32), m, None, 0.9, True, accumulate=False)
+    assert np.array_equal(bits(out.cpu().numpy()), bits(want))
+    mem.update("b", (torch.tensor([1, 5, -1], device=DEV),))
+    mm = mem.momentums["b"].cpu().numpy()
+    assert mm[1] == 0 and mm[5] == 0 and mm[-1] == 0 and mm[2] != 0
+
+
+def test_generic_path_uniform_sampling_and_plain_memory(L):
+    """strided_sample=False and the no-op Memory go through compensate -> _sparsify -> update."""
+    from dgc.compression import DGCCompressor
+    from dgc.memory import Memory
+    N = 200000
+    comp = quiet(DGCCompressor, 0.001, memory=Memory)
+    quiet(comp.initialize, [("w", (N, [N]))])
+    g = synth.gradient(41, N)
+    tg = to_dev(g)
+    (vals, idx), ctx = comp.compress(tg, "w")
+    attrs = O.attributes(N, 0.001)
+    random.seed(0)
+    info = comp.last_info()
+    ov, oi, oinfo = O.sparsify(g, attrs, threshold=info["threshold0"])
+    assert np.array_equal(idx.view(-1).cpu().numpy(), oi) and np.array_equal(tg.cpu().numpy(), g)
+    torch.manual_seed(3)
+    comp2 = quiet(DGCCompressor, 0.001, memory=Memory, strided_sample=False)
+    quiet(comp2.initialize, [("w", (N, [N]))])
+    (v2, i2), _ = comp2.compress(tg, "w")
+    t0 = comp2.last_info()["threshold0"]
+    torch.manual_seed(3)
+    sidx = torch.randint(0, N, (attrs[2],), device=DEV).cpu().numpy()
+    assert np.float32(t0) == O.kth_largest(np.abs(g[sidx]), attrs[3])
+    ov, oi, _ = O.sparsify(g, attrs, threshold=t0)
+    assert np.array_equal(i2.view(-1).cpu().numpy(), oi)
+
+
+# ----------------------------------------------------------------------------- full size
+@pytest.mark.parametrize("N", [100_000_000])
+def test_large_bucket_properties(L, N):
+    """Size-independent properties at a large flat bucket, plus bit-exact state vs numpy."""
+    from dgc.compression import DGCCompressor
+    from dgc.memory import DGCSGDMemory
+    mem = DGCSGDMemory(momentum=0.9, nesterov=True)
+    comp = quiet(DGCCompressor, 0.001, memory=mem)
+    p = torch.zeros(N, device=DEV)
+    quiet(mem.initialize, [("w", p)])
+    quiet(comp.initialize, [("w", p)])
+    g = torch.randn(N, generator=torch.Generator(device=DEV).manual_seed(5), device=DEV)
+    random.seed(42)
+    (vals, idx), ctx = comp.compress(g, "w")
+    info = comp.last_info()
+    k = comp.attributes["w"][2]
+    i = idx.view(-1)
+    assert info["count"] == i.numel() <= k and i.numel() >= 0.8 * k
+    assert bool((i[1:] > i[:-1]).all())                            # ascending, unique
+    vec = mem.velocities["w"]
+    assert bool((vec[i] == 0).all()) and bool((mem.momentums["w"][i] == 0).all())
+    # reconstruct the pre-masking velocity (nesterov, first step: vec = g*0.9 + g)
+    v_np = g.cpu().numpy()
+    m_np = np.zeros(N, np.float32)
+    vv = np.zeros(N, np.float32)
+    O.compensate(v_np, m_np, vv, 0.9, True)
+    ii = i.cpu().numpy()
+    assert np.array_equal(bits(vals.view(-1).cpu().numpy()), bits(vv[ii]))
+    start = random.Random(42).randint(0, comp.attributes["w"][5] - 1)
+    t0 = O.kth_largest(np.abs(vv[start::comp.attributes["w"][5]]), comp.attributes["w"][4])
+    assert bits(np.float32(info["threshold0"])) == bits(t0)
+    ov, oi, _ = O.sparsify(vv, O.attributes(N, 0.001), threshold=t0)
+    assert np.array_equal(ii, oi)
+    O.update(m_np, vv, oi)
+    assert np.array_equal(bits(vec.cpu().numpy()), bits(vv))
+    out = comp.decompress(comp.synchronize(comp.communicate((vals, idx), "w", "Average")), ctx)
+    dense = out.view(-1)
+    assert int((dense != 0).sum()) == int((vals != 0).sum()) and bool((dense[i] == vals.view(-1)).all())

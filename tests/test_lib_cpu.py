@@ -1,0 +1,68 @@
+"""C-ABI library: loads, exports every symbol include/dgc_hip.h declares, and its
+pure-host entry points (layout / workspace sizing) behave. No GPU needed."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "dgc_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dgc_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from dgc import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail(f"{_lib.LIB_PATH} missing: run __graft_entry__.build()")
+    return _lib.lib()
+
+
+def test_exports_every_declared_symbol(L):
+    syms = declared_symbols()
+    assert len(syms) >= 17
+    for s in syms:
+        assert hasattr(L, s), s
+
+
+def test_version_and_error(L):
+    assert b"gfx950" in L.dgc_version()
+    assert isinstance(L.dgc_last_error(), bytes)
+
+
+def test_payload_layout(L):
+    v, i = ctypes.c_int64(), ctypes.c_int64()
+    stride = L.dgc_payload_layout(1000, 0, 0, ctypes.byref(v), ctypes.byref(i))
+    assert v.value == 16 and i.value == 16 + 4000 and stride >= i.value + 8000 and stride % 256 == 0
+    stride16 = L.dgc_payload_layout(1001, 1, 1, ctypes.byref(v), ctypes.byref(i))
+    assert v.value == 16 and i.value % 16 == 0 and i.value >= 16 + 2002 and stride16 >= i.value + 4004
+
+
+def test_workspace_sizes_scale(L):
+    small = L.dgc_select_workspace(4096, 4)
+    big = L.dgc_select_workspace(10 ** 9, 10 ** 6)
+    assert 0 < small < big
+    # candidate lists: 6 B per slot, 256 slots per 4096-element segment (~9.4 % of the fp32 bytes)
+    assert big < 0.12 * 4 * 10 ** 9
+    assert L.dgc_compress_workspace(10 ** 6, 1000, 10309) > L.dgc_select_workspace(10 ** 6, 1000)
+    assert L.dgc_decompress_workspace(10 ** 9, 8) > L.dgc_decompress_workspace(10 ** 6, 8)
+
+
+def test_invalid_arguments_fail_without_gpu(L):
+    from dgc import _lib
+    p = _lib.SelectParams()
+    p.numel, p.num_selects, p.num_samples = 10, 20, 10     # k > n
+    rc = L.dgc_select(None, None, None, ctypes.byref(p), None, None, None, None, None, 0, 0, None)
+    assert rc == 1 and b"num_selects" in L.dgc_last_error()
+    p.num_selects, p.idtype = 5, 1
+    p.numel = p.num_samples = 2 ** 31 + 5                  # int32 indices cannot address this
+    rc = L.dgc_select(None, None, None, ctypes.byref(p), ctypes.c_void_p(16), ctypes.c_void_p(16), None,
+                      None, None, 0, 0, None)
+    assert rc == 3
