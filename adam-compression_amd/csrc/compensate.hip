@@ -12,9 +12,10 @@
 //   plain:    mmt = mmt * m + g   ;  vec = vec + mmt         [accumulate]
 //                                     out = mmt               [dense branch]
 //
-// HBM: 20 B/element (read g, mmt, vec; write mmt, vec), 16-B vector accesses,
-// grid-stride over float4. The sample |vec[start + q*stride]| is written from
-// registers, saving a strided re-read of vec (which touches ~1/3 of its lines).
+// HBM: 20 B/element (read g, mmt, vec; write mmt, vec), non-temporal 16-B accesses,
+// one float4 per lane in one-shot block chunks. The sample |vec[start + q*stride]|
+// is written from registers, saving a strided re-read of vec (which would touch
+// ~1/3 of its lines).
 #include "dgc_common.hpp"
 
 namespace dgc {
@@ -24,7 +25,23 @@ struct SampleSpec {
     int64_t start;
     int64_t stride;    // >= 4 on the fused path
     int64_t count;     // ceil((n - start) / stride)
+    double inv_stride; // 1.0 / stride
 };
+
+// floor/mod of d by s for |d| < 2^53 without a 64-bit integer divide: a double
+// estimate, then an exact integer correction.
+__device__ __forceinline__ void floor_divmod_fast(int64_t d, int64_t s, double inv, int64_t& q, int64_t& r) {
+    q = (int64_t)floor((double)d * inv);
+    r = d - q * s;
+    while (r < 0) {
+        r += s;
+        q -= 1;
+    }
+    while (r >= s) {
+        r -= s;
+        q += 1;
+    }
+}
 
 template <bool NEST, bool ACC>
 __device__ __forceinline__ float comp1(float g, float& m, float& v, float mom) {
@@ -44,56 +61,46 @@ __device__ __forceinline__ float comp1(float g, float& m, float& v, float mom) {
     return m;
 }
 
-__device__ __forceinline__ void floor_divmod(int64_t d, int64_t s, int64_t& q, int64_t& r) {
-    q = d / s;
-    r = d - q * s;
-    if (r < 0) {
-        r += s;
-        q -= 1;
-    }
-}
 
-// Vector path: all four pointers 16-B aligned. Each thread walks float4 index v
-// with a grid stride; (q, r) track floor/mod of (4v - start) by the sample stride
-// incrementally (one real division per thread).
+// Vector path: all pointers 16-B aligned. One-shot chunks (no grid stride): block b
+// owns float4 [256b, 256b + 256), lanes contiguous, non-temporal 16-B loads and
+// stores. Measured on MI355X this shape streams 3R2W at 5.86 TB/s against 4.8 TB/s
+// for the grid-stride loop (tools/membench.hip). The sample bookkeeping is per
+// block: (q0, r0) = floor/mod(4*256b - start, stride) once, then a 32-bit divide
+// of the lane's small offset.
 template <bool NEST, bool ACC, bool SAMPLE>
 __global__ void __launch_bounds__(kBlock)
 k_compensate4(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __restrict__ vec,
-              float4* __restrict__ out, int64_t n4, float mom, SampleSpec sp, int64_t step_q,
-              int64_t step_r) {
-    int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t G = (int64_t)gridDim.x * kBlock;
-    int64_t q = 0, r = 0;
-    if (SAMPLE) floor_divmod(4 * v - sp.start, sp.stride, q, r);
-    for (; v < n4; v += G) {
-        const float4 gv = g[v];
-        float4 mv = mmt[v];
-        float4 vv = ACC ? vec[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 ov;
-        ov.x = comp1<NEST, ACC>(gv.x, mv.x, vv.x, mom);
-        ov.y = comp1<NEST, ACC>(gv.y, mv.y, vv.y, mom);
-        ov.z = comp1<NEST, ACC>(gv.z, mv.z, vv.z, mom);
-        ov.w = comp1<NEST, ACC>(gv.w, mv.w, vv.w, mom);
-        mmt[v] = mv;
-        if (ACC)
-            vec[v] = vv;
-        else
-            out[v] = ov;
-        if (SAMPLE) {
-            // element 4v+j is a sample iff (r + j) % stride == 0, i.e. r + j in {0, stride}
-            const int64_t j = (r == 0) ? 0 : sp.stride - r;
-            if (j < 4) {
-                const int64_t qi = (r == 0) ? q : q + 1;
-                if (qi >= 0 && qi < sp.count) {
-                    const float x = j == 0 ? ov.x : j == 1 ? ov.y : j == 2 ? ov.z : ov.w;
-                    sp.out[qi] = fabsf(x);
-                }
-            }
-            r += step_r;
-            q += step_q;
-            if (r >= sp.stride) {
-                r -= sp.stride;
-                q += 1;
+              float4* __restrict__ out, int64_t n4, float mom, SampleSpec sp) {
+    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (v >= n4) return;
+    const float4 gv = ld_nt(g + v);
+    float4 mv = ld_nt(mmt + v);
+    float4 vv = ACC ? ld_nt(vec + v) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 ov;
+    ov.x = comp1<NEST, ACC>(gv.x, mv.x, vv.x, mom);
+    ov.y = comp1<NEST, ACC>(gv.y, mv.y, vv.y, mom);
+    ov.z = comp1<NEST, ACC>(gv.z, mv.z, vv.z, mom);
+    ov.w = comp1<NEST, ACC>(gv.w, mv.w, vv.w, mom);
+    st_nt(mmt + v, mv);
+    if (ACC)
+        st_nt(vec + v, vv);
+    else
+        st_nt(out + v, ov);
+    if (SAMPLE) {
+        int64_t q0, r0;
+        floor_divmod_fast(4 * ((int64_t)blockIdx.x * kBlock) - sp.start, sp.stride, sp.inv_stride, q0, r0);
+        // element 4v+j is a sample iff (r + j) % stride == 0, with r = (r0 + 4*tid) mod stride
+        const uint32_t t = (uint32_t)r0 + 4u * threadIdx.x;
+        const uint32_t s32 = (uint32_t)sp.stride;
+        const uint32_t q1 = t / s32;
+        const uint32_t r = t - q1 * s32;
+        const uint32_t j = r == 0 ? 0u : s32 - r;
+        if (j < 4) {
+            const int64_t qi = q0 + q1 + (r == 0 ? 0 : 1);
+            if (qi >= 0 && qi < sp.count) {
+                const float x = j == 0 ? ov.x : j == 1 ? ov.y : j == 2 ? ov.z : ov.w;
+                sp.out[qi] = fabsf(x);
             }
         }
     }
@@ -160,24 +167,23 @@ static int launch_comp(const float* g, float* m, float* v, float* o, int64_t n, 
                        SampleSpec sp, hipStream_t st) {
     const bool sample = sp.out != nullptr;
     const bool vec_ok = aligned16(g) && aligned16(m) && (ACC ? aligned16(v) : aligned16(o)) &&
-                        (!sample || sp.stride >= 4);
+                        (!sample || (sp.stride >= 4 && sp.stride < (1LL << 30)));
     int64_t done = 0;
     if (vec_ok) {
         const int64_t n4 = n / 4;
         if (n4 > 0) {
-            const int grid = grid_for(n4);
-            const int64_t G = 4 * (int64_t)grid * kBlock;
-            const int64_t sq = sample ? G / sp.stride : 0, sr = sample ? G % sp.stride : 0;
+            const int64_t grid = ceil_div(n4, kBlock);
+            if (grid > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: n too large");
             auto g4 = reinterpret_cast<const float4*>(g);
             auto m4 = reinterpret_cast<float4*>(m);
             auto v4 = reinterpret_cast<float4*>(v);
             auto o4 = reinterpret_cast<float4*>(o);
             if (sample)
-                hipLaunchKernelGGL((k_compensate4<NEST, ACC, true>), dim3(grid), dim3(kBlock), 0, st,
-                                   g4, m4, v4, o4, n4, mom, sp, sq, sr);
+                hipLaunchKernelGGL((k_compensate4<NEST, ACC, true>), dim3((unsigned)grid), dim3(kBlock), 0, st,
+                                   g4, m4, v4, o4, n4, mom, sp);
             else
-                hipLaunchKernelGGL((k_compensate4<NEST, ACC, false>), dim3(grid), dim3(kBlock), 0, st,
-                                   g4, m4, v4, o4, n4, mom, sp, sq, sr);
+                hipLaunchKernelGGL((k_compensate4<NEST, ACC, false>), dim3((unsigned)grid), dim3(kBlock), 0, st,
+                                   g4, m4, v4, o4, n4, mom, sp);
             DGC_LAUNCHED();
         }
         done = n4 * 4;
@@ -205,14 +211,14 @@ int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n,
     if (accumulate && out && out != vec)
         DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: accumulate writes vec (out must be NULL or vec)");
     if (!accumulate && !out) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: dense branch needs out");
-    SampleSpec sp{nullptr, 0, 1, 0};
+    SampleSpec sp{nullptr, 0, 1, 0, 1.0};
     if (samples) {
         if (!accumulate) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: sampling needs accumulate=1");
         if (s_stride < 1 || s_start < 0 || s_start >= n)
             DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: bad sample start/stride");
         if (s_count != ceil_div(n - s_start, s_stride))
             DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: num_samples must be ceil((n-start)/stride)");
-        sp = SampleSpec{samples, s_start, s_stride, s_count};
+        sp = SampleSpec{samples, s_start, s_stride, s_count, 1.0 / (double)s_stride};
         if (s_stride < 4) {
             // tiny strides (sample_ratio >= 0.25): unfused, samples read back after the pass
             DGC_TRY(compensate(grad, mmt, vec, out, n, momentum, nesterov, accumulate, nullptr, 0,

@@ -65,6 +65,25 @@ __device__ __forceinline__ long long load_idx(const void* p, long long e) {
     return reinterpret_cast<const int64_t*>(p)[e];
 }
 
+// Where the runs come from: a table in the workspace (concatenated input), or the
+// packed allgather buffer itself (rank r's header holds its count) — the latter
+// needs no setup launch.
+struct RunSrc {
+    const Run* table;
+    const int32_t* nruns_dev;
+    const char* payload;          // packed mode when non-null
+    int64_t stride, voff, ioff, capacity;
+    int32_t world;
+    __device__ __forceinline__ int count() const { return payload ? world : *nruns_dev; }
+    __device__ __forceinline__ Run get(int r) const {
+        if (!payload) return table[r];
+        const char* base = payload + (int64_t)r * stride;
+        long long c = *reinterpret_cast<const long long*>(base);
+        c = c < 0 ? 0 : (c > capacity ? capacity : c);
+        return Run{base + voff, base + ioff, c};
+    }
+};
+
 // ---------------------------------------------------------------- run tables
 struct HostRuns {
     int32_t n;
@@ -75,18 +94,6 @@ __global__ void k_runs_host(DecWS w, HostRuns hr, const char* vals, const char* 
     const int r = threadIdx.x;
     if (r < hr.n) w.runs[r] = Run{vals + hr.off[r] * vb, idx + hr.off[r] * ib, hr.off[r + 1] - hr.off[r]};
     if (r == 0) *w.nruns = hr.n;
-}
-
-__global__ void k_runs_packed(DecWS w, const char* payload, int world, int64_t stride, int64_t voff,
-                              int64_t ioff, int64_t capacity) {
-    const int r = threadIdx.x;
-    if (r < world) {
-        const char* base = payload + (int64_t)r * stride;
-        long long c = *reinterpret_cast<const long long*>(base);
-        c = c < 0 ? 0 : (c > capacity ? capacity : c);
-        w.runs[r] = Run{base + voff, base + ioff, c};
-    }
-    if (r == 0) *w.nruns = world;
 }
 
 template <int ID>
@@ -131,15 +138,16 @@ __global__ void k_runs_from_descents(DecWS w, const char* vals, const char* idx,
 // ---------------------------------------------------------------- bounds
 template <int ID>
 __global__ void __launch_bounds__(kBlock)
-k_bounds(DecWS w, int64_t n, int max_runs) {
-    const int nr = *w.nruns;
+k_bounds(DecWS w, RunSrc rs, int64_t n, int max_runs) {
+    const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *w.status = 0;   // set only by the next kernel
     for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < (int64_t)max_runs * stride;
          t += (int64_t)gridDim.x * kBlock) {
         const int r = (int)(t / stride);
         if (r >= nr) break;
         const int64_t c = t - (int64_t)r * stride;
-        const Run run = w.runs[r];
+        const Run run = rs.get(r);
         const long long key = c == w.nchunks ? n : c * (long long)kChunk;
         long long lo = 0, hi = run.count;   // first entry with idx >= key
         while (lo < hi) {
@@ -150,62 +158,142 @@ k_bounds(DecWS w, int64_t n, int max_runs) {
                 hi = mid;
         }
         w.bnd[t] = lo;
-        if ((c == 0 && lo > 0) || (c == w.nchunks && lo < run.count)) atomicOr(w.status, 1);
     }
 }
 
 // ---------------------------------------------------------------- chunk scatter
+constexpr int kStage = 2048;   // staged entries per chunk (avg 4*W at ratio 0.001)
+
+__device__ __forceinline__ int lower_bound_lds(const int* a, int lo, int hi, int key) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// One workgroup per 4096-element chunk (one-shot grid). Phase 1 stages every run's
+// entries for the chunk into LDS in one parallel load sweep (run order kept by
+// position); phase 2 lets the FIRST occurrence of each index (in run order) add
+// all of its occurrences in run order, from +0.0 — the sequential index_put_
+// order — into the LDS tile; phase 3 scales and writes the tile with 16-B stores.
+// Chunks with more than kStage entries fall back to one barrier per run.
 template <int VD, int ID>
 __global__ void __launch_bounds__(kBlock)
-k_scatter_chunks(DecWS w, float* __restrict__ grad, int64_t n, float scale) {
+k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
     __shared__ __attribute__((aligned(16))) float acc[kChunk];
-    const int nr = *w.nruns;
+    __shared__ int sidx[kStage];
+    __shared__ float sval[kStage];
+    __shared__ int roff[kMaxRuns + 1];
+    __shared__ long long rb0[kMaxRuns];
+    __shared__ const void* rval[kMaxRuns];
+    __shared__ const void* ridx[kMaxRuns];
+    const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
-    const bool vec_out = aligned16(grad);
-    for (int64_t c = blockIdx.x; c < w.nchunks; c += gridDim.x) {
-        const long long base = c * (long long)kChunk;
-        for (int j = threadIdx.x; j < kChunk; j += kBlock) acc[j] = 0.f;
+    const int64_t c = blockIdx.x;
+    const long long base = c * (long long)kChunk;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (c == 0 && tid < nr) {   // entries outside [0, n) are skipped: flag them
+        const Run run = rs.get(tid);
+        if (w.bnd[tid * stride] > 0 || w.bnd[tid * stride + w.nchunks] < run.count) atomicOr(w.status, 1);
+    }
+    float4* acc4 = reinterpret_cast<float4*>(acc);
+    for (int j = tid; j < kChunk / 4; j += kBlock) acc4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < 64) {   // run table for this chunk (nr <= 64: one wave)
+        int cnt = 0;
+        if (tid < nr) {
+            const Run run = rs.get(tid);
+            const long long b0 = w.bnd[tid * stride + c], b1 = w.bnd[tid * stride + c + 1];
+            rb0[tid] = b0;
+            rval[tid] = run.vals;
+            ridx[tid] = run.idx;
+            cnt = (int)(b1 - b0);
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (tid < nr) roff[tid] = incl - cnt;
+        if (tid == nr - 1) roff[nr] = incl;
+    }
+    __syncthreads();
+    const int total = roff[nr];
+    if (total <= kStage) {
+        for (int t = tid; t < total; t += kBlock) {
+            int r = 0;
+            while (roff[r + 1] <= t) ++r;   // <= 64 runs, few entries: linear is fine
+            const long long e = rb0[r] + (t - roff[r]);
+            const long long i = load_idx<ID>(ridx[r], e) - base;
+            sidx[t] = (i >= 0 && i < kChunk) ? (int)i : -1;
+            sval[t] = load_val<VD>(rval[r], e);
+        }
         __syncthreads();
+        for (int t = tid; t < total; t += kBlock) {
+            const int i = sidx[t];
+            if (i < 0) {
+                atomicOr(w.status, 2);   // only an unsorted run can land outside its chunk
+                continue;
+            }
+            int r = 0;
+            while (roff[r + 1] <= t) ++r;
+            if (t > roff[r] && sidx[t - 1] == i) continue;   // repeat inside a non-decreasing run
+            bool head = true;
+            for (int q = 0; q < r && head; ++q) {
+                const int p = lower_bound_lds(sidx, roff[q], roff[q + 1], i);
+                head = !(p < roff[q + 1] && sidx[p] == i);
+            }
+            if (!head) continue;
+            float a = 0.f;
+            for (int q = r; q < nr; ++q) {
+                for (int p = (q == r) ? t : lower_bound_lds(sidx, roff[q], roff[q + 1], i);
+                     p < roff[q + 1] && sidx[p] == i; ++p)
+                    a = __fadd_rn(a, sval[p]);
+            }
+            acc[i] = a;
+        }
+    } else {
         for (int r = 0; r < nr; ++r) {
-            const Run run = w.runs[r];
-            const long long b0 = w.bnd[r * stride + c], b1 = w.bnd[r * stride + c + 1];
-            for (long long e = b0 + threadIdx.x; e < b1; e += kBlock) {
-                const long long i = load_idx<ID>(run.idx, e);
-                if (e > b0 && load_idx<ID>(run.idx, e - 1) == i) continue;   // not the first of a repeat
+            const long long b0 = rb0[r], b1 = rb0[r] + (roff[r + 1] - roff[r]);
+            for (long long e = b0 + tid; e < b1; e += kBlock) {
+                const long long i = load_idx<ID>(ridx[r], e);
+                if (e > b0 && load_idx<ID>(ridx[r], e - 1) == i) continue;   // not the first of a repeat
                 const long long off = i - base;
-                if (off < 0 || off >= kChunk) {   // only an unsorted run can land here
+                if (off < 0 || off >= kChunk) {
                     atomicOr(w.status, 2);
                     continue;
                 }
                 float a = acc[off];
                 long long f = e;
                 do {
-                    a = __fadd_rn(a, load_val<VD>(run.vals, f));
+                    a = __fadd_rn(a, load_val<VD>(rval[r], f));
                     ++f;
-                } while (f < b1 && load_idx<ID>(run.idx, f) == i);
+                } while (f < b1 && load_idx<ID>(ridx[r], f) == i);
                 acc[off] = a;
             }
             __syncthreads();
         }
-        const long long len = n - base < kChunk ? n - base : kChunk;
-        if (vec_out && len == kChunk) {
-            float4* g4 = reinterpret_cast<float4*>(grad + base);
-            const float4* a4 = reinterpret_cast<const float4*>(acc);
-            for (int j = threadIdx.x; j < kChunk / 4; j += kBlock) {
-                float4 v = a4[j];
-                if (scale != 1.0f) {
-                    v.x = __fmul_rn(v.x, scale);
-                    v.y = __fmul_rn(v.y, scale);
-                    v.z = __fmul_rn(v.z, scale);
-                    v.w = __fmul_rn(v.w, scale);
-                }
-                g4[j] = v;
+    }
+    __syncthreads();
+    const long long len = n - base < kChunk ? n - base : kChunk;
+    if (aligned16(grad) && len == kChunk) {
+        float4* g4 = reinterpret_cast<float4*>(grad + base);
+        for (int j = tid; j < kChunk / 4; j += kBlock) {
+            float4 v = acc4[j];
+            if (scale != 1.0f) {
+                v.x = __fmul_rn(v.x, scale);
+                v.y = __fmul_rn(v.y, scale);
+                v.z = __fmul_rn(v.z, scale);
+                v.w = __fmul_rn(v.w, scale);
             }
-        } else {
-            for (int j = threadIdx.x; j < len; j += kBlock)
-                grad[base + j] = scale != 1.0f ? __fmul_rn(acc[j], scale) : acc[j];
+            g4[j] = v;
         }
-        __syncthreads();
+    } else {
+        for (int j = tid; j < len; j += kBlock) grad[base + j] = scale != 1.0f ? __fmul_rn(acc[j], scale) : acc[j];
     }
 }
 
@@ -214,22 +302,24 @@ static int vbytes(int vd) { return vd == DGC_F16 ? 2 : 4; }
 static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
 
 template <int VD, int ID>
-static int run_scatter(const DecWS& w, float* grad, int64_t n, float scale, int max_runs, hipStream_t s) {
+static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
+                       hipStream_t s) {
     const int64_t work = (int64_t)max_runs * (w.nchunks + 1);
-    hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, n, max_runs);
+    hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, rs, n, max_runs);
     DGC_LAUNCHED();
-    hipLaunchKernelGGL((k_scatter_chunks<VD, ID>), dim3(grid_for(w.nchunks, 1)), dim3(kBlock), 0, s, w,
+    if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
+    hipLaunchKernelGGL((k_scatter_chunks<VD, ID>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w, rs,
                        grad, n, scale);
     DGC_LAUNCHED();
     return DGC_OK;
 }
 
-static int dispatch_scatter(int vd, int id, const DecWS& w, float* grad, int64_t n, float scale,
-                            int max_runs, hipStream_t s) {
-    if (vd == DGC_F32 && id == DGC_I64) return run_scatter<DGC_F32, DGC_I64>(w, grad, n, scale, max_runs, s);
-    if (vd == DGC_F32 && id == DGC_I32) return run_scatter<DGC_F32, DGC_I32>(w, grad, n, scale, max_runs, s);
-    if (vd == DGC_F16 && id == DGC_I64) return run_scatter<DGC_F16, DGC_I64>(w, grad, n, scale, max_runs, s);
-    if (vd == DGC_F16 && id == DGC_I32) return run_scatter<DGC_F16, DGC_I32>(w, grad, n, scale, max_runs, s);
+static int dispatch_scatter(int vd, int id, const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
+                            float scale, int max_runs, hipStream_t s) {
+    if (vd == DGC_F32 && id == DGC_I64) return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, s);
+    if (vd == DGC_F32 && id == DGC_I32) return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, s);
+    if (vd == DGC_F16 && id == DGC_I64) return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, s);
+    if (vd == DGC_F16 && id == DGC_I32) return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, s);
     DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
 }
 
@@ -282,7 +372,8 @@ int decompress(const void* values, int vd, const void* indices, int id, int64_t 
         if (nr == 0)
             DGC_FAIL(DGC_ERR_UNSORTED, "dgc_decompress: input has more than %d descending runs", kMaxRuns);
     }
-    return dispatch_scatter(vd, id, w, grad, n, scale, max_runs, s);
+    RunSrc rs{w.runs, w.nruns, nullptr, 0, 0, 0, 0, 0};
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, max_runs, s);
 }
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff) {
@@ -302,11 +393,8 @@ int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, i
         DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed: rank_stride %lld < layout %lld",
                  (long long)rank_stride, (long long)min_stride);
     DecWS w = carve_dec(ws, n, world);
-    DGC_HIP(hipMemsetAsync(w.nruns, 0, 4 * sizeof(int32_t), s));
-    hipLaunchKernelGGL(k_runs_packed, dim3(1), dim3(kMaxRuns), 0, s, w, static_cast<const char*>(payload),
-                       world, rank_stride, voff, ioff, capacity);
-    DGC_LAUNCHED();
-    return dispatch_scatter(vd, id, w, grad, n, scale, world, s);
+    RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world};
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, s);
 }
 
 }  // namespace dgc

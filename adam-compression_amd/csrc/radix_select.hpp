@@ -8,11 +8,13 @@
 // topk ranks NaN. torch.min over a top-k set that holds a NaN returns NaN, so the
 // result is NaN whenever any NaN key exists (counted in pass 0).
 //
-// Digits: 11 + 11 + 10 bits (2048/2048/1024 bins). Each pass = one histogram
-// launch (LDS histogram per block, non-zero bins flushed with 64-bit global
-// atomics) + one single-block scan launch that picks the bin holding the k-th
-// largest key and narrows (prefix, k). Inputs of <= kSmallN keys run the three
-// passes inside ONE workgroup from LDS.
+// Digits: 11 + 11 + 10 bits (2048/2048/1024 bins). One launch per pass: every
+// workgroup builds an LDS histogram of the keys that match the current prefix and
+// flushes its non-zero bins with 64-bit device atomics; the LAST workgroup to
+// arrive (agent-scope release -> ticket -> acquire, cdna_hip_programming.md G16)
+// reads the totals with agent-scope atomic loads and picks the bin holding the
+// k-th largest key, narrowing (prefix, k) for the next pass. Inputs of <= kSmallN
+// keys run all three passes inside ONE workgroup from LDS.
 //
 // The scalar result is written to a device float; nothing returns to the host.
 #pragma once
@@ -30,8 +32,8 @@ struct RSState {
     uint32_t found;
     uint64_t k_rem;
     uint64_t nan_count;
-    uint64_t pad;
-    unsigned long long hist[kRsBins];
+    uint32_t tickets[4];
+    unsigned long long hist[3][kRsBins];
 };
 
 __host__ __device__ constexpr int rs_shift(int pass) { return pass == 0 ? 21 : pass == 1 ? 10 : 0; }
@@ -68,10 +70,9 @@ struct DenseKeys {
 };
 
 // ---------------------------------------------------------------- block scan
-// Exclusive scan of one u64 per thread over a 1024-thread block; returns the
-// exclusive prefix and writes the block total to *total (all threads).
-__device__ __forceinline__ uint64_t block_exclusive_scan_1024(uint64_t v, uint64_t* lds16,
-                                                              uint64_t* total) {
+// Exclusive scan of one u64 per thread over the block (blockDim a multiple of 64,
+// <= 1024); returns the exclusive prefix and writes the block total to *total.
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds16, uint64_t* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint64_t incl = v;
 #pragma unroll
@@ -92,39 +93,93 @@ __device__ __forceinline__ uint64_t block_exclusive_scan_1024(uint64_t v, uint64
     return wbase + incl - v;
 }
 
-// Pick the bin of the k-th largest key from counts[0..bins) (one block of 1024).
-// Thread t owns descending positions {2t, 2t+1} (2048 bins) or {t} (1024 bins).
-// Returns true in exactly one thread, setting *bin and *above (keys in higher bins).
+__device__ __forceinline__ uint64_t block_exclusive_scan_1024(uint64_t v, uint64_t* lds16, uint64_t* total) {
+    return block_exclusive_scan(v, lds16, total);
+}
+
 template <typename CountT>
-__device__ __forceinline__ bool pick_bin(const CountT* counts, int bins, uint64_t k,
-                                         uint64_t* lds16, int* bin, uint64_t* above) {
-    const int per = bins / kScanThreads;   // 2 or 1
+__device__ __forceinline__ uint64_t load_count(const CountT* p) {
+    return (uint64_t)*p;
+}
+// totals flushed by other workgroups' atomics: read them where atomics are performed
+__device__ __forceinline__ uint64_t load_count(const unsigned long long* p) {
+    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Pick the bin of the k-th largest key from counts[0..bins). Thread t owns the
+// descending positions [per*t, per*t + per). Returns true in exactly one thread.
+template <typename CountT>
+__device__ __forceinline__ bool pick_bin(const CountT* counts, int bins, uint64_t k, uint64_t* lds16, int* bin,
+                                         uint64_t* above) {
+    const int per = bins / (int)blockDim.x;
     const int t = threadIdx.x;
-    uint64_t c[2] = {0, 0};
-    for (int j = 0; j < per; ++j) c[j] = counts[bins - 1 - (per * t + j)];
+    uint64_t sum = 0;
+    for (int j = 0; j < per; ++j) sum += load_count(&counts[bins - 1 - (per * t + j)]);
     uint64_t total;
-    uint64_t run = block_exclusive_scan_1024(c[0] + c[1], lds16, &total);
+    uint64_t run = block_exclusive_scan(sum, lds16, &total);
     bool hit = false;
-    for (int j = 0; j < per; ++j) {
-        if (!hit && run < k && k <= run + c[j]) {
-            hit = true;
-            *bin = bins - 1 - (per * t + j);
-            *above = run;
+    if (run < k && k <= run + sum) {
+        for (int j = 0; j < per; ++j) {
+            const uint64_t c = load_count(&counts[bins - 1 - (per * t + j)]);
+            if (!hit && run < k && k <= run + c) {
+                hit = true;
+                *bin = bins - 1 - (per * t + j);
+                *above = run;
+            }
+            run += c;
         }
-        run += c[j];
     }
     return hit;
 }
 
+// True in every thread of the workgroup that arrives last at `ticket` among
+// `nblocks`. The data handed to the last workgroup is ONLY device-scope atomics
+// (histogram / count adds) that it reads back with agent-scope atomic loads — the
+// "agent atomics both sides" form of cdna_hip_programming.md G16 — so no L2
+// write-back (release) or L1 invalidate (acquire) fence is needed: every wave
+// drains its atomics (vmcnt(0): acknowledged = performed at the coherence point)
+// before the barrier, then one lane draws the ticket.
+__device__ __forceinline__ bool last_block_arrival(uint32_t* ticket, uint32_t nblocks) {
+    __shared__ int is_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = t == nblocks - 1;
+        if (is_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reusable
+    }
+    __syncthreads();
+    return is_last;
+}
+
 // ---------------------------------------------------------------- kernels
+__device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
+    for (int b = threadIdx.x; b < 3 * kRsBins; b += blockDim.x) (&st->hist[0][0])[b] = 0;
+    if (threadIdx.x == 0) {
+        st->prefix = 0;
+        st->found = 0;
+        st->k_rem = k;
+        st->nan_count = 0;
+        for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
+    }
+}
+
+__global__ void k_rs_init(RSState* st, uint64_t k) { rs_reset(st, k); }
+
 template <class Src>
 __global__ void __launch_bounds__(kBlock)
-k_rs_hist(Src src, RSState* st, int pass, const int32_t* gate) {
+k_rs_hist(Src src, RSState* st, int pass, float* out, const int32_t* gate) {
     if (gate && *gate == 0) return;
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t nan_cnt;
+    __shared__ uint64_t lds16[16];
+    __shared__ int sel_bin;
+    __shared__ uint64_t sel_above;
     for (int b = threadIdx.x; b < kRsBins; b += kBlock) h[b] = 0;
-    if (threadIdx.x == 0) nan_cnt = 0;
+    if (threadIdx.x == 0) {
+        nan_cnt = 0;
+        sel_bin = -1;
+    }
     __syncthreads();
     const uint32_t prefix = st->prefix;
     const uint32_t pmask = rs_pmask(pass), dmask = rs_dmask(pass);
@@ -134,52 +189,35 @@ k_rs_hist(Src src, RSState* st, int pass, const int32_t* gate) {
         if (pass == 0 && key > 0x7F800000u) atomicAdd(&nan_cnt, 1u);
     });
     __syncthreads();
+    unsigned long long* gh = st->hist[pass];
     for (int b = threadIdx.x; b < rs_bins(pass); b += kBlock)
-        if (h[b]) atomicAdd(&st->hist[b], (unsigned long long)h[b]);
+        if (h[b]) atomicAdd(&gh[b], (unsigned long long)h[b]);
     if (pass == 0 && threadIdx.x == 0 && nan_cnt)
         atomicAdd((unsigned long long*)&st->nan_count, (unsigned long long)nan_cnt);
-}
-
-__global__ void __launch_bounds__(kScanThreads)
-k_rs_scan(RSState* st, int pass, float* out, const int32_t* gate) {
-    if (gate && *gate == 0) return;
-    __shared__ uint64_t lds16[16];
-    __shared__ int sel_bin;
-    __shared__ uint64_t sel_above;
-    if (threadIdx.x == 0) sel_bin = -1;
-    __syncthreads();
+    if (!last_block_arrival(&st->tickets[pass], gridDim.x)) return;
+    // the last workgroup picks the bin for everyone
     const uint64_t k = st->k_rem;
     int bin;
     uint64_t above;
-    if (pick_bin(st->hist, rs_bins(pass), k, lds16, &bin, &above)) {
+    if (pick_bin(gh, rs_bins(pass), k, lds16, &bin, &above)) {
         sel_bin = bin;
         sel_above = above;
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < kRsBins; b += kScanThreads) st->hist[b] = 0;
     if (threadIdx.x == 0) {
         if (sel_bin < 0) {
             st->found = 0;   // k exceeded the key count: report NaN
             if (out) *out = __uint_as_float(0x7FC00000u);
         } else {
-            st->prefix |= (uint32_t)sel_bin << rs_shift(pass);
+            st->prefix = prefix | ((uint32_t)sel_bin << shift);
             st->k_rem = k - sel_above;
             if (pass == 2) {
                 st->found = 1;
-                if (out) *out = st->nan_count ? __uint_as_float(0x7FC00000u) : __uint_as_float(st->prefix);
+                const uint64_t nans = __hip_atomic_load((unsigned long long*)&st->nan_count, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+                if (out) *out = nans ? __uint_as_float(0x7FC00000u) : __uint_as_float(st->prefix);
             }
         }
-    }
-}
-
-__global__ void k_rs_init(RSState* st, uint64_t k, const int32_t* gate) {
-    if (gate && *gate == 0) return;
-    for (int b = threadIdx.x; b < kRsBins; b += blockDim.x) st->hist[b] = 0;
-    if (threadIdx.x == 0) {
-        st->prefix = 0;
-        st->found = 0;
-        st->k_rem = k;
-        st->nan_count = 0;
     }
 }
 
@@ -234,21 +272,25 @@ k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
         *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
 }
 
-// Host launcher over any key source. `gate` (device int, may be null) turns every
-// launch into a no-op when zero, so the chain can sit in a device-decided pipeline.
+// The three histogram passes over any key source; the state must have been reset
+// (k_rs_init, or fused into an earlier kernel) with k. `gate` (device int, may be
+// null) turns every launch into a no-op when zero.
 template <class Src>
-inline int radix_select_launch(const Src& src, int64_t work_items, uint64_t k, float* out,
-                               RSState* st, const int32_t* gate, hipStream_t s) {
-    hipLaunchKernelGGL(k_rs_init, dim3(1), dim3(kBlock), 0, s, st, k, gate);
-    DGC_LAUNCHED();
-    const int grid = grid_for(work_items, kBlock * 4);
+inline int radix_select_passes(const Src& src, int grid, float* out, RSState* st, const int32_t* gate,
+                               hipStream_t s) {
     for (int pass = 0; pass < 3; ++pass) {
-        hipLaunchKernelGGL((k_rs_hist<Src>), dim3(grid), dim3(kBlock), 0, s, src, st, pass, gate);
-        DGC_LAUNCHED();
-        hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(kScanThreads), 0, s, st, pass, out, gate);
+        hipLaunchKernelGGL((k_rs_hist<Src>), dim3(grid), dim3(kBlock), 0, s, src, st, pass, out, gate);
         DGC_LAUNCHED();
     }
     return DGC_OK;
+}
+
+template <class Src>
+inline int radix_select_launch(const Src& src, int64_t work_items, uint64_t k, float* out, RSState* st,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_rs_init, dim3(1), dim3(kBlock), 0, s, st, k);
+    DGC_LAUNCHED();
+    return radix_select_passes(src, grid_for(work_items, kBlock * 16, 512), out, st, nullptr, s);
 }
 
 }  // namespace dgc

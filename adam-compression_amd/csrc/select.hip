@@ -34,6 +34,12 @@ constexpr int kSegPerBlock = kBlock / kWave;   // 4
 constexpr int kCap = 256;
 constexpr int kGroupSegs = 256;
 constexpr int kTiles = kSeg / (kWave * 4);    // 16 float4 tiles per lane
+#ifndef DGC_SEL_BATCH
+#define DGC_SEL_BATCH 16
+#endif
+constexpr int kSelBatch = DGC_SEL_BATCH;       // tile loads in flight per lane
+
+constexpr int kMaxLower = 16;                  // thresholds per multi-threshold pass
 
 enum { MODE_FIRSTK = 0, MODE_RESAMPLE = 1 };
 
@@ -45,7 +51,9 @@ struct SelState {
     long long n_greater;   // RESAMPLE: candidates > tk
     long long tie_quota;   // RESAMPLE: k - n_greater ties, lowest index first
     int32_t iter, recounts, active, resample_pending;
-    int32_t overflow, done, pad0, pad1;
+    int32_t overflow, done, lower_pending, pad0;
+    uint32_t tickets[4];
+    unsigned long long lower_cnt[kMaxLower + 1];   // counts at t_1..t_m (multi-threshold pass)
 };
 
 struct SelWS {
@@ -101,7 +109,7 @@ template <bool ALIGNED>
 __device__ __forceinline__ void load_tile(const float* __restrict__ v, int64_t n, int64_t e0,
                                           float (&x)[4], uint32_t& valid) {
     if (ALIGNED && e0 + 3 < n) {
-        const float4 q = *reinterpret_cast<const float4*>(v + e0);
+        const float4 q = ld_nt(reinterpret_cast<const float4*>(v + e0));
         x[0] = q.x;
         x[1] = q.y;
         x[2] = q.z;
@@ -126,7 +134,9 @@ __device__ __forceinline__ uint32_t ge_mask(const float (&x)[4], uint32_t valid,
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ void k_sel_init(SelState* st, const float* thr0) {
+__global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, const float* thr0) {
+    SelState* st = w.st;
+    for (int64_t i = threadIdx.x; i < 3 * w.ngrp; i += blockDim.x) w.grp_cnt[i] = 0;
     if (threadIdx.x == 0) {
         const float t = *thr0;
         st->t0 = t;
@@ -139,6 +149,9 @@ __global__ void k_sel_init(SelState* st, const float* thr0) {
         st->resample_pending = 0;
         st->overflow = 0;
         st->done = 0;
+        st->lower_pending = 0;
+        for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
+        for (int i = 0; i <= kMaxLower; ++i) st->lower_cnt[i] = 0;
     }
 }
 
@@ -151,6 +164,8 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ uint32_t wcnt[kSegPerBlock];
     __shared__ uint32_t wovf[kSegPerBlock];
+    // launched one-shot (grid = nseg/4: each block one iteration) for the first pass,
+    // grid-stride with a capped grid for the gated recount passes
     for (int64_t bi = blockIdx.x; bi * kSegPerBlock < w.nseg; bi += gridDim.x) {
         const int64_t seg = bi * kSegPerBlock + wave;
         uint32_t c = 0;
@@ -159,14 +174,14 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
             uint16_t* lo = w.lst_off + seg * kCap;
             float* lv = w.lst_val + seg * kCap;
 #pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                float x[8][4];
-                uint32_t valid[8];
+            for (int half = 0; half < kTiles / kSelBatch; ++half) {
+                float x[kSelBatch][4];
+                uint32_t valid[kSelBatch];
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    load_tile<ALIGNED>(vec, n, base + (half * 8 + u) * 256 + 4 * lane, x[u], valid[u]);
+                for (int u = 0; u < kSelBatch; ++u)
+                    load_tile<ALIGNED>(vec, n, base + (half * kSelBatch + u) * 256 + 4 * lane, x[u], valid[u]);
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < kSelBatch; ++u) {
                     const uint32_t p = ge_mask(x[u], valid[u], t);
                     if (__ballot(p != 0)) {
                         uint32_t lb, tot;
@@ -176,7 +191,7 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
                         for (int j = 0; j < 4; ++j) {
                             if (p & (1u << j)) {
                                 if (r < kCap) {
-                                    lo[r] = (uint16_t)((half * 8 + u) * 256 + 4 * lane + j);
+                                    lo[r] = (uint16_t)((half * kSelBatch + u) * 256 + 4 * lane + j);
                                     lv[r] = x[u][j];
                                 }
                                 ++r;
@@ -203,39 +218,45 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
     }
 }
 
-// Chunked exclusive scan of a[0..m) into out[] by one 1024-thread workgroup; returns the total.
+// Chunked exclusive scan of a[0..m) into out[] by one workgroup; returns the total.
+// a[] holds totals accumulated by device atomics: read with agent-scope loads.
 __device__ uint64_t block_scan_array(const unsigned long long* a, long long* out, int64_t m,
                                      uint64_t* lds16) {
-    const int64_t per = ceil_div(m, (int64_t)kScanThreads);
+    const int64_t per = ceil_div(m, (int64_t)blockDim.x);
     const int64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
     uint64_t local = 0;
-    for (int64_t i = b; i < e; ++i) local += a[i];
+    for (int64_t i = b; i < e; ++i) local += load_count(&a[i]);
     uint64_t total;
-    uint64_t run = block_exclusive_scan_1024(local, lds16, &total);
+    uint64_t run = block_exclusive_scan(local, lds16, &total);
     for (int64_t i = b; i < e; ++i) {
         out[i] = (long long)run;
-        run += a[i];
+        run += load_count(&a[i]);
     }
     return total;
 }
 
 // One step of the reference's adaptation loop (dgc/compression.py:128-149) on the
-// count of the pass that just ran.
+// count of the pass that just ran. With resample (the default) the loop can only
+// lower the threshold until the count reaches lower*k, so the first "lower" step
+// hands over to ONE multi-threshold pass (k_lower_counts) instead of recounting
+// one threshold per pass; without resample the threshold may also rise, and each
+// step is a recount (select pass + decide), exactly like the reference.
 __global__ void __launch_bounds__(kScanThreads)
 k_decide(SelWS w, dgc_select_params p) {
     SelState* st = w.st;
     if (!st->active) return;
     __shared__ uint64_t lds16[16];
-    __shared__ int finished;
+    __shared__ int finished, reset_rs;
     uint64_t local = 0;
     for (int64_t i = threadIdx.x; i < w.ngrp; i += kScanThreads) local += w.grp_cnt[i];
     uint64_t n;
-    block_exclusive_scan_1024(local, lds16, &n);
+    block_exclusive_scan(local, lds16, &n);
     if (threadIdx.x == 0) {
         const long long cnt = (long long)n, k = p.num_selects;
         const bool adapt = p.numel > p.num_samples;
         st->n_cur = cnt;
         int done = 1;
+        reset_rs = 0;
         if (!adapt) {
             st->branch = DGC_BRANCH_DIRECT;
             st->limit = cnt < k ? cnt : k;
@@ -247,6 +268,7 @@ k_decide(SelWS w, dgc_select_params p) {
                 if (p.resample) {
                     st->branch = DGC_BRANCH_RESAMPLE;
                     st->resample_pending = 1;
+                    reset_rs = 1;
                 } else {
                     st->t_cur = __fmul_rn(st->t_cur, p.upper);
                     done = 0;
@@ -256,27 +278,101 @@ k_decide(SelWS w, dgc_select_params p) {
                 st->limit = k;
             }
         } else if (cnt < p.lower_count) {
-            st->t_cur = __fmul_rn(st->t_cur, p.lower);
-            done = 0;
+            if (p.resample && st->iter == 0 && p.max_iters <= kMaxLower) {
+                st->lower_pending = 1;   // k_lower_counts finds the final threshold in one pass
+                done = 2;
+            } else {
+                st->t_cur = __fmul_rn(st->t_cur, p.lower);
+                done = 0;
+            }
         } else {
             st->branch = DGC_BRANCH_OK;
             st->limit = cnt;
         }
-        if (!done) {
+        if (done == 0) {
             st->iter += 1;
             st->recounts += 1;
             st->overflow = 0;
-        } else {
+        } else if (done == 1) {
             st->active = 0;
             st->done = 1;
+        } else {
+            st->active = 0;
         }
         finished = done;
     }
     __syncthreads();
-    if (finished) block_scan_array(w.grp_cnt, w.grp_off, w.ngrp, lds16);
+    if (finished == 1) block_scan_array(w.grp_cnt, w.grp_off, w.ngrp, lds16);
+    if (reset_rs) rs_reset(w.rs, (uint64_t)p.num_selects);
     __syncthreads();
-    if (!finished)
+    if (finished != 1)
         for (int64_t i = threadIdx.x; i < w.ngrp; i += kScanThreads) w.grp_cnt[i] = 0;
+}
+
+// Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
+// reference's "lower" recounts, dgc/compression.py:140-148, all at once). The last
+// workgroup to arrive picks j* = the first j whose count reaches lower*k (else
+// max_iters) and arms the list pass + decide at t_{j*}.
+template <bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)
+k_lower_counts(const float* __restrict__ vec, int64_t n, SelWS w, dgc_select_params p) {
+    SelState* st = w.st;
+    if (!st->lower_pending) return;
+    const int m = p.max_iters;
+    float t[kMaxLower + 1];
+    t[0] = st->t_cur;
+#pragma unroll
+    for (int j = 1; j <= kMaxLower; ++j) t[j] = __fmul_rn(t[j - 1], p.lower);
+    const float tmin = t[m];
+    uint32_t c[kMaxLower + 1];
+#pragma unroll
+    for (int j = 0; j <= kMaxLower; ++j) c[j] = 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t seg = (int64_t)blockIdx.x * kSegPerBlock + wave; seg < w.nseg;
+         seg += (int64_t)gridDim.x * kSegPerBlock) {
+        for (int tile = 0; tile < kTiles; ++tile) {
+            float x[4];
+            uint32_t valid;
+            load_tile<ALIGNED>(vec, n, seg * kSeg + tile * 256 + 4 * lane, x, valid);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float a = fabsf(x[q]);
+                if (((valid >> q) & 1u) && a >= tmin) {
+#pragma unroll
+                    for (int j = 1; j <= kMaxLower; ++j) c[j] += (j <= m) && a >= t[j];
+                }
+            }
+        }
+    }
+    __shared__ uint32_t part[kSegPerBlock][kMaxLower + 1];
+#pragma unroll
+    for (int j = 1; j <= kMaxLower; ++j) {
+        const uint32_t v = wave_sum(c[j]);
+        if (lane == 0) part[wave][j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 1 && threadIdx.x <= m) {
+        const int j = threadIdx.x;
+        const uint64_t v = (uint64_t)part[0][j] + part[1][j] + part[2][j] + part[3][j];
+        if (v) atomicAdd(&st->lower_cnt[j], (unsigned long long)v);
+    }
+    if (!last_block_arrival(&st->tickets[0], gridDim.x)) return;
+    if (threadIdx.x == 0) {
+        int js = m;
+        for (int j = 1; j <= m; ++j) {
+            const long long nj = (long long)load_count(&st->lower_cnt[j]);
+            if (nj >= p.lower_count) {
+                js = j;
+                break;
+            }
+        }
+        st->t_cur = t[js];
+        st->iter = js;
+        st->recounts = js;
+        st->overflow = 0;
+        st->lower_pending = 0;
+        st->active = 1;   // list pass + decide at t_{j*}
+    }
 }
 
 // Candidate keys of the final threshold, for the resample radix select: the
@@ -310,11 +406,13 @@ struct CandKeys {
     }
 };
 
-// Per-segment counts of |x| > tk and |x| == tk among the candidates (resample).
+// Per-segment counts of |x| > tk and |x| == tk among the candidates (resample);
+// the last workgroup scans the group totals and sets the tie quota k - #greater.
 __global__ void __launch_bounds__(kBlock)
-k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w) {
-    if (!w.st->resample_pending) return;
-    const float tk = w.st->tk;
+k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w, int64_t k) {
+    SelState* st = w.st;
+    if (!st->resample_pending) return;
+    const float tk = st->tk;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t bi = blockIdx.x; bi * kSegPerBlock < w.nseg; bi += gridDim.x) {
         const int64_t seg = bi * kSegPerBlock + wave;
@@ -351,12 +449,7 @@ k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w) {
             if (eq) atomicAdd(&w.grp_eq[g], (unsigned long long)eq);
         }
     }
-}
-
-__global__ void __launch_bounds__(kScanThreads)
-k_resample_finalize(SelWS w, int64_t k) {
-    SelState* st = w.st;
-    if (!st->resample_pending) return;
+    if (!last_block_arrival(&st->tickets[1], gridDim.x)) return;
     __shared__ uint64_t lds16[16];
     const uint64_t G = block_scan_array(w.grp_gt, w.grp_gt_off, w.ngrp, lds16);
     __syncthreads();
@@ -379,8 +472,9 @@ struct EmitOut {
 __device__ __forceinline__ void emit_one(const EmitOut& o, int64_t pos, int64_t gidx, float x) {
     store_value(o.values, pos, x, o.vdtype);
     store_index(o.indices, pos, gidx, o.idtype);
-    if (o.vec) o.vec[gidx] = 0.f;
-    if (o.mmt) o.mmt[gidx] = 0.f;
+    // scattered 4-B writes, one per 128-B line: non-temporal (no L2 allocation)
+    if (o.vec) __builtin_nontemporal_store(0.f, o.vec + gidx);
+    if (o.mmt) __builtin_nontemporal_store(0.f, o.mmt + gidx);
 }
 
 // Block-wide exclusive scan of one u32 per thread over a 256-thread block.
@@ -400,7 +494,75 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_256(uint32_t v, uint32_
     return base + incl - v;
 }
 
-// One workgroup per group of 256 segments; each wave emits segments wave, wave+4, ...
+// Wave-cooperative emit of one segment by re-reading vec (a spilled list).
+// FIRSTK: positions base + rank for |x| >= t, kept while < limit.
+__device__ void emit_reread_firstk(const float* __restrict__ vec_in, int64_t n, int64_t seg, long long base,
+                                   long long limit, float t, const EmitOut& o) {
+    const int lane = threadIdx.x & 63;
+    uint32_t run = 0;
+    for (int tile = 0; tile < kTiles; ++tile) {
+        float x[4];
+        uint32_t valid;
+        const int64_t e0 = seg * kSeg + tile * 256 + 4 * lane;
+        load_tile<false>(vec_in, n, e0, x, valid);
+        const uint32_t p = ge_mask(x, valid, t);
+        if (__ballot(p != 0)) {
+            uint32_t lb, tot;
+            wave_prefix4(p, lb, tot);
+            uint32_t r = run + lb;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (p & (1u << j)) {
+                    const long long pos = base + r;
+                    if (pos < limit) emit_one(o, pos, e0 + j, x[j]);
+                    ++r;
+                }
+            run += tot;
+        }
+    }
+}
+
+// RESAMPLE: |x| > tk always, |x| == tk while the running tie rank is below T.
+__device__ void emit_reread_resample(const float* __restrict__ vec_in, int64_t n, int64_t seg, long long bg,
+                                     long long bt, float tk, long long T, const EmitOut& o) {
+    const int lane = threadIdx.x & 63;
+    uint32_t run_g = 0, run_t = 0;
+    for (int tile = 0; tile < kTiles; ++tile) {
+        float x[4];
+        uint32_t valid;
+        const int64_t e0 = seg * kSeg + tile * 256 + 4 * lane;
+        load_tile<false>(vec_in, n, e0, x, valid);
+        uint32_t pg = 0, pe = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float a = fabsf(x[j]);
+            pg |= (uint32_t)(a > tk) << j;
+            pe |= (uint32_t)(a == tk) << j;
+        }
+        pg &= valid;
+        pe &= valid;
+        if (__ballot((pg | pe) != 0)) {
+            uint32_t lg, tg, lt, tt;
+            wave_prefix4(pg, lg, tg);
+            wave_prefix4(pe, lt, tt);
+            uint32_t rg = run_g + lg, rt = run_t + lt;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool gt = (pg >> j) & 1u, eq = (pe >> j) & 1u;
+                const long long tb = bt + rt;
+                if (gt || (eq && tb < T)) emit_one(o, bg + rg + (tb < T ? tb : T), e0 + j, x[j]);
+                rg += gt;
+                rt += eq;
+            }
+            run_g += tg;
+            run_t += tt;
+        }
+    }
+}
+
+// One workgroup per group of 256 segments, ONE THREAD PER SEGMENT for complete
+// lists (a few entries each: no serial per-wave walk over segments), then the
+// group's spilled segments, if any, one wave each.
 __global__ void __launch_bounds__(kBlock)
 k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
     const SelState* st = w.st;
@@ -408,121 +570,68 @@ k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
     const int64_t g = blockIdx.x;
     const int64_t s0 = g * kGroupSegs;
     const int nsg = (int)((w.nseg - s0) < kGroupSegs ? (w.nseg - s0) : kGroupSegs);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ts = threadIdx.x, wave = threadIdx.x >> 6;
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs];
-    const int ts = threadIdx.x;
+    __shared__ int spill[kGroupSegs];
+    __shared__ int nspill;
+    if (ts == 0) nspill = 0;
+    const int64_t seg = s0 + ts;
+    const uint32_t c = ts < nsg ? w.seg_cnt[seg] : 0;
     if (mode == MODE_FIRSTK) {
-        const uint32_t c = ts < nsg ? w.seg_cnt[s0 + ts] : 0;
         off_a[ts] = block_exclusive_scan_256(c, lds4);
     } else {
-        const uint32_t a = ts < nsg ? w.seg_gt[s0 + ts] : 0;
-        const uint32_t b = ts < nsg ? w.seg_eq[s0 + ts] : 0;
+        const uint32_t a = ts < nsg ? w.seg_gt[seg] : 0;
+        const uint32_t b = ts < nsg ? w.seg_eq[seg] : 0;
         off_a[ts] = block_exclusive_scan_256(a, lds4);
         off_b[ts] = block_exclusive_scan_256(b, lds4);
     }
     __syncthreads();
+    const uint16_t* lo = w.lst_off + seg * kCap;
+    const float* lv = w.lst_val + seg * kCap;
     if (mode == MODE_FIRSTK) {
         const long long limit = st->limit;
-        const float t = st->t_cur;
-        for (int sl = wave; sl < nsg; sl += kSegPerBlock) {
-            const int64_t seg = s0 + sl;
-            const long long base = w.grp_off[g] + off_a[sl];
-            if (base >= limit) break;   // later segments start even further on
-            const uint32_t c = w.seg_cnt[seg];
+        const long long base = w.grp_off[g] + off_a[ts];
+        if (ts < nsg && c > 0 && base < limit) {
             if (c <= (uint32_t)kCap) {
-                for (uint32_t e = lane; e < c; e += 64) {
-                    const long long pos = base + e;
-                    if (pos < limit)
-                        emit_one(o, pos, seg * kSeg + w.lst_off[seg * kCap + e], w.lst_val[seg * kCap + e]);
-                }
+                const long long m = (limit - base) < (long long)c ? (limit - base) : (long long)c;
+                for (long long e = 0; e < m; ++e) emit_one(o, base + e, seg * kSeg + lo[e], lv[e]);
             } else {
-                uint32_t run = 0;
-                for (int tile = 0; tile < kTiles; ++tile) {
-                    float x[4];
-                    uint32_t valid;
-                    const int64_t e0 = seg * kSeg + tile * 256 + 4 * lane;
-                    load_tile<false>(vec_in, n, e0, x, valid);
-                    const uint32_t p = ge_mask(x, valid, t);
-                    if (__ballot(p != 0)) {
-                        uint32_t lb, tot;
-                        wave_prefix4(p, lb, tot);
-                        uint32_t r = run + lb;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (p & (1u << j)) {
-                                const long long pos = base + r;
-                                if (pos < limit) emit_one(o, pos, e0 + j, x[j]);
-                                ++r;
-                            }
-                        run += tot;
-                    }
-                }
+                spill[atomicAdd(&nspill, 1)] = ts;
             }
+        }
+        __syncthreads();
+        const float t = st->t_cur;
+        for (int q = wave; q < nspill; q += kSegPerBlock) {
+            const int sl = spill[q];
+            emit_reread_firstk(vec_in, n, s0 + sl, w.grp_off[g] + off_a[sl], limit, t, o);
         }
     } else {
         const float tk = st->tk;
         const long long T = st->tie_quota;
-        for (int sl = wave; sl < nsg; sl += kSegPerBlock) {
-            const int64_t seg = s0 + sl;
-            const long long bg = w.grp_gt_off[g] + off_a[sl];
-            const long long bt = w.grp_eq_off[g] + off_b[sl];
-            if (w.seg_gt[seg] == 0 && (w.seg_eq[seg] == 0 || bt >= T)) continue;
-            const uint32_t c = w.seg_cnt[seg];
-            uint32_t run_g = 0, run_t = 0;
+        if (ts < nsg && c > 0) {
+            const long long bg = w.grp_gt_off[g] + off_a[ts];
+            const long long bt = w.grp_eq_off[g] + off_b[ts];
             if (c <= (uint32_t)kCap) {
-                for (uint32_t e0 = 0; e0 < c; e0 += 64) {
-                    const uint32_t e = e0 + lane;
-                    const float x = e < c ? w.lst_val[seg * kCap + e] : 0.f;
+                long long rg = 0, rt = 0;
+                for (uint32_t e = 0; e < c; ++e) {
+                    const float x = lv[e];
                     const float a = fabsf(x);
-                    const bool gt = e < c && a > tk, eq = e < c && a == tk;
-                    uint32_t lg, tg, lt, tt;
-                    wave_prefix1(gt, lg, tg);
-                    wave_prefix1(eq, lt, tt);
-                    const long long tb = bt + run_t + lt;
-                    if (gt || (eq && tb < T)) {
-                        const long long pos = bg + run_g + lg + (tb < T ? tb : T);
-                        emit_one(o, pos, seg * kSeg + w.lst_off[seg * kCap + e], x);
-                    }
-                    run_g += tg;
-                    run_t += tt;
+                    const bool gt = a > tk, eq = a == tk;
+                    const long long tb = bt + rt;
+                    if (gt || (eq && tb < T)) emit_one(o, bg + rg + (tb < T ? tb : T), seg * kSeg + lo[e], x);
+                    rg += gt;
+                    rt += eq;
                 }
             } else {
-                for (int tile = 0; tile < kTiles; ++tile) {
-                    float x[4];
-                    uint32_t valid;
-                    const int64_t e0 = seg * kSeg + tile * 256 + 4 * lane;
-                    load_tile<false>(vec_in, n, e0, x, valid);
-                    uint32_t pg = 0, pe = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float a = fabsf(x[j]);
-                        pg |= (uint32_t)(a > tk) << j;
-                        pe |= (uint32_t)(a == tk) << j;
-                    }
-                    pg &= valid;
-                    pe &= valid;
-                    if (__ballot((pg | pe) != 0)) {
-                        uint32_t lg, tg, lt, tt;
-                        wave_prefix4(pg, lg, tg);
-                        wave_prefix4(pe, lt, tt);
-                        uint32_t rg = run_g + lg, rt = run_t + lt;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const bool gt = (pg >> j) & 1u, eq = (pe >> j) & 1u;
-                            const long long tb = bt + rt;
-                            if (gt || (eq && tb < T)) {
-                                const long long pos = bg + rg + (tb < T ? tb : T);
-                                emit_one(o, pos, e0 + j, x[j]);
-                            }
-                            rg += gt;
-                            rt += eq;
-                        }
-                        run_g += tg;
-                        run_t += tt;
-                    }
-                }
+                spill[atomicAdd(&nspill, 1)] = ts;
             }
+        }
+        __syncthreads();
+        for (int q = wave; q < nspill; q += kSegPerBlock) {
+            const int sl = spill[q];
+            emit_reread_resample(vec_in, n, s0 + sl, w.grp_gt_off[g] + off_a[sl], w.grp_eq_off[g] + off_b[sl], tk,
+                                 T, o);
         }
     }
 }
@@ -572,46 +681,60 @@ int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_select: workspace needs %zu bytes, 256-B aligned",
                  select_ws_bytes(n));
     SelWS w = carve_select(ws, n);
-    DGC_HIP(hipMemsetAsync(w.grp_cnt, 0, w.zero_bytes, s));
-    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, s, w.st, thr0);
+    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(kScanThreads), 0, s, w, thr0);
     DGC_LAUNCHED();
-    const int grid = grid_for(w.nseg, kSegPerBlock);
+    const int grid = (int)ceil_div(w.nseg, kSegPerBlock);      // one-shot select-pass blocks
+    const int grid_gs = grid_for(w.nseg, kSegPerBlock);         // grid-stride (gated) kernels
     const bool al = aligned16(vec);
-    auto pass = [&]() -> int {
+    const bool adapt = p->numel > p->num_samples;
+    const bool lower_fast = p->resample && p->max_iters <= kMaxLower;
+    auto pass = [&](int blocks) -> int {
         if (al)
-            hipLaunchKernelGGL(k_select_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, n, w);
+            hipLaunchKernelGGL(k_select_pass<true>, dim3(blocks), dim3(kBlock), 0, s, vec, n, w);
         else
-            hipLaunchKernelGGL(k_select_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, n, w);
+            hipLaunchKernelGGL(k_select_pass<false>, dim3(blocks), dim3(kBlock), 0, s, vec, n, w);
         DGC_LAUNCHED();
         hipLaunchKernelGGL(k_decide, dim3(1), dim3(kScanThreads), 0, s, w, *p);
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    SelState hs{};
-    DGC_TRY(pass());
+    auto lower = [&]() -> int {
+        if (al)
+            hipLaunchKernelGGL(k_lower_counts<true>, dim3(grid_gs), dim3(kBlock), 0, s, vec, n, w, *p);
+        else
+            hipLaunchKernelGGL(k_lower_counts<false>, dim3(grid_gs), dim3(kBlock), 0, s, vec, n, w, *p);
+        DGC_LAUNCHED();
+        return DGC_OK;
+    };
+    auto resample = [&]() -> int {
+        // rs state reset by k_decide when it chose the resample branch
+        CandKeys src{vec, n, w};
+        DGC_TRY(radix_select_passes(src, grid_gs, &w.st->tk, w.rs, &w.st->resample_pending, s));
+        hipLaunchKernelGGL(k_count_gt_eq, dim3(grid_gs), dim3(kBlock), 0, s, vec, n, w, (int64_t)p->num_selects);
+        DGC_LAUNCHED();
+        return DGC_OK;
+    };
+    DGC_TRY(pass(grid));
     if (sync_mode == DGC_SYNC_HOST) {
-        // read the decision back and launch only what is needed
+        // read each decision back and launch only what it needs
+        SelState hs{};
         for (;;) {
             DGC_HIP(hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s));
             DGC_HIP(hipStreamSynchronize(s));
             if (hs.done) break;
-            DGC_TRY(pass());
+            if (hs.lower_pending) DGC_TRY(lower());
+            DGC_TRY(pass(grid));
         }
-    } else if (p->numel > p->num_samples) {
-        for (int i = 0; i < p->max_iters; ++i) DGC_TRY(pass());
-    }
-    const bool need_resample = sync_mode == DGC_SYNC_HOST ? hs.branch == DGC_BRANCH_RESAMPLE
-                                                          : (p->resample && p->numel > p->num_samples);
-    if (need_resample) {
-        const int32_t* gate = &w.st->resample_pending;
-        CandKeys src{vec, n, w};
-        DGC_TRY(radix_select_launch(src, w.nseg * 64 * 4, (uint64_t)p->num_selects, &w.st->tk, w.rs,
-                                    gate, s));
-        hipLaunchKernelGGL(k_count_gt_eq, dim3(grid), dim3(kBlock), 0, s, vec, n, w);
-        DGC_LAUNCHED();
-        hipLaunchKernelGGL(k_resample_finalize, dim3(1), dim3(kScanThreads), 0, s, w,
-                           (int64_t)p->num_selects);
-        DGC_LAUNCHED();
+        if (hs.branch == DGC_BRANCH_RESAMPLE) DGC_TRY(resample());
+    } else if (adapt) {
+        // every kernel below early-exits on a device flag when it is not needed
+        if (lower_fast) {
+            DGC_TRY(lower());
+            DGC_TRY(pass(grid_gs));
+        } else {
+            for (int i = 0; i < p->max_iters; ++i) DGC_TRY(pass(grid_gs));
+        }
+        if (p->resample) DGC_TRY(resample());
     }
     EmitOut o{p->update_memory ? vec : nullptr, (p->update_memory && p->masking) ? mmt : nullptr, values,
               indices, p->vdtype, p->idtype};
@@ -627,19 +750,18 @@ int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p
 static size_t kth_ws_bytes(int64_t n) { return n <= kSmallN ? 256 : align_up(sizeof(RSState), 256); }
 
 int kth_largest(const float* x, int64_t n, int64_t k, float* out, void* ws, size_t ws_bytes,
-                hipStream_t s, const int32_t* gate = nullptr) {
+                hipStream_t s) {
     if (!x || !out || n < 1 || k < 1 || k > n)
         DGC_FAIL(DGC_ERR_INVALID, "dgc_kth_largest: need 1 <= k <= n (k=%lld n=%lld)", (long long)k,
                  (long long)n);
-    if (n <= kSmallN && !gate) {
+    if (n <= kSmallN) {
         hipLaunchKernelGGL(k_rs_small, dim3(1), dim3(kScanThreads), 0, s, x, n, (uint64_t)k, out);
         DGC_LAUNCHED();
         return DGC_OK;
     }
     if (!ws || ws_bytes < sizeof(RSState) || (reinterpret_cast<uintptr_t>(ws) & 255))
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_kth_largest: workspace needs %zu bytes", sizeof(RSState));
-    return radix_select_launch(DenseKeys{x, n}, n, (uint64_t)k, out, reinterpret_cast<RSState*>(ws),
-                               gate, s);
+    return radix_select_launch(DenseKeys{x, n}, n, (uint64_t)k, out, reinterpret_cast<RSState*>(ws), s);
 }
 
 // ------------------------------------------------------------------ fused compress

@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-numel", type=float, default=2e8, help="CPU-baseline sample size")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
     return ap.parse_args()
 
 
@@ -100,7 +101,8 @@ def main():
     for i in range(args.warmup):
         bucket.step(grads[i % 2], out)
     torch.cuda.synchronize()
-    evs = [{p: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for p in phases}
+    timed = phases if args.phases else ("compensate", "allgather")
+    evs = [{p: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for p in timed}
            for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -115,7 +117,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    ms = {p: sum(e[p][0].elapsed_time(e[p][1]) for e in evs) / args.steps for p in phases}
+    ms = {p: sum(e[p][0].elapsed_time(e[p][1]) for e in evs) / args.steps for p in timed}
     info = bucket.last_info()
     ms_step = elapsed * 1e3 / args.steps
     k, S = bucket.k, bucket.num_samples
