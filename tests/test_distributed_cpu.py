@@ -1,0 +1,45 @@
+"""World-size-2 gloo tests on CPU: the drop-in DistributedOptimizer, the packed
+sparse allgather (communicate / synchronize) and dgc.comm collectives, checked
+against the weights the REFERENCE produced for the same 3 training steps
+(tests/golden/optimizer.npz)."""
+import os
+
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+import dist_helpers as H
+
+
+def run(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = H.free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    out = {}
+    while not q.empty():
+        rank, res = q.get()
+        out[rank] = res
+    assert sorted(out) == list(range(world))
+    return out
+
+
+@pytest.mark.timeout(300)
+def test_distributed_optimizer_matches_reference_weights():
+    out = run(H.optimizer_worker, 2, os.path.join(GOLDEN, "optimizer.npz"))
+    for rank, mismatches in out.items():
+        assert mismatches == [], (rank, mismatches)
+
+
+@pytest.mark.timeout(300)
+def test_comm_collectives_gloo():
+    out = run(H.comm_worker, 2)
+    for rank, (gathered, avg, sm, (size, rk)) in out.items():
+        assert gathered == [0.0, 1.0, 10.0, 11.0, 12.0]       # rank order, ragged rows
+        assert avg == [1.5, 1.5, 1.5] and sm == [3.0, 3.0]
+        assert size == 2 and rk == rank
