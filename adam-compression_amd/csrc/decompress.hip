@@ -162,7 +162,7 @@ k_bounds(DecWS w, RunSrc rs, int64_t n, int max_runs) {
 }
 
 // ---------------------------------------------------------------- chunk scatter
-constexpr int kStage = 2048;   // staged entries per chunk (avg 4*W at ratio 0.001)
+constexpr int kStage = 512;    // staged entries per chunk (avg 4*W at ratio 0.001); LDS ~21 KB -> 7 blocks/CU
 
 __device__ __forceinline__ int lower_bound_lds(const int* a, int lo, int hi, int key) {
     while (lo < hi) {

@@ -77,6 +77,22 @@ def cpu_baseline(numel, ratio, steps):
                       f"{dt * 1e3:.1f} ms/step on {threads} threads; {model}"}
 
 
+def pmc_traffic(kernel_key="k_compensate4"):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC profile
+    of this bench (tools/gpu_check.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes; FETCH_SIZE x2 for gfx950's half count of wide reads, KB x 1024)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", "pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if kernel_key in k:
+            return v["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], REPO)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,6 +141,7 @@ def main():
     k1_bytes = 20 * N + 4 * bucket.cnt            # read g, mmt, vec; write mmt, vec; write samples
     k1_gbs = k1_bytes / (ms["compensate"] * 1e-3) / 1e9
     payload = bucket.rank_stride
+    traffic, traffic_src = pmc_traffic()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -149,7 +166,8 @@ def main():
                    "wire": "fp32 values / int64 indices", "parallelism": f"dp{world}"},
         "roofline": {"kernel": "K1 compensate+sample (k_compensate4)", "bound": "hbm",
                      "achieved": k1_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k1_gbs / HBM_PEAK_GBS,
-                     "traffic": None, "algorithmic_bytes_per_launch": k1_bytes,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": k1_bytes,
                      "avg_launch_ms": ms["compensate"]},
         "step_hbm": {"algorithmic_bytes_per_rank": step_bytes,
                      "achieved_GBs": step_bytes / (ms_step * 1e-3) / 1e9,
