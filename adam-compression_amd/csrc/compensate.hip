@@ -20,47 +20,6 @@
 
 namespace dgc {
 
-struct SampleSpec {
-    float* out;        // nullptr: no sampling
-    int64_t start;
-    int64_t stride;    // >= 4 on the fused path
-    int64_t count;     // ceil((n - start) / stride)
-    double inv_stride; // 1.0 / stride
-};
-
-// floor/mod of d by s for |d| < 2^53 without a 64-bit integer divide: a double
-// estimate, then an exact integer correction.
-__device__ __forceinline__ void floor_divmod_fast(int64_t d, int64_t s, double inv, int64_t& q, int64_t& r) {
-    q = (int64_t)floor((double)d * inv);
-    r = d - q * s;
-    while (r < 0) {
-        r += s;
-        q -= 1;
-    }
-    while (r >= s) {
-        r -= s;
-        q += 1;
-    }
-}
-
-template <bool NEST, bool ACC>
-__device__ __forceinline__ float comp1(float g, float& m, float& v, float mom) {
-    if (NEST) {
-        m = __fmul_rn(__fadd_rn(m, g), mom);
-        if (ACC) {
-            v = __fadd_rn(__fadd_rn(v, m), g);
-            return v;
-        }
-        return __fadd_rn(m, g);
-    }
-    m = __fadd_rn(__fmul_rn(m, mom), g);
-    if (ACC) {
-        v = __fadd_rn(v, m);
-        return v;
-    }
-    return m;
-}
-
 
 // Vector path: all pointers 16-B aligned. One-shot chunks (no grid stride): block b
 // owns float4 [256b, 256b + 256), lanes contiguous, non-temporal 16-B loads and
@@ -160,6 +119,14 @@ k_mask(float* __restrict__ mmt, float* __restrict__ vec, const I* __restrict__ i
         if (mmt) mmt[i] = 0.f;
         vec[i] = 0.f;
     }
+}
+
+int sample_strided_launch(const float* vec, int64_t start, int64_t stride, int64_t count, float* out,
+                          hipStream_t s) {
+    if (count <= 0) return DGC_OK;
+    hipLaunchKernelGGL(k_sample_strided, dim3(grid_for(count)), dim3(kBlock), 0, s, vec, start, stride, count, out);
+    DGC_LAUNCHED();
+    return DGC_OK;
 }
 
 template <bool NEST, bool ACC>

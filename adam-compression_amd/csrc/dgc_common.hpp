@@ -135,3 +135,51 @@ __device__ __forceinline__ void st_nt(float4* p, const float4& v) {
     __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
 }
 }  // namespace dgc
+
+namespace dgc {
+// Strided sample of |vec| fused into K1 (dgc/compression.py:113,119).
+struct SampleSpec {
+    float* out;        // nullptr: no sampling
+    int64_t start;
+    int64_t stride;    // >= 4 on the fused path
+    int64_t count;     // ceil((n - start) / stride)
+    double inv_stride; // 1.0 / stride
+};
+
+// floor/mod of d by s for |d| < 2^53 without a 64-bit integer divide: a double
+// estimate, then an exact integer correction.
+__device__ __forceinline__ void floor_divmod_fast(int64_t d, int64_t s, double inv, int64_t& q, int64_t& r) {
+    q = (int64_t)floor((double)d * inv);
+    r = d - q * s;
+    while (r < 0) {
+        r += s;
+        q -= 1;
+    }
+    while (r >= s) {
+        r -= s;
+        q += 1;
+    }
+}
+
+// DGCSGDMemory.compensate on one element (dgc/memory.py:50-70), every op rounded
+// to fp32 like the reference's separate ATen add_/mul_ ops (no FMA contraction):
+//   nesterov: m = (m + g) * mom;  v = (v + m) + g      (dense branch: out = m + g)
+//   plain:    m = m * mom + g;    v = v + m            (dense branch: out = m)
+template <bool NEST, bool ACC>
+__device__ __forceinline__ float comp1(float g, float& m, float& v, float mom) {
+    if (NEST) {
+        m = __fmul_rn(__fadd_rn(m, g), mom);
+        if (ACC) {
+            v = __fadd_rn(__fadd_rn(v, m), g);
+            return v;
+        }
+        return __fadd_rn(m, g);
+    }
+    m = __fadd_rn(__fmul_rn(m, mom), g);
+    if (ACC) {
+        v = __fadd_rn(v, m);
+        return v;
+    }
+    return m;
+}
+}  // namespace dgc

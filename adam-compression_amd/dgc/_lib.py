@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get(
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libdgc_hip.so"))
 
 DGC_OK = 0
+SPEC_MARGIN = 0.8      # speculative list threshold = 0.8 x the previous final threshold
 SYNC_DEVICE, SYNC_HOST = 0, 1
 VD = {torch.float32: 0, torch.float16: 1}
 ID = {torch.int64: 0, torch.int32: 1}
@@ -34,7 +35,7 @@ class SelectInfo(ctypes.Structure):
     _fields_ = [("count", ctypes.c_int64), ("candidates", ctypes.c_int64),
                 ("threshold0", ctypes.c_float), ("threshold", ctypes.c_float),
                 ("branch", ctypes.c_int32), ("recounts", ctypes.c_int32),
-                ("overflow_segments", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("overflow_segments", ctypes.c_int32), ("full_passes", ctypes.c_int32)]
 
 
 INFO_BYTES = ctypes.sizeof(SelectInfo)
@@ -59,7 +60,11 @@ _SIGNATURES = {
                                   _I32, _P]),
     "dgc_compress_workspace": (_SZ, [_I64, _I64, _I64]),
     "dgc_compress": (ctypes.c_int, [_P, _P, _P, _F, _I32, _I64, _I64, _I64, ctypes.POINTER(SelectParams),
-                                    _P, _P, _P, _P, _P, _SZ, _I32, _P]),
+                                    _P, _F, _P, _P, _P, _P, _P, _SZ, _I32, _P]),
+    "dgc_compress_begin": (ctypes.c_int, [_P, _P, _P, _F, _I32, _I64, _I64, ctypes.POINTER(SelectParams), _P, _P,
+                                          _SZ, _P]),
+    "dgc_compress_finish": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, ctypes.POINTER(SelectParams), _P, _F, _P, _P,
+                                           _P, _P, _P, _SZ, _I32, _P]),
     "dgc_decompress_workspace": (_SZ, [_I64, _I32]),
     "dgc_decompress": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, ctypes.POINTER(ctypes.c_int64), _I32, _P,
                                       _I64, _F, _P, _SZ, _P]),

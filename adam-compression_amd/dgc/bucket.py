@@ -16,6 +16,7 @@ The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
 kernels); the sample start is drawn from a ``random.Random`` seeded identically on
 every rank, one draw per step, like the reference's global ``random`` call.
 """
+import ctypes
 import math
 import random
 
@@ -67,11 +68,9 @@ class DGCBucket:
         self.vec = torch.zeros(N, dtype=torch.float32, device=dev)
         L = _lib.lib()
         self.sampled = N != self.num_samples
-        self.samples = torch.empty(self.num_samples + 2 if self.sampled else 1, dtype=torch.float32, device=dev)
-        self.thr = torch.empty(64, dtype=torch.float32, device=dev)
-        n_thr = self.num_samples + 1 if self.sampled else N
-        self.kth_ws = torch.empty(max(256, L.dgc_kth_largest_workspace(n_thr)), dtype=torch.uint8, device=dev)
-        self.sel_ws = torch.empty(L.dgc_select_workspace(N, self.k), dtype=torch.uint8, device=dev)
+        self.ws = torch.empty(L.dgc_compress_workspace(N, self.k, self.num_samples), dtype=torch.uint8,
+                              device=dev)
+        self.spec = torch.full((2,), float("inf"), dtype=torch.float32, device=dev)
         self.info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
         self.rank_stride, self.voff, self.ioff = _layout(self.k, self.vdtype, self.idtype)
         self.payload = torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev)
@@ -83,36 +82,24 @@ class DGCBucket:
 
     # ---------------------------------------------------------------- phases
     def compensate(self, grad):
-        """K1 with the strided sample fused in; returns the sample count L."""
+        """K1: compensate + fused strided sample + speculative candidate lists."""
         L = self._L
-        N = self.numel
-        if self.sampled:
-            self.start = self.rng.randint(0, self.stride - 1)
-            cnt = (N - self.start + self.stride - 1) // self.stride
-        else:
-            self.start, cnt = 0, 0
-        _lib.check(L.dgc_compensate(grad.data_ptr(), self.mmt.data_ptr(), self.vec.data_ptr(), None, N,
-                                    self.momentum, int(self.nesterov), 1,
-                                    self.samples.data_ptr() if self.sampled else None, self.start, self.stride,
-                                    cnt, _lib.stream_of(self.device)), "dgc_compensate")
-        self.cnt = cnt if self.sampled else N
-        return self.cnt
-
-    def threshold(self):
-        L = self._L
-        src = self.samples if self.sampled else self.vec
-        _lib.check(L.dgc_kth_largest(src.data_ptr(), self.cnt, self.top_k_samples, self.thr.data_ptr(),
-                                     self.kth_ws.data_ptr(), self.kth_ws.numel(), _lib.stream_of(self.device)),
-                   "dgc_kth_largest")
+        self.start = self.rng.randint(0, self.stride - 1) if self.sampled else 0
+        _lib.check(L.dgc_compress_begin(grad.data_ptr(), self.mmt.data_ptr(), self.vec.data_ptr(), self.momentum,
+                                        int(self.nesterov), self.start, self.stride, ctypes.byref(self.params),
+                                        self.spec.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                        _lib.stream_of(self.device)), "dgc_compress_begin")
+        self.cnt = (self.numel - self.start + self.stride - 1) // self.stride if self.sampled else self.numel
 
     def select(self):
+        """K3 threshold + K4 selection / adaptation / resample / emit + masking, into the payload."""
         L = self._L
         base = self.payload.data_ptr()
-        import ctypes
-        _lib.check(L.dgc_select(self.vec.data_ptr(), self.mmt.data_ptr(), self.thr.data_ptr(),
-                                ctypes.byref(self.params), base + self.voff, base + self.ioff, base,
-                                self.info.data_ptr(), self.sel_ws.data_ptr(), self.sel_ws.numel(),
-                                _lib.SYNC_DEVICE, _lib.stream_of(self.device)), "dgc_select")
+        _lib.check(L.dgc_compress_finish(self.vec.data_ptr(), self.mmt.data_ptr(), self.start, self.stride,
+                                         self.top_k_samples, ctypes.byref(self.params), self.spec.data_ptr(),
+                                         _lib.SPEC_MARGIN, base + self.voff, base + self.ioff, base,
+                                         self.info.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                         _lib.SYNC_DEVICE, _lib.stream_of(self.device)), "dgc_compress_finish")
 
     def exchange(self):
         if self.world > 1:
@@ -129,9 +116,8 @@ class DGCBucket:
         """compensate -> threshold -> select -> allgather -> decompress; ``events`` maps a
         phase name to a (start, end) pair of torch.cuda.Event recorded around it."""
         ev = events or {}
-        for name, fn in (("compensate", lambda: self.compensate(grad)), ("threshold", self.threshold),
-                         ("select", self.select), ("allgather", self.exchange),
-                         ("decompress", lambda: self.decompress(out))):
+        for name, fn in (("compensate", lambda: self.compensate(grad)), ("select", self.select),
+                         ("allgather", self.exchange), ("decompress", lambda: self.decompress(out))):
             pair = ev.get(name)
             if pair:
                 pair[0].record()
@@ -144,4 +130,4 @@ class DGCBucket:
         i = _lib.SelectInfo.from_buffer_copy(raw)
         return dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
                     branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
-                    overflow_segments=i.overflow_segments)
+                    overflow_segments=i.overflow_segments, full_passes=i.full_passes)

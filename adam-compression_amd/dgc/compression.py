@@ -98,6 +98,7 @@ class DGCCompressor:
         self._ws = _lib.Workspace()
         self._params = {}
         self._payloads = {}
+        self._spec = {}        # name -> device float: speculative list threshold (dgc_compress)
 
     # ------------------------------------------------------------------ host math
     @staticmethod
@@ -133,7 +134,8 @@ class DGCCompressor:
             top_k_samples = int(math.ceil(samples * self.compress_ratio))
             num_selects = int(math.ceil(numel * self.compress_ratio))
             self.attributes[name] = (numel, shape, num_selects, samples, top_k_samples, stride)
-            self._params.pop(name, None)
+            self._params = {key: v for key, v in self._params.items() if key[0] != name}
+            self._spec.pop(name, None)
             if comm.rank() == 0:
                 how = f"at stride {stride}" if self.strided_sample else "uniformly"
                 print(f"   {name:<25}: transmit {num_selects} / {numel} elements of shape {shape}\n"
@@ -261,13 +263,16 @@ class DGCCompressor:
                 L = _lib.lib()
                 wsz = L.dgc_compress_workspace(numel, k, S)
                 ws = self._ws.get(dev, wsz, name)
+                spec = self._spec.get(name)
+                if spec is None or spec.device != dev:
+                    spec = self._spec[name] = torch.full((2,), float("inf"), dtype=torch.float32, device=dev)
                 info = torch.empty(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
                 base = payload.data_ptr()
                 voff, ioff = lay[4], lay[5]
                 _lib.check(L.dgc_compress(_lib.ptr(grad), _lib.ptr(mmt), _lib.ptr(vec), float(mem.momentum),
-                                          int(bool(mem.nesterov)), start, stride, ks, params,
-                                          base + voff, base + ioff, base, _lib.ptr(info), _lib.ptr(ws), wsz,
-                                          _lib.SYNC_HOST, _lib.stream_of(dev)), "dgc_compress")
+                                          int(bool(mem.nesterov)), start, stride, ks, params, _lib.ptr(spec),
+                                          _lib.SPEC_MARGIN, base + voff, base + ioff, base, _lib.ptr(info),
+                                          _lib.ptr(ws), wsz, _lib.SYNC_HOST, _lib.stream_of(dev)), "dgc_compress")
                 n = int(payload[:8].view(torch.int64).item())
                 values, indices = self._views(payload, lay, n)
                 self._last_info = info
@@ -291,7 +296,8 @@ class DGCCompressor:
         info = _lib.SelectInfo.from_buffer_copy(raw)
         return dict(count=info.count, candidates=info.candidates, threshold0=info.threshold0,
                     threshold=info.threshold, branch=_lib.BRANCHES.get(info.branch, info.branch),
-                    recounts=info.recounts, overflow_segments=info.overflow_segments)
+                    recounts=info.recounts, overflow_segments=info.overflow_segments,
+                    full_passes=info.full_passes)
 
     def decompress(self, tensor, ctx):
         """dgc/compression.py:179-198."""

@@ -77,7 +77,7 @@ def cpu_baseline(numel, ratio, steps):
                       f"{dt * 1e3:.1f} ms/step on {threads} threads; {model}"}
 
 
-def pmc_traffic(kernel_key="k_compensate4"):
+def pmc_traffic(kernel_key="k_compensate_list"):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC profile
     of this bench (tools/gpu_check.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
     passes; FETCH_SIZE x2 for gfx950's half count of wide reads, KB x 1024)."""
@@ -113,7 +113,7 @@ def main():
         grads.append(torch.randn(N, generator=gen, device=dev))
     out = torch.empty(N, device=dev)
 
-    phases = ("compensate", "threshold", "select", "allgather", "decompress")
+    phases = ("compensate", "select", "allgather", "decompress")
     for i in range(args.warmup):
         bucket.step(grads[i % 2], out)
     torch.cuda.synchronize()
@@ -164,7 +164,8 @@ def main():
                    "numel": N, "compress_ratio": args.ratio, "num_selects": k, "num_samples": S,
                    "sample_stride": bucket.stride, "nesterov": True, "momentum": 0.9, "momentum_masking": True,
                    "wire": "fp32 values / int64 indices", "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "K1 compensate+sample (k_compensate4)", "bound": "hbm",
+        "roofline": {"kernel": "K1 compensate + fused sample + speculative lists (k_compensate_list)",
+                     "bound": "hbm",
                      "achieved": k1_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k1_gbs / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": k1_bytes,

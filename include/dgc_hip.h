@@ -98,7 +98,7 @@ typedef struct dgc_select_info {
     int32_t branch;           /* enum dgc_branch                            */
     int32_t recounts;         /* adaptation recounts executed               */
     int32_t overflow_segments;/* segments whose candidate list spilled      */
-    int32_t reserved;
+    int32_t full_passes;      /* full re-reads of vec (0: served by the K1 lists) */
 } dgc_select_info;
 
 const char* dgc_last_error(void);
@@ -142,13 +142,31 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
                dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
                void* stream);
 
-/* ---- fused compress: compensate + sample + threshold + select ---- */
+/* ---- fused compress: compensate + sample + threshold + select ----
+ * Speculative listing: K1 also lists every element with |vec_new| >= spec_threshold[0]
+ * into the selection workspace. spec_threshold is a device float[2], in/out, per
+ * tensor (NULL = off); initialise both to +inf. When the sampled threshold comes out
+ * >= spec[0] and few segment lists overflowed, every count and selection is served
+ * from the lists and the separate re-read of vec is skipped; otherwise one full pass
+ * runs. Results are identical either way (spec only chooses the work).
+ * On return spec[1] = the final threshold t and spec[0] = spec_margin x t x growth,
+ * growth = t / (previous t) clamped to [1, 1.5] (0.8 is a good margin).
+ * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
+ * one workspace and must see the same sample_start/stride/params. */
 size_t dgc_compress_workspace(int64_t numel, int64_t num_selects, int64_t num_samples);
 int dgc_compress(const float* grad, float* mmt, float* vec, float momentum, int32_t nesterov,
                  int64_t sample_start, int64_t sample_stride, int64_t top_k_samples,
-                 const dgc_select_params* params, void* values_out, void* indices_out,
-                 int64_t* count_out, dgc_select_info* info_out, void* ws, size_t ws_bytes,
-                 int32_t sync_mode, void* stream);
+                 const dgc_select_params* params, float* spec_threshold, float spec_margin,
+                 void* values_out, void* indices_out, int64_t* count_out, dgc_select_info* info_out,
+                 void* ws, size_t ws_bytes, int32_t sync_mode, void* stream);
+int dgc_compress_begin(const float* grad, float* mmt, float* vec, float momentum, int32_t nesterov,
+                       int64_t sample_start, int64_t sample_stride, const dgc_select_params* params,
+                       const float* spec_threshold, void* ws, size_t ws_bytes, void* stream);
+int dgc_compress_finish(float* vec, float* mmt, int64_t sample_start, int64_t sample_stride,
+                        int64_t top_k_samples, const dgc_select_params* params, float* spec_threshold,
+                        float spec_margin, void* values_out, void* indices_out, int64_t* count_out,
+                        dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
+                        void* stream);
 
 /* ---- K6: deterministic decompress ----
  * grad[0..n) = scale * (rank-order sequential sum of the entries), every other

@@ -24,6 +24,7 @@ from dgc.compression import DGCCompressor, _Gathered  # noqa: E402
 from dgc.comm import Average  # noqa: E402
 from dgc.memory import DGCSGDMemory  # noqa: E402
 from oracle import dgc_oracle as O  # noqa: E402
+from models import ResNet20, TinyNet  # noqa: E402
 
 
 def free_port():
@@ -85,18 +86,6 @@ class OracleDGCCompressor(DGCCompressor):
         return self.memory.compensate(tensor, name, accumulate=False)
 
 
-class TinyNet(torch.nn.Module):
-    """The model of tests/golden/make_goldens.py::gen_optimizer."""
-
-    def __init__(self):
-        super().__init__()
-        self.fc1 = torch.nn.Linear(64, 128)
-        self.fc2 = torch.nn.Linear(128, 10)
-
-    def forward(self, x):
-        return self.fc2(torch.relu(self.fc1(x)))
-
-
 def optimizer_worker(rank, world, port, golden_path, queue):
     """One rank of the reference's DistributedOptimizer + DGCSGD + DGC training loop,
     checked step by step against the weights the reference produced."""
@@ -137,6 +126,75 @@ def optimizer_worker(rank, world, port, golden_path, queue):
                 if not np.array_equal(p.detach().numpy().view(np.uint32), want.view(np.uint32)):
                     mismatches.append((s, n, float(np.abs(p.detach().numpy() - want).max())))
         queue.put((rank, mismatches))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        queue.put((rank, [("error", repr(e))]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _digest(model):
+    import hashlib
+    h = hashlib.sha256()
+    for _, p in model.named_parameters():
+        h.update(p.detach().numpy().tobytes())
+    return h.hexdigest()
+
+
+def resnet20_worker(rank, world, port, golden_dir, queue):
+    """BASELINE.json configs[0] on the product plumbing: ResNet-20, DGC ratio 0.001 with
+    5-epoch warmup, fp16 values, int32 indices, 2 gloo ranks (horovodrun -np 2 in the
+    reference). Compared with the reference's per-step parameter digests and final
+    weights (tests/golden/optimizer_resnet20.*)."""
+    import contextlib
+    import io
+    import json
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dgc.horovod import DistributedOptimizer
+        from dgc.optim import DGCSGD
+        meta = json.load(open(os.path.join(golden_dir, "optimizer_resnet20.json")))
+        final = np.load(os.path.join(golden_dir, "optimizer_resnet20.npz"))
+        torch.manual_seed(meta["model_seed"])
+        model = ResNet20()
+        problems = [] if _digest(model) == meta["init_digest"] else [("init", "digest")]
+        opt = DGCSGD(model.parameters(), lr=meta["lr"], momentum=meta["momentum"],
+                     weight_decay=meta["weight_decay"], nesterov=meta["nesterov_sgd"])
+        mem = OracleMemory(momentum=meta["momentum"])
+        with contextlib.redirect_stdout(io.StringIO()):
+            comp = OracleDGCCompressor(meta["ratio"], memory=mem, sample_ratio=meta["sample_ratio"],
+                                       fp16_values=meta["fp16_values"], int32_indices=meta["int32_indices"],
+                                       warmup_epochs=meta["warmup_epochs"])
+            mem.initialize(model.named_parameters())
+            comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                    backward_passes_per_step=1, op=Average)
+        random.seed(meta["random_seed"])
+        spe, batch, s = meta["steps_per_epoch"], meta["batch"], 0
+        for ei, e in enumerate((0, 1, 5)):
+            with contextlib.redirect_stdout(io.StringIO()):
+                comp.warmup_compress_ratio(e)
+            if comp.compress_ratio != meta["epoch_ratios"][ei]:
+                problems.append(("ratio", e, comp.compress_ratio))
+            for _ in range(spe):
+                gen = torch.Generator().manual_seed(1900 + 10 * s + rank)
+                x = torch.randn(batch, 3, 32, 32, generator=gen)
+                y = torch.randint(0, 10, (batch,), generator=gen)
+                torch.nn.functional.cross_entropy(model(x), y).backward()
+                dopt.step()
+                dopt.zero_grad()
+                if _digest(model) != meta["step_digests"][s][rank]:
+                    problems.append(("step", s))
+                s += 1
+        for n, p in model.named_parameters():
+            want = final[f"final/{n}"]
+            if not np.array_equal(p.detach().numpy().view(np.uint32), want.view(np.uint32)):
+                problems.append(("final", n, float(np.abs(p.detach().numpy() - want).max())))
+        queue.put((rank, problems))
     except Exception as e:  # pragma: no cover - reported to the parent
         queue.put((rank, [("error", repr(e))]))
     finally:

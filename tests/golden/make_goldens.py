@@ -31,7 +31,9 @@ REF = "/root/reference"
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(HERE))
 from oracle import synth  # noqa: E402
+from models import ResNet20, TinyNet  # noqa: E402
 
 
 # ------------------------------------------------------------------ horovod stub
@@ -322,16 +324,6 @@ def gen_decompress(C, M, rec):
         json.dump(meta, f, indent=1)
 
 
-class TinyNet(torch.nn.Module):
-    def __init__(self):
-        super().__init__()
-        self.fc1 = torch.nn.Linear(64, 128)
-        self.fc2 = torch.nn.Linear(128, 10)
-
-    def forward(self, x):
-        return self.fc2(torch.relu(self.fc1(x)))
-
-
 def gen_optimizer(C, M, H, O):
     """The reference's DistributedOptimizer + DGCSGD + DGCCompressor, 2 ranks emulated
     in one process. Records the weights after every step."""
@@ -386,14 +378,95 @@ def gen_optimizer(C, M, H, O):
     print(f"optimizer: {steps} steps, replicas bit-identical: {same}")
 
 
-def main():
+def _digest(model):
+    import hashlib
+    h = hashlib.sha256()
+    for _, p in model.named_parameters():
+        h.update(p.detach().numpy().tobytes())
+    return h.hexdigest()
+
+
+def gen_optimizer_resnet20(C, M, H, O):
+    """BASELINE.json configs[0]: ResNet-20 / CIFAR-shaped batches with the reference's
+    configs/cifar + configs/dgc + wm5 + fp16 + int32 settings (SGD lr 0.1, momentum
+    0.9, wd 1e-4, no Nesterov; DGC ratio 0.001, sample 0.01, warmup 5 epochs,
+    fp16 values, int32 indices), 2 ranks emulated in one process, 2 steps in each of
+    epochs 0, 1 and 5 (ratios 0.316, 0.1, 0.001) with warmup_compress_ratio(epoch)
+    called at each epoch start as train.py:203-208 does. Stores per-step SHA-256 digests of every rank's parameters and the final
+    weights (replicas are bit-identical)."""
+    torch.set_num_threads(1)
+    W, epochs, spe, batch = 2, (0, 1, 5), 2, 8
+    _World.size = W
+    ranks = []
+    for q in range(W):
+        _World.rank = q
+        torch.manual_seed(11)
+        model = ResNet20()
+        opt = O.DGCSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=False)
+        mem = M.DGCSGDMemory(momentum=0.9)
+        comp = _quiet(C.DGCCompressor, 0.001, memory=mem, sample_ratio=0.01, fp16_values=True,
+                      int32_indices=True, warmup_epochs=5)
+        _quiet(mem.initialize, model.named_parameters())
+        _quiet(comp.initialize, [(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+        dopt = H.DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                      backward_passes_per_step=1, op="Average")
+        ranks.append((model, dopt, comp))
+    random.seed(42)
+    digests, ratios = [], []
+    for ei, e in enumerate(epochs):
+        for q, (_, _, comp) in enumerate(ranks):
+            _World.rank = q
+            _quiet(comp.warmup_compress_ratio, e)
+        ratios.append(ranks[0][2].compress_ratio)
+        for t in range(spe):
+            s = ei * spe + t
+            _World.registry.clear()
+            _World.reduced.clear()
+            rstate = random.getstate()
+            for q, (model, dopt, comp) in enumerate(ranks):
+                _World.rank = q
+                random.setstate(rstate)
+                gen = torch.Generator().manual_seed(1900 + 10 * s + q)
+                x = torch.randn(batch, 3, 32, 32, generator=gen)
+                y = torch.randint(0, 10, (batch,), generator=gen)
+                loss = torch.nn.functional.cross_entropy(model(x), y)
+                loss.backward()
+            for q, (model, dopt, comp) in enumerate(ranks):
+                _World.rank = q
+                dopt.step()
+                dopt.zero_grad()
+            digests.append([_digest(m) for m, _, _ in ranks])
+    arrays = {f"final/{n}": p.detach().numpy().copy() for n, p in ranks[0][0].named_parameters()}
+    torch.manual_seed(11)
+    init_digest = _digest(ResNet20())
+    np.savez_compressed(os.path.join(HERE, "optimizer_resnet20.npz"), **arrays)
+    with open(os.path.join(HERE, "optimizer_resnet20.json"), "w") as f:
+        json.dump(dict(W=W, epochs=epochs, steps_per_epoch=spe, batch=batch, lr=0.1, momentum=0.9,
+                       weight_decay=1e-4, nesterov_sgd=False, ratio=0.001, sample_ratio=0.01, warmup_epochs=5,
+                       fp16_values=True, int32_indices=True, model_seed=11, random_seed=42,
+                       data_seed="1900 + 10*step + rank", epoch_ratios=ratios, init_digest=init_digest,
+                       step_digests=digests), f, indent=1)
+    same = all(a == b for a, b in digests)
+    print(f"optimizer_resnet20: {len(epochs) * spe} steps, ratios {ratios}, replicas bit-identical: {same}")
+
+
+GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20")
+
+
+def main(which=GENERATORS):
     C, M, H, O = _import_reference()
     rec = _Recorder()
-    gen_attributes(C)
-    gen_compress(C, M, rec)
-    gen_decompress(C, M, rec)
-    gen_optimizer(C, M, H, O)
+    if "attributes" in which:
+        gen_attributes(C)
+    if "compress" in which:
+        gen_compress(C, M, rec)
+    if "decompress" in which:
+        gen_decompress(C, M, rec)
+    if "optimizer" in which:
+        gen_optimizer(C, M, H, O)
+    if "optimizer_resnet20" in which:
+        gen_optimizer_resnet20(C, M, H, O)
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or GENERATORS)

@@ -37,6 +37,14 @@ def test_distributed_optimizer_matches_reference_weights():
 
 
 @pytest.mark.timeout(300)
+def test_resnet20_config0_matches_reference():
+    """BASELINE configs[0]: ResNet-20, ratio 0.001, warmup 5, fp16 values, int32 indices, 2 ranks."""
+    out = run(H.resnet20_worker, 2, GOLDEN)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)
+
+
+@pytest.mark.timeout(300)
 def test_comm_collectives_gloo():
     out = run(H.comm_worker, 2)
     for rank, (gathered, avg, sm, (size, rk)) in out.items():

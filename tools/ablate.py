@@ -3,10 +3,8 @@
   python tools/ablate.py [--numel 1e9]
 
 Times, with HIP events on the current stream, 10 reps each:
-  * dgc_select with / without the memory update (masking writes);
-  * dgc_kth_largest over the 1B bucket's strided samples;
+  * dgc_compress_begin (K1 + sample + speculative lists) and dgc_compress_finish;
   * dgc_decompress_packed at W = 1, 2, 4, 8 (synthetic ascending payloads);
-  * dgc_compensate (K1) alone.
 """
 import argparse
 import ctypes
@@ -47,26 +45,7 @@ def main():
     out = torch.empty(N, device=dev)
     res = {}
     res["k1_ms"] = timeit(lambda: b.compensate(g))
-    b.compensate(g)
-    res["threshold_ms"] = timeit(b.threshold)
-    b.threshold()
-    vec0, mmt0 = b.vec.clone(), b.mmt.clone()
-
-    def sel(update):
-        b.params.update_memory = update
-        b.vec.copy_(vec0)
-        b.mmt.copy_(mmt0)
-        torch.cuda.synchronize()
-        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        b.select()
-        e.record()
-        torch.cuda.synchronize()
-        return a.elapsed_time(e)
-
-    for upd in (1, 0, 1, 0):
-        res.setdefault(f"select_update{upd}_ms", []).append(sel(upd))
-    b.params.update_memory = 1
+    res["finish_ms"] = timeit(b.select)        # threshold + selection + emit (lists from K1)
     res["selection"] = b.last_info()
     k = b.k
     stride, voff, ioff = b.rank_stride, b.voff, b.ioff

@@ -31,7 +31,7 @@ def main():
     shutil.copy(stats, f"{out}/kernel_stats.csv")
     trace = glob.glob(f"{prof}/**/*kernel_trace.csv", recursive=True)[0]
     tr = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(tr) if "k_compensate4" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(tr) if "k_compensate_list" in r["Kernel_Name"]]
     with open(f"{out}/step_timeline.txt", "w") as f:
         i0, i1 = idx[-2], idx[-1]
         prev = None

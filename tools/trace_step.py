@@ -8,7 +8,7 @@ d = sys.argv[1]
 min_us = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
 path = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_compensate4" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if "k_compensate_list" in r["Kernel_Name"]]
 i0, i1 = idx[-2], idx[-1]
 prev = None
 small = 0.0
