@@ -52,8 +52,8 @@ k_compensate4(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __
         // element 4v+j is a sample iff (r + j) % stride == 0, with r = (r0 + 4*tid) mod stride
         const uint32_t t = (uint32_t)r0 + 4u * threadIdx.x;
         const uint32_t s32 = (uint32_t)sp.stride;
-        const uint32_t q1 = t / s32;
-        const uint32_t r = t - q1 * s32;
+        uint32_t q1, r;
+        divmod_u32(t, s32, sp.inv_stride_f, q1, r);
         const uint32_t j = r == 0 ? 0u : s32 - r;
         if (j < 4) {
             const int64_t qi = q0 + q1 + (r == 0 ? 0 : 1);
@@ -178,14 +178,14 @@ int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n,
     if (accumulate && out && out != vec)
         DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: accumulate writes vec (out must be NULL or vec)");
     if (!accumulate && !out) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: dense branch needs out");
-    SampleSpec sp{nullptr, 0, 1, 0, 1.0};
+    SampleSpec sp{nullptr, 0, 1, 0, 1.0, 1.0f};
     if (samples) {
         if (!accumulate) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: sampling needs accumulate=1");
         if (s_stride < 1 || s_start < 0 || s_start >= n)
             DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: bad sample start/stride");
         if (s_count != ceil_div(n - s_start, s_stride))
             DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate: num_samples must be ceil((n-start)/stride)");
-        sp = SampleSpec{samples, s_start, s_stride, s_count, 1.0 / (double)s_stride};
+        sp = SampleSpec{samples, s_start, s_stride, s_count, 1.0 / (double)s_stride, 1.0f / (float)s_stride};
         if (s_stride < 4) {
             // tiny strides (sample_ratio >= 0.25): unfused, samples read back after the pass
             DGC_TRY(compensate(grad, mmt, vec, out, n, momentum, nesterov, accumulate, nullptr, 0,

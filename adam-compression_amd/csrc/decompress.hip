@@ -181,7 +181,10 @@ __device__ __forceinline__ int lower_bound_lds(const int* a, int lo, int hi, int
 // all of its occurrences in run order, from +0.0 — the sequential index_put_
 // order — into the LDS tile; phase 3 scales and writes the tile with 16-B stores.
 // Chunks with more than kStage entries fall back to one barrier per run.
-template <int VD, int ID>
+// DENSE = false (sparse scatter): grad already holds +0.0 everywhere (zeroed by the
+// caller, e.g. on a side stream while the compress and the allgather run), so only
+// the indices present are written: the same sums, scaled, with no tile write.
+template <int VD, int ID, bool DENSE>
 __global__ void __launch_bounds__(kBlock)
 k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
     __shared__ __attribute__((aligned(16))) float acc[kChunk];
@@ -201,7 +204,8 @@ k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
         if (w.bnd[tid * stride] > 0 || w.bnd[tid * stride + w.nchunks] < run.count) atomicOr(w.status, 1);
     }
     float4* acc4 = reinterpret_cast<float4*>(acc);
-    for (int j = tid; j < kChunk / 4; j += kBlock) acc4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (DENSE)
+        for (int j = tid; j < kChunk / 4; j += kBlock) acc4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tid < 64) {   // run table for this chunk (nr <= 64: one wave)
         int cnt = 0;
         if (tid < nr) {
@@ -254,9 +258,18 @@ k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
                      p < roff[q + 1] && sidx[p] == i; ++p)
                     a = __fadd_rn(a, sval[p]);
             }
-            acc[i] = a;
+            if (DENSE)
+                acc[i] = a;
+            else
+                grad[base + i] = scale != 1.0f ? __fmul_rn(a, scale) : a;
         }
+        if (!DENSE) return;
     } else {
+        if (!DENSE) {   // rare (> kStage entries in one chunk): accumulate in LDS after all
+            __syncthreads();
+            for (int j = tid; j < kChunk / 4; j += kBlock) acc4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            __syncthreads();
+        }
         for (int r = 0; r < nr; ++r) {
             const long long b0 = rb0[r], b1 = rb0[r] + (roff[r + 1] - roff[r]);
             for (long long e = b0 + tid; e < b1; e += kBlock) {
@@ -276,6 +289,17 @@ k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
                 acc[off] = a;
             }
             __syncthreads();
+        }
+        if (!DENSE) {   // write back the touched slots only (every entry rewrites its own)
+            for (int r = 0; r < nr; ++r) {
+                const long long b0 = rb0[r], b1 = rb0[r] + (roff[r + 1] - roff[r]);
+                for (long long e = b0 + tid; e < b1; e += kBlock) {
+                    const long long off = load_idx<ID>(ridx[r], e) - base;
+                    if (off >= 0 && off < kChunk)
+                        grad[base + off] = scale != 1.0f ? __fmul_rn(acc[off], scale) : acc[off];
+                }
+            }
+            return;
         }
     }
     __syncthreads();
@@ -303,23 +327,31 @@ static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
 
 template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
-                       hipStream_t s) {
+                       bool dense, hipStream_t s) {
     const int64_t work = (int64_t)max_runs * (w.nchunks + 1);
     hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, rs, n, max_runs);
     DGC_LAUNCHED();
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
-    hipLaunchKernelGGL((k_scatter_chunks<VD, ID>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w, rs,
-                       grad, n, scale);
+    if (dense)
+        hipLaunchKernelGGL((k_scatter_chunks<VD, ID, true>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w,
+                           rs, grad, n, scale);
+    else
+        hipLaunchKernelGGL((k_scatter_chunks<VD, ID, false>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w,
+                           rs, grad, n, scale);
     DGC_LAUNCHED();
     return DGC_OK;
 }
 
 static int dispatch_scatter(int vd, int id, const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
-                            float scale, int max_runs, hipStream_t s) {
-    if (vd == DGC_F32 && id == DGC_I64) return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, s);
-    if (vd == DGC_F32 && id == DGC_I32) return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, s);
-    if (vd == DGC_F16 && id == DGC_I64) return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, s);
-    if (vd == DGC_F16 && id == DGC_I32) return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, s);
+                            float scale, int max_runs, hipStream_t s, bool dense = true) {
+    if (vd == DGC_F32 && id == DGC_I64)
+        return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, s);
+    if (vd == DGC_F32 && id == DGC_I32)
+        return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, s);
+    if (vd == DGC_F16 && id == DGC_I64)
+        return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, s);
+    if (vd == DGC_F16 && id == DGC_I32)
+        return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, s);
     DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
 }
 
@@ -385,7 +417,8 @@ int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t*
 }
 
 int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity, int vd,
-                      int id, float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, hipStream_t s) {
+                      int id, float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, hipStream_t s,
+                      bool dense) {
     DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world));
     int64_t voff, ioff;
     const int64_t min_stride = payload_layout(capacity, vd, id, &voff, &ioff);
@@ -394,7 +427,37 @@ int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, i
                  (long long)rank_stride, (long long)min_stride);
     DecWS w = carve_dec(ws, n, world);
     RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world};
-    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, s);
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, s, dense);
+}
+
+// Zero fill with 16-B non-temporal stores (the sparse scatter's precondition).
+__global__ void __launch_bounds__(kBlock) k_fill_zero(float4* __restrict__ x, int64_t n4) {
+    const f4v z = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
+        __builtin_nontemporal_store(z, reinterpret_cast<f4v*>(x) + i);
+}
+
+__global__ void k_fill_zero1(float* __restrict__ x, int64_t begin, int64_t n) {
+    const int64_t i = begin + threadIdx.x;
+    if (i < n) x[i] = 0.f;
+}
+
+int fill_zero(float* x, int64_t n, hipStream_t s) {
+    if (!x || n < 0) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: null buffer or n < 0");
+    if (n == 0) return DGC_OK;
+    if (!aligned16(x)) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: buffer must be 16-B aligned");
+    const int64_t n4 = n / 4;
+    if (n4 > 0) {
+        hipLaunchKernelGGL(k_fill_zero, dim3(grid_for(n4, kBlock, 8192)), dim3(kBlock), 0, s,
+                           reinterpret_cast<float4*>(x), n4);
+        DGC_LAUNCHED();
+    }
+    const int64_t head = n4 * 4;
+    if (head < n) {
+        hipLaunchKernelGGL(k_fill_zero1, dim3(1), dim3(64), 0, s, x, head, n);
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
 }
 
 }  // namespace dgc
@@ -413,6 +476,10 @@ extern "C" int dgc_decompress(const void* values, int32_t vdtype, const void* in
                            ws_bytes, static_cast<hipStream_t>(stream));
 }
 
+extern "C" int dgc_fill_zero(float* x, int64_t n, void* stream) {
+    return dgc::fill_zero(x, n, static_cast<hipStream_t>(stream));
+}
+
 extern "C" int64_t dgc_payload_layout(int64_t capacity, int32_t vdtype, int32_t idtype,
                                       int64_t* values_offset, int64_t* indices_offset) {
     return dgc::payload_layout(capacity, vdtype, idtype, values_offset, indices_offset);
@@ -422,7 +489,14 @@ extern "C" int dgc_decompress_packed(const void* payload, int32_t world, int64_t
                                      int64_t capacity, int32_t vdtype, int32_t idtype, float* grad,
                                      int64_t n, float scale, void* ws, size_t ws_bytes, void* stream) {
     return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
-                                  ws_bytes, static_cast<hipStream_t>(stream));
+                                  ws_bytes, static_cast<hipStream_t>(stream), true);
+}
+
+extern "C" int dgc_scatter_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                                  int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
+                                  ws_bytes, static_cast<hipStream_t>(stream), false);
 }
 
 extern "C" int dgc_decompress_status(const void* ws, int32_t* status, void* stream) {

@@ -144,7 +144,29 @@ struct SampleSpec {
     int64_t stride;    // >= 4 on the fused path
     int64_t count;     // ceil((n - start) / stride)
     double inv_stride; // 1.0 / stride
+    float inv_stride_f;
 };
+
+// q = t / s, r = t % s for 4 <= s < 2^23 and t < 2^24: a float-reciprocal estimate
+// is within one of the quotient (relative error <= 2^-23, |q error| <= 2/s), then
+// one correction step. Larger strides take the integer divide (uniform branch).
+__device__ __forceinline__ void divmod_u32(uint32_t t, uint32_t s, float inv, uint32_t& q, uint32_t& r) {
+    if (s < (1u << 23)) {
+        q = (uint32_t)__fmul_rn((float)t, inv);
+        int32_t rr = (int32_t)(t - q * s);
+        if (rr < 0) {
+            q -= 1;
+            rr += (int32_t)s;
+        } else if (rr >= (int32_t)s) {
+            q += 1;
+            rr -= (int32_t)s;
+        }
+        r = (uint32_t)rr;
+    } else {
+        q = t / s;
+        r = t - q * s;
+    }
+}
 
 // floor/mod of d by s for |d| < 2^53 without a 64-bit integer divide: a double
 // estimate, then an exact integer correction.

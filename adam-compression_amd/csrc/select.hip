@@ -44,7 +44,6 @@ constexpr int kCap = 64;                        // list slots per segment (6.25 
 constexpr int kSegTiles = kSeg / (kWave * 4);   // 4 float4 per lane per segment
 constexpr int kSuper = 4;                       // segments per wave in the full select pass
 constexpr int kGroupSegs = 1024;                // segments per group (1M elements)
-constexpr int kSegPerThread = kGroupSegs / kBlock;   // 4 (emit)
 constexpr int kSegPerBlock4 = kBlock / kWave;        // 4 waves per workgroup
 constexpr int kMaxLower = 16;                   // thresholds per multi-threshold pass
 constexpr int kSpillShards = 64;
@@ -228,8 +227,8 @@ k_compensate_list(const float4* __restrict__ g, float4* __restrict__ mmt, float4
             if (SAMPLE) {
                 const uint32_t t = (uint32_t)r0 + 4u * (uint32_t)(u * 64 + lane);
                 const uint32_t s32 = (uint32_t)sp.stride;
-                const uint32_t q1 = t / s32;
-                const uint32_t r = t - q1 * s32;
+                uint32_t q1, r;
+                divmod_u32(t, s32, sp.inv_stride_f, q1, r);
                 const uint32_t j = r == 0 ? 0u : s32 - r;
                 if (j < 4) {
                     const int64_t qi = q0 + q1 + (r == 0 ? 0 : 1);
@@ -701,23 +700,6 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, int64_t pos, int64_t 
     if (o.mmt) __builtin_nontemporal_store(0.f, o.mmt + gidx);
 }
 
-// Block-wide exclusive scan of one u32 per thread over a 256-thread block.
-__device__ __forceinline__ uint32_t block_exclusive_scan_256(uint32_t v, uint32_t* lds4) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) lds4[wid] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int q = 0; q < wid; ++q) base += lds4[q];
-    __syncthreads();
-    return base + incl - v;
-}
-
 // Wave-cooperative emit of one spilled segment by re-reading vec.
 // FIRSTK: positions base + rank for |x| >= t, kept while < limit.
 __device__ void emit_reread_firstk(const float* __restrict__ vec_in, int64_t n, int64_t seg, long long base,
@@ -784,104 +766,91 @@ __device__ void emit_reread_resample(const float* __restrict__ vec_in, int64_t n
     }
 }
 
-// One workgroup per group (1024 segments), kSegPerThread consecutive segments per
-// thread for complete lists; the group's spilled segments, if any, one wave each.
-__global__ void __launch_bounds__(kBlock)
+// One workgroup per group of kGroupSegs segments, one thread per segment for the
+// in-group offset scan; then wave-per-segment emission: kCap == 64 list slots, so
+// lane l takes list entry l (one coalesced load per list) and ballot ranks give the
+// output positions. Each wave emits 64 consecutive segments, kEmitBatch lists in
+// flight; a spilled segment is re-read from vec by the same wave.
+constexpr int kEmitThreads = kGroupSegs;
+constexpr int kEmitBatch = 8;
+constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
+static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
+
+__global__ void __launch_bounds__(kEmitThreads)
 k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
     const SelState* st = w.st;
-    const int mode = st->branch == DGC_BRANCH_RESAMPLE ? MODE_RESAMPLE : MODE_FIRSTK;
+    const bool rs = st->branch == DGC_BRANCH_RESAMPLE;
     const int64_t g = blockIdx.x;
-    const int64_t s0 = g * kGroupSegs + (int64_t)threadIdx.x * kSegPerThread;
-    const int wave = threadIdx.x >> 6;
-    __shared__ uint32_t lds4[4];
-    __shared__ int spill[kGroupSegs];
-    __shared__ long long spill_a[kGroupSegs], spill_b[kGroupSegs];
-    __shared__ int nspill;
-    if (threadIdx.x == 0) nspill = 0;
-    uint32_t ca[kSegPerThread], cb[kSegPerThread];
-    uint32_t sa = 0, sb = 0;
-#pragma unroll
-    for (int q = 0; q < kSegPerThread; ++q) {
-        const int64_t seg = s0 + q;
-        const bool ok = seg < w.nseg;
-        if (mode == MODE_FIRSTK) {
-            ca[q] = ok ? w.seg_cnt[seg] : 0;
-            cb[q] = 0;
-        } else {
-            ca[q] = ok ? w.seg_gt[seg] : 0;
-            cb[q] = ok ? w.seg_eq[seg] : 0;
+    const int64_t seg0 = g * kGroupSegs;
+    __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs], lcn[kGroupSegs];
+    __shared__ uint64_t lds16[16];
+    const long long limit = st->limit;
+    const long long T = st->tie_quota;
+    const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
+    const long long gb = rs ? w.grp_eq_off[g] : 0;
+    {
+        const int64_t seg = seg0 + threadIdx.x;
+        uint32_t ca = 0, cb = 0, lc = 0;
+        if (seg < w.nseg) {
+            ca = rs ? w.seg_gt[seg] : w.seg_cnt[seg];
+            cb = rs ? w.seg_eq[seg] : 0;
+            lc = w.seg_lcnt[seg];
         }
-        sa += ca[q];
-        sb += cb[q];
+        uint64_t tot;
+        const uint32_t oa = (uint32_t)block_exclusive_scan((uint64_t)ca, lds16, &tot);
+        __syncthreads();
+        const uint32_t ob = rs ? (uint32_t)block_exclusive_scan((uint64_t)cb, lds16, &tot) : 0u;
+        const bool work = rs ? (ca > 0 || (cb > 0 && gb + ob < T)) : (ca > 0 && ga + oa < limit);
+        off_a[threadIdx.x] = oa;
+        off_b[threadIdx.x] = ob;
+        lcn[threadIdx.x] = work ? lc : kEmitSkip;
     }
-    const uint32_t oa = block_exclusive_scan_256(sa, lds4);
-    const uint32_t ob = mode == MODE_RESAMPLE ? block_exclusive_scan_256(sb, lds4) : 0;
-    const float t = st->t_cur;
-    if (mode == MODE_FIRSTK) {
-        const long long limit = st->limit;
-        long long base = w.grp_off[g] + oa;
+    __syncthreads();
+    const float t = st->t_cur, tk = st->tk;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt();
+    for (int j0 = wv * 64; j0 < wv * 64 + 64; j0 += kEmitBatch) {
+        float x[kEmitBatch];
+        uint32_t e[kEmitBatch];
 #pragma unroll
-        for (int q = 0; q < kSegPerThread; ++q) {
-            const int64_t seg = s0 + q;
-            if (seg < w.nseg && ca[q] > 0 && base < limit) {
-                const uint32_t lc = w.seg_lcnt[seg];
-                if (lc <= (uint32_t)kCap) {
-                    const uint16_t* lo = w.lst_off + seg * kCap;
-                    const float* lv = w.lst_val + seg * kCap;
-                    long long pos = base;
-                    for (uint32_t e = 0; e < lc && pos < limit; ++e) {
-                        const float x = lv[e];
-                        if (fabsf(x) >= t) {
-                            emit_one(o, pos, seg * kSeg + lo[e], x);
-                            ++pos;
-                        }
-                    }
-                } else {
-                    const int slot = atomicAdd(&nspill, 1);
-                    spill[slot] = (int)(seg - g * kGroupSegs);
-                    spill_a[slot] = base;
-                }
+        for (int q = 0; q < kEmitBatch; ++q) {   // all list loads issued first
+            const uint32_t L = lcn[j0 + q];
+            x[q] = 0.f;
+            e[q] = 0;
+            if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
+                const int64_t slot = (seg0 + j0 + q) * kCap + lane;
+                x[q] = w.lst_val[slot];
+                e[q] = w.lst_off[slot];
             }
-            base += ca[q];
         }
-        __syncthreads();
-        for (int q = wave; q < nspill; q += kSegPerBlock4)
-            emit_reread_firstk(vec_in, n, g * kGroupSegs + spill[q], spill_a[q], limit, t, o);
-    } else {
-        const float tk = st->tk;
-        const long long T = st->tie_quota;
-        long long bg = w.grp_gt_off[g] + oa, bt = w.grp_eq_off[g] + ob;
 #pragma unroll
-        for (int q = 0; q < kSegPerThread; ++q) {
-            const int64_t seg = s0 + q;
-            if (seg < w.nseg && (ca[q] > 0 || (cb[q] > 0 && bt < T))) {
-                const uint32_t lc = w.seg_lcnt[seg];
-                if (lc <= (uint32_t)kCap) {
-                    const uint16_t* lo = w.lst_off + seg * kCap;
-                    const float* lv = w.lst_val + seg * kCap;
-                    long long rg = 0, rt = 0;
-                    for (uint32_t e = 0; e < lc; ++e) {
-                        const float x = lv[e];
-                        const float a = fabsf(x);
-                        const bool gt = a > tk, eq = a == tk;
-                        const long long tb = bt + rt;
-                        if (gt || (eq && tb < T)) emit_one(o, bg + rg + (tb < T ? tb : T), seg * kSeg + lo[e], x);
-                        rg += gt;
-                        rt += eq;
-                    }
-                } else {
-                    const int slot = atomicAdd(&nspill, 1);
-                    spill[slot] = (int)(seg - g * kGroupSegs);
-                    spill_a[slot] = bg;
-                    spill_b[slot] = bt;
-                }
+        for (int q = 0; q < kEmitBatch; ++q) {
+            const uint32_t L = lcn[j0 + q];
+            if (L == kEmitSkip) continue;
+            const int64_t seg = seg0 + j0 + q;
+            const long long ba = ga + off_a[j0 + q], bb = gb + off_b[j0 + q];
+            if (L > (uint32_t)kCap) {
+                if (rs)
+                    emit_reread_resample(vec_in, n, seg, ba, bb, tk, T, o);
+                else
+                    emit_reread_firstk(vec_in, n, seg, ba, limit, t, o);
+                continue;
             }
-            bg += ca[q];
-            bt += cb[q];
+            const bool in = (uint32_t)lane < L;
+            const float a = fabsf(x[q]);
+            const int64_t gidx = seg * kSeg + e[q];
+            if (!rs) {
+                const bool sel = in && a >= t;
+                const uint64_t m = __ballot(sel);
+                const long long pos = ba + __popcll(m & lt);
+                if (sel && pos < limit) emit_one(o, pos, gidx, x[q]);
+            } else {
+                const bool gt = in && a > tk, eq = in && a == tk;
+                const uint64_t mg = __ballot(gt), me = __ballot(eq);
+                const long long tb = bb + __popcll(me & lt);
+                if (gt || (eq && tb < T)) emit_one(o, ba + __popcll(mg & lt) + (tb < T ? tb : T), gidx, x[q]);
+            }
         }
-        __syncthreads();
-        for (int q = wave; q < nspill; q += kSegPerBlock4)
-            emit_reread_resample(vec_in, n, g * kGroupSegs + spill[q], spill_a[q], spill_b[q], tk, T, o);
     }
 }
 
@@ -1011,7 +980,7 @@ static int select_core(float* vec, float* mmt, const float* thr0, const dgc_sele
     }
     EmitOut o{p->update_memory ? vec : nullptr, (p->update_memory && p->masking) ? mmt : nullptr, values,
               indices, p->vdtype, p->idtype};
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)w.ngrp), dim3(kBlock), 0, s, vec, n, w, o);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)w.ngrp), dim3(kEmitThreads), 0, s, vec, n, w, o);
     DGC_LAUNCHED();
     hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, w.st, (int64_t)p->num_selects, count_out, info,
                        spec, margin);
@@ -1128,7 +1097,7 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
         return DGC_OK;
     }
     SampleSpec sp{a.sampled ? cw.samples : nullptr, s_start, s_stride, a.sampled ? a.L : 0,
-                  1.0 / (double)s_stride};
+                  1.0 / (double)s_stride, 1.0f / (float)s_stride};
     const int64_t grid = ceil_div(w.nseg, kSegPerBlock4);
     if (grid > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: n too large");
     auto g4 = reinterpret_cast<const float4*>(grad);

@@ -71,6 +71,8 @@ _SIGNATURES = {
     "dgc_payload_layout": (_I64, [_I64, _I32, _I32, ctypes.POINTER(ctypes.c_int64),
                                   ctypes.POINTER(ctypes.c_int64)]),
     "dgc_decompress_packed": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
+    "dgc_scatter_packed": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
+    "dgc_fill_zero": (ctypes.c_int, [_P, _I64, _P]),
     "dgc_decompress_status": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
 }
 

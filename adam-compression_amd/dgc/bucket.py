@@ -10,7 +10,13 @@ every decision kept on the device:
   (``dgc_payload_layout``), so the RCCL allgather needs no size exchange and the
   decompress reads each rank's count on the device;
 * the selection runs in ``DGC_SYNC_DEVICE`` mode (adaptation recounts and the
-  resample chain are launched and early-exit on a device flag).
+  resample chain are launched and early-exit on a device flag);
+* the decompress's ``grad.zero_()`` (dgc/compression.py:191) is issued on a side
+  stream (``dgc_fill_zero``) so it overlaps the compress and the allgather, and the
+  critical path ends with a sparse scatter of the gathered entries
+  (``dgc_scatter_packed``). ``fill="start"`` runs the fill alongside K1, ``"k1"``
+  after K1 (alongside the selection and the allgather), ``"inline"`` keeps the
+  dense one-kernel decompress.
 
 The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
 kernels); the sample start is drawn from a ``random.Random`` seeded identically on
@@ -39,7 +45,7 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42):
+                 device=None, world_size=None, seed=42, fill="start"):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)
@@ -79,6 +85,13 @@ class DGCBucket:
         self.dec_ws = torch.empty(L.dgc_decompress_workspace(N, self.world), dtype=torch.uint8, device=dev)
         self.scale = 1.0 / self.world
         self._L = L
+        if fill not in ("start", "k1", "inline"):
+            raise ValueError(f"fill must be 'start', 'k1' or 'inline', not {fill!r}")
+        self.fill = fill
+        if fill != "inline":
+            self.side = torch.cuda.Stream(device=dev)
+            self._ev_go = torch.cuda.Event()
+            self._ev_filled = torch.cuda.Event()
 
     # ---------------------------------------------------------------- phases
     def compensate(self, grad):
@@ -105,25 +118,50 @@ class DGCBucket:
         if self.world > 1:
             dist.all_gather_into_tensor(self.gathered, self.payload)
 
-    def decompress(self, out):
+    def decompress(self, out, dense=True):
+        """dense: out = scale * (rank-order sum of the gathered entries), zeros elsewhere.
+        dense=False: out already holds +0.0 (see fill_zero); only the entries are written."""
         L = self._L
-        _lib.check(L.dgc_decompress_packed(self.gathered.data_ptr(), self.world, self.rank_stride, self.k,
-                                           _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
-                                           self.numel, self.scale, self.dec_ws.data_ptr(), self.dec_ws.numel(),
-                                           _lib.stream_of(self.device)), "dgc_decompress_packed")
+        fn = L.dgc_decompress_packed if dense else L.dgc_scatter_packed
+        _lib.check(fn(self.gathered.data_ptr(), self.world, self.rank_stride, self.k, _lib.VD[self.vdtype],
+                      _lib.ID[self.idtype], out.data_ptr(), self.numel, self.scale, self.dec_ws.data_ptr(),
+                      self.dec_ws.numel(), _lib.stream_of(self.device)),
+                   "dgc_decompress_packed" if dense else "dgc_scatter_packed")
+
+    def _fill_on_side(self, out):
+        """zero_() of the output on the side stream, ordered after everything issued so far."""
+        self._ev_go.record(torch.cuda.current_stream(self.device))
+        self.side.wait_event(self._ev_go)
+        _lib.check(self._L.dgc_fill_zero(out.data_ptr(), self.numel, self.side.cuda_stream), "dgc_fill_zero")
+        self._ev_filled.record(self.side)
 
     def step(self, grad, out, events=None):
-        """compensate -> threshold -> select -> allgather -> decompress; ``events`` maps a
-        phase name to a (start, end) pair of torch.cuda.Event recorded around it."""
+        """compensate -> threshold -> select -> allgather -> decompress into ``out``
+        (a separate buffer from ``grad``); ``events`` maps a phase name to a (start, end)
+        pair of torch.cuda.Event recorded around it on the current stream."""
         ev = events or {}
+        if self.fill == "start" and out.data_ptr() == grad.data_ptr():
+            raise ValueError("fill='start' zeroes out while K1 reads grad: pass a separate out buffer")
+
+        def decompress():
+            if self.fill == "inline":
+                self.decompress(out)
+            else:
+                torch.cuda.current_stream(self.device).wait_event(self._ev_filled)
+                self.decompress(out, dense=False)
+
+        if self.fill == "start":
+            self._fill_on_side(out)
         for name, fn in (("compensate", lambda: self.compensate(grad)), ("select", self.select),
-                         ("allgather", self.exchange), ("decompress", lambda: self.decompress(out))):
+                         ("allgather", self.exchange), ("decompress", decompress)):
             pair = ev.get(name)
             if pair:
                 pair[0].record()
             fn()
             if pair:
                 pair[1].record()
+            if name == "compensate" and self.fill == "k1":
+                self._fill_on_side(out)
 
     def last_info(self):
         raw = self.info.cpu().numpy().tobytes()

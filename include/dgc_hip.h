@@ -19,6 +19,7 @@
  *                         + mul_(1/W) over the rank-order
  *                         concatenation of the allgather     dgc/compression.py:200-212
  *   dgc_decompress_packed the same, straight from the padded RCCL allgather buffer
+ *   dgc_scatter_packed    its sparse form (zero_() done earlier by dgc_fill_zero)
  *
  * Conventions
  *   - All tensor pointers are DEVICE pointers owned by the caller (PyTorch's caching
@@ -187,6 +188,15 @@ int dgc_decompress_packed(const void* payload, int32_t world, int64_t rank_strid
                           int64_t capacity, int32_t vdtype, int32_t idtype,
                           float* grad, int64_t n, float scale, void* ws, size_t ws_bytes,
                           void* stream);
+/* Sparse form of dgc_decompress_packed: grad must already hold +0.0 everywhere (the
+ * reference's grad.zero_(), dgc/compression.py:191, issued earlier — e.g. with
+ * dgc_fill_zero on a second stream while compress and the allgather run); only the
+ * indices present are written, with the same run-order sums and scale. */
+int dgc_scatter_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                       int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, void* ws,
+                       size_t ws_bytes, void* stream);
+/* grad[0..n) = +0.0 with 16-B non-temporal stores (16-B aligned buffer). */
+int dgc_fill_zero(float* grad, int64_t n, void* stream);
 
 /* Status word written by the decompress kernels: bit 0 = an index was out of
  * range [0, n) and was ignored; bit 1 = a run given by run_offsets was not

@@ -491,21 +491,24 @@ def test_large_bucket_properties(L, N):
 
 
 # ----------------------------------------------------------------------------- bucket engine
-@pytest.mark.parametrize("N,ratio,kind,scales", [
-    (3_000_003, 0.001, "normal", [1, 1, 1, 1, 1]),        # lists serve steps 2+ (tail segment spills)
-    (2_000_000, 0.001, "normal", [1, 1, 0.1, 0.1, 3]),     # scale drop: speculation fails -> full pass
-    (1_048_576, 0.05, "layered", [1, 1, 1]),              # dense candidates: lists spill, re-reads
-    (500_000, 0.01, "bf16", [1, 1, 1, 1]),
-    (1_000_000, 0.001, "normal", [1, 3, 9, 27]),          # fast growth: K1 lists overflow -> dropped
+@pytest.mark.parametrize("N,ratio,kind,scales,fill", [
+    (3_000_003, 0.001, "normal", [1, 1, 1, 1, 1], "start"),   # lists serve steps 2+ (tail segment spills)
+    (3_000_003, 0.001, "normal", [1, 1, 1], "k1"),
+    (3_000_003, 0.001, "normal", [1, 1, 1], "inline"),
+    (2_000_000, 0.001, "normal", [1, 1, 0.1, 0.1, 3], "start"),   # scale drop: speculation fails
+    (1_048_576, 0.05, "layered", [1, 1, 1], "start"),         # dense candidates: lists spill, re-reads
+    (500_000, 0.01, "bf16", [1, 1, 1, 1], "start"),
+    (1_000_000, 0.001, "normal", [1, 3, 9, 27], "start"),     # fast growth: K1 lists overflow -> dropped
 ])
-def test_bucket_steps_match_oracle(L, N, ratio, kind, scales):
-    """DGCBucket (speculative K1 lists, DGC_SYNC_DEVICE) vs the oracle, step by step."""
+def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill):
+    """DGCBucket (speculative K1 lists, DGC_SYNC_DEVICE, side-stream zero fill + sparse
+    scatter or the dense decompress) vs the oracle, step by step."""
     from dgc.bucket import DGCBucket
-    b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=7)
+    b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=7, fill=fill)
     attrs = O.attributes(N, ratio)
     m_o, v_o = np.zeros(N, np.float32), np.zeros(N, np.float32)
     rng = random.Random(7)
-    out = torch.empty(N, device=DEV)
+    out = torch.full((N,), float("nan"), device=DEV)   # the fill must clear it
     served_by_lists = 0
     for s, sc in enumerate(scales):
         g = synth.gradient(300 + s, N, kind, float(sc))

@@ -22,6 +22,7 @@ from dgc.bucket import DGCBucket  # noqa: E402
 
 
 def timeit(fn, reps=10):
+    """Average ms of fn over reps (after one untimed call)."""
     fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -44,9 +45,38 @@ def main():
     g = torch.randn(N, device=dev)
     out = torch.empty(N, device=dev)
     res = {}
-    res["k1_ms"] = timeit(lambda: b.compensate(g))
-    res["finish_ms"] = timeit(b.select)        # threshold + selection + emit (lists from K1)
+    S = (N - 5 + b.stride - 1) // b.stride          # samples from start 5
+    smp = torch.empty(S, device=dev)
+    stream = _lib.stream_of(dev)
+
+    def comp(samples):
+        _lib.check(L.dgc_compensate(g.data_ptr(), b.mmt.data_ptr(), b.vec.data_ptr(), None, N, 0.9, 1, 1,
+                                    smp.data_ptr() if samples else None, 5, b.stride, S if samples else 0,
+                                    stream), "dgc_compensate")
+    res["compensate_plain_ms"] = timeit(lambda: comp(False))     # K1 arithmetic only (3R2W)
+    res["compensate_sample_ms"] = timeit(lambda: comp(True))     # + fused strided sample
+    b.spec.fill_(float("inf"))
+    res["k1_nolist_ms"] = timeit(lambda: b.compensate(g))       # listing K1, nothing listed
+    b.compensate(g)
+    b.select()
+    t = b.last_info()["threshold"]
+    spec = torch.tensor([0.8 * t, t], device=dev)
+    b.spec.copy_(spec)
+    res["k1_list_ms"] = timeit(lambda: b.compensate(g))         # lists at 0.8 x the threshold
+    b.spec.copy_(spec)
+    b.compensate(g)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    b.select()                                                   # served by the lists (one call:
+    e1.record()                                                  # select masks vec, lists go stale)
+    torch.cuda.synchronize()
+    res["finish_ms"] = e0.elapsed_time(e1)
     res["selection"] = b.last_info()
+    for fill in ("inline", "k1", "start"):                      # whole step, three decompress schedules
+        bf = DGCBucket(N, device=dev, fill=fill)
+        res[f"step_fill_{fill}_ms"] = timeit(lambda: bf.step(g, out), reps=5)
+        del bf
     k = b.k
     stride, voff, ioff = b.rank_stride, b.voff, b.ioff
     for W in (1, 2, 4, 8):
@@ -64,6 +94,11 @@ def main():
             _lib.check(L.dgc_decompress_packed(pay.data_ptr(), W, stride, k, 0, 0, out.data_ptr(), N, 1.0 / W,
                                                ws.data_ptr(), ws.numel(), _lib.stream_of(dev)))
         res[f"decompress_W{W}_ms"] = timeit(dec)
+
+        def scat():
+            _lib.check(L.dgc_scatter_packed(pay.data_ptr(), W, stride, k, 0, 0, out.data_ptr(), N, 1.0 / W,
+                                            ws.data_ptr(), ws.numel(), _lib.stream_of(dev)))
+        res[f"scatter_W{W}_ms"] = timeit(scat)
         del pay
     print(json.dumps(res))
 

@@ -64,6 +64,18 @@ __global__ void __launch_bounds__(256) k3r2w_chunk(const float4* __restrict__ g,
     for (int u = 0; u < U; ++u) { long i = base + u * 256 + threadIdx.x; if (i < n4) { upd(a[u], b[u], c[u], mom); st<NTS>(m + i, b[u]); st<NTS>(v + i, c[u]); } }
 }
 
+// 3 reads, 3 writes: the gradient chunk is zeroed after it is read (in-place decompress target)
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) k3r3w_chunk(float4* __restrict__ g, float4* __restrict__ m,
+                                                  float4* __restrict__ v, long n4, float mom) {
+    const long base = (long)blockIdx.x * 256 * U;
+    float4 a[U], b[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { long i = base + u * 256 + threadIdx.x; if (i < n4) { a[u] = ld<NT>(g + i); b[u] = ld<NT>(m + i); c[u] = ld<NT>(v + i); } }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { long i = base + u * 256 + threadIdx.x; if (i < n4) { upd(a[u], b[u], c[u], mom); st<NT>(m + i, b[u]); st<NT>(v + i, c[u]); st<NT>(g + i, make_float4(0, 0, 0, 0)); } }
+}
+
 template <bool NT>
 __global__ void __launch_bounds__(256) kcopy(const float4* __restrict__ a, float4* __restrict__ b, long n4) {
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) st<NT>(b + i, ld<NT>(a + i));
@@ -110,7 +122,18 @@ int main(int argc, char** argv) {
     auto G4 = (const float4*)g; auto M4 = (float4*)m; auto V4 = (float4*)v;
     const int reps = 10;
     auto rep = [&](const char* name, double bytes, float ms) { printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"GBs\": %.1f}\n", name, ms, bytes / (ms * 1e-3) / 1e9); fflush(stdout); };
+    const bool chunk_only = argc > 2 && argv[2][0] == 'c';
+    for (int U : {1, 2, 4}) {
+        long blocks = (n4 + 256L * U - 1) / (256L * U);
+        char nm[96];
+        auto G4w = (float4*)g;
+        snprintf(nm, 96, "3r3w chunk U%d nt (zero g)", U);
+        if (U == 1) rep(nm, 24.0 * n, timeit([&] { k3r3w_chunk<1, true><<<blocks, 256>>>(G4w, M4, V4, n4, 0.9f); }, reps));
+        if (U == 2) rep(nm, 24.0 * n, timeit([&] { k3r3w_chunk<2, true><<<blocks, 256>>>(G4w, M4, V4, n4, 0.9f); }, reps));
+        if (U == 4) rep(nm, 24.0 * n, timeit([&] { k3r3w_chunk<4, true><<<blocks, 256>>>(G4w, M4, V4, n4, 0.9f); }, reps));
+    }
     for (int grid : {1024, 2048, 4096, 8192}) {
+        if (chunk_only) break;
         char nm[96];
         snprintf(nm, 96, "3r2w U1 grid%d", grid);
         rep(nm, 20.0 * n, timeit([&] { k3r2w<1, false, false><<<grid, 256>>>(G4, M4, V4, n4, 0.9f); }, reps));
