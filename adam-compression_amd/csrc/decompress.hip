@@ -22,6 +22,7 @@ namespace dgc {
 
 constexpr int kChunk = 4096;
 constexpr int kMaxRuns = 64;
+constexpr int kSegWaves = kBlock / kWave;   // waves per workgroup
 
 struct Run {
     const void* vals;
@@ -34,6 +35,8 @@ struct DecWS {
     int32_t* nruns;
     int32_t* status;      // bit 0: index out of range
     int32_t* ndesc;       // detected descents
+    int32_t* ovf_cnt;     // sparse scatter: super-chunks queued for the workgroup path
+    int32_t* ovf_list;
     long long* desc;      // their positions (unsorted)
     long long* bnd;       // [kMaxRuns][nchunks + 1]
     int64_t nchunks;
@@ -47,8 +50,10 @@ static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, size_t* bytes = 
     w.nruns = c.take<int32_t>(4);
     w.status = w.nruns ? w.nruns + 1 : nullptr;
     w.ndesc = w.nruns ? w.nruns + 2 : nullptr;
+    w.ovf_cnt = w.nruns ? w.nruns + 3 : nullptr;
     w.desc = c.take<long long>(kMaxRuns);
     w.bnd = c.take<long long>((size_t)max_runs * (w.nchunks + 1));
+    w.ovf_list = c.take<int32_t>(w.nchunks);
     if (bytes) *bytes = c.bytes();
     return w;
 }
@@ -141,7 +146,10 @@ __global__ void __launch_bounds__(kBlock)
 k_bounds(DecWS w, RunSrc rs, int64_t n, int max_runs) {
     const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *w.status = 0;   // set only by the next kernel
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // set only by the next kernels
+        *w.status = 0;
+        *w.ovf_cnt = 0;
+    }
     for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < (int64_t)max_runs * stride;
          t += (int64_t)gridDim.x * kBlock) {
         const int r = (int)(t / stride);
@@ -185,8 +193,8 @@ __device__ __forceinline__ int lower_bound_lds(const int* a, int lo, int hi, int
 // caller, e.g. on a side stream while the compress and the allgather run), so only
 // the indices present are written: the same sums, scaled, with no tile write.
 template <int VD, int ID, bool DENSE>
-__global__ void __launch_bounds__(kBlock)
-k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
+__device__ void scatter_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__ grad, int64_t n, float scale,
+                              int64_t c) {
     __shared__ __attribute__((aligned(16))) float acc[kChunk];
     __shared__ int sidx[kStage];
     __shared__ float sval[kStage];
@@ -196,7 +204,6 @@ k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
     __shared__ const void* ridx[kMaxRuns];
     const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
-    const int64_t c = blockIdx.x;
     const long long base = c * (long long)kChunk;
     const int tid = threadIdx.x, lane = tid & 63;
     if (c == 0 && tid < nr) {   // entries outside [0, n) are skipped: flag them
@@ -321,6 +328,120 @@ k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
     }
 }
 
+template <int VD, int ID, bool DENSE>
+__global__ void __launch_bounds__(kBlock)
+k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
+    scatter_chunk<VD, ID, DENSE>(w, rs, grad, n, scale, blockIdx.x);
+}
+
+// ---------------------------------------------------------------- sparse scatter
+// grad holds +0.0 on entry (the reference's zero_(), done earlier); only the entries
+// are written. The work scales with the entries, not with n.
+//
+// One run (W = 1): one thread per entry. The first of a repeat sums the repeats in
+// order (index_put_ order); a descent or an index outside [0, n) sets the status.
+template <int VD, int ID>
+__global__ void __launch_bounds__(kBlock)
+k_scatter_single(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
+    const Run run = rs.get(0);
+    const long long j = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= run.count) return;
+    const long long i = load_idx<ID>(run.idx, j);
+    const long long ip = j > 0 ? load_idx<ID>(run.idx, j - 1) : -1;
+    if (j > 0 && ip > i) atomicOr(w.status, 2);
+    if (i < 0 || i >= n) {
+        atomicOr(w.status, 1);
+        return;
+    }
+    if (j > 0 && ip == i) return;   // not the first of a repeat
+    float a = __fadd_rn(0.f, load_val<VD>(run.vals, j));
+    for (long long f = j + 1; f < run.count && load_idx<ID>(run.idx, f) == i; ++f)
+        a = __fadd_rn(a, load_val<VD>(run.vals, f));
+    grad[i] = scale != 1.0f ? __fmul_rn(a, scale) : a;
+}
+
+// Several runs: one wave per super-chunk of m 4096-element chunks, m chosen on the
+// host so a super-chunk holds ~32 entries. Lane l takes entry l of the super-chunk
+// (runs concatenated in rank order, so lane order IS the index_put_ order); the
+// lane holding the first occurrence of an index sums every occurrence in lane order
+// through wave shuffles. A super-chunk with more than 64 entries is queued for the
+// workgroup path (scatter_chunk per 4096-element chunk).
+template <int VD, int ID>
+__global__ void __launch_bounds__(kBlock)
+k_scatter_waves(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale, int m) {
+    const int lane = threadIdx.x & 63;
+    const int64_t sc = (int64_t)blockIdx.x * kSegWaves + (threadIdx.x >> 6);
+    const int64_t c0 = sc * m;
+    if (c0 >= w.nchunks) return;
+    const int64_t c1 = c0 + m < w.nchunks ? c0 + m : w.nchunks;
+    const int nr = rs.count();
+    const int64_t stride = w.nchunks + 1;
+    long long b0 = 0, cnt = 0;
+    if (lane < nr) {
+        b0 = w.bnd[lane * stride + c0];
+        cnt = w.bnd[lane * stride + c1] - b0;
+        if (c0 == 0) {   // entries below 0 or at/after n are in no chunk: flag them once
+            const Run run = rs.get(lane);
+            if (b0 > 0 || w.bnd[lane * stride + w.nchunks] < run.count) atomicOr(w.status, 1);
+        }
+    }
+    long long incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const long long T = __shfl(incl, nr - 1);
+    if (T == 0) return;
+    if (T > 64) {
+        if (lane == 0) w.ovf_list[atomicAdd(w.ovf_cnt, 1)] = (int32_t)sc;
+        return;
+    }
+    int r = 0;   // this lane's run: the number of runs ending at or before it
+    for (int q = 0; q < nr; ++q) r += __shfl(incl, q) <= lane;
+    r = r < nr ? r : nr - 1;
+    const bool valid = lane < T;
+    const long long first = __shfl(incl - cnt, r);   // shuffles with every lane active
+    const long long e = __shfl(b0, r) + (lane - first);
+    long long i = -1;
+    float v = 0.f;
+    if (valid) {
+        const Run run = rs.get(r);
+        i = load_idx<ID>(run.idx, e);
+        v = load_val<VD>(run.vals, e);
+    }
+    bool head = valid;
+    float a = 0.f;
+    for (int q = 0; q < (int)T; ++q) {
+        const long long iq = __shfl(i, q);
+        const float vq = __shfl(v, q);
+        if (valid && iq == i) {
+            if (q < lane)
+                head = false;
+            else
+                a = __fadd_rn(a, vq);
+        }
+    }
+    if (!head) return;
+    if (i < c0 * (long long)kChunk || i >= c1 * (long long)kChunk || i >= n) {
+        atomicOr(w.status, 2);   // only an unsorted run lands outside its chunks
+        return;
+    }
+    grad[i] = scale != 1.0f ? __fmul_rn(a, scale) : a;
+}
+
+// The queued super-chunks, one 4096-element chunk per workgroup iteration.
+template <int VD, int ID>
+__global__ void __launch_bounds__(kBlock)
+k_scatter_overflow(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale, int m) {
+    const int64_t total = (int64_t)(*w.ovf_cnt) * m;
+    for (int64_t q = blockIdx.x; q < total; q += gridDim.x) {
+        const int64_t c = (int64_t)w.ovf_list[q / m] * m + q % m;
+        if (c < w.nchunks) scatter_chunk<VD, ID, false>(w, rs, grad, n, scale, c);
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- host side
 static int vbytes(int vd) { return vd == DGC_F16 ? 2 : 4; }
 static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
@@ -328,16 +449,36 @@ static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
 template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
                        bool dense, hipStream_t s) {
+    if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
+    if (!dense && rs.payload && rs.world == 1) {   // one packed run: a thread per entry
+        DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
+        if (rs.capacity > 0) {
+            hipLaunchKernelGGL((k_scatter_single<VD, ID>), dim3((unsigned)ceil_div(rs.capacity, (int64_t)kBlock)),
+                               dim3(kBlock), 0, s, w, rs, grad, n, scale);
+            DGC_LAUNCHED();
+        }
+        return DGC_OK;
+    }
     const int64_t work = (int64_t)max_runs * (w.nchunks + 1);
     hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, rs, n, max_runs);
     DGC_LAUNCHED();
-    if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
-    if (dense)
+    if (dense) {
         hipLaunchKernelGGL((k_scatter_chunks<VD, ID, true>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w,
                            rs, grad, n, scale);
-    else
-        hipLaunchKernelGGL((k_scatter_chunks<VD, ID, false>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w,
-                           rs, grad, n, scale);
+        DGC_LAUNCHED();
+        return DGC_OK;
+    }
+    // super-chunk of m chunks holding ~32 entries on average (capacity per run known)
+    int m = 1;
+    if (rs.payload && rs.capacity > 0) {
+        const double per_chunk = (double)kChunk * max_runs * (double)rs.capacity / (double)n;
+        while (m < 64 && per_chunk * (2 * m) <= 32.0) m *= 2;
+    }
+    const int64_t nsc = ceil_div(w.nchunks, (int64_t)m);
+    hipLaunchKernelGGL((k_scatter_waves<VD, ID>), dim3((unsigned)ceil_div(nsc, (int64_t)kSegWaves)), dim3(kBlock), 0,
+                       s, w, rs, grad, n, scale, m);
+    DGC_LAUNCHED();
+    hipLaunchKernelGGL((k_scatter_overflow<VD, ID>), dim3(512), dim3(kBlock), 0, s, w, rs, grad, n, scale, m);
     DGC_LAUNCHED();
     return DGC_OK;
 }

@@ -45,7 +45,7 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42, fill="start"):
+                 device=None, world_size=None, seed=42, fill="k1"):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)

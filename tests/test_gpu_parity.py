@@ -389,6 +389,79 @@ def test_decompress_packed_and_repeats(L):
     assert st.value == 1 and grad[3].item() == 1.0 and grad.sum().item() == 1.0
 
 
+def _packed(L, runs, cap, fp16, int32):
+    """Pack per-rank (values, indices) runs into the padded allgather layout."""
+    vd, idt = (1 if fp16 else 0), (1 if int32 else 0)
+    vo, io = ctypes.c_int64(0), ctypes.c_int64(0)
+    stride = L.dgc_payload_layout(cap, vd, idt, ctypes.byref(vo), ctypes.byref(io))
+    payload = np.zeros(len(runs) * stride, np.uint8)
+    for r, (v, i) in enumerate(runs):
+        base = r * stride
+        v = v.astype(np.float16 if fp16 else np.float32)
+        i = i.astype(np.int32 if int32 else np.int64)
+        payload[base: base + 8] = np.frombuffer(np.int64(len(i)).tobytes(), np.uint8)
+        payload[base + vo.value: base + vo.value + v.nbytes] = np.frombuffer(v.tobytes(), np.uint8)
+        payload[base + io.value: base + io.value + i.nbytes] = np.frombuffer(i.tobytes(), np.uint8)
+    return payload, stride, vd, idt
+
+
+@pytest.mark.parametrize("N,W,cap,overlap,fp16,int32", [
+    (1_000_003, 1, 1000, 0.0, False, False),     # single run: thread per entry
+    (1_000_003, 1, 1000, 0.0, True, True),
+    (1_000_003, 2, 1000, 0.5, False, False),     # wave per super-chunk, cross-rank duplicates
+    (1_000_003, 8, 1000, 0.3, True, False),
+    (1_000_000, 4, 10000, 0.2, False, False),    # ~160 per chunk: overflow to the staged workgroup path
+    (300_000, 8, 30000, 0.3, False, True),       # denser: the workgroup path's LDS accumulate
+    (50_000, 5, 20000, 0.9, False, False),       # > kStage entries per chunk: LDS accumulate
+])
+def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, int32):
+    """dgc_fill_zero + dgc_scatter_packed == dgc_decompress_packed == the oracle, bit for bit."""
+    rng = np.random.default_rng(N + W)
+    shared = np.sort(rng.choice(N, cap, replace=False))
+    runs = []
+    for r in range(W):
+        c = int(rng.integers(cap // 2, cap + 1))
+        own = rng.choice(N, c, replace=False)
+        pick = rng.random(c) < overlap
+        idx = np.unique(np.where(pick, shared[:c], own))[:c]
+        runs.append((rng.standard_normal(idx.size).astype(np.float32), idx.astype(np.int64)))
+    payload, stride, vd, idt = _packed(L, runs, cap, fp16, int32)
+    wv = [v.astype(np.float16).astype(np.float32) if fp16 else v for v, _ in runs]
+    want = O.decompress(wv, [i for _, i in runs], N, W)
+    tp = to_dev(payload)
+    wsz = L.dgc_decompress_workspace(N, W)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    dense = torch.full((N,), float("nan"), device=DEV)
+    check(L, L.dgc_decompress_packed(P(tp), W, stride, cap, vd, idt, P(dense), N, 1.0 / W, P(ws), wsz, stream()))
+    sparse = torch.full((N,), float("nan"), device=DEV)
+    check(L, L.dgc_fill_zero(P(sparse), N, stream()))
+    check(L, L.dgc_scatter_packed(P(tp), W, stride, cap, vd, idt, P(sparse), N, 1.0 / W, P(ws), wsz, stream()))
+    st = ctypes.c_int32(-1)
+    check(L, L.dgc_decompress_status(P(ws), ctypes.byref(st), stream()))
+    torch.cuda.synchronize()
+    assert st.value == 0
+    assert np.array_equal(bits(dense.cpu().numpy()), bits(want))
+    assert np.array_equal(bits(sparse.cpu().numpy()), bits(want))
+
+
+def test_sparse_scatter_flags_out_of_range(L):
+    N, cap = 10_000, 8
+    for W in (1, 3):
+        runs = [(np.ones(3, np.float32), np.array([-1, 3, N], np.int64))] + \
+               [(np.ones(2, np.float32), np.array([3, 7], np.int64))] * (W - 1)
+        payload, stride, vd, idt = _packed(L, runs, cap, False, False)
+        tp = to_dev(payload)
+        wsz = L.dgc_decompress_workspace(N, W)
+        ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+        out = torch.empty(N, device=DEV)
+        check(L, L.dgc_fill_zero(P(out), N, stream()))
+        check(L, L.dgc_scatter_packed(P(tp), W, stride, cap, vd, idt, P(out), N, 1.0, P(ws), wsz, stream()))
+        st = ctypes.c_int32(-1)
+        check(L, L.dgc_decompress_status(P(ws), ctypes.byref(st), stream()))
+        assert st.value & 1, W
+        assert out[3].item() == float(W) and out.sum().item() == float(W + (W - 1))
+
+
 def test_decompress_unsorted_falls_back_to_stable_order(L):
     from dgc.compression import DGCCompressor
     N = 3000
