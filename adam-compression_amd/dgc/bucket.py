@@ -11,12 +11,12 @@ every decision kept on the device:
   decompress reads each rank's count on the device;
 * the selection runs in ``DGC_SYNC_DEVICE`` mode (adaptation recounts and the
   resample chain are launched and early-exit on a device flag);
-* the decompress's ``grad.zero_()`` (dgc/compression.py:191) is issued on a side
-  stream (``dgc_fill_zero``) so it overlaps the compress and the allgather, and the
-  critical path ends with a sparse scatter of the gathered entries
-  (``dgc_scatter_packed``). ``fill="start"`` runs the fill alongside K1, ``"k1"``
-  after K1 (alongside the selection and the allgather), ``"inline"`` keeps the
-  dense one-kernel decompress.
+* the decompress is ``grad.zero_()`` (dgc/compression.py:191) as a one-shot
+  ``dgc_fill_zero`` followed by a sparse scatter of the gathered entries.
+  ``fill="allgather"`` issues the fill on a side stream once the selection is done,
+  so at W > 1 it overlaps the RCCL allgather. Measured on one MI355X, overlapping
+  the fill with the selection kernels loses (they are latency-bound and slow down
+  under a concurrent 7 TB/s write stream), so the default is ``"inline"``.
 
 The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
 kernels); the sample start is drawn from a ``random.Random`` seeded identically on
@@ -45,7 +45,7 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42, fill="k1"):
+                 device=None, world_size=None, seed=42, fill="inline"):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)
@@ -85,10 +85,10 @@ class DGCBucket:
         self.dec_ws = torch.empty(L.dgc_decompress_workspace(N, self.world), dtype=torch.uint8, device=dev)
         self.scale = 1.0 / self.world
         self._L = L
-        if fill not in ("start", "k1", "inline"):
-            raise ValueError(f"fill must be 'start', 'k1' or 'inline', not {fill!r}")
+        if fill not in ("inline", "allgather"):
+            raise ValueError(f"fill must be 'inline' or 'allgather', not {fill!r}")
         self.fill = fill
-        if fill != "inline":
+        if fill == "allgather":
             self.side = torch.cuda.Stream(device=dev)
             self._ev_go = torch.cuda.Event()
             self._ev_filled = torch.cuda.Event()
@@ -136,12 +136,10 @@ class DGCBucket:
         self._ev_filled.record(self.side)
 
     def step(self, grad, out, events=None):
-        """compensate -> threshold -> select -> allgather -> decompress into ``out``
-        (a separate buffer from ``grad``); ``events`` maps a phase name to a (start, end)
-        pair of torch.cuda.Event recorded around it on the current stream."""
+        """compensate -> threshold -> select -> allgather -> decompress into ``out``;
+        ``events`` maps a phase name to a (start, end) pair of torch.cuda.Event recorded
+        around it on the current stream."""
         ev = events or {}
-        if self.fill == "start" and out.data_ptr() == grad.data_ptr():
-            raise ValueError("fill='start' zeroes out while K1 reads grad: pass a separate out buffer")
 
         def decompress():
             if self.fill == "inline":
@@ -150,8 +148,6 @@ class DGCBucket:
                 torch.cuda.current_stream(self.device).wait_event(self._ev_filled)
                 self.decompress(out, dense=False)
 
-        if self.fill == "start":
-            self._fill_on_side(out)
         for name, fn in (("compensate", lambda: self.compensate(grad)), ("select", self.select),
                          ("allgather", self.exchange), ("decompress", decompress)):
             pair = ev.get(name)
@@ -160,7 +156,7 @@ class DGCBucket:
             fn()
             if pair:
                 pair[1].record()
-            if name == "compensate" and self.fill == "k1":
+            if name == "select" and self.fill == "allgather":
                 self._fill_on_side(out)
 
     def last_info(self):

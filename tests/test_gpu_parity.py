@@ -565,13 +565,12 @@ def test_large_bucket_properties(L, N):
 
 # ----------------------------------------------------------------------------- bucket engine
 @pytest.mark.parametrize("N,ratio,kind,scales,fill", [
-    (3_000_003, 0.001, "normal", [1, 1, 1, 1, 1], "start"),   # lists serve steps 2+ (tail segment spills)
-    (3_000_003, 0.001, "normal", [1, 1, 1], "k1"),
-    (3_000_003, 0.001, "normal", [1, 1, 1], "inline"),
-    (2_000_000, 0.001, "normal", [1, 1, 0.1, 0.1, 3], "start"),   # scale drop: speculation fails
-    (1_048_576, 0.05, "layered", [1, 1, 1], "start"),         # dense candidates: lists spill, re-reads
-    (500_000, 0.01, "bf16", [1, 1, 1, 1], "start"),
-    (1_000_000, 0.001, "normal", [1, 3, 9, 27], "start"),     # fast growth: K1 lists overflow -> dropped
+    (3_000_003, 0.001, "normal", [1, 1, 1, 1, 1], "inline"),  # lists serve steps 2+ (tail segment spills)
+    (3_000_003, 0.001, "normal", [1, 1, 1], "allgather"),
+    (2_000_000, 0.001, "normal", [1, 1, 0.1, 0.1, 3], "inline"),   # scale drop: speculation fails
+    (1_048_576, 0.05, "layered", [1, 1, 1], "inline"),         # dense candidates: lists spill, re-reads
+    (500_000, 0.01, "bf16", [1, 1, 1, 1], "inline"),
+    (1_000_000, 0.001, "normal", [1, 3, 9, 27], "inline"),     # fast growth: K1 lists overflow -> dropped
 ])
 def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill):
     """DGCBucket (speculative K1 lists, DGC_SYNC_DEVICE, side-stream zero fill + sparse

@@ -34,6 +34,29 @@ def timeit(fn, reps=10):
     return a.elapsed_time(b) / reps
 
 
+def steady(N, dev, grads, out, steps=7, **kw):
+    """Phase times (HIP events on the current stream) averaged over the last 3 of
+    `steps` bucket steps on alternating gradients, as bench.py runs them."""
+    b = DGCBucket(N, device=dev, **kw)
+    names = ("compensate", "select", "allgather", "decompress")
+    acc = dict.fromkeys(names + ("step",), 0.0)
+    for s in range(steps):
+        ev = {n: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for n in names}
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        b.step(grads[s % 2], out, ev)
+        t1.record()
+        torch.cuda.synchronize()
+        if s >= steps - 3:
+            for n in names:
+                acc[n] += ev[n][0].elapsed_time(ev[n][1]) / 3
+            acc["step"] += t0.elapsed_time(t1) / 3
+    info = b.last_info()
+    acc["full_passes"], acc["overflow_segments"] = info["full_passes"], info["overflow_segments"]
+    del b
+    return {k: round(v, 4) if isinstance(v, float) else v for k, v in acc.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--numel", type=float, default=1e9)
@@ -73,10 +96,13 @@ def main():
     torch.cuda.synchronize()
     res["finish_ms"] = e0.elapsed_time(e1)
     res["selection"] = b.last_info()
-    for fill in ("inline", "k1", "start"):                      # whole step, three decompress schedules
-        bf = DGCBucket(N, device=dev, fill=fill)
-        res[f"step_fill_{fill}_ms"] = timeit(lambda: bf.step(g, out), reps=5)
-        del bf
+    del b
+    g2 = torch.randn(N, generator=torch.Generator(device=dev).manual_seed(1), device=dev)
+    variants = {"default": {}, "fill_allgather": dict(fill="allgather"),
+                "no_momentum_masking": dict(momentum_masking=False)}
+    for name, kw in variants.items():                           # steady-state steps, like bench.py
+        res[f"steady_{name}"] = steady(N, dev, (g, g2), out, **kw)
+    b = DGCBucket(N, device=dev)
     k = b.k
     stride, voff, ioff = b.rank_stride, b.voff, b.ioff
     for W in (1, 2, 4, 8):

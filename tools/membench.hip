@@ -76,6 +76,14 @@ __global__ void __launch_bounds__(256) k3r3w_chunk(float4* __restrict__ g, float
     for (int u = 0; u < U; ++u) { long i = base + u * 256 + threadIdx.x; if (i < n4) { upd(a[u], b[u], c[u], mom); st<NT>(m + i, b[u]); st<NT>(v + i, c[u]); st<NT>(g + i, make_float4(0, 0, 0, 0)); } }
 }
 
+// one-shot fill: each block owns U*256 float4
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) kfill_chunk(float4* __restrict__ a, long n4) {
+    const long base = (long)blockIdx.x * 256 * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) { long i = base + u * 256 + threadIdx.x; if (i < n4) st<NT>(a + i, make_float4(0, 0, 0, 0)); }
+}
+
 template <bool NT>
 __global__ void __launch_bounds__(256) kcopy(const float4* __restrict__ a, float4* __restrict__ b, long n4) {
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) st<NT>(b + i, ld<NT>(a + i));
@@ -132,6 +140,25 @@ int main(int argc, char** argv) {
         if (U == 2) rep(nm, 24.0 * n, timeit([&] { k3r3w_chunk<2, true><<<blocks, 256>>>(G4w, M4, V4, n4, 0.9f); }, reps));
         if (U == 4) rep(nm, 24.0 * n, timeit([&] { k3r3w_chunk<4, true><<<blocks, 256>>>(G4w, M4, V4, n4, 0.9f); }, reps));
     }
+    for (int U : {1, 4, 16}) {
+        long blocks = (n4 + 256L * U - 1) / (256L * U);
+        char nm[96];
+        snprintf(nm, 96, "fill chunk U%d", U);
+        if (U == 1) rep(nm, 4.0 * n, timeit([&] { kfill_chunk<1, false><<<blocks, 256>>>(M4, n4); }, reps));
+        if (U == 4) rep(nm, 4.0 * n, timeit([&] { kfill_chunk<4, false><<<blocks, 256>>>(M4, n4); }, reps));
+        if (U == 16) rep(nm, 4.0 * n, timeit([&] { kfill_chunk<16, false><<<blocks, 256>>>(M4, n4); }, reps));
+        snprintf(nm, 96, "fill chunk U%d nt", U);
+        if (U == 1) rep(nm, 4.0 * n, timeit([&] { kfill_chunk<1, true><<<blocks, 256>>>(M4, n4); }, reps));
+        if (U == 4) rep(nm, 4.0 * n, timeit([&] { kfill_chunk<4, true><<<blocks, 256>>>(M4, n4); }, reps));
+        if (U == 16) rep(nm, 4.0 * n, timeit([&] { kfill_chunk<16, true><<<blocks, 256>>>(M4, n4); }, reps));
+    }
+    for (int grid : {1024, 4096, 16384}) {
+        char nm[96];
+        snprintf(nm, 96, "fill grid%d", grid); rep(nm, 4.0 * n, timeit([&] { kfill<false><<<grid, 256>>>(M4, n4); }, reps));
+        snprintf(nm, 96, "fill nt grid%d", grid); rep(nm, 4.0 * n, timeit([&] { kfill<true><<<grid, 256>>>(M4, n4); }, reps));
+    }
+    CK(hipMemsetAsync(m, 0, n * 4));
+    rep("hipMemsetAsync", 4.0 * n, timeit([&] { CK(hipMemsetAsync(m, 0, n * 4)); }, reps));
     for (int grid : {1024, 2048, 4096, 8192}) {
         if (chunk_only) break;
         char nm[96];
