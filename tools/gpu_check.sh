@@ -6,7 +6,7 @@ TAG=${1:-x}
 shift
 mkdir -p gpurun_out
 rm -rf gpurun_out/prof_$TAG gpurun_out/bench.json gpurun_out/ablate.json
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
