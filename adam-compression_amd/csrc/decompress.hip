@@ -6,16 +6,19 @@
 // input is a sequence of RUNS (one per rank; our compress emits each rank's indices
 // ascending), so the dense result is reproduced bit-for-bit without atomics:
 //
-//   bounds  one thread per (run, chunk) binary-searches the first entry of the run
-//           whose index reaches the chunk (runs are non-decreasing);
-//   chunk   one workgroup per 4096-element chunk: zero a 16 KB LDS tile, add the
-//           runs' entries for the chunk IN RUN ORDER (a barrier between runs; inside
-//           a run an index appears once — or, for a non-decreasing run with
-//           repeats, its first occurrence sums the repeats in order), scale by
-//           1/W, and write the tile out with 16-B stores.
+//   zero    dgc_fill_zero: one-shot 16-B stores over grad (the reference's zero_());
+//   bounds  one coalesced pass over every run's entries marks, per (run, 4096-element
+//           chunk), the first entry whose index reaches the chunk;
+//   scatter one run: a thread per entry. Several runs: a wave per super-chunk of
+//           ~32 entries, lane order = rank order; an index seen in two runs (an LDS
+//           bitmap finds it) is summed in lane order by its first occurrence, so
+//           every sum has the sequential order; then * (1/W) and one 4-B store per
+//           index. Crowded super-chunks go to a workgroup path that accumulates in
+//           registers in the same order.
 //
-// HBM: the dense write (4 B/elem) plus the sparse reads W*k*(vb+ib). Untouched
-// slots come out +0.0 exactly as zero_() * (1/W).
+// HBM: the dense write (4 B/elem) plus the sparse reads W*k*(vb+ib) and one
+// scattered store per distinct index. Untouched slots come out +0.0 exactly as
+// zero_() * (1/W).
 #include "dgc_common.hpp"
 
 namespace dgc {
@@ -141,63 +144,82 @@ __global__ void k_runs_from_descents(DecWS w, const char* vals, const char* idx,
 }
 
 // ---------------------------------------------------------------- bounds
+// bnd[r][c] = the first entry of run r whose index reaches key_c (key_c = 4096c for
+// c < nchunks, key_nchunks = n), i.e. what a binary search per (run, chunk) would
+// give — built instead from one coalesced pass over the entries. With
+// G(v) = #{c : key_c <= v}, entry e owns the chunks c in [G(idx[e-1]), G(idx[e]))
+// (G(idx[-1]) = 0, G(idx[count]) = nchunks + 1), so every bnd slot is written once
+// by the entry that starts it. Ranges longer than 8 chunks (gaps, empty runs) are
+// written by the whole wave. A descending pair (an unsorted run) sets status bit 2;
+// such a run can leave slots unwritten, so readers clamp bnd to [0, count].
+__device__ __forceinline__ long long chunk_rank(long long v, int64_t n, int64_t nchunks) {
+    if (v < 0) return 0;
+    const long long c = (v >> 12) < nchunks - 1 ? (v >> 12) : nchunks - 1;
+    return c + 1 + (v >= n ? 1 : 0);
+}
+
 template <int ID>
 __global__ void __launch_bounds__(kBlock)
-k_bounds(DecWS w, RunSrc rs, int64_t n, int max_runs) {
-    const int nr = rs.count();
+k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap) {
+    const int r = blockIdx.y;
     const int64_t stride = w.nchunks + 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {   // set only by the next kernels
+    if (blockIdx.x == 0 && r == 0 && threadIdx.x == 0) {   // set only by the next kernels
         *w.status = 0;
         *w.ovf_cnt = 0;
     }
-    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < (int64_t)max_runs * stride;
-         t += (int64_t)gridDim.x * kBlock) {
-        const int r = (int)(t / stride);
-        if (r >= nr) break;
-        const int64_t c = t - (int64_t)r * stride;
-        const Run run = rs.get(r);
-        const long long key = c == w.nchunks ? n : c * (long long)kChunk;
-        long long lo = 0, hi = run.count;   // first entry with idx >= key
-        while (lo < hi) {
-            const long long mid = (lo + hi) >> 1;
-            if (load_idx<ID>(run.idx, mid) < key)
-                lo = mid + 1;
-            else
-                hi = mid;
+    if (r >= rs.count()) return;   // uniform per workgroup
+    const Run run = rs.get(r);
+    long long* bnd = w.bnd + (int64_t)r * stride;
+    const int lane = threadIdx.x & 63;
+    for (int64_t e0 = (int64_t)blockIdx.x * kBlock; e0 <= run.count; e0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t e = e0 + threadIdx.x;
+        long long lo = 0, hi = 0;
+        if (e <= run.count) {
+            const long long ip = e > 0 ? load_idx<ID>(run.idx, e - 1) : -1;
+            const long long ic = e < run.count ? load_idx<ID>(run.idx, e) : 0;
+            lo = e > 0 ? chunk_rank(ip, n, w.nchunks) : 0;
+            hi = e < run.count ? chunk_rank(ic, n, w.nchunks) : stride;
+            if (e > 0 && e < run.count && ic < ip) atomicOr(w.status, 2);
+            if (hi < lo) hi = lo;
         }
-        w.bnd[t] = lo;
+        if (hi - lo <= 8) {
+            for (long long c = lo; c < hi; ++c) bnd[c] = e;
+        }
+        uint64_t longs = __ballot(hi - lo > 8);
+        while (longs) {
+            const int L = __builtin_ctzll(longs);
+            longs &= longs - 1;
+            const long long a = __shfl(lo, L), b = __shfl(hi, L);
+            const long long v = e0 + (threadIdx.x & ~63) + L;
+            for (long long c = a + lane; c < b; c += 64) bnd[c] = v;
+        }
     }
 }
 
-// ---------------------------------------------------------------- chunk scatter
-constexpr int kStage = 512;    // staged entries per chunk (avg 4*W at ratio 0.001); LDS ~21 KB -> 7 blocks/CU
-
-__device__ __forceinline__ int lower_bound_lds(const int* a, int lo, int hi, int key) {
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (a[mid] < key)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
+// Entries [b0, b1) of run r for chunk c, clamped so stale bounds (unsorted runs) stay in range.
+__device__ __forceinline__ void chunk_range(const long long* bnd, int64_t c, long long count, long long& b0,
+                                            long long& b1) {
+    b0 = bnd[c];
+    b1 = bnd[c + 1];
+    b0 = b0 < 0 ? 0 : (b0 > count ? count : b0);
+    b1 = b1 < b0 ? b0 : (b1 > count ? count : b1);
 }
 
-// One workgroup per 4096-element chunk (one-shot grid). Phase 1 stages every run's
-// entries for the chunk into LDS in one parallel load sweep (run order kept by
-// position); phase 2 lets the FIRST occurrence of each index (in run order) add
-// all of its occurrences in run order, from +0.0 — the sequential index_put_
-// order — into the LDS tile; phase 3 scales and writes the tile with 16-B stores.
-// Chunks with more than kStage entries fall back to one barrier per run.
-// DENSE = false (sparse scatter): grad already holds +0.0 everywhere (zeroed by the
-// caller, e.g. on a side stream while the compress and the allgather run), so only
-// the indices present are written: the same sums, scaled, with no tile write.
-template <int VD, int ID, bool DENSE>
-__device__ void scatter_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__ grad, int64_t n, float scale,
-                              int64_t c) {
-    __shared__ __attribute__((aligned(16))) float acc[kChunk];
-    __shared__ int sidx[kStage];
-    __shared__ float sval[kStage];
+// ---------------------------------------------------------------- crowded chunks
+// One 4096-element chunk per workgroup, for chunks too crowded for one wave (see
+// k_scatter_waves); grad already holds +0.0 there. Thread t owns the float4s t,
+// t+256, t+512, t+768 of the chunk in registers, starting at +0.0. The chunk's
+// entries are staged in LDS in RUN ORDER (batches of kTileStage) and every wave walks
+// them in that order, adding each entry it owns into the owning lane's register —
+// the sequential index_put_ order (repeats included), so sums are bit-exact with no
+// atomics. Then * (1/W), and the touched elements are stored.
+constexpr int kTileStage = 1024;
+
+template <int VD, int ID>
+__device__ void tile_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__ grad, int64_t n, float scale,
+                           int64_t c) {
+    __shared__ int soff[kTileStage];
+    __shared__ float sval[kTileStage];
     __shared__ int roff[kMaxRuns + 1];
     __shared__ long long rb0[kMaxRuns];
     __shared__ const void* rval[kMaxRuns];
@@ -205,133 +227,77 @@ __device__ void scatter_chunk(const DecWS& w, const RunSrc& rs, float* __restric
     const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
     const long long base = c * (long long)kChunk;
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (c == 0 && tid < nr) {   // entries outside [0, n) are skipped: flag them
-        const Run run = rs.get(tid);
-        if (w.bnd[tid * stride] > 0 || w.bnd[tid * stride + w.nchunks] < run.count) atomicOr(w.status, 1);
-    }
-    float4* acc4 = reinterpret_cast<float4*>(acc);
-    if (DENSE)
-        for (int j = tid; j < kChunk / 4; j += kBlock) acc4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < 64) {   // run table for this chunk (nr <= 64: one wave)
-        int cnt = 0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) {   // run table of this chunk (nr <= 64: one wave)
+        long long cnt = 0;
         if (tid < nr) {
             const Run run = rs.get(tid);
-            const long long b0 = w.bnd[tid * stride + c], b1 = w.bnd[tid * stride + c + 1];
+            const long long* bnd = w.bnd + (int64_t)tid * stride;
+            long long b0, b1;
+            chunk_range(bnd, c, run.count, b0, b1);
             rb0[tid] = b0;
             rval[tid] = run.vals;
             ridx[tid] = run.idx;
-            cnt = (int)(b1 - b0);
+            cnt = b1 - b0;
+            if (c == 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);   // idx < 0 or >= n
         }
-        int incl = cnt;
+        long long incl = cnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
+            const long long y = __shfl_up(incl, o);
             if (lane >= o) incl += y;
         }
-        if (tid < nr) roff[tid] = incl - cnt;
-        if (tid == nr - 1) roff[nr] = incl;
+        if (tid < nr) roff[tid] = (int)(incl - cnt);
+        if (tid == nr - 1) roff[nr] = (int)incl;
     }
     __syncthreads();
     const int total = roff[nr];
-    if (total <= kStage) {
-        for (int t = tid; t < total; t += kBlock) {
+    float a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = 0.f;
+    uint32_t touched = 0;
+    for (int t0 = 0; t0 < total; t0 += kTileStage) {
+        const int m = total - t0 < kTileStage ? total - t0 : kTileStage;
+        for (int t = tid; t < m; t += kBlock) {
             int r = 0;
-            while (roff[r + 1] <= t) ++r;   // <= 64 runs, few entries: linear is fine
-            const long long e = rb0[r] + (t - roff[r]);
-            const long long i = load_idx<ID>(ridx[r], e) - base;
-            sidx[t] = (i >= 0 && i < kChunk) ? (int)i : -1;
+            while (roff[r + 1] <= t0 + t) ++r;   // <= 64 runs
+            const long long e = rb0[r] + (t0 + t - roff[r]);
+            const long long off = load_idx<ID>(ridx[r], e) - base;
+            soff[t] = (off >= 0 && off < kChunk) ? (int)off : -1;
             sval[t] = load_val<VD>(rval[r], e);
         }
         __syncthreads();
-        for (int t = tid; t < total; t += kBlock) {
-            const int i = sidx[t];
-            if (i < 0) {
-                atomicOr(w.status, 2);   // only an unsorted run can land outside its chunk
+        for (int t = 0; t < m; ++t) {
+            const int off = __builtin_amdgcn_readfirstlane(soff[t]);   // uniform: scalar branches
+            if (off < 0) {
+                if (tid == 0) atomicOr(w.status, 2);   // only an unsorted run lands outside its chunk
                 continue;
             }
-            int r = 0;
-            while (roff[r + 1] <= t) ++r;
-            if (t > roff[r] && sidx[t - 1] == i) continue;   // repeat inside a non-decreasing run
-            bool head = true;
-            for (int q = 0; q < r && head; ++q) {
-                const int p = lower_bound_lds(sidx, roff[q], roff[q + 1], i);
-                head = !(p < roff[q + 1] && sidx[p] == i);
+            if (((off >> 8) & 3) != wave) continue;
+            const float v = sval[t];
+            if (((off >> 2) & 63) == lane) {
+                const int slot = ((off >> 10) << 2) | (off & 3);
+                touched |= 1u << slot;
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (j == slot) a[j] = __fadd_rn(a[j], v);
             }
-            if (!head) continue;
-            float a = 0.f;
-            for (int q = r; q < nr; ++q) {
-                for (int p = (q == r) ? t : lower_bound_lds(sidx, roff[q], roff[q + 1], i);
-                     p < roff[q + 1] && sidx[p] == i; ++p)
-                    a = __fadd_rn(a, sval[p]);
-            }
-            if (DENSE)
-                acc[i] = a;
-            else
-                grad[base + i] = scale != 1.0f ? __fmul_rn(a, scale) : a;
         }
-        if (!DENSE) return;
-    } else {
-        if (!DENSE) {   // rare (> kStage entries in one chunk): accumulate in LDS after all
-            __syncthreads();
-            for (int j = tid; j < kChunk / 4; j += kBlock) acc4[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            __syncthreads();
-        }
-        for (int r = 0; r < nr; ++r) {
-            const long long b0 = rb0[r], b1 = rb0[r] + (roff[r + 1] - roff[r]);
-            for (long long e = b0 + tid; e < b1; e += kBlock) {
-                const long long i = load_idx<ID>(ridx[r], e);
-                if (e > b0 && load_idx<ID>(ridx[r], e - 1) == i) continue;   // not the first of a repeat
-                const long long off = i - base;
-                if (off < 0 || off >= kChunk) {
-                    atomicOr(w.status, 2);
-                    continue;
-                }
-                float a = acc[off];
-                long long f = e;
-                do {
-                    a = __fadd_rn(a, load_val<VD>(rval[r], f));
-                    ++f;
-                } while (f < b1 && load_idx<ID>(ridx[r], f) == i);
-                acc[off] = a;
-            }
-            __syncthreads();
-        }
-        if (!DENSE) {   // write back the touched slots only (every entry rewrites its own)
-            for (int r = 0; r < nr; ++r) {
-                const long long b0 = rb0[r], b1 = rb0[r] + (roff[r + 1] - roff[r]);
-                for (long long e = b0 + tid; e < b1; e += kBlock) {
-                    const long long off = load_idx<ID>(ridx[r], e) - base;
-                    if (off >= 0 && off < kChunk)
-                        grad[base + off] = scale != 1.0f ? __fmul_rn(acc[off], scale) : acc[off];
-                }
-            }
-            return;
-        }
+        __syncthreads();
     }
-    __syncthreads();
+    if (scale != 1.0f) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = __fmul_rn(a[j], scale);
+    }
+    if (!touched) return;
     const long long len = n - base < kChunk ? n - base : kChunk;
-    if (aligned16(grad) && len == kChunk) {
-        float4* g4 = reinterpret_cast<float4*>(grad + base);
-        for (int j = tid; j < kChunk / 4; j += kBlock) {
-            float4 v = acc4[j];
-            if (scale != 1.0f) {
-                v.x = __fmul_rn(v.x, scale);
-                v.y = __fmul_rn(v.y, scale);
-                v.z = __fmul_rn(v.z, scale);
-                v.w = __fmul_rn(v.w, scale);
-            }
-            g4[j] = v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const long long e = (long long)(u * kBlock + tid) * 4 + j;
+            if (e < len && ((touched >> (4 * u + j)) & 1u)) grad[base + e] = a[4 * u + j];
         }
-    } else {
-        for (int j = tid; j < len; j += kBlock) grad[base + j] = scale != 1.0f ? __fmul_rn(acc[j], scale) : acc[j];
-    }
-}
-
-template <int VD, int ID, bool DENSE>
-__global__ void __launch_bounds__(kBlock)
-k_scatter_chunks(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
-    scatter_chunk<VD, ID, DENSE>(w, rs, grad, n, scale, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- sparse scatter
@@ -360,74 +326,135 @@ k_scatter_single(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
     grad[i] = scale != 1.0f ? __fmul_rn(a, scale) : a;
 }
 
-// Several runs: one wave per super-chunk of m 4096-element chunks, m chosen on the
-// host so a super-chunk holds ~32 entries. Lane l takes entry l of the super-chunk
-// (runs concatenated in rank order, so lane order IS the index_put_ order); the
-// lane holding the first occurrence of an index sums every occurrence in lane order
-// through wave shuffles. A super-chunk with more than 64 entries is queued for the
-// workgroup path (scatter_chunk per 4096-element chunk).
+// Several runs: one wave per kSCB super-chunks of m 4096-element chunks each, m
+// chosen on the host so a super-chunk holds ~32 entries. Every load the wave needs is
+// issued up front for all kSCB super-chunks (the run bounds, then the entries), so a
+// wave waits for two memory round trips per kSCB super-chunks, not per super-chunk.
+// Inside a super-chunk, lane l takes entry l (runs concatenated in rank order, so
+// lane order IS the index_put_ order); the lane holding the first occurrence of an
+// index sums every occurrence in lane order through wave shuffles. A super-chunk
+// with more than 64 entries is queued for the workgroup path (tile_chunk per
+// 4096-element chunk, a second kernel).
+constexpr int kSCB = 4;
+
 template <int VD, int ID>
 __global__ void __launch_bounds__(kBlock)
 k_scatter_waves(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale, int m) {
-    const int lane = threadIdx.x & 63;
-    const int64_t sc = (int64_t)blockIdx.x * kSegWaves + (threadIdx.x >> 6);
-    const int64_t c0 = sc * m;
-    if (c0 >= w.nchunks) return;
-    const int64_t c1 = c0 + m < w.nchunks ? c0 + m : w.nchunks;
+    // per-wave duplicate filter: one bit per (offset mod 4096) of the super-chunk
+    __shared__ uint32_t dup_bits[kSegWaves][kChunk / 32];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t sc0 = (xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv) * kSCB;
+    uint32_t* bits = dup_bits[wv];
+    for (int q = lane; q < kChunk / 32; q += 64) bits[q] = 0;
+    if (sc0 * m >= w.nchunks) return;
     const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
-    long long b0 = 0, cnt = 0;
+    // run bounds at the kSCB + 1 super-chunk edges, lanes < nr (one run each)
+    long long bb[kSCB + 1];
+    uintptr_t rv = 0, ri = 0;
     if (lane < nr) {
-        b0 = w.bnd[lane * stride + c0];
-        cnt = w.bnd[lane * stride + c1] - b0;
-        if (c0 == 0) {   // entries below 0 or at/after n are in no chunk: flag them once
-            const Run run = rs.get(lane);
-            if (b0 > 0 || w.bnd[lane * stride + w.nchunks] < run.count) atomicOr(w.status, 1);
-        }
-    }
-    long long incl = cnt;
+        const Run run = rs.get(lane);
+        rv = reinterpret_cast<uintptr_t>(run.vals);
+        ri = reinterpret_cast<uintptr_t>(run.idx);
+        const long long* bnd = w.bnd + (int64_t)lane * stride;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
+        for (int j = 0; j <= kSCB; ++j) {
+            const int64_t c = (sc0 + j) * m < w.nchunks ? (sc0 + j) * m : w.nchunks;
+            bb[j] = bnd[c];
+        }
+        long long prev = 0;
+#pragma unroll
+        for (int j = 0; j <= kSCB; ++j) {   // clamp: stale bounds of an unsorted run stay in range
+            bb[j] = bb[j] < prev ? prev : (bb[j] > run.count ? run.count : bb[j]);
+            prev = bb[j];
+        }
+        // entries below 0 or at/after n are in no chunk: flag them once
+        if (sc0 == 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);
+    } else {
+#pragma unroll
+        for (int j = 0; j <= kSCB; ++j) bb[j] = 0;
     }
-    const long long T = __shfl(incl, nr - 1);
-    if (T == 0) return;
-    if (T > 64) {
-        if (lane == 0) w.ovf_list[atomicAdd(w.ovf_cnt, 1)] = (int32_t)sc;
-        return;
-    }
-    int r = 0;   // this lane's run: the number of runs ending at or before it
-    for (int q = 0; q < nr; ++q) r += __shfl(incl, q) <= lane;
-    r = r < nr ? r : nr - 1;
-    const bool valid = lane < T;
-    const long long first = __shfl(incl - cnt, r);   // shuffles with every lane active
-    const long long e = __shfl(b0, r) + (lane - first);
-    long long i = -1;
-    float v = 0.f;
-    if (valid) {
-        const Run run = rs.get(r);
-        i = load_idx<ID>(run.idx, e);
-        v = load_val<VD>(run.vals, e);
-    }
-    bool head = valid;
-    float a = 0.f;
-    for (int q = 0; q < (int)T; ++q) {
-        const long long iq = __shfl(i, q);
-        const float vq = __shfl(v, q);
-        if (valid && iq == i) {
-            if (q < lane)
-                head = false;
+    // Lane l takes entry l of each super-chunk: its run r = #{q : roff[q+1] <= l},
+    // found with scalar run offsets (readlane) — no cross-lane shuffles.
+    int T[kSCB], off[kSCB];
+    float v[kSCB];
+#pragma unroll
+    for (int j = 0; j < kSCB; ++j) {
+        const long long c64 = bb[j + 1] - bb[j];
+        const int cnt = c64 > 65 ? 65 : (int)c64;   // > 64 entries overflow anyway
+        int roff = 0, r = 0, first = 0;
+        long long e0 = 0;
+        uintptr_t pv = 0, pi = 0;
+        for (int q = 0; q < nr; ++q) {   // uniform loop, scalar bookkeeping
+            const int cq = __builtin_amdgcn_readlane(cnt, q);
+            if (lane >= roff) {
+                r = q;
+                first = roff;
+            }
+            roff += cq;
+        }
+        T[j] = roff;
+        for (int q = 0; q < nr; ++q) {
+            const long long bq = ((long long)__builtin_amdgcn_readlane((int)(bb[j] >> 32), q) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)bb[j], q);
+            const uintptr_t vq = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(rv >> 32), q) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)rv, q);
+            const uintptr_t iq = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(ri >> 32), q) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)ri, q);
+            if (r == q) {
+                e0 = bq;
+                pv = vq;
+                pi = iq;
+            }
+        }
+        off[j] = -1;
+        v[j] = 0.f;
+        if (T[j] <= 64 && lane < T[j]) {
+            const long long e = e0 + (lane - first);
+            v[j] = load_val<VD>(reinterpret_cast<const void*>(pv), e);
+            const long long i = load_idx<ID>(reinterpret_cast<const void*>(pi), e);
+            const long long lo_i = (sc0 + j) * m * (long long)kChunk;
+            const long long hi_i = (sc0 + j + 1) * m < w.nchunks ? (sc0 + j + 1) * m * (long long)kChunk : n;
+            if (i >= lo_i && i < hi_i)
+                off[j] = (int)(i - lo_i);
             else
-                a = __fadd_rn(a, vq);
+                atomicOr(w.status, 2);   // only an unsorted run lands outside its chunks
         }
     }
-    if (!head) return;
-    if (i < c0 * (long long)kChunk || i >= c1 * (long long)kChunk || i >= n) {
-        atomicOr(w.status, 2);   // only an unsorted run lands outside its chunks
-        return;
+#pragma unroll
+    for (int j = 0; j < kSCB; ++j) {
+        if ((sc0 + j) * m >= w.nchunks || T[j] == 0) continue;   // uniform
+        if (T[j] > 64) {
+            if (lane == 0) w.ovf_list[atomicAdd(w.ovf_cnt, 1)] = (int32_t)(sc0 + j);
+            continue;
+        }
+        // an index in two runs (rare: ~W*ratio per entry) sets a bit another lane set
+        bool dup = false;
+        if (off[j] >= 0) {
+            const uint32_t bit = 1u << (off[j] & 31);
+            dup = (atomicOr(&bits[(off[j] & (kChunk - 1)) >> 5], bit) & bit) != 0;
+        }
+        const bool any_dup = __ballot(dup) != 0;
+        if (off[j] >= 0) bits[(off[j] & (kChunk - 1)) >> 5] = 0;   // clean for the next super-chunk
+        bool head = off[j] >= 0;
+        float a = v[j];
+        if (any_dup) {   // slow path: the first occurrence sums all of them in lane order
+            a = 0.f;
+            for (int q = 0; q < T[j]; ++q) {
+                const int oq = __shfl(off[j], q);
+                const float vq = __shfl(v[j], q);
+                if (head && oq == off[j]) {
+                    if (q < lane)
+                        head = false;
+                    else
+                        a = __fadd_rn(a, vq);
+                }
+            }
+        } else {
+            a = __fadd_rn(0.f, a);   // index_put_ onto +0.0 (-0.0 -> +0.0)
+        }
+        if (head) grad[(sc0 + j) * m * (long long)kChunk + off[j]] = scale != 1.0f ? __fmul_rn(a, scale) : a;
     }
-    grad[i] = scale != 1.0f ? __fmul_rn(a, scale) : a;
 }
 
 // The queued super-chunks, one 4096-element chunk per workgroup iteration.
@@ -437,7 +464,7 @@ k_scatter_overflow(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, floa
     const int64_t total = (int64_t)(*w.ovf_cnt) * m;
     for (int64_t q = blockIdx.x; q < total; q += gridDim.x) {
         const int64_t c = (int64_t)w.ovf_list[q / m] * m + q % m;
-        if (c < w.nchunks) scatter_chunk<VD, ID, false>(w, rs, grad, n, scale, c);
+        if (c < w.nchunks) tile_chunk<VD, ID>(w, rs, grad, n, scale, c);
         __syncthreads();
     }
 }
@@ -448,26 +475,19 @@ static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
 
 int fill_zero(float* x, int64_t n, hipStream_t s);
 
-// Decompress schedule. `entries` is a host-side upper bound on the total entries and
-// `runs` the number of runs when the host knows it (0 otherwise).
-//   dense, density > 1/16   one pass: LDS tiles, every element written once
-//   dense, sparser          dgc_fill_zero (7 TB/s one-shot stores) + sparse scatter
-//   sparse (grad pre-zeroed) sparse scatter only
-// Sparse scatter: one run -> a thread per entry; several -> a wave per super-chunk.
+// Decompress schedule. `entries` is a host-side upper bound on the total entries,
+// `run_cap` on the entries of one run, and `runs` the number of runs when the host
+// knows it (0 otherwise). dense: grad is first zeroed by dgc_fill_zero (one-shot
+// 16-B stores, 7 TB/s — the fastest whole-line writer measured; tiles that also
+// place the entries ran 0.69-1.2 ms against fill + scatter 0.61-0.98 ms at 1B,
+// W = 1..8); then the sparse scatter:
+//   one run          a thread per entry
+//   several runs     bounds + a wave per kSCB super-chunks + the workgroup path for
+//                    crowded super-chunks
 template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
-                       bool dense, int64_t entries, int runs, hipStream_t s) {
+                       bool dense, int64_t entries, int64_t run_cap, int runs, hipStream_t s) {
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
-    const double density = (double)entries / (double)n;
-    if (dense && density > 1.0 / 16) {
-        const int64_t work = (int64_t)max_runs * (w.nchunks + 1);
-        hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, rs, n, max_runs);
-        DGC_LAUNCHED();
-        hipLaunchKernelGGL((k_scatter_chunks<VD, ID, true>), dim3((unsigned)w.nchunks), dim3(kBlock), 0, s, w,
-                           rs, grad, n, scale);
-        DGC_LAUNCHED();
-        return DGC_OK;
-    }
     if (dense) DGC_TRY(fill_zero(grad, n, s));
     if (runs == 1) {   // a thread per entry
         DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
@@ -478,16 +498,16 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
         }
         return DGC_OK;
     }
-    const int64_t work = (int64_t)max_runs * (w.nchunks + 1);
-    hipLaunchKernelGGL(k_bounds<ID>, dim3(grid_for(work)), dim3(kBlock), 0, s, w, rs, n, max_runs);
+    const unsigned bx = (unsigned)grid_for(run_cap + 1, kBlock, kMaxGrid / 2);
+    hipLaunchKernelGGL(k_bounds<ID>, dim3(bx, (unsigned)max_runs), dim3(kBlock), 0, s, w, rs, n, run_cap);
     DGC_LAUNCHED();
     // super-chunk of m chunks holding ~32 entries on average
     int m = 1;
-    const double per_chunk = (double)kChunk * density;
+    const double per_chunk = (double)kChunk * (double)entries / (double)n;
     while (m < 64 && per_chunk * (2 * m) <= 32.0) m *= 2;
     const int64_t nsc = ceil_div(w.nchunks, (int64_t)m);
-    hipLaunchKernelGGL((k_scatter_waves<VD, ID>), dim3((unsigned)ceil_div(nsc, (int64_t)kSegWaves)), dim3(kBlock), 0,
-                       s, w, rs, grad, n, scale, m);
+    const dim3 grid((unsigned)ceil_div(nsc, (int64_t)kSegWaves * kSCB));
+    hipLaunchKernelGGL((k_scatter_waves<VD, ID>), grid, dim3(kBlock), 0, s, w, rs, grad, n, scale, m);
     DGC_LAUNCHED();
     hipLaunchKernelGGL((k_scatter_overflow<VD, ID>), dim3(512), dim3(kBlock), 0, s, w, rs, grad, n, scale, m);
     DGC_LAUNCHED();
@@ -495,15 +515,16 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
 }
 
 static int dispatch_scatter(int vd, int id, const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
-                            float scale, int max_runs, bool dense, int64_t entries, int runs, hipStream_t s) {
+                            float scale, int max_runs, bool dense, int64_t entries, int64_t run_cap, int runs,
+                            hipStream_t s) {
     if (vd == DGC_F32 && id == DGC_I64)
-        return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, runs, s);
+        return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
     if (vd == DGC_F32 && id == DGC_I32)
-        return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, runs, s);
+        return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
     if (vd == DGC_F16 && id == DGC_I64)
-        return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, runs, s);
+        return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
     if (vd == DGC_F16 && id == DGC_I32)
-        return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, runs, s);
+        return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
     DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
 }
 
@@ -560,7 +581,7 @@ int decompress(const void* values, int vd, const void* indices, int id, int64_t 
         known_runs = nr;
     }
     RunSrc rs{w.runs, w.nruns, nullptr, 0, 0, 0, 0, 0};
-    return dispatch_scatter(vd, id, w, rs, grad, n, scale, max_runs, true, total, known_runs, s);
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, max_runs, true, total, total, known_runs, s);
 }
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff) {
@@ -582,7 +603,8 @@ int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, i
                  (long long)rank_stride, (long long)min_stride);
     DecWS w = carve_dec(ws, n, world);
     RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world};
-    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, dense, (int64_t)world * capacity, world, s);
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, dense, (int64_t)world * capacity, capacity,
+                            world, s);
 }
 
 // Zero fill (the sparse scatter's precondition): one-shot workgroups, one 16-B

@@ -70,6 +70,15 @@ struct Carver {
 };
 
 // ------------------------------------------------------------------ device helpers
+// Workgroups are dispatched round-robin over the 8 XCDs (b % 8), each with its own
+// L2. Renumber so every XCD gets a contiguous range of logical blocks: neighbours
+// that share cache lines (list boundaries, run bounds, payload lines) then share an
+// L2. A bijection on [0, nb) for any nb; speed only, never correctness.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+    return x * q + (x < r ? x : r) + i;
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));

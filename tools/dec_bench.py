@@ -1,0 +1,78 @@
+"""Decompress-only timing at one world size (for rocprofv3 per-kernel breakdowns).
+
+  python tools/dec_bench.py [--W 8] [--numel 1e9] [--reps 10]
+
+Builds W synthetic packed payloads of k = N/1000 ascending random indices each (the
+shape of the 1B-bucket allgather output) and times dgc_fill_zero, dgc_scatter_packed
+(sparse, onto a zeroed buffer) and dgc_decompress_packed (dense), `reps` times each;
+prints the average ms of each (HIP events on the current stream).
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "adam-compression_amd"))
+
+import torch  # noqa: E402
+
+from dgc import _lib  # noqa: E402
+from dgc.compression import _layout  # noqa: E402
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--W", type=int, default=8)
+    ap.add_argument("--numel", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    N, W = int(args.numel), args.W
+    k = (N + 999) // 1000
+    dev = torch.device("cuda:0")
+    L = _lib.lib()
+    stride, voff, ioff = _layout(k, torch.float32, torch.int64)
+    pay = torch.zeros(W * stride, dtype=torch.uint8, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for r in range(W):
+        idx = torch.sort(torch.randperm(N, device=dev, generator=gen)[:k]).values
+        row = pay[r * stride:(r + 1) * stride]
+        row[:8].view(torch.int64).fill_(k)
+        row[voff:voff + 4 * k].view(torch.float32).copy_(torch.randn(k, device=dev, generator=gen))
+        row[ioff:ioff + 8 * k].view(torch.int64).copy_(idx)
+        del idx
+    out = torch.empty(N, device=dev)
+    ws = torch.empty(L.dgc_decompress_workspace(N, W), dtype=torch.uint8, device=dev)
+    s = _lib.stream_of(dev)
+
+    def fill():
+        _lib.check(L.dgc_fill_zero(out.data_ptr(), N, s), "dgc_fill_zero")
+
+    def scatter():
+        _lib.check(L.dgc_scatter_packed(pay.data_ptr(), W, stride, k, 0, 0, out.data_ptr(), N, 1.0 / W,
+                                        ws.data_ptr(), ws.numel(), s), "dgc_scatter_packed")
+
+    def dense():
+        _lib.check(L.dgc_decompress_packed(pay.data_ptr(), W, stride, k, 0, 0, out.data_ptr(), N, 1.0 / W,
+                                           ws.data_ptr(), ws.numel(), s), "dgc_decompress_packed")
+
+    res = {"W": W, "numel": N, "k": k,
+           "fill_ms": timeit(fill, args.reps), "scatter_ms": timeit(scatter, args.reps),
+           "dense_ms": timeit(dense, args.reps)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
