@@ -13,10 +13,14 @@ every decision kept on the device:
   resample chain are launched and early-exit on a device flag);
 * the decompress is ``grad.zero_()`` (dgc/compression.py:191) as a one-shot
   ``dgc_fill_zero`` followed by a sparse scatter of the gathered entries.
-  ``fill="allgather"`` issues the fill on a side stream once the selection is done,
-  so at W > 1 it overlaps the RCCL allgather. Measured on one MI355X, overlapping
-  the fill with the selection kernels loses (they are latency-bound and slow down
-  under a concurrent 7 TB/s write stream), so the default is ``"inline"``.
+  ``fill="allgather"`` issues the fill on a side stream right after the RCCL
+  allgather is enqueued (ordered after the selection), so at W > 1 the 4 B/elem
+  zero fill runs under the xGMI transfer instead of after it; the decompress then
+  only scatters. ``"inline"`` runs fill + scatter after the allgather. ``"auto"``
+  (default) picks ``"allgather"`` at W > 1 and ``"inline"`` at W = 1, where there
+  is no transfer to hide under (measured on one MI355X, overlapping the fill with
+  the selection kernels instead loses: they are latency-bound and slow down under
+  a concurrent 7 TB/s write stream).
 
 The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
 kernels); the sample start is drawn from a ``random.Random`` seeded identically on
@@ -45,7 +49,7 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42, fill="inline"):
+                 device=None, world_size=None, seed=42, fill="auto"):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)
@@ -85,8 +89,10 @@ class DGCBucket:
         self.dec_ws = torch.empty(L.dgc_decompress_workspace(N, self.world), dtype=torch.uint8, device=dev)
         self.scale = 1.0 / self.world
         self._L = L
-        if fill not in ("inline", "allgather"):
-            raise ValueError(f"fill must be 'inline' or 'allgather', not {fill!r}")
+        if fill not in ("auto", "inline", "allgather"):
+            raise ValueError(f"fill must be 'auto', 'inline' or 'allgather', not {fill!r}")
+        if fill == "auto":
+            fill = "allgather" if self.world > 1 else "inline"
         self.fill = fill
         if fill == "allgather":
             self.side = torch.cuda.Stream(device=dev)
@@ -129,8 +135,8 @@ class DGCBucket:
                    "dgc_decompress_packed" if dense else "dgc_scatter_packed")
 
     def _fill_on_side(self, out):
-        """zero_() of the output on the side stream, ordered after everything issued so far."""
-        self._ev_go.record(torch.cuda.current_stream(self.device))
+        """zero_() of the output on the side stream, ordered after the event recorded
+        at the end of the selection (so it never races a reader of the previous step)."""
         self.side.wait_event(self._ev_go)
         _lib.check(self._L.dgc_fill_zero(out.data_ptr(), self.numel, self.side.cuda_stream), "dgc_fill_zero")
         self._ev_filled.record(self.side)
@@ -156,8 +162,11 @@ class DGCBucket:
             fn()
             if pair:
                 pair[1].record()
-            if name == "select" and self.fill == "allgather":
-                self._fill_on_side(out)
+            if self.fill == "allgather":
+                if name == "select":      # the fill may start once the selection is done ...
+                    self._ev_go.record(torch.cuda.current_stream(self.device))
+                elif name == "allgather":  # ... and is enqueued behind the RCCL launch
+                    self._fill_on_side(out)
 
     def last_info(self):
         raw = self.info.cpu().numpy().tobytes()

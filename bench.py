@@ -39,8 +39,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--numel", type=float, default=1e9)
     ap.add_argument("--ratio", type=float, default=0.001)
-    ap.add_argument("--cpu-numel", type=float, default=2e8, help="CPU-baseline sample size")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-numel", type=float, default=1e9, help="CPU-baseline sample size")
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
     return ap.parse_args()
