@@ -43,9 +43,17 @@ struct DecWS {
     long long* desc;      // their positions (unsorted)
     long long* bnd;       // [kMaxRuns][nchunks + 1]
     int64_t nchunks;
+    // runs that are not non-decreasing (a resample payload in the reference's topk
+    // order) are regrouped by chunk before the scatter: flag, regrouped run, cursors,
+    // and a copy area of sort_cap entries per run (0: no regrouping, the flag only)
+    int32_t* unsorted;    // [kMaxRuns]
+    Run* sorted;          // [kMaxRuns]
+    uint32_t* cursor;     // [max_runs][nchunks]
+    char* sort_buf;       // [max_runs][sort_cap * 12 B]
+    int64_t sort_cap;
 };
 
-static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, size_t* bytes = nullptr) {
+static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, int64_t sort_cap = 0, size_t* bytes = nullptr) {
     Carver c(base);
     DecWS w{};
     w.nchunks = ceil_div(n, kChunk);
@@ -57,6 +65,11 @@ static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, size_t* bytes = 
     w.desc = c.take<long long>(kMaxRuns);
     w.bnd = c.take<long long>((size_t)max_runs * (w.nchunks + 1));
     w.ovf_list = c.take<int32_t>(w.nchunks);
+    w.unsorted = c.take<int32_t>(kMaxRuns);
+    w.sorted = c.take<Run>(kMaxRuns);
+    w.sort_cap = sort_cap;
+    w.cursor = c.take<uint32_t>(sort_cap ? (size_t)max_runs * w.nchunks : 0);
+    w.sort_buf = c.take<char>(sort_cap ? (size_t)max_runs * sort_cap * 12 : 0);
     if (bytes) *bytes = c.bytes();
     return w;
 }
@@ -82,8 +95,14 @@ struct RunSrc {
     const char* payload;          // packed mode when non-null
     int64_t stride, voff, ioff, capacity;
     int32_t world;
+    const int32_t* unsorted;      // regrouped runs (null: none): read them from `sorted`
+    const Run* sorted;
     __device__ __forceinline__ int count() const { return payload ? world : *nruns_dev; }
     __device__ __forceinline__ Run get(int r) const {
+        if (unsorted && unsorted[r]) return sorted[r];
+        return get_raw(r);
+    }
+    __device__ __forceinline__ Run get_raw(int r) const {
         if (!payload) return table[r];
         const char* base = payload + (int64_t)r * stride;
         long long c = *reinterpret_cast<const long long*>(base);
@@ -163,12 +182,8 @@ __global__ void __launch_bounds__(kBlock)
 k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap) {
     const int r = blockIdx.y;
     const int64_t stride = w.nchunks + 1;
-    if (blockIdx.x == 0 && r == 0 && threadIdx.x == 0) {   // set only by the next kernels
-        *w.status = 0;
-        *w.ovf_cnt = 0;
-    }
     if (r >= rs.count()) return;   // uniform per workgroup
-    const Run run = rs.get(r);
+    const Run run = rs.get_raw(r);
     long long* bnd = w.bnd + (int64_t)r * stride;
     const int lane = threadIdx.x & 63;
     for (int64_t e0 = (int64_t)blockIdx.x * kBlock; e0 <= run.count; e0 += (int64_t)gridDim.x * kBlock) {
@@ -179,7 +194,10 @@ k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap) {
             const long long ic = e < run.count ? load_idx<ID>(run.idx, e) : 0;
             lo = e > 0 ? chunk_rank(ip, n, w.nchunks) : 0;
             hi = e < run.count ? chunk_rank(ic, n, w.nchunks) : stride;
-            if (e > 0 && e < run.count && ic < ip) atomicOr(w.status, 2);
+            if (e > 0 && e < run.count && ic < ip) {
+                atomicOr(w.status, 2);
+                if (w.sort_cap) atomicOr(&w.unsorted[r], 1);
+            }
             if (hi < lo) hi = lo;
         }
         if (hi - lo <= 8) {
@@ -203,6 +221,69 @@ __device__ __forceinline__ void chunk_range(const long long* bnd, int64_t c, lon
     b1 = bnd[c + 1];
     b0 = b0 < 0 ? 0 : (b0 > count ? count : b0);
     b1 = b1 < b0 ? b0 : (b1 > count ? count : b1);
+}
+
+// ---------------------------------------------------------------- unsorted runs
+// A run k_bounds found out of order — the reference's resample sends its indices in
+// torch.topk's order (dgc/compression.py:134-137) — is regrouped by chunk, one
+// workgroup per run: counts per chunk, scan (= its bnd row), then every entry is
+// copied to its chunk's next slot. Within a chunk the copy's order is arbitrary;
+// indices are unique within a run (every DGC payload), so each index still gets one
+// term per run and the scatter keeps the rank order of the terms: the sums are the
+// sequential index_put_ sums.
+constexpr int kRegroupThreads = 1024;
+
+template <int VD, int ID>
+__global__ void __launch_bounds__(kRegroupThreads) k_regroup(DecWS w, RunSrc rs, int64_t n) {
+    const int r = blockIdx.x;
+    if (r >= rs.count() || !w.unsorted[r]) return;   // uniform per workgroup
+    const Run run = rs.get_raw(r);
+    const int64_t stride = w.nchunks + 1;
+    long long* bnd = w.bnd + (int64_t)r * stride;
+    uint32_t* cur = w.cursor + (int64_t)r * w.nchunks;
+    const int tid = threadIdx.x;
+    for (int64_t c = tid; c < stride; c += kRegroupThreads) bnd[c] = 0;
+    __syncthreads();
+    for (long long e = tid; e < run.count; e += kRegroupThreads) {
+        const long long i = load_idx<ID>(run.idx, e);
+        if (i < 0 || i >= n) {
+            atomicOr(w.status, 1);
+            continue;
+        }
+        atomicAdd((unsigned long long*)&bnd[(i >> 12) + 1], 1ull);
+    }
+    __syncthreads();
+    // inclusive scan of bnd[0..stride): bnd[c] = first slot of chunk c, bnd[nchunks] = in-range entries
+    __shared__ uint64_t lds16[16];
+    const int64_t per = ceil_div(stride, (int64_t)kRegroupThreads);
+    const int64_t b = tid * per, e = b + per < stride ? b + per : stride;
+    uint64_t local = 0;
+    for (int64_t c = b; c < e; ++c) local += (uint64_t)bnd[c];
+    uint64_t total;
+    uint64_t run_sum = block_exclusive_scan(local, lds16, &total);
+    for (int64_t c = b; c < e; ++c) {
+        run_sum += (uint64_t)bnd[c];
+        bnd[c] = (long long)run_sum;
+        if (c < w.nchunks) cur[c] = (uint32_t)run_sum;
+    }
+    __syncthreads();
+    char* base = w.sort_buf + (int64_t)r * w.sort_cap * 12;
+    void* sv = base;
+    void* si = base + w.sort_cap * 4;
+    for (long long e2 = tid; e2 < run.count; e2 += kRegroupThreads) {
+        const long long i = load_idx<ID>(run.idx, e2);
+        if (i < 0 || i >= n) continue;
+        const uint32_t pos = atomicAdd(&cur[i >> 12], 1u);
+        if (VD == DGC_F16)
+            reinterpret_cast<__half*>(sv)[pos] = reinterpret_cast<const __half*>(run.vals)[e2];
+        else
+            reinterpret_cast<float*>(sv)[pos] = reinterpret_cast<const float*>(run.vals)[e2];
+        if (ID == DGC_I32)
+            reinterpret_cast<int32_t*>(si)[pos] = (int32_t)i;
+        else
+            reinterpret_cast<int64_t*>(si)[pos] = i;
+    }
+    if (tid == 0) w.sorted[r] = Run{sv, si, (long long)bnd[w.nchunks]};
 }
 
 // ---------------------------------------------------------------- crowded chunks
@@ -499,8 +580,18 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
         return DGC_OK;
     }
     const unsigned bx = (unsigned)grid_for(run_cap + 1, kBlock, kMaxGrid / 2);
+    // status, the overflow queue and the unsorted flags are reset before any kernel of
+    // this call can set them
+    DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
+    DGC_HIP(hipMemsetAsync(w.ovf_cnt, 0, sizeof(int32_t), s));
+    if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
     hipLaunchKernelGGL(k_bounds<ID>, dim3(bx, (unsigned)max_runs), dim3(kBlock), 0, s, w, rs, n, run_cap);
     DGC_LAUNCHED();
+    if (w.sort_cap) {
+        if (run_cap > w.sort_cap) DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_decompress: run capacity above the regroup area");
+        hipLaunchKernelGGL((k_regroup<VD, ID>), dim3((unsigned)max_runs), dim3(kRegroupThreads), 0, s, w, rs, n);
+        DGC_LAUNCHED();
+    }
     // super-chunk of m chunks holding ~32 entries on average
     int m = 1;
     const double per_chunk = (double)kChunk * (double)entries / (double)n;
@@ -528,13 +619,14 @@ static int dispatch_scatter(int vd, int id, const DecWS& w, const RunSrc& rs, fl
     DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
 }
 
-static int check_common(int vd, int id, float* grad, int64_t n, void* ws, size_t ws_bytes, int runs) {
+static int check_common(int vd, int id, float* grad, int64_t n, void* ws, size_t ws_bytes, int runs,
+                        int64_t sort_cap = 0) {
     if ((vd != DGC_F32 && vd != DGC_F16) || (id != DGC_I64 && id != DGC_I32))
         DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
     if (!grad || n < 1) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: null grad or n < 1");
     if (runs < 1 || runs > kMaxRuns) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: 1..%d runs supported", kMaxRuns);
     size_t need = 0;
-    carve_dec(nullptr, n, runs, &need);
+    carve_dec(nullptr, n, runs, sort_cap, &need);
     if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_decompress: workspace needs %zu bytes, 256-B aligned", need);
     return DGC_OK;
@@ -580,7 +672,7 @@ int decompress(const void* values, int vd, const void* indices, int id, int64_t 
             DGC_FAIL(DGC_ERR_UNSORTED, "dgc_decompress: input has more than %d descending runs", kMaxRuns);
         known_runs = nr;
     }
-    RunSrc rs{w.runs, w.nruns, nullptr, 0, 0, 0, 0, 0};
+    RunSrc rs{w.runs, w.nruns, nullptr, 0, 0, 0, 0, 0, nullptr, nullptr};
     return dispatch_scatter(vd, id, w, rs, grad, n, scale, max_runs, true, total, total, known_runs, s);
 }
 
@@ -595,14 +687,15 @@ int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t*
 int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity, int vd,
                       int id, float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, hipStream_t s,
                       bool dense) {
-    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world));
+    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world, capacity));
     int64_t voff, ioff;
     const int64_t min_stride = payload_layout(capacity, vd, id, &voff, &ioff);
     if (!payload || rank_stride < min_stride || capacity < 0)
         DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed: rank_stride %lld < layout %lld",
                  (long long)rank_stride, (long long)min_stride);
-    DecWS w = carve_dec(ws, n, world);
-    RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world};
+    DecWS w = carve_dec(ws, n, world, capacity);
+    RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world,
+              w.unsorted, w.sorted};
     return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, dense, (int64_t)world * capacity, capacity,
                             world, s);
 }
@@ -623,7 +716,15 @@ __global__ void k_fill_zero1(float* __restrict__ x, int64_t begin, int64_t n) {
 int fill_zero(float* x, int64_t n, hipStream_t s) {
     if (!x || n < 0) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: null buffer or n < 0");
     if (n == 0) return DGC_OK;
-    if (!aligned16(x)) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: buffer must be 16-B aligned");
+    if (reinterpret_cast<uintptr_t>(x) & 3) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: buffer must be 4-B aligned");
+    // scalar head up to the first 16-B boundary (a grad that is an offset view), then 16-B stores
+    const int64_t lead = std::min<int64_t>(n, (int64_t)((16 - (reinterpret_cast<uintptr_t>(x) & 15)) & 15) / 4);
+    if (lead > 0) {
+        hipLaunchKernelGGL(k_fill_zero1, dim3(1), dim3(64), 0, s, x, 0, lead);
+        DGC_LAUNCHED();
+        x += lead;
+        n -= lead;
+    }
     const int64_t n4 = n / 4;
     if (n4 > 0) {
         if (ceil_div(n4, (int64_t)kBlock) > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: n too large");
@@ -641,10 +742,16 @@ int fill_zero(float* x, int64_t n, hipStream_t s) {
 
 }  // namespace dgc
 
+extern "C" size_t dgc_decompress_packed_workspace(int64_t n, int32_t world, int64_t capacity) {
+    size_t b = 0;
+    dgc::carve_dec(nullptr, n, world, capacity, &b);
+    return b;
+}
+
 extern "C" size_t dgc_decompress_workspace(int64_t n, int32_t max_runs) {
     size_t b = 0;
     if (max_runs < 1 || max_runs > dgc::kMaxRuns) max_runs = dgc::kMaxRuns;
-    dgc::carve_dec(nullptr, n, max_runs, &b);
+    dgc::carve_dec(nullptr, n, max_runs, 0, &b);
     return b;
 }
 

@@ -126,6 +126,30 @@ __device__ __forceinline__ void store_index(void* out, int64_t pos, int64_t idx,
         reinterpret_cast<int64_t*>(out)[pos] = idx;
 }
 
+// ---------------------------------------------------------------- block scan
+// Exclusive scan of one u64 per thread over the block (blockDim a multiple of 64,
+// <= 1024); returns the exclusive prefix and writes the block total to *total.
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds16, uint64_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) lds16[wid] = incl;
+    __syncthreads();
+    uint64_t wbase = 0, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        const uint64_t s = lds16[w];
+        if (w < wid) wbase += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + incl - v;
+}
+
 }  // namespace dgc
 
 namespace dgc {

@@ -36,6 +36,7 @@
 // Everything is stream-ordered; in DGC_SYNC_DEVICE mode kernels that turn out to
 // be unneeded early-exit on a device flag, so no host synchronisation happens.
 #include "radix_select.hpp"
+#include "introselect.hpp"
 
 namespace dgc {
 
@@ -59,7 +60,9 @@ struct SelState {
     long long n_greater;   // RESAMPLE: candidates > tk
     long long tie_quota;   // RESAMPLE: k - n_greater ties, lowest index first
     int32_t resample_pending, overflow, done, lower_pending;
-    int32_t full_passes, list_spills, epoch, pad0;
+    int32_t full_passes, list_spills, epoch;
+    int32_t rs_nth;        // RESAMPLE served by the exact nth_element replay (K5)
+    int32_t tie_rule;      // DGC_TIES_*: how the resample chose among boundary ties
     uint32_t tickets[4];
     // Segments whose K1 list overflowed, counted by K1 into slot [epoch & 1] (64
     // shards against atomic contention); k_sel_init reads it and zeroes the other
@@ -83,10 +86,22 @@ struct SelWS {
     long long* grp_off;
     long long* grp_gt_off;
     long long* grp_eq_off;
+    uint64_t* queue;       // K5: (|x| key << 32 | j) for the candidates j, ascending index order
+    int64_t* cand_idx;     // K5: the candidates' element indices
+    uint32_t* gpos_l;      // K5: pair slots of the global-memory partition passes
+    uint32_t* gpos_r;
     int64_t nseg, ngrp;
+    int64_t cand_cap;      // K5 serves resamples of up to cand_cap candidates
 };
 
-static SelWS carve_select(void* base, int64_t numel, size_t* bytes = nullptr) {
+// Candidates the exact resample replays: torch's CPU topk runs nth_element while
+// k * 64 > n (else partial_sort, which is not replayed), so at most 64k - 1 of them.
+__host__ __device__ inline int64_t nth_cand_cap(int64_t numel, int64_t k) {
+    const int64_t c = 64 * k - 1;
+    return c < numel ? c : numel;
+}
+
+static SelWS carve_select(void* base, int64_t numel, int64_t k, size_t* bytes = nullptr) {
     SelWS w{};
     w.nseg = ceil_div(numel, kSeg);
     w.ngrp = ceil_div(w.nseg, kGroupSegs);
@@ -105,13 +120,18 @@ static SelWS carve_select(void* base, int64_t numel, size_t* bytes = nullptr) {
     w.seg_eq = c.take<uint32_t>(w.nseg);
     w.lst_off = c.take<uint16_t>(w.nseg * kCap);
     w.lst_val = c.take<float>(w.nseg * kCap);
+    w.cand_cap = nth_cand_cap(numel, k);
+    w.queue = c.take<uint64_t>(w.cand_cap);
+    w.cand_idx = c.take<int64_t>(w.cand_cap);
+    w.gpos_l = c.take<uint32_t>(w.cand_cap / 2 + 1);
+    w.gpos_r = c.take<uint32_t>(w.cand_cap / 2 + 1);
     if (bytes) *bytes = c.bytes();
     return w;
 }
 
-static size_t select_ws_bytes(int64_t numel) {
+static size_t select_ws_bytes(int64_t numel, int64_t k) {
     size_t b = 0;
-    carve_select(nullptr, numel, &b);
+    carve_select(nullptr, numel, k, &b);
     return b;
 }
 
@@ -289,6 +309,8 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, const float*
         st->done = 0;
         st->lower_pending = 0;
         st->full_passes = 0;
+        st->rs_nth = 0;
+        st->tie_rule = DGC_TIES_NONE;
         for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
         for (int i = 0; i <= kMaxLower; ++i) st->lower_cnt[i] = 0;
     }
@@ -458,8 +480,14 @@ k_decide(SelWS w, dgc_select_params p) {
             if (cnt > p.upper_count) {
                 if (p.resample) {
                     st->branch = DGC_BRANCH_RESAMPLE;
-                    st->resample_pending = 1;
-                    reset_rs = 1;
+                    if (cnt < 64 * k && cnt <= w.cand_cap) {   // torch's nth_element path: replayed
+                        st->rs_nth = 1;
+                        st->tie_rule = DGC_TIES_EXACT;
+                    } else {                                    // partial_sort path: lowest-index ties
+                        st->resample_pending = 1;
+                        st->tie_rule = DGC_TIES_LOWEST_INDEX;
+                        reset_rs = 1;
+                    }
                 } else {
                     st->t_cur = __fmul_rn(st->t_cur, p.upper);
                     done = 0;
@@ -690,9 +718,16 @@ struct EmitOut {
     void* values;
     void* indices;
     int32_t vdtype, idtype;
+    uint64_t* queue;     // non-null: K5 candidate gather (queue[pos] = key << 32 | pos, cand[pos] = index)
+    int64_t* cand;
 };
 
 __device__ __forceinline__ void emit_one(const EmitOut& o, int64_t pos, int64_t gidx, float x) {
+    if (o.queue) {
+        o.queue[pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
+        o.cand[pos] = gidx;
+        return;
+    }
     store_value(o.values, pos, x, o.vdtype);
     store_index(o.indices, pos, gidx, o.idtype);
     // scattered 4-B writes, one per 128-B line: non-temporal (no L2 allocation)
@@ -776,15 +811,20 @@ constexpr int kEmitBatch = 8;
 constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
 static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
 
+// o.queue == null: the payload (every branch but a K5 resample, which k_emit_queue
+// writes). o.queue != null: K5's candidate gather — every element >= t_cur, ascending
+// (the reference's `indices` before its resample topk), only when K5 serves the step.
 __global__ void __launch_bounds__(kEmitThreads)
 k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
     const SelState* st = w.st;
-    const bool rs = st->branch == DGC_BRANCH_RESAMPLE;
+    const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth;
+    if (k5 != (o.queue != nullptr)) return;
+    const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const int64_t g = blockIdx.x;
     const int64_t seg0 = g * kGroupSegs;
     __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs], lcn[kGroupSegs];
     __shared__ uint64_t lds16[16];
-    const long long limit = st->limit;
+    const long long limit = k5 ? st->n_cur : st->limit;
     const long long T = st->tie_quota;
     const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
     const long long gb = rs ? w.grp_eq_off[g] : 0;
@@ -854,6 +894,26 @@ k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
     }
 }
 
+// K5: the reference's resample topk replayed on the gathered candidates (introselect.hpp).
+__global__ void __launch_bounds__(kNthThreads) k_nth_select(SelWS w, int64_t k) {
+    const SelState* st = w.st;
+    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
+    nth_element_wg(w.queue, st->n_cur, k - 1, w.gpos_l, w.gpos_r);
+}
+
+// K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
+// wire casts and the masking of DGCSGDMemory.update.
+__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_in, SelWS w, EmitOut o,
+                                                      int64_t k) {
+    const SelState* st = w.st;
+    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < k; q += (int64_t)gridDim.x * kBlock) {
+        const uint32_t j = (uint32_t)w.queue[q];
+        const int64_t gidx = w.cand_idx[j];
+        emit_one(o, q, gidx, vec_in[gidx]);
+    }
+}
+
 // Result record; and the next call's speculative list threshold, margin x t_cur.
 __global__ void k_sel_finish(SelState* st, int64_t k, int64_t* count_out, dgc_select_info* info,
                              float* spec, float margin) {
@@ -870,6 +930,8 @@ __global__ void k_sel_finish(SelState* st, int64_t k, int64_t* count_out, dgc_se
         info->recounts = st->recounts;
         info->overflow_segments = st->full_passes ? st->overflow : st->list_spills;
         info->full_passes = st->full_passes;
+        info->tie_rule = st->tie_rule;
+        info->pad = 0;
     }
     if (spec) {
         // spec[0]: next call's list threshold = margin * t * growth, growth = t / spec[1]
@@ -943,12 +1005,29 @@ static int select_core(float* vec, float* mmt, const float* thr0, const dgc_sele
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    auto resample = [&]() -> int {
-        // rs state reset by k_decide when it chose the resample branch
+    EmitOut o{p->update_memory ? vec : nullptr, (p->update_memory && p->masking) ? mmt : nullptr, values,
+              indices, p->vdtype, p->idtype, nullptr, nullptr};
+    auto resample_lowest = [&]() -> int {
+        // partial_sort path (>= 64k candidates): radix k-th value, ties lowest index first.
+        // rs state reset by k_decide when it chose this path
         CandKeys src{vec, n, w};
         DGC_TRY(radix_select_passes(src, grid_for(w.nseg, kSegPerBlock4), &w.st->tk, w.rs,
                                     &w.st->resample_pending, s));
         hipLaunchKernelGGL(k_count_gt_eq, dim3(grid_cl), dim3(kBlock), 0, s, vec, n, w, (int64_t)p->num_selects);
+        DGC_LAUNCHED();
+        return DGC_OK;
+    };
+    auto resample_exact = [&]() -> int {
+        // nth_element path: gather candidates, replay the introselect, emit in its order
+        EmitOut g = o;
+        g.queue = w.queue;
+        g.cand = w.cand_idx;
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)w.ngrp), dim3(kEmitThreads), 0, s, vec, n, w, g);
+        DGC_LAUNCHED();
+        hipLaunchKernelGGL(k_nth_select, dim3(1), dim3(kNthThreads), 0, s, w, (int64_t)p->num_selects);
+        DGC_LAUNCHED();
+        hipLaunchKernelGGL(k_emit_queue, dim3(grid_for(p->num_selects)), dim3(kBlock), 0, s, vec, w, o,
+                           (int64_t)p->num_selects);
         DGC_LAUNCHED();
         return DGC_OK;
     };
@@ -967,7 +1046,7 @@ static int select_core(float* vec, float* mmt, const float* thr0, const dgc_sele
                 DGC_TRY(pass(hs.t_cur >= hs.t_list ? 1 : 2, false));
             }
         }
-        if (hs.branch == DGC_BRANCH_RESAMPLE) DGC_TRY(resample());
+        if (hs.branch == DGC_BRANCH_RESAMPLE) DGC_TRY(hs.rs_nth ? resample_exact() : resample_lowest());
     } else if (adapt) {
         // every kernel below early-exits on a device flag when it is not needed
         if (lower_fast) {
@@ -976,10 +1055,11 @@ static int select_core(float* vec, float* mmt, const float* thr0, const dgc_sele
         } else {
             for (int i = 0; i < p->max_iters; ++i) DGC_TRY(pass(3, true));
         }
-        if (p->resample) DGC_TRY(resample());
+        if (p->resample) {
+            DGC_TRY(resample_lowest());
+            DGC_TRY(resample_exact());
+        }
     }
-    EmitOut o{p->update_memory ? vec : nullptr, (p->update_memory && p->masking) ? mmt : nullptr, values,
-              indices, p->vdtype, p->idtype};
     hipLaunchKernelGGL(k_emit, dim3((unsigned)w.ngrp), dim3(kEmitThreads), 0, s, vec, n, w, o);
     DGC_LAUNCHED();
     hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, w.st, (int64_t)p->num_selects, count_out, info,
@@ -995,10 +1075,10 @@ int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p
     if (!vec || !thr0 || (p->update_memory && p->masking && !mmt))
         DGC_FAIL(DGC_ERR_INVALID, "dgc_select: null vec/thr0/mmt");
     const int64_t n = p->numel;
-    if (!ws || ws_bytes < select_ws_bytes(n) || (reinterpret_cast<uintptr_t>(ws) & 255))
+    if (!ws || ws_bytes < select_ws_bytes(n, p->num_selects) || (reinterpret_cast<uintptr_t>(ws) & 255))
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_select: workspace needs %zu bytes, 256-B aligned",
-                 select_ws_bytes(n));
-    SelWS w = carve_select(ws, n);
+                 select_ws_bytes(n, p->num_selects));
+    SelWS w = carve_select(ws, n, p->num_selects);
     return select_core(vec, mmt, thr0, p, values, indices, count_out, info, w, 0, sync_mode, nullptr, 1.f, s);
 }
 
@@ -1035,21 +1115,21 @@ struct CompressWS {
 };
 
 // sample_buf: floats reserved for the strided samples (0 when numel == num_samples)
-static CompressWS carve_compress(void* base, int64_t numel, int64_t sample_buf, size_t* bytes = nullptr) {
+static CompressWS carve_compress(void* base, int64_t numel, int64_t k, int64_t sample_buf, size_t* bytes = nullptr) {
     Carver c(base);
     CompressWS w{};
     w.thr = c.take<float>(64);
     w.rs = c.take<RSState>(1);
     w.samples = c.take<float>(sample_buf);
-    w.sel_bytes = select_ws_bytes(numel);
+    w.sel_bytes = select_ws_bytes(numel, k);
     w.sel = c.take<char>(w.sel_bytes);
     if (bytes) *bytes = c.bytes();
     return w;
 }
 
-static size_t compress_ws_bytes(int64_t numel, int64_t sample_buf) {
+static size_t compress_ws_bytes(int64_t numel, int64_t k, int64_t sample_buf) {
     size_t b = 0;
-    carve_compress(nullptr, numel, sample_buf, &b);
+    carve_compress(nullptr, numel, k, sample_buf, &b);
     return b;
 }
 
@@ -1072,9 +1152,9 @@ static int compress_check(const dgc_select_params* p, void* values, void* indice
         DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: top_k_samples %lld outside [1, %lld]",
                  (long long)top_k_samples, (long long)a->L);
     a->sbuf = a->sampled ? a->L : 0;
-    if (!ws || ws_bytes < compress_ws_bytes(a->n, a->sbuf) || (reinterpret_cast<uintptr_t>(ws) & 255))
+    if (!ws || ws_bytes < compress_ws_bytes(a->n, p->num_selects, a->sbuf) || (reinterpret_cast<uintptr_t>(ws) & 255))
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_compress: workspace needs %zu bytes, 256-B aligned",
-                 compress_ws_bytes(a->n, a->sbuf));
+                 compress_ws_bytes(a->n, p->num_selects, a->sbuf));
     return DGC_OK;
 }
 
@@ -1085,8 +1165,8 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
     CompressArgs a{};
     DGC_TRY(compress_check(p, nullptr, nullptr, s_start, s_stride, 1, ws, ws_bytes, &a, false));
     if (!grad || !mmt || !vec) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: null grad/mmt/vec");
-    CompressWS cw = carve_compress(ws, a.n, a.sbuf);
-    SelWS w = carve_select(cw.sel, a.n);
+    CompressWS cw = carve_compress(ws, a.n, p->num_selects, a.sbuf);
+    SelWS w = carve_select(cw.sel, a.n, p->num_selects);
     const bool list_path = aligned16(grad) && aligned16(mmt) && aligned16(vec) &&
                            (!a.sampled || (s_stride >= 4 && s_stride < (1LL << 30)));
     if (!list_path) {
@@ -1144,10 +1224,10 @@ int compress_finish(float* vec, float* mmt, int64_t s_start, int64_t s_stride, i
     CompressArgs a{};
     DGC_TRY(compress_check(p, values, indices, s_start, s_stride, top_k_samples, ws, ws_bytes, &a, true));
     if (!vec || (p->masking && !mmt)) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: null vec/mmt");
-    CompressWS cw = carve_compress(ws, a.n, a.sbuf);
+    CompressWS cw = carve_compress(ws, a.n, p->num_selects, a.sbuf);
     const float* src = a.sampled ? cw.samples : vec;
     DGC_TRY(kth_largest(src, a.L, top_k_samples, cw.thr, cw.rs, sizeof(RSState), s));
-    SelWS w = carve_select(cw.sel, a.n);
+    SelWS w = carve_select(cw.sel, a.n, p->num_selects);
     dgc_select_params q = *p;
     q.update_memory = 1;   // DGCSGDMemory.update fused into the emit
     return select_core(vec, mmt, cw.thr, &q, values, indices, count_out, info, w, 1, sync_mode, spec, margin, s);
@@ -1164,8 +1244,7 @@ extern "C" int dgc_kth_largest(const float* x, int64_t n, int64_t k, float* thr_
 }
 
 extern "C" size_t dgc_select_workspace(int64_t numel, int64_t num_selects) {
-    (void)num_selects;
-    return dgc::select_ws_bytes(numel);
+    return dgc::select_ws_bytes(numel, num_selects);
 }
 
 extern "C" int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_params* params,
@@ -1177,9 +1256,8 @@ extern "C" int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_s
 }
 
 extern "C" size_t dgc_compress_workspace(int64_t numel, int64_t num_selects, int64_t num_samples) {
-    (void)num_selects;
     // the strided slice holds ceil((numel - start) / stride) <= num_samples + 1 samples
-    return dgc::compress_ws_bytes(numel, numel == num_samples ? 0 : num_samples + 1);
+    return dgc::compress_ws_bytes(numel, num_selects, numel == num_samples ? 0 : num_samples + 1);
 }
 
 extern "C" int dgc_compress_begin(const float* grad, float* mmt, float* vec, float momentum, int32_t nesterov,

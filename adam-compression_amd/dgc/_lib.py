@@ -21,6 +21,7 @@ SYNC_DEVICE, SYNC_HOST = 0, 1
 VD = {torch.float32: 0, torch.float16: 1}
 ID = {torch.int64: 0, torch.int32: 1}
 BRANCHES = {0: "direct", 1: "ok", 2: "trunc", 3: "resample", 4: "exhausted"}
+TIE_RULES = {0: "none", 1: "exact", 2: "lowest_index"}
 
 
 class SelectParams(ctypes.Structure):
@@ -35,7 +36,8 @@ class SelectInfo(ctypes.Structure):
     _fields_ = [("count", ctypes.c_int64), ("candidates", ctypes.c_int64),
                 ("threshold0", ctypes.c_float), ("threshold", ctypes.c_float),
                 ("branch", ctypes.c_int32), ("recounts", ctypes.c_int32),
-                ("overflow_segments", ctypes.c_int32), ("full_passes", ctypes.c_int32)]
+                ("overflow_segments", ctypes.c_int32), ("full_passes", ctypes.c_int32),
+                ("tie_rule", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 INFO_BYTES = ctypes.sizeof(SelectInfo)
@@ -66,6 +68,7 @@ _SIGNATURES = {
     "dgc_compress_finish": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, ctypes.POINTER(SelectParams), _P, _F, _P, _P,
                                            _P, _P, _P, _SZ, _I32, _P]),
     "dgc_decompress_workspace": (_SZ, [_I64, _I32]),
+    "dgc_decompress_packed_workspace": (_SZ, [_I64, _I32, _I64]),
     "dgc_decompress": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, ctypes.POINTER(ctypes.c_int64), _I32, _P,
                                       _I64, _F, _P, _SZ, _P]),
     "dgc_payload_layout": (_I64, [_I64, _I32, _I32, ctypes.POINTER(ctypes.c_int64),
@@ -74,6 +77,8 @@ _SIGNATURES = {
     "dgc_scatter_packed": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
     "dgc_fill_zero": (ctypes.c_int, [_P, _I64, _P]),
     "dgc_decompress_status": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dgc_sgd_step": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                    ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _P]),
 }
 
 _lib = None

@@ -34,6 +34,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from . import comm
 
 __all__ = ["DGCBucket", "algorithmic_bytes"]
 
@@ -86,7 +87,7 @@ class DGCBucket:
         self.payload = torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev)
         self.gathered = (torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=dev)
                          if self.world > 1 else self.payload)
-        self.dec_ws = torch.empty(L.dgc_decompress_workspace(N, self.world), dtype=torch.uint8, device=dev)
+        self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(N, self.world, self.k), dtype=torch.uint8, device=dev)
         self.scale = 1.0 / self.world
         self._L = L
         if fill not in ("auto", "inline", "allgather"):
@@ -121,8 +122,9 @@ class DGCBucket:
                                          _lib.SYNC_DEVICE, _lib.stream_of(self.device)), "dgc_compress_finish")
 
     def exchange(self):
+        """The packed allgather (RCCL over xGMI; gloo stages through the host)."""
         if self.world > 1:
-            dist.all_gather_into_tensor(self.gathered, self.payload)
+            comm.allgather_packed_async(self.payload, out=self.gathered).wait()
 
     def decompress(self, out, dense=True):
         """dense: out = scale * (rank-order sum of the gathered entries), zeros elsewhere.
@@ -173,4 +175,5 @@ class DGCBucket:
         i = _lib.SelectInfo.from_buffer_copy(raw)
         return dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
                     branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
-                    overflow_segments=i.overflow_segments, full_passes=i.full_passes)
+                    overflow_segments=i.overflow_segments, full_passes=i.full_passes,
+                    tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule))

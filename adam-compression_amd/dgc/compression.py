@@ -297,7 +297,7 @@ class DGCCompressor:
         return dict(count=info.count, candidates=info.candidates, threshold0=info.threshold0,
                     threshold=info.threshold, branch=_lib.BRANCHES.get(info.branch, info.branch),
                     recounts=info.recounts, overflow_segments=info.overflow_segments,
-                    full_passes=info.full_passes)
+                    full_passes=info.full_passes, tie_rule=_lib.TIE_RULES.get(info.tie_rule, info.tie_rule))
 
     def decompress(self, tensor, ctx):
         """dgc/compression.py:179-198."""
@@ -311,7 +311,7 @@ class DGCCompressor:
             stream = _lib.stream_of(dev)
             if isinstance(tensor, _Gathered) and tensor.packed is not None:
                 p = tensor
-                wsz = L.dgc_decompress_workspace(numel, p.world)
+                wsz = L.dgc_decompress_packed_workspace(numel, p.world, p.capacity)
                 ws = self._ws.get(dev, wsz, "decompress")
                 vd = _lib.VD[p.vdtype]
                 idd = _lib.ID[p.idtype]

@@ -1,4 +1,4 @@
-"""DGC's SGD step (dgc/optim/sgd.py:9-71).
+"""DGC's SGD step — drop-in for the reference ``dgc/optim/sgd.py`` (``DGCSGD``, :9-71).
 
 The gradient's momentum is already applied by ``DGCSGDMemory.compensate``, so the
 optimizer keeps momentum only for the weight-decay term: with weight decay wd,
@@ -6,8 +6,15 @@ optimizer keeps momentum only for the weight-decay term: with weight decay wd,
 first step); ``d = d + momentum * buf`` (nesterov) or ``d = buf``; then
 ``p -= lr * (d + grad)``. Without weight decay ``p -= lr * grad``.
 
-This step sits after the hot path; it runs as torch ops.
+On the MI355X every parameter group is ONE fused pass (``dgc_sgd_step``, K7 in
+``csrc/sgd.hip``): read p, grad (+ the momentum buffer), write p (+ buffer), with
+the reference's torch-CPU rounding (``add(alpha)`` is one fused multiply-add), so the
+weights are bit-identical to the reference's. Parameters that live on the CPU (the
+gloo plumbing tests) take the reference's own op sequence. The optimizer state keeps
+the reference's layout (``state[p]["momentum_buffer"]``).
 """
+import ctypes
+
 import torch
 from torch.optim.optimizer import Optimizer, required
 
@@ -32,6 +39,53 @@ class DGCSGD(Optimizer):
         for group in self.param_groups:
             group.setdefault("nesterov", False)
 
+    @staticmethod
+    def _cpu_param(p, d_p, group, state):
+        """The reference's op sequence (dgc/optim/sgd.py:50-68) for a CPU parameter."""
+        wd, mom = group["weight_decay"], group["momentum"]
+        if wd == 0:
+            p.add_(d_p, alpha=-group["lr"])
+            return
+        d = wd * p.data
+        if mom != 0:
+            buf = state.get("momentum_buffer")
+            if buf is None:
+                buf = state["momentum_buffer"] = d
+            else:
+                buf.mul_(mom).add_(d, alpha=1 - group["dampening"])
+            d = d.add(buf, alpha=mom) if group["nesterov"] else buf
+        p.add_(d.add(d_p), alpha=-group["lr"])
+
+    def _fused_group(self, group, params):
+        """One dgc_sgd_step launch (per 48 tensors) over the group's CUDA parameters."""
+        from dgc import _lib
+        wd, mom = float(group["weight_decay"]), float(group["momentum"])
+        use_buf = wd != 0 and mom != 0
+        n = len(params)
+        P, G, B = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+        N, F = (ctypes.c_int64 * n)(), (ctypes.c_int32 * n)()
+        keep = []
+        for i, p in enumerate(params):
+            g = p.grad
+            _lib.require_cuda_f32(p.data, "DGCSGD.step")
+            _lib.require_cuda_f32(g, "DGCSGD.step")
+            if g.device != p.device:
+                raise ValueError("DGCSGD.step: parameter and gradient on different devices")
+            P[i], G[i], N[i] = p.data.data_ptr(), g.data_ptr(), p.numel()
+            if use_buf:
+                state = self.state[p]
+                buf = state.get("momentum_buffer")
+                F[i] = int(buf is None)
+                if buf is None:
+                    buf = state["momentum_buffer"] = torch.empty_like(p.data)
+                _lib.require_cuda_f32(buf, "DGCSGD.step")
+                B[i] = buf.data_ptr()
+            keep.append(g)
+        dev = params[0].device
+        L = _lib.lib()
+        _lib.check(L.dgc_sgd_step(P, G, B, N, F, n, float(group["lr"]), mom, float(group["dampening"]), wd,
+                                  int(bool(group["nesterov"])), _lib.stream_of(dev)), "dgc_sgd_step")
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -39,22 +93,14 @@ class DGCSGD(Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for group in self.param_groups:
-            wd, mom = group["weight_decay"], group["momentum"]
-            damp, nest, lr = group["dampening"], group["nesterov"], group["lr"]
+            by_dev = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if wd == 0:
-                    p.add_(p.grad, alpha=-lr)
-                    continue
-                d = wd * p.data
-                if mom != 0:
-                    state = self.state[p]
-                    buf = state.get("momentum_buffer")
-                    if buf is None:
-                        buf = state["momentum_buffer"] = d
-                    else:
-                        buf.mul_(mom).add_(d, alpha=1 - damp)
-                    d = d.add(buf, alpha=mom) if nest else buf
-                p.add_(d.add(p.grad), alpha=-lr)
+                if p.is_cuda:
+                    by_dev.setdefault(p.device, []).append(p)
+                else:
+                    self._cpu_param(p, p.grad, group, self.state[p])
+            for params in by_dev.values():
+                self._fused_group(group, params)
         return loss

@@ -93,8 +93,48 @@ def pmc_traffic(kernel_key="k_compensate_list"):
     return None, None
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, environ):
+    """How ``bench.py --gpus N`` runs: None when this process is one rank already
+    (torchrun set WORLD_SIZE, or N == 1), else the environments of N child ranks to
+    spawn on 127.0.0.1. Raises SystemExit when --gpus disagrees with WORLD_SIZE."""
+    if "WORLD_SIZE" in environ:
+        world = int(environ["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; they must agree")
+        return None
+    if gpus <= 1:
+        return None
+    port = str(free_port())
+    envs = []
+    for r in range(gpus):
+        env = dict(environ)
+        env.update(WORLD_SIZE=str(gpus), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        envs.append(env)
+    return envs
+
+
+def spawn(envs):
+    """One child process per rank (started before this process touches the GPU);
+    returns the first non-zero exit code, or 0."""
+    import subprocess
+    procs = [subprocess.Popen([sys.executable] + sys.argv, env=e) for e in envs]
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c != 0), 0)
+
+
 def main():
     args = parse()
+    envs = launch_plan(args.gpus, os.environ)
+    if envs is not None:
+        sys.exit(spawn(envs))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -20,6 +20,7 @@
  *                         concatenation of the allgather     dgc/compression.py:200-212
  *   dgc_decompress_packed the same, straight from the padded RCCL allgather buffer
  *   dgc_scatter_packed    its sparse form (zero_() done earlier by dgc_fill_zero)
+ *   dgc_sgd_step          DGCSGD.step (weight-decay momentum + update) dgc/optim/sgd.py:42-68
  *
  * Conventions
  *   - All tensor pointers are DEVICE pointers owned by the caller (PyTorch's caching
@@ -70,6 +71,15 @@ enum dgc_branch {
     DGC_BRANCH_EXHAUSTED = 4  /* max_adaptation_iters recounts used up    */
 };
 
+/* How a resample chose among the candidates tied at its k-th value. */
+enum dgc_tie_rule {
+    DGC_TIES_NONE = 0,          /* no resample this call                                   */
+    DGC_TIES_EXACT = 1,         /* torch's CPU topk replayed (nth_element path, k*64 > n):  */
+                                /* the reference's indices in the reference's order         */
+    DGC_TIES_LOWEST_INDEX = 2   /* partial_sort path (k*64 <= n candidates, not replayed):  */
+                                /* strictly greater, then the lowest-index ties, ascending  */
+};
+
 /* Per-tensor selection parameters: DGCCompressor.attributes[name]
  * (dgc/compression.py:85) plus the compressor's knobs (dgc/compression.py:18-54). */
 typedef struct dgc_select_params {
@@ -100,6 +110,8 @@ typedef struct dgc_select_info {
     int32_t recounts;         /* adaptation recounts executed               */
     int32_t overflow_segments;/* segments whose candidate list spilled      */
     int32_t full_passes;      /* full re-reads of vec (0: served by the K1 lists) */
+    int32_t tie_rule;         /* enum dgc_tie_rule                          */
+    int32_t pad;
 } dgc_select_info;
 
 const char* dgc_last_error(void);
@@ -184,6 +196,10 @@ int dgc_decompress(const void* values, int32_t vdtype, const void* indices, int3
  * rank r starts at payload + r * rank_stride. */
 int64_t dgc_payload_layout(int64_t capacity, int32_t vdtype, int32_t idtype,
                            int64_t* values_offset, int64_t* indices_offset);
+/* Workspace of dgc_decompress_packed / dgc_scatter_packed: it includes the area in
+ * which a rank's run that is not in ascending index order (the reference's resample
+ * sends torch.topk's order, dgc/compression.py:134-137) is regrouped by chunk. */
+size_t dgc_decompress_packed_workspace(int64_t n, int32_t world, int64_t capacity);
 int dgc_decompress_packed(const void* payload, int32_t world, int64_t rank_stride,
                           int64_t capacity, int32_t vdtype, int32_t idtype,
                           float* grad, int64_t n, float scale, void* ws, size_t ws_bytes,
@@ -199,9 +215,20 @@ int dgc_scatter_packed(const void* payload, int32_t world, int64_t rank_stride, 
 int dgc_fill_zero(float* grad, int64_t n, void* stream);
 
 /* Status word written by the decompress kernels: bit 0 = an index was out of
- * range [0, n) and was ignored; bit 1 = a run given by run_offsets was not
- * non-decreasing (its stray entries were ignored). Reads 4 bytes from the workspace (synchronous). */
+ * range [0, n) and was ignored; bit 1 = a run was not non-decreasing. Packed runs
+ * are then regrouped and summed exactly (indices unique within a run); a run given by
+ * run_offsets to dgc_decompress is not regrouped (its stray entries were ignored).
+ * Reads 4 bytes from the workspace (synchronous). */
 int dgc_decompress_status(const void* ws, int32_t* status, void* stream);
+
+/* ---- K7: DGCSGD.step over `count` parameters of one group (dgc/optim/sgd.py:42-68) ----
+ * params[i], grads[i] (and bufs[i], the momentum_buffer, when weight_decay != 0 and
+ * momentum != 0) are fp32 device arrays of numels[i] elements; first[i] = 1 when the
+ * buffer is created on this step (buf = wd * p). Rounding follows the reference's
+ * torch-CPU ops (add with alpha is one fused multiply-add). Stream-ordered. */
+int dgc_sgd_step(float* const* params, const float* const* grads, float* const* bufs, const int64_t* numels,
+                 const int32_t* first, int32_t count, float lr, float momentum, float dampening,
+                 float weight_decay, int32_t nesterov, void* stream);
 
 #ifdef __cplusplus
 }

@@ -324,7 +324,26 @@ def gen_decompress(C, M, rec):
         json.dump(meta, f, indent=1)
 
 
-def gen_optimizer(C, M, H, O):
+def _trace_compress(comp, rank, trace, step):
+    """Record every compress(p.grad, name) call of one rank: the order the reference's
+    hooks fire in and the gradient each call sees (the GPU test replays both)."""
+    orig = comp.compress
+
+    def compress(tensor, name):
+        trace.setdefault((step[0], rank), []).append((name, tensor.detach().clone().numpy()))
+        return orig(tensor, name)
+
+    comp.compress = compress
+
+
+def _save_trace(label, trace, arrays, meta):
+    for (s, q), calls in sorted(trace.items()):
+        meta[f"{label}/s{s}/r{q}"] = [name for name, _ in calls]
+        for j, (name, g) in enumerate(calls):
+            arrays[f"{label}/s{s}/r{q}/{j}"] = g
+
+
+def gen_optimizer(C, M, H, O, trace=None):
     """The reference's DistributedOptimizer + DGCSGD + DGCCompressor, 2 ranks emulated
     in one process. Records the weights after every step."""
     torch.set_num_threads(1)
@@ -344,9 +363,14 @@ def gen_optimizer(C, M, H, O):
         dopt = H.DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
                                       backward_passes_per_step=1, op="Average")
         ranks.append((model, dopt, comp))
+    step_ref = [0]
+    if trace is not None:
+        for q, (_, _, comp) in enumerate(ranks):
+            _trace_compress(comp, q, trace, step_ref)
     random.seed(42)
     arrays = {}
     for s in range(steps):
+        step_ref[0] = s
         _World.registry.clear()
         _World.reduced.clear()
         rstate = random.getstate()
@@ -386,7 +410,7 @@ def _digest(model):
     return h.hexdigest()
 
 
-def gen_optimizer_resnet20(C, M, H, O):
+def gen_optimizer_resnet20(C, M, H, O, trace=None):
     """BASELINE.json configs[0]: ResNet-20 / CIFAR-shaped batches with the reference's
     configs/cifar + configs/dgc + wm5 + fp16 + int32 settings (SGD lr 0.1, momentum
     0.9, wd 1e-4, no Nesterov; DGC ratio 0.001, sample 0.01, warmup 5 epochs,
@@ -411,6 +435,10 @@ def gen_optimizer_resnet20(C, M, H, O):
         dopt = H.DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
                                       backward_passes_per_step=1, op="Average")
         ranks.append((model, dopt, comp))
+    step_ref = [0]
+    if trace is not None:
+        for q, (_, _, comp) in enumerate(ranks):
+            _trace_compress(comp, q, trace, step_ref)
     random.seed(42)
     digests, ratios = [], []
     for ei, e in enumerate(epochs):
@@ -420,6 +448,7 @@ def gen_optimizer_resnet20(C, M, H, O):
         ratios.append(ranks[0][2].compress_ratio)
         for t in range(spe):
             s = ei * spe + t
+            step_ref[0] = s
             _World.registry.clear()
             _World.reduced.clear()
             rstate = random.getstate()
@@ -450,7 +479,24 @@ def gen_optimizer_resnet20(C, M, H, O):
     print(f"optimizer_resnet20: {len(epochs) * spe} steps, ratios {ratios}, replicas bit-identical: {same}")
 
 
-GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20")
+def gen_optimizer_trace(C, M, H, O):
+    """The two DistributedOptimizer runs again, recording per step and rank the
+    compress-call order and gradients (tests/golden/optimizer_trace.*): the GPU
+    multi-rank test replays them through the product path on cuda:0 and must reach the
+    reference's weights (optimizer.npz, optimizer_resnet20.*) bit for bit."""
+    arrays, meta = {}, {}
+    t1, t2 = {}, {}
+    gen_optimizer(C, M, H, O, trace=t1)
+    gen_optimizer_resnet20(C, M, H, O, trace=t2)
+    _save_trace("tinynet", t1, arrays, meta)
+    _save_trace("resnet20", t2, arrays, meta)
+    np.savez_compressed(os.path.join(HERE, "optimizer_trace.npz"), **arrays)
+    with open(os.path.join(HERE, "optimizer_trace.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(f"optimizer_trace: {len(meta)} (step, rank) call sequences")
+
+
+GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20", "optimizer_trace")
 
 
 def main(which=GENERATORS):
@@ -466,6 +512,8 @@ def main(which=GENERATORS):
         gen_optimizer(C, M, H, O)
     if "optimizer_resnet20" in which:
         gen_optimizer_resnet20(C, M, H, O)
+    if "optimizer_trace" in which:
+        gen_optimizer_trace(C, M, H, O)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,210 @@
+"""Workers of the multi-rank GPU tests (tests/test_gpu_multirank.py): 2 processes on
+cuda:0 over gloo, running the PRODUCT path — DGCSGDMemory / DGCCompressor /
+DistributedOptimizer / DGCSGD / DGCBucket through libdgc_hip.so — with the exchange
+staged through the host by ``dgc.comm`` (gloo moves host tensors). No oracle double
+is involved: the oracle only checks.
+
+The optimizer replays use the reference's own per-step gradients and hook order
+(tests/golden/optimizer_trace.*, recorded from the reference run that produced
+optimizer.npz / optimizer_resnet20.*): a chain of autograd nodes hands each parameter
+its recorded gradient, in the recorded order, so the product DistributedOptimizer's
+grad-accumulator hooks fire exactly as the reference's did (same compress order, same
+``random.randint`` draws), then ``step()`` runs synchronize -> decompress -> DGCSGD.
+"""
+import contextlib
+import hashlib
+import io
+import json
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+for _p in (REPO, os.path.join(REPO, "adam-compression_amd"), HERE):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+GOLDEN = os.path.join(HERE, "golden")
+
+
+class _Feed(torch.autograd.Function):
+    """x -> x; backward hands ``g`` to ``p``. Chained, the last one created runs first,
+    and each parameter's AccumulateGrad (and so its DistributedOptimizer hook) runs as
+    soon as its Feed has (AccumulateGrad nodes have the top scheduling priority)."""
+
+    @staticmethod
+    def forward(ctx, x, p, g):
+        ctx.g = g
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, gx):
+        return gx, ctx.g, None
+
+
+def replay_backward(params, order, grads, dev):
+    x = torch.zeros((), device=dev)
+    for name, g in reversed(list(zip(order, grads))):
+        x = _Feed.apply(x, params[name], torch.from_numpy(np.ascontiguousarray(g)).to(dev))
+    x.backward()
+
+
+def _digest(model):
+    h = hashlib.sha256()
+    for _, p in model.named_parameters():
+        h.update(p.detach().cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def optimizer_replay_worker(rank, world, port, label, queue):
+    """label "tinynet": optimizer.npz (3 steps, nesterov DGCSGD, fp32/int64, ratio 0.01);
+    label "resnet20": BASELINE configs[0] (ResNet-20, ratio 0.001 with the 5-epoch warmup
+    0.316 -> 0.1 -> 0.001 re-initialising mid-run, fp16 values, int32 indices)."""
+    import torch.distributed as dist
+    _init(rank, world, port)
+    problems = []
+    try:
+        from dgc.comm import Average
+        from dgc.compression import DGCCompressor
+        from dgc.horovod import DistributedOptimizer
+        from dgc.memory import DGCSGDMemory
+        from dgc.optim import DGCSGD
+        from models import ResNet20, TinyNet
+        dev = torch.device("cuda:0")
+        meta = json.load(open(os.path.join(GOLDEN, "optimizer_trace.json")))
+        trace = np.load(os.path.join(GOLDEN, "optimizer_trace.npz"))
+        if label == "tinynet":
+            cfg = json.load(open(os.path.join(GOLDEN, "optimizer.json")))
+            want = np.load(os.path.join(GOLDEN, "optimizer.npz"))
+            torch.manual_seed(cfg["model_seed"])
+            model = TinyNet().to(dev)
+            comp_kw = dict(fp16_values=False, int32_indices=False, warmup_epochs=-1)
+            schedule = [(None, s) for s in range(cfg["steps"])]
+        else:
+            cfg = json.load(open(os.path.join(GOLDEN, "optimizer_resnet20.json")))
+            final = np.load(os.path.join(GOLDEN, "optimizer_resnet20.npz"))
+            torch.manual_seed(cfg["model_seed"])
+            model = ResNet20().to(dev)
+            if _digest(model) != cfg["init_digest"]:
+                problems.append(("init", "digest"))
+            comp_kw = dict(sample_ratio=cfg["sample_ratio"], fp16_values=cfg["fp16_values"],
+                           int32_indices=cfg["int32_indices"], warmup_epochs=cfg["warmup_epochs"])
+            spe = cfg["steps_per_epoch"]
+            schedule = [(e if t == 0 else None, ei * spe + t) for ei, e in enumerate(cfg["epochs"])
+                        for t in range(spe)]
+        opt = DGCSGD(model.parameters(), lr=cfg["lr"], momentum=cfg["momentum"],
+                     weight_decay=cfg["weight_decay"], nesterov=cfg["nesterov_sgd"])
+        mem = DGCSGDMemory(momentum=cfg["momentum"])
+        with contextlib.redirect_stdout(io.StringIO()):
+            comp = DGCCompressor(cfg["ratio"], memory=mem, **comp_kw)
+            mem.initialize(model.named_parameters())
+            comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                    backward_passes_per_step=1, op=Average)
+        params = dict(model.named_parameters())
+        random.seed(cfg["random_seed"])
+        calls = []
+        orig = comp.compress
+
+        def spy(tensor, name):
+            calls.append(name)
+            return orig(tensor, name)
+
+        comp.compress = spy
+        for epoch, s in schedule:
+            if epoch is not None:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    comp.warmup_compress_ratio(epoch)
+            key = f"{label}/s{s}/r{rank}"
+            order = meta[key]
+            grads = [trace[f"{key}/{j}"] for j in range(len(order))]
+            calls.clear()
+            replay_backward(params, order, grads, dev)
+            if calls != order:
+                problems.append(("hook order", s))
+            dopt.step()
+            dopt.zero_grad()
+            torch.cuda.synchronize()
+            if label == "tinynet":
+                for n, p in model.named_parameters():
+                    w = want[f"s{s}/r{rank}/{n}"]
+                    got = p.detach().cpu().numpy()
+                    if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
+                        problems.append(("weights", s, n, float(np.abs(got - w).max())))
+            elif _digest(model) != cfg["step_digests"][s][rank]:
+                problems.append(("step digest", s))
+        if label == "resnet20":
+            for n, p in model.named_parameters():
+                got = p.detach().cpu().numpy()
+                w = final[f"final/{n}"]
+                if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
+                    problems.append(("final", n, float(np.abs(got - w).max())))
+        queue.put((rank, problems))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        queue.put((rank, [("error", repr(e), traceback.format_exc())]))
+    finally:
+        dist.destroy_process_group()
+
+
+def bucket_worker(rank, world, port, fill, kind, queue):
+    """DGCBucket at W=2 (fixed-capacity packed payload, allgather, sparse or dense
+    decompress) against the oracle over both ranks' payloads, step by step."""
+    import torch.distributed as dist
+    _init(rank, world, port)
+    problems = []
+    try:
+        from dgc.bucket import DGCBucket
+        from oracle import dgc_oracle as O
+        from oracle import synth
+        dev = torch.device("cuda:0")
+        N, ratio = 3_000_017, 0.001
+        b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=dev, world_size=world,
+                      seed=42, fill=fill)
+        attrs = O.attributes(N, ratio)
+        state = [(np.zeros(N, np.float32), np.zeros(N, np.float32)) for _ in range(world)]
+        rng = random.Random(42)
+        out = torch.full((N,), float("nan"), device=dev)
+        branches = []
+        for s in range(5):
+            gs = [synth.gradient(100 * s + q, N, kind) for q in range(world)]
+            start = rng.randint(0, attrs[4] - 1)
+            b.step(torch.from_numpy(gs[rank]).to(dev), out)
+            torch.cuda.synchronize()
+            vals, idxs = [], []
+            for q in range(world):
+                m, v = state[q]
+                ov, oi, info = O.compress_step(gs[q], m, v, attrs, start, nesterov=True)
+                vals.append(ov)
+                idxs.append(oi)
+                if q == rank:
+                    branches.append(info["branch"])
+                    if not (np.array_equal(b.vec.cpu().numpy().view(np.uint32), v.view(np.uint32)) and
+                            np.array_equal(b.mmt.cpu().numpy().view(np.uint32), m.view(np.uint32))):
+                        problems.append(("state", s))
+                    n = b.last_info()["count"]
+                    pi = b.payload[b.ioff: b.ioff + 8 * n].view(torch.int64).cpu().numpy()
+                    if not np.array_equal(pi, oi):
+                        problems.append(("indices", s, info["branch"]))
+            want = O.decompress(vals, idxs, N, world)
+            if not np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32)):
+                problems.append(("decompress", s, branches[-1]))
+        queue.put((rank, problems + [("branches", branches)]))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        queue.put((rank, [("error", repr(e), traceback.format_exc())]))
+    finally:
+        dist.destroy_process_group()

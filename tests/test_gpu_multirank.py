@@ -1,0 +1,60 @@
+"""The product path at world size 2 on one MI355X: two processes on cuda:0 over gloo
+(dgc.comm stages the exchange through the host), everything else the HIP path —
+compress (K1/K3/K4/K5), the packed allgather, synchronize, the packed decompress with
+its regrouping of topk-ordered runs, DGCSGD's fused step.
+
+* The reference's DistributedOptimizer runs (optimizer.npz: 3 steps; ResNet-20 =
+  BASELINE configs[0]: 6 steps over the 0.316 -> 0.1 -> 0.001 warmup with
+  re-initialisation, fp16 values / int32 indices) are replayed from the recorded
+  per-step gradients and hook order; the weights must equal the reference's bit for bit.
+* DGCBucket at W=2, both fill modes, against the oracle over both ranks' payloads.
+"""
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import dist_helpers as H
+import gpu_dist_helpers as G
+
+pytestmark = pytest.mark.gpu
+
+
+def run(fn, world, *args):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = H.free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=150)
+        if p.exitcode is None:
+            p.kill()
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    out = {}
+    while not q.empty():
+        rank, res = q.get()
+        out[rank] = res
+    assert sorted(out) == list(range(world))
+    return out
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("label", ["tinynet", "resnet20"])
+def test_distributed_optimizer_w2_reproduces_reference_weights(label):
+    out = run(G.optimizer_replay_worker, 2, label)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("fill,kind", [("inline", "normal"), ("allgather", "normal"), ("allgather", "layered")])
+def test_bucket_w2_matches_oracle(fill, kind):
+    out = run(G.bucket_worker, 2, fill, kind)
+    for rank, res in out.items():
+        problems = [r for r in res if r[0] != "branches"]
+        assert problems == [], (rank, res)
+    if kind == "layered":
+        assert "resample" in dict(out[0])["branches"]

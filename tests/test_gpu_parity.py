@@ -225,6 +225,43 @@ def test_select_matches_oracle(L, case, thr_scale):
         assert inf.overflow_segments > 0      # the spill path really ran
 
 
+RESAMPLE_CASES = [
+    # name, N, ratio, kind, candidates targeted at the given threshold
+    ("lds_only", 400_000, 0.001, "normal", 3_000),          # <= 12288 candidates: LDS phase only
+    ("global_phase", 2_000_003, 0.001, "normal", 60_000),   # global-memory partitions first
+    ("bf16_ties", 1_000_000, 0.001, "bf16", 20_000),        # dense boundary ties
+    ("int_ties", 300_000, 0.002, "ties", 30_000),           # every key tied many times
+    ("near_64k", 100_000, 0.001, "normal", 6_390),          # k * 64 > n just barely (nth path)
+    ("big", 20_000_000, 0.001, "normal", 1_000_000),        # 1M candidates: many global steps
+]
+
+
+@pytest.mark.parametrize("case", RESAMPLE_CASES, ids=[c[0] for c in RESAMPLE_CASES])
+def test_resample_replays_torch_topk(L, case):
+    """K5: the resample's indices are torch.topk(importance[indices], k, sorted=False)'s,
+    IN ORDER (dgc/compression.py:134-137), so the payload bytes equal the reference's."""
+    name, n, ratio, kind, target = case
+    attrs = O.attributes(n, ratio)
+    k = attrs[1]
+    vec = synth.gradient(zlib.crc32(name.encode()) % 997, n, kind)
+    mmt = synth.gradient(5, n)
+    imp = np.abs(vec)
+    t0 = np.float32(np.partition(imp, n - target)[n - target])
+    ov, oi, info = O.sparsify(vec, attrs, threshold=t0)
+    assert info["branch"] == "resample" and info["counts"][0] < 64 * k, info["counts"]
+    cand = np.flatnonzero(imp >= t0)
+    want = cand[torch.topk(torch.from_numpy(imp[cand]), k, 0, largest=True, sorted=False)[1].numpy()]
+    assert np.array_equal(oi, want)                       # the oracle is torch's topk
+    for sync in (1, 0):
+        gv, gi, gvec, gmmt, branch, inf = select_dev(L, vec, mmt, t0, attrs, sync=sync)
+        assert branch == "resample" and inf.tie_rule == 1, (name, sync)
+        assert np.array_equal(gi, want), (name, sync)
+        assert np.array_equal(bits(gv), bits(vec[want])), (name, sync)
+        ev, em = vec.copy(), mmt.copy()
+        O.update(em, ev, want, True)
+        assert np.array_equal(bits(gvec), bits(ev)) and np.array_equal(bits(gmmt), bits(em))
+
+
 @pytest.mark.parametrize("fp16,int32,masking,update", [(True, True, True, True), (False, True, False, True),
                                                         (True, False, True, False)])
 def test_select_wire_and_memory_flags(L, fp16, int32, masking, update):
@@ -358,7 +395,7 @@ def test_decompress_packed_and_repeats(L):
         idxs.append(i)
     want = O.decompress(vals, idxs, N, W)
     grad = torch.empty(N, device=DEV)
-    wsz = L.dgc_decompress_workspace(N, W)
+    wsz = L.dgc_decompress_packed_workspace(N, W, cap)
     ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
     tp = to_dev(payload)
     check(L, L.dgc_decompress_packed(P(tp), W, stride, cap, 0, 0, P(grad), N, 1.0 / W, P(ws), wsz,
@@ -405,16 +442,21 @@ def _packed(L, runs, cap, fp16, int32):
     return payload, stride, vd, idt
 
 
-@pytest.mark.parametrize("N,W,cap,overlap,fp16,int32", [
-    (1_000_003, 1, 1000, 0.0, False, False),     # single run: thread per entry
-    (1_000_003, 1, 1000, 0.0, True, True),
-    (1_000_003, 2, 1000, 0.5, False, False),     # wave per super-chunk, cross-rank duplicates
-    (1_000_003, 8, 1000, 0.3, True, False),
-    (1_000_000, 4, 10000, 0.2, False, False),    # ~160 per chunk: overflow to the staged workgroup path
-    (300_000, 8, 30000, 0.3, False, True),       # denser: the workgroup path's LDS accumulate
-    (50_000, 5, 20000, 0.9, False, False),       # > kStage entries per chunk: LDS accumulate
+@pytest.mark.parametrize("N,W,cap,overlap,fp16,int32,shuffled", [
+    (1_000_003, 1, 1000, 0.0, False, False, 0),     # single run: thread per entry
+    (1_000_003, 1, 1000, 0.0, True, True, 0),
+    (1_000_003, 2, 1000, 0.5, False, False, 0),     # wave per super-chunk, cross-rank duplicates
+    (1_000_003, 8, 1000, 0.3, True, False, 0),
+    (1_000_000, 4, 10000, 0.2, False, False, 0),    # ~160 per chunk: overflow to the staged workgroup path
+    (300_000, 8, 30000, 0.3, False, True, 0),       # denser: the workgroup path's LDS accumulate
+    (50_000, 5, 20000, 0.9, False, False, 0),       # > kStage entries per chunk: LDS accumulate
+    # runs in a resample's topk order (not ascending): regrouped by chunk, same sums
+    (1_000_003, 1, 1000, 0.0, False, False, 1),
+    (1_000_003, 2, 1000, 0.5, False, False, 1),     # rank 0 shuffled only
+    (1_000_003, 8, 1000, 0.3, True, True, 2),       # every rank shuffled
+    (300_000, 8, 30000, 0.3, False, False, 2),      # crowded chunks after regrouping
 ])
-def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, int32):
+def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, int32, shuffled):
     """dgc_fill_zero + dgc_scatter_packed == dgc_decompress_packed == the oracle, bit for bit."""
     rng = np.random.default_rng(N + W)
     shared = np.sort(rng.choice(N, cap, replace=False))
@@ -424,12 +466,16 @@ def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, in
         own = rng.choice(N, c, replace=False)
         pick = rng.random(c) < overlap
         idx = np.unique(np.where(pick, shared[:c], own))[:c]
-        runs.append((rng.standard_normal(idx.size).astype(np.float32), idx.astype(np.int64)))
+        v = rng.standard_normal(idx.size).astype(np.float32)
+        if shuffled == 2 or (shuffled == 1 and r == 0):
+            o = rng.permutation(idx.size)
+            v, idx = v[o], idx[o]
+        runs.append((v, idx.astype(np.int64)))
     payload, stride, vd, idt = _packed(L, runs, cap, fp16, int32)
     wv = [v.astype(np.float16).astype(np.float32) if fp16 else v for v, _ in runs]
     want = O.decompress(wv, [i for _, i in runs], N, W)
     tp = to_dev(payload)
-    wsz = L.dgc_decompress_workspace(N, W)
+    wsz = L.dgc_decompress_packed_workspace(N, W, cap)
     ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
     dense = torch.full((N,), float("nan"), device=DEV)
     check(L, L.dgc_decompress_packed(P(tp), W, stride, cap, vd, idt, P(dense), N, 1.0 / W, P(ws), wsz, stream()))
@@ -439,7 +485,7 @@ def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, in
     st = ctypes.c_int32(-1)
     check(L, L.dgc_decompress_status(P(ws), ctypes.byref(st), stream()))
     torch.cuda.synchronize()
-    assert st.value == 0
+    assert st.value == (2 if shuffled else 0)
     assert np.array_equal(bits(dense.cpu().numpy()), bits(want))
     assert np.array_equal(bits(sparse.cpu().numpy()), bits(want))
 
@@ -451,7 +497,7 @@ def test_sparse_scatter_flags_out_of_range(L):
                [(np.ones(2, np.float32), np.array([3, 7], np.int64))] * (W - 1)
         payload, stride, vd, idt = _packed(L, runs, cap, False, False)
         tp = to_dev(payload)
-        wsz = L.dgc_decompress_workspace(N, W)
+        wsz = L.dgc_decompress_packed_workspace(N, W, cap)
         ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
         out = torch.empty(N, device=DEV)
         check(L, L.dgc_fill_zero(P(out), N, stream()))

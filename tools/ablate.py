@@ -114,7 +114,7 @@ def main():
             row[:8].view(torch.int64).fill_(k)
             row[voff:voff + 4 * k].view(torch.float32).copy_(vals)
             row[ioff:ioff + 8 * k].view(torch.int64).copy_(idx)
-        ws = torch.empty(L.dgc_decompress_workspace(N, W), dtype=torch.uint8, device=dev)
+        ws = torch.empty(L.dgc_decompress_packed_workspace(N, W, k), dtype=torch.uint8, device=dev)
 
         def dec():
             _lib.check(L.dgc_decompress_packed(pay.data_ptr(), W, stride, k, 0, 0, out.data_ptr(), N, 1.0 / W,

@@ -54,7 +54,7 @@ def main():
         row[ioff:ioff + 8 * k].view(torch.int64).copy_(idx)
         del idx
     out = torch.empty(N, device=dev)
-    ws = torch.empty(L.dgc_decompress_workspace(N, W), dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.dgc_decompress_packed_workspace(N, W, k), dtype=torch.uint8, device=dev)
     s = _lib.stream_of(dev)
 
     def fill():
