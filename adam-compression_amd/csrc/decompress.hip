@@ -390,7 +390,7 @@ __device__ void tile_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__
 template <int VD, int ID>
 __global__ void __launch_bounds__(kBlock)
 k_scatter_single(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
-    const Run run = rs.get(0);
+    const Run run = rs.get_raw(0);   // any order: one run's unique indices need no regrouping
     const long long j = (long long)blockIdx.x * kBlock + threadIdx.x;
     if (j >= run.count) return;
     const long long i = load_idx<ID>(run.idx, j);
@@ -570,6 +570,7 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
                        bool dense, int64_t entries, int64_t run_cap, int runs, hipStream_t s) {
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
     if (dense) DGC_TRY(fill_zero(grad, n, s));
+    if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
     if (runs == 1) {   // a thread per entry
         DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
         if (entries > 0) {
@@ -584,7 +585,6 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
     // this call can set them
     DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
     DGC_HIP(hipMemsetAsync(w.ovf_cnt, 0, sizeof(int32_t), s));
-    if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
     hipLaunchKernelGGL(k_bounds<ID>, dim3(bx, (unsigned)max_runs), dim3(kBlock), 0, s, w, rs, n, run_cap);
     DGC_LAUNCHED();
     if (w.sort_cap) {
