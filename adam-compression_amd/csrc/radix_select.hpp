@@ -1,22 +1,25 @@
-// K3: k-th largest |x| by MSB-first radix select on the fp32 bit pattern.
+// K3: k-th largest |x| by MSB-first radix select on the fp32 bit pattern, for one
+// or many independent key sets in the same launches.
 //
 // Replaces torch.min(torch.topk(samples, k, sorted=False)[0]) (dgc/compression.py:123)
-// and, over the candidate set, the resample topk (dgc/compression.py:134-137).
+// per compressed tensor and, over the candidate set, the value of the resample topk's
+// k-th key on its partial_sort path (dgc/compression.py:134-137).
 //
 // Keys are |x| bit patterns (sign cleared): for non-negative floats uint order is
 // float order, +0 == -0, and NaN keys (> 0x7F800000) sort above +inf exactly as
 // topk ranks NaN. torch.min over a top-k set that holds a NaN returns NaN, so the
 // result is NaN whenever any NaN key exists (counted in pass 0).
 //
-// Digits: 11 + 11 + 10 bits (2048/2048/1024 bins). One launch per pass: every
-// workgroup builds an LDS histogram of the keys that match the current prefix and
-// flushes its non-zero bins with 64-bit device atomics; the LAST workgroup to
-// arrive (agent-scope release -> ticket -> acquire, cdna_hip_programming.md G16)
-// reads the totals with agent-scope atomic loads and picks the bin holding the
-// k-th largest key, narrowing (prefix, k) for the next pass. Inputs of <= kSmallN
-// keys run all three passes inside ONE workgroup from LDS.
+// Digits: 11 + 11 + 10 bits (2048/2048/1024 bins). One launch per pass covers every
+// key set ("task"): each workgroup serves ONE task (a prefix table of block counts
+// maps blockIdx to the task), builds an LDS histogram of the task's keys that match
+// the task's current prefix and flushes its non-zero bins with 64-bit device atomics
+// into the task's state; the LAST of the task's workgroups to arrive (agent-scope
+// atomics both sides, cdna_hip_programming.md G16) picks the bin holding the k-th
+// largest key and narrows (prefix, k) for the next pass. Tasks of <= kSmallN keys run
+// all three passes inside ONE workgroup from LDS (k_rs_small, one workgroup per task).
 //
-// The scalar result is written to a device float; nothing returns to the host.
+// Results are device floats; nothing returns to the host.
 #pragma once
 
 #include "dgc_common.hpp"
@@ -43,35 +46,58 @@ __host__ __device__ constexpr uint32_t rs_pmask(int pass) {
 }
 __host__ __device__ constexpr int rs_bins(int pass) { return pass == 2 ? 1024 : 2048; }
 
-// ---------------------------------------------------------------- key sources
-// Dense array of floats (the strided samples, or a full tensor).
+// The task served by block b, from an ascending prefix table blk[0..T] of block counts
+// (blk[T] = grid): the largest t with blk[t] <= b. Every thread computes the same t.
+__device__ __forceinline__ int task_of_block(const int32_t* blk, int T, int b) {
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (blk[mid] <= b)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+// Strided visit of n floats' keys by the `nb` blocks of one task (lb = block index in the task).
+template <class F>
+__device__ __forceinline__ void visit_dense(const float* x, int64_t n, int64_t lb, int64_t nb, F&& f) {
+    const int64_t tid = lb * blockDim.x + threadIdx.x;
+    const int64_t G = nb * blockDim.x;
+    if (aligned16(x)) {
+        const int64_t n4 = n / 4;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        for (int64_t i = tid; i < n4; i += G) {
+            const float4 v = x4[i];
+            f(abs_key(v.x));
+            f(abs_key(v.y));
+            f(abs_key(v.z));
+            f(abs_key(v.w));
+        }
+        for (int64_t i = n4 * 4 + tid; i < n; i += G) f(abs_key(x[i]));
+    } else {
+        for (int64_t i = tid; i < n; i += G) f(abs_key(x[i]));
+    }
+}
+
+// One dense key set: dgc_kth_largest.
 struct DenseKeys {
     const float* x;
     int64_t n;
+    RSState* st;
+    float* result;
+    __device__ __forceinline__ int task(int) const { return 0; }
+    __device__ __forceinline__ int first_block(int) const { return 0; }
+    __device__ __forceinline__ int blocks(int) const { return (int)gridDim.x; }
+    __device__ __forceinline__ bool active(int) const { return true; }
+    __device__ __forceinline__ RSState* state(int) const { return st; }
+    __device__ __forceinline__ float* out(int) const { return result; }
     template <class F>
-    __device__ __forceinline__ void visit(F&& f) const {
-        const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        const int64_t G = (int64_t)gridDim.x * blockDim.x;
-        if (aligned16(x)) {
-            const int64_t n4 = n / 4;
-            const float4* x4 = reinterpret_cast<const float4*>(x);
-            for (int64_t i = tid; i < n4; i += G) {
-                const float4 v = x4[i];
-                f(abs_key(v.x));
-                f(abs_key(v.y));
-                f(abs_key(v.z));
-                f(abs_key(v.w));
-            }
-            for (int64_t i = n4 * 4 + tid; i < n; i += G) f(abs_key(x[i]));
-        } else {
-            for (int64_t i = tid; i < n; i += G) f(abs_key(x[i]));
-        }
+    __device__ __forceinline__ void visit(int, int64_t lb, int64_t nb, F&& f) const {
+        visit_dense(x, n, lb, nb, f);
     }
 };
-
-__device__ __forceinline__ uint64_t block_exclusive_scan_1024(uint64_t v, uint64_t* lds16, uint64_t* total) {
-    return block_exclusive_scan(v, lds16, total);
-}
 
 template <typename CountT>
 __device__ __forceinline__ uint64_t load_count(const CountT* p) {
@@ -143,14 +169,15 @@ __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
 __global__ void k_rs_init(RSState* st, uint64_t k) { rs_reset(st, k); }
 
 template <class Src>
-__global__ void __launch_bounds__(kBlock)
-k_rs_hist(Src src, RSState* st, int pass, float* out, const int32_t* gate) {
-    if (gate && *gate == 0) return;
+__global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
+    const int t = src.task(blockIdx.x);
+    if (!src.active(t)) return;   // uniform per workgroup
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t nan_cnt;
     __shared__ uint64_t lds16[16];
     __shared__ int sel_bin;
     __shared__ uint64_t sel_above;
+    RSState* st = src.state(t);
     for (int b = threadIdx.x; b < kRsBins; b += kBlock) h[b] = 0;
     if (threadIdx.x == 0) {
         nan_cnt = 0;
@@ -160,7 +187,8 @@ k_rs_hist(Src src, RSState* st, int pass, float* out, const int32_t* gate) {
     const uint32_t prefix = st->prefix;
     const uint32_t pmask = rs_pmask(pass), dmask = rs_dmask(pass);
     const int shift = rs_shift(pass);
-    src.visit([&](uint32_t key) {
+    const int b0 = src.first_block(t), nb = src.blocks(t);
+    src.visit(t, (int64_t)blockIdx.x - b0, nb, [&](uint32_t key) {
         if ((key & pmask) == prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
         if (pass == 0 && key > 0x7F800000u) atomicAdd(&nan_cnt, 1u);
     });
@@ -170,8 +198,8 @@ k_rs_hist(Src src, RSState* st, int pass, float* out, const int32_t* gate) {
         if (h[b]) atomicAdd(&gh[b], (unsigned long long)h[b]);
     if (pass == 0 && threadIdx.x == 0 && nan_cnt)
         atomicAdd((unsigned long long*)&st->nan_count, (unsigned long long)nan_cnt);
-    if (!last_block_arrival(&st->tickets[pass], gridDim.x)) return;
-    // the last workgroup picks the bin for everyone
+    if (!last_block_arrival(&st->tickets[pass], (uint32_t)nb)) return;
+    // the last workgroup of the task picks the bin for the task
     const uint64_t k = st->k_rem;
     int bin;
     uint64_t above;
@@ -181,6 +209,7 @@ k_rs_hist(Src src, RSState* st, int pass, float* out, const int32_t* gate) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        float* out = src.out(t);
         if (sel_bin < 0) {
             st->found = 0;   // k exceeded the key count: report NaN
             if (out) *out = __uint_as_float(0x7FC00000u);
@@ -197,9 +226,9 @@ k_rs_hist(Src src, RSState* st, int pass, float* out, const int32_t* gate) {
     }
 }
 
-// All three passes in one 1024-thread workgroup, keys staged in LDS.
-__global__ void __launch_bounds__(kScanThreads)
-k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
+// All three passes of one key set of <= kSmallN keys in ONE 1024-thread workgroup,
+// keys staged in LDS: x[0..n) -> *out = k-th largest |x| (NaN if any |x| is NaN).
+__device__ void rs_small_wg(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
     __shared__ uint32_t keys[kSmallN];
     __shared__ uint32_t h[kRsBins];
     __shared__ uint64_t lds16[16];
@@ -246,27 +275,24 @@ k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
     }
     if (threadIdx.x == 0)
         *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
+    __syncthreads();
 }
 
-// The three histogram passes over any key source; the state must have been reset
-// (k_rs_init, or fused into an earlier kernel) with k. `gate` (device int, may be
-// null) turns every launch into a no-op when zero.
+__global__ void __launch_bounds__(kScanThreads)
+k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
+    rs_small_wg(x, n, k, out);
+}
+
+// The three histogram passes over any task source; every active task's state must
+// have been reset with its k (rs_reset).
 template <class Src>
-inline int radix_select_passes(const Src& src, int grid, float* out, RSState* st, const int32_t* gate,
-                               hipStream_t s) {
+inline int radix_select_passes(const Src& src, int grid, hipStream_t s) {
+    if (grid <= 0) return DGC_OK;
     for (int pass = 0; pass < 3; ++pass) {
-        hipLaunchKernelGGL((k_rs_hist<Src>), dim3(grid), dim3(kBlock), 0, s, src, st, pass, out, gate);
+        hipLaunchKernelGGL((k_rs_hist<Src>), dim3(grid), dim3(kBlock), 0, s, src, pass);
         DGC_LAUNCHED();
     }
     return DGC_OK;
-}
-
-template <class Src>
-inline int radix_select_launch(const Src& src, int64_t work_items, uint64_t k, float* out, RSState* st,
-                               hipStream_t s) {
-    hipLaunchKernelGGL(k_rs_init, dim3(1), dim3(kBlock), 0, s, st, k);
-    DGC_LAUNCHED();
-    return radix_select_passes(src, grid_for(work_items, kBlock * 16, 512), out, st, nullptr, s);
 }
 
 }  // namespace dgc

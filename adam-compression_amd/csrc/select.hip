@@ -1,40 +1,50 @@
 // K4: selection — the `importance >= threshold` mask, `nonzero()`, the adaptation
 // loop, resample, truncation, value gather, momentum masking and wire packing —
-// plus the listing K1 of the fused compress.
+// plus the listing K1 of the fused compress and the K3 thresholds, for ONE tensor or
+// for a BATCH of T tensors in the same launches.
 //
 // Reference: DGCCompressor._sparsify (dgc/compression.py:109-153),
 // DGCSGDMemory.update (dgc/memory.py:72-77), compress's casts (dgc/compression.py:168-171),
-// compress's call order (dgc/compression.py:155-172).
+// compress's call order (dgc/compression.py:155-172); the batch serves every
+// compressed tensor of a step, which the reference handles one hook at a time
+// (dgc/horovod/optimizer.py:116-155).
 //
-// Layout. vec is cut into SEGMENTS of 1024 elements; 1024 segments form a GROUP
-// (the scan granule and one emit workgroup). Every segment owns a candidate list of
-// kCap = 64 slots (u16 offset + the fp32 value, ascending) and two exact counts:
-// seg_lcnt at the LIST threshold t_list (a list is complete iff seg_lcnt <= kCap; a
+// Layout. A tensor's elements are cut into SEGMENTS of 1024; 1024 segments form a
+// GROUP (the scan granule and one emit workgroup). In a batch the tensors sit at
+// segment-aligned offsets of flat grad/mmt/vec buffers; segments and groups are
+// numbered globally, and every launch maps each workgroup to ONE tensor through a
+// prefix table of per-tensor block counts (task_of_block), so per-tensor state,
+// per-tensor tickets and group atomics never mix tensors. Every segment owns a
+// candidate list of kCap = 64 slots (u16 offset + fp32 value, ascending) and two
+// exact counts: seg_lcnt at the LIST threshold t_list (complete iff <= kCap; a
 // spilled segment is re-read from vec when needed) and seg_cnt at the current
 // threshold t_cur >= t_list.
 //
-// Speculative listing. The fused compress lists candidates INSIDE K1, at
-// t_list = margin x (the previous call's final threshold), kept on device. When the
-// sampled threshold comes out >= t_list — the steady state — every count and every
-// selection is served from the lists and the separate 4 B/elem re-read of vec
-// disappears; otherwise a full select pass at t_cur re-lists (t_list := t_cur).
+// Speculative listing. K1 lists candidates at t_list = margin x (the previous call's
+// final threshold), per tensor. When the sampled threshold comes out >= t_list — the
+// steady state — every count and selection is served from the lists and the separate
+// 4 B/elem re-read of vec disappears; otherwise a full select pass at t_cur re-lists.
 // Results are identical either way: a list at t_list holds EVERY element >= t_list.
 //
 //   count pass   t_cur >= t_list: one thread per segment counts its list entries
-//                >= t_cur (spilled segments: one wave re-reads 1024 elements);
-//                t_cur < t_list: full select pass (16 non-temporal float4 loads in
-//                flight per lane, ballot compaction, re-lists at t_cur).
-//   decide       (1 workgroup): total count -> the reference's loop step
-//                (ok / trunc / resample / lower / raise / exhausted) + scan of the
-//                group totals. resample=True: the first "lower" hands over to ONE
-//                multi-threshold pass; resample=False: a recount per step.
-//   resample     radix select of the k-th largest candidate, per-segment greater /
-//                tied counts, scans. Ties go to the lowest indices (see oracle).
-//   emit         (1 workgroup per group, 4 segments per thread): ascending positions,
-//                fp32/fp16 values, int64/int32 indices, masking writes.
+//                (spilled segments: one wave re-reads 1024 elements); else the full
+//                select pass (16 non-temporal float4 loads in flight per lane).
+//   decide       (1 workgroup per tensor): the reference's loop step (ok / trunc /
+//                resample / lower / raise / exhausted) + scan of the group totals.
+//                resample=True: the first "lower" hands over to ONE multi-threshold
+//                pass; resample=False: a recount per step.
+//   resample     nth_element path (< 64k candidates): the candidates are gathered in
+//                index order and torch's CPU topk is replayed exactly (K5,
+//                introselect.hpp); partial_sort path: radix k-th value, lowest-index ties.
+//   emit         (1 workgroup per group): positions (after the tensors before it in
+//                the batch), fp32/fp16 values, int64/int32 indices, masking writes.
 //
 // Everything is stream-ordered; in DGC_SYNC_DEVICE mode kernels that turn out to
 // be unneeded early-exit on a device flag, so no host synchronisation happens.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
 #include "radix_select.hpp"
 #include "introselect.hpp"
 
@@ -45,12 +55,33 @@ constexpr int kCap = 64;                        // list slots per segment (6.25 
 constexpr int kSegTiles = kSeg / (kWave * 4);   // 4 float4 per lane per segment
 constexpr int kSuper = 4;                       // segments per wave in the full select pass
 constexpr int kGroupSegs = 1024;                // segments per group (1M elements)
-constexpr int kSegPerBlock4 = kBlock / kWave;        // 4 waves per workgroup
+constexpr int kSegPerBlock4 = kBlock / kWave;   // 4 waves per workgroup
+constexpr int kSegPerBlock16 = kSegPerBlock4 * kSuper;
 constexpr int kMaxLower = 16;                   // thresholds per multi-threshold pass
 constexpr int kSpillShards = 64;
 constexpr int kSpillDiv = 32;                   // lists dropped when > nseg/32 segments spill
+constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgroup
+constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole batch
 
-enum { MODE_FIRSTK = 0, MODE_RESAMPLE = 1 };
+int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
+
+// One compressed tensor (device table, built on the host).
+struct TDesc {
+    int64_t n;              // numel
+    int64_t off;            // element offset in the flat grad / mmt / vec buffers (multiple of kSeg)
+    int64_t seg0, nseg;     // global segments
+    int64_t grp0, ngrp;     // global groups
+    int64_t k, S, ks, stride;          // num_selects, num_samples, top_k_samples, sample_stride
+    int64_t upper_count, lower_count;  // floor(k * upper), ceil(lower * k)
+    int64_t samp_off;       // offset of its samples in the flat sample buffer; -1: none / N == S
+    int64_t cand_off, cand_cap;        // K5 queue region: min(N, 64k - 1) candidates
+    int64_t gpos_off;       // K5 pair slots: 2 x (cand_cap / 2 + 1)
+    int64_t idx_base;       // added to the emitted indices (its flat offset in a batch, 0 alone)
+    int64_t nv4;            // float4s that K1 streams (n/4 unpadded, ceil(n/4) padded)
+    double inv_stride;
+    float inv_stride_f;
+    int32_t tail;           // the elements [4*nv4, n) are compensated outside K1 (unpadded)
+};
 
 struct SelState {
     float t0, t_cur, tk, t_list;
@@ -63,6 +94,7 @@ struct SelState {
     int32_t full_passes, list_spills, epoch;
     int32_t rs_nth;        // RESAMPLE served by the exact nth_element replay (K5)
     int32_t tie_rule;      // DGC_TIES_*: how the resample chose among boundary ties
+    int32_t pad;
     uint32_t tickets[4];
     // Segments whose K1 list overflowed, counted by K1 into slot [epoch & 1] (64
     // shards against atomic contention); k_sel_init reads it and zeroes the other
@@ -71,27 +103,43 @@ struct SelState {
     unsigned long long lower_cnt[kMaxLower + 1];   // counts at t_1..t_m (multi-threshold pass)
 };
 
+// Per-call settings shared by the tensors.
+struct SelCfg {
+    float upper, lower;         // fl32(compress_upper_bound), fl32(compress_lower_bound)
+    int32_t max_iters, resample, masking, vdtype, idtype, update_memory;
+};
+
+// Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
+enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_COUNT };
+
 struct SelWS {
+    int32_t T;
+    TDesc* td;
     SelState* st;
-    RSState* rs;
+    RSState* rs;               // [T]: K3 thresholds, then the resample's radix select
+    float* thr;                // [T] sampled thresholds
+    float* spec;               // [2T] speculative list thresholds (null: none), persistent
+    int64_t* starts;           // [T] sample starts of this call
+    int64_t* scnt;             // [T] strided sample counts of this call
+    float* samples;            // flat sample buffer
+    int32_t* bt[BT_COUNT];     // block tables
+    int32_t* small;            // tensors whose threshold runs in one workgroup
     uint32_t* seg_lcnt;
     uint32_t* seg_cnt;
     uint32_t* seg_gt;
     uint32_t* seg_eq;
     uint16_t* lst_off;
     float* lst_val;
-    unsigned long long* grp_cnt;   // grp_cnt, grp_gt, grp_eq: contiguous, zeroed by k_sel_init
+    unsigned long long* grp_cnt;   // grp_cnt, grp_gt, grp_eq: contiguous
     unsigned long long* grp_gt;
     unsigned long long* grp_eq;
     long long* grp_off;
     long long* grp_gt_off;
     long long* grp_eq_off;
-    uint64_t* queue;       // K5: (|x| key << 32 | j) for the candidates j, ascending index order
-    int64_t* cand_idx;     // K5: the candidates' element indices
-    uint32_t* gpos_l;      // K5: pair slots of the global-memory partition passes
-    uint32_t* gpos_r;
+    uint64_t* queue;           // K5: (|x| key << 32 | j) for the candidates j, ascending index order
+    int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
+    uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     int64_t nseg, ngrp;
-    int64_t cand_cap;      // K5 serves resamples of up to cand_cap candidates
 };
 
 // Candidates the exact resample replays: torch's CPU topk runs nth_element while
@@ -101,45 +149,176 @@ __host__ __device__ inline int64_t nth_cand_cap(int64_t numel, int64_t k) {
     return c < numel ? c : numel;
 }
 
-static SelWS carve_select(void* base, int64_t numel, int64_t k, size_t* bytes = nullptr) {
+// ------------------------------------------------------------------ host layout
+// Everything the host derives from the tensor list: the device table image, the
+// block tables and the workspace carve. Recomputed on every call (O(T)).
+struct TensorIn {
+    int64_t n, off, k, S, ks, stride, upper_count, lower_count;
+    bool samples;   // reserve a sample buffer (compress); false for a pure selection
+};
+
+struct Layout {
+    int32_t T = 0;
+    int64_t nseg = 0, ngrp = 0, nsamp = 0, ncand = 0, ngpos = 0;
+    int32_t nsmall = 0;
+    bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
+    int64_t grid[BT_COUNT] = {};
+};
+
+static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg) {
+    const int64_t cap = std::max<int64_t>(1, ceil_div((int64_t)kCapBlocks * d.nseg, std::max<int64_t>(1, total_seg)));
+    switch (which) {
+        case BT_K1: return ceil_div(d.nseg, (int64_t)kSegPerBlock4);
+        case BT_FULL: return ceil_div(d.nseg, (int64_t)kSegPerBlock16);
+        case BT_CAP16: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock16), cap);
+        case BT_CAP4: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock4), cap);
+        case BT_SEG: return ceil_div(d.nseg, (int64_t)kBlock);
+        case BT_GRP: return d.ngrp;
+        case BT_QUEUE: return ceil_div(d.k, (int64_t)kQueuePerBlock);
+        case BT_SAMP: {
+            const int64_t cnt = d.samp_off < 0 ? d.n : d.S + 1;
+            if (cnt <= kSmallN) return 0;   // one-workgroup threshold (k_rs_small_multi)
+            return std::min<int64_t>(512, ceil_div(cnt, (int64_t)kBlock * 16));
+        }
+    }
+    return 0;
+}
+
+static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, std::vector<TDesc>& td,
+                         std::vector<int32_t> (&bt)[BT_COUNT], std::vector<int32_t>& small) {
+    L = Layout{};
+    L.T = T;
+    td.assign(T, TDesc{});
+    small.clear();
+    int64_t seg_end = 0, grp = 0, samp = 0, cand = 0, gpos = 0;
+    for (int32_t t = 0; t < T; ++t) {
+        TDesc& d = td[t];
+        d.n = in[t].n;
+        d.off = in[t].off;
+        d.seg0 = d.off / kSeg;
+        d.nseg = ceil_div(d.n, (int64_t)kSeg);
+        d.grp0 = grp;
+        d.ngrp = ceil_div(d.nseg, (int64_t)kGroupSegs);
+        grp += d.ngrp;
+        d.k = in[t].k;
+        d.S = in[t].S;
+        d.ks = in[t].ks;
+        d.stride = in[t].stride;
+        d.upper_count = in[t].upper_count;
+        d.lower_count = in[t].lower_count;
+        const bool sampled = d.n != d.S;
+        L.adapt_any |= sampled;
+        d.samp_off = (sampled && in[t].samples) ? samp : -1;
+        if (d.samp_off >= 0) samp += (int64_t)align_up((size_t)(d.S + 1), 64);
+        d.cand_off = cand;
+        d.cand_cap = nth_cand_cap(d.n, d.k);
+        cand += d.cand_cap;
+        d.gpos_off = gpos;
+        gpos += 2 * (d.cand_cap / 2 + 1);
+        d.idx_base = T > 1 ? d.off : 0;
+        d.nv4 = padded ? ceil_div(d.n, (int64_t)4) : d.n / 4;
+        d.tail = (!padded && (d.n & 3)) ? 1 : 0;
+        d.inv_stride = 1.0 / (double)(d.stride > 0 ? d.stride : 1);
+        d.inv_stride_f = 1.0f / (float)(d.stride > 0 ? d.stride : 1);
+        seg_end = std::max(seg_end, d.seg0 + d.nseg);
+        const int64_t scnt = sampled ? d.S + 1 : d.n;
+        if (scnt <= kSmallN) small.push_back(t);
+    }
+    L.nseg = seg_end;
+    L.ngrp = grp;
+    L.nsamp = samp;
+    L.ncand = cand;
+    L.ngpos = gpos;
+    L.nsmall = (int32_t)small.size();
+    for (int which = 0; which < BT_COUNT; ++which) {
+        bt[which].assign(T + 1, 0);
+        int64_t acc = 0;
+        for (int32_t t = 0; t < T; ++t) {
+            bt[which][t] = (int32_t)acc;
+            acc += bt_blocks(which, td[t], L.nseg);
+        }
+        bt[which][T] = (int32_t)acc;
+        L.grid[which] = acc;
+    }
+}
+
+static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) {
     SelWS w{};
-    w.nseg = ceil_div(numel, kSeg);
-    w.ngrp = ceil_div(w.nseg, kGroupSegs);
+    w.T = L.T;
+    w.nseg = L.nseg;
+    w.ngrp = L.ngrp;
     Carver c(base);
-    w.st = c.take<SelState>(1);
-    w.rs = c.take<RSState>(1);
-    w.grp_cnt = c.take<unsigned long long>(3 * w.ngrp);
-    w.grp_gt = w.grp_cnt ? w.grp_cnt + w.ngrp : nullptr;
-    w.grp_eq = w.grp_gt ? w.grp_gt + w.ngrp : nullptr;
-    w.grp_off = c.take<long long>(w.ngrp);
-    w.grp_gt_off = c.take<long long>(w.ngrp);
-    w.grp_eq_off = c.take<long long>(w.ngrp);
-    w.seg_lcnt = c.take<uint32_t>(w.nseg);
-    w.seg_cnt = c.take<uint32_t>(w.nseg);
-    w.seg_gt = c.take<uint32_t>(w.nseg);
-    w.seg_eq = c.take<uint32_t>(w.nseg);
-    w.lst_off = c.take<uint16_t>(w.nseg * kCap);
-    w.lst_val = c.take<float>(w.nseg * kCap);
-    w.cand_cap = nth_cand_cap(numel, k);
-    w.queue = c.take<uint64_t>(w.cand_cap);
-    w.cand_idx = c.take<int64_t>(w.cand_cap);
-    w.gpos_l = c.take<uint32_t>(w.cand_cap / 2 + 1);
-    w.gpos_r = c.take<uint32_t>(w.cand_cap / 2 + 1);
+    w.td = c.take<TDesc>(L.T);
+    w.st = c.take<SelState>(L.T);
+    w.rs = c.take<RSState>(L.T);
+    w.thr = c.take<float>(L.T);
+    w.spec = c.take<float>(2 * L.T);
+    w.starts = c.take<int64_t>(L.T);
+    w.scnt = c.take<int64_t>(L.T);
+    for (int which = 0; which < BT_COUNT; ++which) w.bt[which] = c.take<int32_t>(L.T + 1);
+    w.small = c.take<int32_t>(L.T);
+    w.samples = c.take<float>(L.nsamp);
+    w.grp_cnt = c.take<unsigned long long>(3 * L.ngrp);
+    w.grp_gt = w.grp_cnt ? w.grp_cnt + L.ngrp : nullptr;
+    w.grp_eq = w.grp_gt ? w.grp_gt + L.ngrp : nullptr;
+    w.grp_off = c.take<long long>(L.ngrp);
+    w.grp_gt_off = c.take<long long>(L.ngrp);
+    w.grp_eq_off = c.take<long long>(L.ngrp);
+    w.seg_lcnt = c.take<uint32_t>(L.nseg);
+    w.seg_cnt = c.take<uint32_t>(L.nseg);
+    w.seg_gt = c.take<uint32_t>(L.nseg);
+    w.seg_eq = c.take<uint32_t>(L.nseg);
+    w.lst_off = c.take<uint16_t>(L.nseg * kCap);
+    w.lst_val = c.take<float>(L.nseg * kCap);
+    w.queue = c.take<uint64_t>(L.ncand);
+    w.cand_idx = c.take<int64_t>(L.ncand);
+    w.gpos = c.take<uint32_t>(L.ngpos);
     if (bytes) *bytes = c.bytes();
     return w;
 }
 
-static size_t select_ws_bytes(int64_t numel, int64_t k) {
-    size_t b = 0;
-    carve_select(nullptr, numel, k, &b);
-    return b;
+// The tables of a one-tensor call, written by one tiny kernel (no host copy).
+struct OneTable {
+    TDesc d;
+    int32_t bt[BT_COUNT][2];
+    int64_t start;
+};
+
+__global__ void k_put_one(SelWS w, OneTable o) {
+    if (threadIdx.x != 0) return;
+    w.td[0] = o.d;
+    for (int which = 0; which < BT_COUNT; ++which) {
+        w.bt[which][0] = o.bt[which][0];
+        w.bt[which][1] = o.bt[which][1];
+    }
+    w.small[0] = 0;
+    w.starts[0] = o.start;
+    const TDesc& d = o.d;
+    w.scnt[0] = d.samp_off < 0 ? d.n : ceil_div(d.n - o.start, d.stride);
+}
+
+// Per-call sample starts of a batch (random.randint per tensor, drawn on the host),
+// 64 per launch in the kernel arguments; also the sample counts.
+struct StartChunk {
+    int32_t first, count;
+    int64_t start[64];
+};
+
+__global__ void k_put_starts(SelWS w, StartChunk c) {
+    const int i = threadIdx.x;
+    if (i >= c.count) return;
+    const int t = c.first + i;
+    const TDesc& d = w.td[t];
+    w.starts[t] = c.start[i];
+    w.scnt[t] = d.samp_off < 0 ? d.n : ceil_div(d.n - c.start[i], d.stride);
 }
 
 // ------------------------------------------------------------------ tile helpers
-// Lane holds elements e0..e0+3 of a 256-element tile (e0 = tile base + 4*lane).
+// Lane holds elements e0..e0+3 of a 256-element tile (e0 = tile base + 4*lane) of a
+// tensor whose elements start at v (local indices, n of them).
 template <bool ALIGNED>
-__device__ __forceinline__ void load_tile(const float* __restrict__ v, int64_t n, int64_t e0,
-                                          float (&x)[4], uint32_t& valid) {
+__device__ __forceinline__ void load_tile(const float* __restrict__ v, int64_t n, int64_t e0, float (&x)[4],
+                                          uint32_t& valid) {
     if (ALIGNED && e0 + 3 < n) {
         const float4 q = ld_nt(reinterpret_cast<const float4*>(v + e0));
         x[0] = q.x;
@@ -187,42 +366,53 @@ __device__ __forceinline__ void list_append(uint32_t p, const float (&x)[4], int
     }
 }
 
-// Count of |x| >= t over one segment, re-read from vec by the calling wave.
-__device__ uint32_t wave_count_segment(const float* __restrict__ vec, int64_t n, int64_t seg, float t) {
+// Count of |x| >= t over local segment ls of a tensor (elements v[0..n)), re-read by the calling wave.
+__device__ uint32_t wave_count_segment(const float* __restrict__ v, int64_t n, int64_t ls, float t) {
     const int lane = threadIdx.x & 63;
     uint32_t c = 0;
     for (int tile = 0; tile < kSegTiles; ++tile) {
         float x[4];
         uint32_t valid;
-        load_tile<false>(vec, n, seg * kSeg + tile * 256 + 4 * lane, x, valid);
+        load_tile<false>(v, n, ls * kSeg + tile * 256 + 4 * lane, x, valid);
         c += __popc(ge_mask(x, valid, t));
     }
     return wave_sum(c);
 }
 
+__device__ __forceinline__ int task(const SelWS& w, int which, int b) { return task_of_block(w.bt[which], w.T, b); }
+
 // ------------------------------------------------------------------ K1 with lists
 // K1 (compensate + strided sample, see compensate.hip) that also lists every
 // element with |vec_new| >= t_list into its segment's list. One wave per segment:
 // float4 index = 256*seg + 64*u + lane (u = 0..3), each instruction 1 KB contiguous;
-// non-temporal loads and stores. seg_lcnt = exact count at t_list; the segment that
-// holds the < 4-element scalar tail is marked spilled (re-read when needed).
-template <bool NEST, bool SAMPLE>
+// non-temporal loads and stores. seg_lcnt = exact count at t_list; a segment that
+// holds an unpadded scalar tail is marked spilled (re-read when needed).
+template <bool NEST>
 __global__ void __launch_bounds__(kBlock)
-k_compensate_list(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __restrict__ vec, int64_t n,
-                  float mom, SampleSpec sp, const float* __restrict__ tspec, SelWS w) {
+k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat, float* __restrict__ vec_flat,
+                  float mom, SelWS w) {
+    const int t = task(w, BT_K1, blockIdx.x);
+    const TDesc& d = w.td[t];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t seg = (int64_t)blockIdx.x * kSegPerBlock4 + wave;
-    const int64_t n4 = n / 4;
-    const float tl = tspec ? *tspec : __builtin_huge_valf();
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.st->t_list = tl;
-    // waves past the last segment load nothing and list nothing (v >= n4 below), but
-    // stay for the block barrier of the spill count
+    const int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_K1][t]) * kSegPerBlock4 + wave;   // local segment
+    const float4* g = reinterpret_cast<const float4*>(g_flat + d.off);
+    float4* mmt = reinterpret_cast<float4*>(mmt_flat + d.off);
+    float4* vec = reinterpret_cast<float4*>(vec_flat + d.off);
+    const int64_t n4 = d.nv4, n = d.n;
+    const float tl = w.spec ? w.spec[2 * t] : __builtin_huge_valf();
+    SelState* st = w.st + t;
+    if (blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) st->t_list = tl;
+    const bool sample = d.samp_off >= 0;
+    const int64_t start = sample ? w.starts[t] : 0, scount = sample ? w.scnt[t] : 0;
+    float* sout = sample ? w.samples + d.samp_off : nullptr;
+    // waves past the tensor's last segment load nothing and list nothing, but stay for
+    // the block barrier of the spill count
     int64_t q0 = 0, r0 = 0;
-    if (SAMPLE) floor_divmod_fast(seg * kSeg - sp.start, sp.stride, sp.inv_stride, q0, r0);
+    if (sample) floor_divmod_fast(ls * kSeg - start, d.stride, d.inv_stride, q0, r0);
     float4 gv[kSegTiles], mv[kSegTiles], vv[kSegTiles];
 #pragma unroll
     for (int u = 0; u < kSegTiles; ++u) {
-        const int64_t v = seg * (kSeg / 4) + u * 64 + lane;
+        const int64_t v = ls * (kSeg / 4) + u * 64 + lane;
         if (v < n4) {
             gv[u] = ld_nt(g + v);
             mv[u] = ld_nt(mmt + v);
@@ -230,13 +420,15 @@ k_compensate_list(const float4* __restrict__ g, float4* __restrict__ mmt, float4
         }
     }
     uint32_t c = 0;
+    const int64_t seg = d.seg0 + ls;
     uint16_t* lo = w.lst_off + seg * kCap;
     float* lv = w.lst_val + seg * kCap;
 #pragma unroll
     for (int u = 0; u < kSegTiles; ++u) {
-        const int64_t v = seg * (kSeg / 4) + u * 64 + lane;
+        const int64_t v = ls * (kSeg / 4) + u * 64 + lane;
         const bool ok = v < n4;
         float x[4] = {0.f, 0.f, 0.f, 0.f};
+        uint32_t valid = 0;
         if (ok) {
             x[0] = comp1<NEST, true>(gv[u].x, mv[u].x, vv[u].x, mom);
             x[1] = comp1<NEST, true>(gv[u].y, mv[u].y, vv[u].y, mom);
@@ -244,25 +436,24 @@ k_compensate_list(const float4* __restrict__ g, float4* __restrict__ mmt, float4
             x[3] = comp1<NEST, true>(gv[u].w, mv[u].w, vv[u].w, mom);
             st_nt(mmt + v, mv[u]);
             st_nt(vec + v, vv[u]);
-            if (SAMPLE) {
-                const uint32_t t = (uint32_t)r0 + 4u * (uint32_t)(u * 64 + lane);
-                const uint32_t s32 = (uint32_t)sp.stride;
+            const int64_t e = 4 * v;
+            valid = e + 3 < n ? 0xFu : (e + 2 < n ? 7u : (e + 1 < n ? 3u : (e < n ? 1u : 0u)));
+            if (sample) {
+                const uint32_t tt = (uint32_t)r0 + 4u * (uint32_t)(u * 64 + lane);
+                const uint32_t s32 = (uint32_t)d.stride;
                 uint32_t q1, r;
-                divmod_u32(t, s32, sp.inv_stride_f, q1, r);
+                divmod_u32(tt, s32, d.inv_stride_f, q1, r);
                 const uint32_t j = r == 0 ? 0u : s32 - r;
-                if (j < 4) {
+                if (j < 4 && ((valid >> j) & 1u)) {
                     const int64_t qi = q0 + q1 + (r == 0 ? 0 : 1);
-                    if (qi >= 0 && qi < sp.count) sp.out[qi] = fabsf(x[j]);
+                    if (qi >= 0 && qi < scount) sout[qi] = fabsf(x[j]);
                 }
             }
         }
-        list_append(ge_mask(x, ok ? 0xFu : 0u, tl), x, u * 256, c, lo, lv);
+        list_append(ge_mask(x, valid, tl), x, u * 256, c, lo, lv);
     }
     const bool spilled = c > (uint32_t)kCap;
-    if (lane == 0 && seg < w.nseg) {
-        const bool tail = (n & 3) && seg == w.nseg - 1;
-        w.seg_lcnt[seg] = tail ? (uint32_t)(kCap + 1) : c;
-    }
+    if (lane == 0 && ls < d.nseg) w.seg_lcnt[seg] = (d.tail && ls == d.nseg - 1) ? (uint32_t)(kCap + 1) : c;
     // one atomic per workgroup with a spilled segment (shard by block)
     const uint64_t any = __ballot(spilled);
     __shared__ uint32_t nsp;
@@ -270,18 +461,58 @@ k_compensate_list(const float4* __restrict__ g, float4* __restrict__ mmt, float4
     __syncthreads();
     if (lane == 0 && any) atomicAdd(&nsp, 1u);
     __syncthreads();
-    if (threadIdx.x == 0 && nsp)
-        atomicAdd(&w.st->spill[w.st->epoch & 1][blockIdx.x % kSpillShards], nsp);
+    if (threadIdx.x == 0 && nsp) atomicAdd(&st->spill[st->epoch & 1][blockIdx.x % kSpillShards], nsp);
 }
 
 __global__ void k_no_lists(SelWS w) {
-    if (threadIdx.x == 0) w.st->t_list = __builtin_huge_valf();
+    for (int t = threadIdx.x; t < w.T; t += blockDim.x) w.st[t].t_list = __builtin_huge_valf();
+}
+
+// ------------------------------------------------------------------ K3 thresholds
+// Sample keys of the tensors (or |vec| itself for a direct tensor, N == S).
+struct SampleKeys {
+    SelWS w;
+    const float* vec_flat;
+    __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_SAMP], w.T, b); }
+    __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_SAMP][t]; }
+    __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_SAMP][t + 1] - w.bt[BT_SAMP][t]; }
+    __device__ __forceinline__ bool active(int) const { return true; }
+    __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
+    __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
+    template <class F>
+    __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
+        const TDesc& d = w.td[t];
+        const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
+        visit_dense(x, w.scnt[t], lb, nb, f);
+    }
+};
+
+// Resets the radix state of every multi-block threshold task with its k (top_k_samples).
+__global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
+    const int t = blockIdx.x;
+    if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
+    rs_reset(w.rs + t, (uint64_t)w.td[t].ks);
+}
+
+// One workgroup per small tensor: all three passes from LDS.
+__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat) {
+    const int t = w.small[blockIdx.x];
+    const TDesc& d = w.td[t];
+    const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
+    rs_small_wg(x, w.scnt[t], (uint64_t)d.ks, w.thr + t);
 }
 
 // ------------------------------------------------------------------ state
-__global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, const float* thr0, int keep_lists) {
-    SelState* st = w.st;
-    for (int64_t i = threadIdx.x; i < 3 * w.ngrp; i += blockDim.x) w.grp_cnt[i] = 0;
+// One workgroup per tensor: reset the tensor's state for this call.
+__global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lists) {
+    const int t = blockIdx.x;
+    const TDesc& d = w.td[t];
+    SelState* st = w.st + t;
+    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
+        w.grp_cnt[d.grp0 + i] = 0;
+        w.grp_gt[d.grp0 + i] = 0;
+        w.grp_eq[d.grp0 + i] = 0;
+    }
     __shared__ uint32_t spills;
     if (threadIdx.x == 0) spills = 0;
     __syncthreads();
@@ -293,12 +524,12 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, const float*
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float t = *thr0;
-        st->t0 = t;
-        st->t_cur = t;
+        const float t0 = w.thr[t];
+        st->t0 = t0;
+        st->t_cur = t0;
         st->list_spills = keep_lists ? (int32_t)spills : 0;
         // no K1 lists, or too many overflowed lists to be worth serving: one full pass
-        if (!keep_lists || (int64_t)spills * kSpillDiv > w.nseg) st->t_list = __builtin_huge_valf();
+        if (!keep_lists || (int64_t)spills * kSpillDiv > d.nseg) st->t_list = __builtin_huge_valf();
         st->tk = 0.f;
         st->branch = -1;
         st->n_cur = st->limit = st->n_greater = st->tie_quota = 0;
@@ -317,13 +548,16 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, const float*
 }
 
 // ------------------------------------------------------------------ count passes
-// t_cur >= t_list: counts from the lists, one thread per segment; spilled
-// segments are re-read by the block's waves. One atomic per block into its group.
+// t_cur >= t_list: counts from the lists, one thread per segment; spilled segments
+// are re-read by the block's waves. One atomic per block into its group.
 __global__ void __launch_bounds__(kBlock)
-k_count_lists(const float* __restrict__ vec, int64_t n, SelWS w) {
-    const SelState* st = w.st;
+k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
+    const int t = task(w, BT_SEG, blockIdx.x);
+    const SelState* st = w.st + t;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
-    const float t = st->t_cur;
+    const TDesc& d = w.td[t];
+    const float* vec = vec_flat + d.off;
+    const float tc = st->t_cur;
     __shared__ int spill[kBlock];
     __shared__ int nspill;
     __shared__ uint32_t bsum;
@@ -332,9 +566,11 @@ k_count_lists(const float* __restrict__ vec, int64_t n, SelWS w) {
         bsum = 0;
     }
     __syncthreads();
-    const int64_t seg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_SEG][t]) * kBlock;
+    const int64_t ls = lseg0 + threadIdx.x;
     uint32_t c = 0;
-    if (seg < w.nseg) {
+    if (ls < d.nseg) {
+        const int64_t seg = d.seg0 + ls;
         const uint32_t lc = w.seg_lcnt[seg];
         if (lc <= (uint32_t)kCap) {
             const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
@@ -346,8 +582,8 @@ k_count_lists(const float* __restrict__ vec, int64_t n, SelWS w) {
             for (int q = 0; q < kCap / 4; ++q) {
                 const uint32_t e = 4 * q;
                 if (e < lc)
-                    c += (fabsf(v[q].x) >= t) + (e + 1 < lc && fabsf(v[q].y) >= t) +
-                         (e + 2 < lc && fabsf(v[q].z) >= t) + (e + 3 < lc && fabsf(v[q].w) >= t);
+                    c += (fabsf(v[q].x) >= tc) + (e + 1 < lc && fabsf(v[q].y) >= tc) +
+                         (e + 2 < lc && fabsf(v[q].z) >= tc) + (e + 3 < lc && fabsf(v[q].w) >= tc);
             }
             w.seg_cnt[seg] = c;
         } else {
@@ -359,33 +595,37 @@ k_count_lists(const float* __restrict__ vec, int64_t n, SelWS w) {
     __syncthreads();
     const int wave = threadIdx.x >> 6;
     for (int q = wave; q < nspill; q += kSegPerBlock4) {
-        const int64_t s2 = (int64_t)blockIdx.x * kBlock + spill[q];
-        const uint32_t cs = wave_count_segment(vec, n, s2, t);
+        const int64_t ls2 = lseg0 + spill[q];
+        const uint32_t cs = wave_count_segment(vec, d.n, ls2, tc);
         if ((threadIdx.x & 63) == 0) {
-            w.seg_cnt[s2] = cs;
+            w.seg_cnt[d.seg0 + ls2] = cs;
             if (cs) atomicAdd(&bsum, cs);
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0 && bsum)
-        atomicAdd(&w.grp_cnt[((int64_t)blockIdx.x * kBlock) / kGroupSegs], (unsigned long long)bsum);
+    if (threadIdx.x == 0 && bsum) atomicAdd(&w.grp_cnt[d.grp0 + lseg0 / kGroupSegs], (unsigned long long)bsum);
 }
 
 // t_cur < t_list: full select pass at t_cur — one wave per kSuper segments (16
 // float4 loads in flight per lane), re-lists every segment; seg_lcnt = seg_cnt.
+// `which` = BT_FULL (one-shot) or BT_CAP16 (grid-stride within the tensor, for a
+// launch that is most likely a gated no-op).
 template <bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
-k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
-    const SelState* st = w.st;
+k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
+    const int t = task(w, which, blockIdx.x);
+    const SelState* st = w.st + t;
     if (!st->active || st->t_cur >= st->t_list) return;
-    const float t = st->t_cur;
+    const TDesc& d = w.td[t];
+    const float* vec = vec_flat + d.off;
+    const float tc = st->t_cur;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int kTiles = kSuper * kSegTiles;   // 16
     __shared__ uint32_t wcnt[kSegPerBlock4];
     __shared__ uint32_t wovf[kSegPerBlock4];
-    const int64_t nsuper = ceil_div(w.nseg, (int64_t)kSuper);
-    // one-shot (grid = nsuper/4) or grid-stride with a capped grid (gated launches)
-    for (int64_t bi = blockIdx.x; bi * kSegPerBlock4 < nsuper; bi += gridDim.x) {
+    const int64_t nsuper = ceil_div(d.nseg, (int64_t)kSuper);
+    const int64_t nb = w.bt[which][t + 1] - w.bt[which][t];
+    for (int64_t bi = (int64_t)blockIdx.x - w.bt[which][t]; bi * kSegPerBlock4 < nsuper; bi += nb) {
         const int64_t sup = bi * kSegPerBlock4 + wave;
         uint32_t ctot = 0, novf = 0;
         if (sup < nsuper) {
@@ -393,20 +633,23 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
             uint32_t valid[kTiles];
 #pragma unroll
             for (int u = 0; u < kTiles; ++u)
-                load_tile<ALIGNED>(vec, n, sup * (kSuper * kSeg) + u * 256 + 4 * lane, x[u], valid[u]);
+                load_tile<ALIGNED>(vec, d.n, sup * (kSuper * kSeg) + u * 256 + 4 * lane, x[u], valid[u]);
 #pragma unroll
             for (int sg = 0; sg < kSuper; ++sg) {
-                const int64_t seg = sup * kSuper + sg;
+                const int64_t ls = sup * kSuper + sg;
+                const int64_t seg = d.seg0 + ls;
                 uint32_t c = 0;
                 uint16_t* lo = w.lst_off + seg * kCap;
                 float* lv = w.lst_val + seg * kCap;
+                if (ls < d.nseg) {   // uniform per wave
 #pragma unroll
-                for (int u = 0; u < kSegTiles; ++u)
-                    list_append(ge_mask(x[sg * kSegTiles + u], valid[sg * kSegTiles + u], t), x[sg * kSegTiles + u],
-                                u * 256, c, lo, lv);
-                if (lane == 0 && seg < w.nseg) {
-                    w.seg_lcnt[seg] = c;
-                    w.seg_cnt[seg] = c;
+                    for (int u = 0; u < kSegTiles; ++u)
+                        list_append(ge_mask(x[sg * kSegTiles + u], valid[sg * kSegTiles + u], tc),
+                                    x[sg * kSegTiles + u], u * 256, c, lo, lv);
+                    if (lane == 0) {
+                        w.seg_lcnt[seg] = c;
+                        w.seg_cnt[seg] = c;
+                    }
                 }
                 ctot += c;
                 novf += c > (uint32_t)kCap;
@@ -420,8 +663,8 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
         if (threadIdx.x == 0) {
             const uint32_t s = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
             const uint32_t o = wovf[0] + wovf[1] + wovf[2] + wovf[3];
-            if (s) atomicAdd(&w.grp_cnt[(bi * kSegPerBlock4 * kSuper) / kGroupSegs], (unsigned long long)s);
-            if (o) atomicAdd(&w.st->overflow, (int)o);
+            if (s) atomicAdd(&w.grp_cnt[d.grp0 + (bi * kSegPerBlock16) / kGroupSegs], (unsigned long long)s);
+            if (o) atomicAdd(&w.st[t].overflow, (int)o);
         }
         __syncthreads();
     }
@@ -429,8 +672,7 @@ k_select_pass(const float* __restrict__ vec, int64_t n, SelWS w) {
 
 // Chunked exclusive scan of a[0..m) into out[] by one workgroup; returns the total.
 // a[] holds totals accumulated by device atomics: read with agent-scope loads.
-__device__ uint64_t block_scan_array(const unsigned long long* a, long long* out, int64_t m,
-                                     uint64_t* lds16) {
+__device__ uint64_t block_scan_array(const unsigned long long* a, long long* out, int64_t m, uint64_t* lds16) {
     const int64_t per = ceil_div(m, (int64_t)blockDim.x);
     const int64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
     uint64_t local = 0;
@@ -445,19 +687,20 @@ __device__ uint64_t block_scan_array(const unsigned long long* a, long long* out
 }
 
 // One step of the reference's adaptation loop (dgc/compression.py:128-149) on the
-// count of the pass that just ran. With resample (the default) the loop can only
-// lower the threshold until the count reaches lower*k, so the first "lower" step
-// hands over to ONE multi-threshold pass (k_lower_counts) instead of recounting
-// one threshold per pass; without resample the threshold may also rise, and each
-// step is a recount (count pass + decide), exactly like the reference.
-__global__ void __launch_bounds__(kScanThreads)
-k_decide(SelWS w, dgc_select_params p) {
-    SelState* st = w.st;
+// count of the pass that just ran, one workgroup per tensor. With resample (the
+// default) the loop can only lower the threshold until the count reaches lower*k,
+// so the first "lower" step hands over to ONE multi-threshold pass (k_lower_counts)
+// instead of recounting one threshold per pass; without resample the threshold may
+// also rise, and each step is a recount (count pass + decide), like the reference.
+__global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
+    const int t = blockIdx.x;
+    SelState* st = w.st + t;
     if (!st->active) return;
+    const TDesc& d = w.td[t];
     __shared__ uint64_t lds16[16];
     __shared__ int finished, reset_rs;
     uint64_t local = 0;
-    for (int64_t i = threadIdx.x; i < w.ngrp; i += kScanThreads) local += w.grp_cnt[i];
+    for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) local += w.grp_cnt[d.grp0 + i];
     uint64_t n;
     block_exclusive_scan(local, lds16, &n);
     if (threadIdx.x == 0) {
@@ -465,8 +708,8 @@ k_decide(SelWS w, dgc_select_params p) {
             st->t_list = st->t_cur;
             st->full_passes += 1;
         }
-        const long long cnt = (long long)n, k = p.num_selects;
-        const bool adapt = p.numel > p.num_samples;
+        const long long cnt = (long long)n, k = d.k;
+        const bool adapt = d.n > d.S;
         st->n_cur = cnt;
         int done = 1;
         reset_rs = 0;
@@ -477,10 +720,10 @@ k_decide(SelWS w, dgc_select_params p) {
             st->branch = DGC_BRANCH_EXHAUSTED;
             st->limit = cnt < k ? cnt : k;
         } else if (cnt > k) {
-            if (cnt > p.upper_count) {
+            if (cnt > d.upper_count) {
                 if (p.resample) {
                     st->branch = DGC_BRANCH_RESAMPLE;
-                    if (cnt < 64 * k && cnt <= w.cand_cap) {   // torch's nth_element path: replayed
+                    if (cnt < 64 * k && cnt <= d.cand_cap) {   // torch's nth_element path: replayed
                         st->rs_nth = 1;
                         st->tie_rule = DGC_TIES_EXACT;
                     } else {                                    // partial_sort path: lowest-index ties
@@ -496,7 +739,7 @@ k_decide(SelWS w, dgc_select_params p) {
                 st->branch = DGC_BRANCH_TRUNC;
                 st->limit = k;
             }
-        } else if (cnt < p.lower_count) {
+        } else if (cnt < d.lower_count) {
             if (p.resample && st->iter == 0 && p.max_iters <= kMaxLower) {
                 st->lower_pending = 1;   // k_lower_counts finds the final threshold in one pass
                 done = 2;
@@ -521,44 +764,48 @@ k_decide(SelWS w, dgc_select_params p) {
         finished = done;
     }
     __syncthreads();
-    if (finished == 1) block_scan_array(w.grp_cnt, w.grp_off, w.ngrp, lds16);
-    if (reset_rs) rs_reset(w.rs, (uint64_t)p.num_selects);
+    if (finished == 1) block_scan_array(w.grp_cnt + d.grp0, w.grp_off + d.grp0, d.ngrp, lds16);
+    if (reset_rs) rs_reset(w.rs + t, (uint64_t)d.k);
     __syncthreads();
     if (finished != 1)
-        for (int64_t i = threadIdx.x; i < w.ngrp; i += kScanThreads) w.grp_cnt[i] = 0;
+        for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) w.grp_cnt[d.grp0 + i] = 0;
 }
 
 // Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
 // reference's "lower" recounts, dgc/compression.py:140-148, all at once). The last
-// workgroup to arrive picks j* = the first j whose count reaches lower*k (else
+// workgroup of the tensor picks j* = the first j whose count reaches lower*k (else
 // max_iters) and arms the count pass + decide at t_{j*}.
 template <bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
-k_lower_counts(const float* __restrict__ vec, int64_t n, SelWS w, dgc_select_params p) {
-    SelState* st = w.st;
+k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
+    const int t = task(w, BT_CAP4, blockIdx.x);
+    SelState* st = w.st + t;
     if (!st->lower_pending) return;
+    const TDesc& d = w.td[t];
+    const float* vec = vec_flat + d.off;
     const int m = p.max_iters;
-    float t[kMaxLower + 1];
-    t[0] = st->t_cur;
+    float th[kMaxLower + 1];
+    th[0] = st->t_cur;
 #pragma unroll
-    for (int j = 1; j <= kMaxLower; ++j) t[j] = __fmul_rn(t[j - 1], p.lower);
-    const float tmin = t[m];
+    for (int j = 1; j <= kMaxLower; ++j) th[j] = __fmul_rn(th[j - 1], p.lower);
+    const float tmin = th[m];
     uint32_t c[kMaxLower + 1];
 #pragma unroll
     for (int j = 0; j <= kMaxLower; ++j) c[j] = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t seg = (int64_t)blockIdx.x * kSegPerBlock4 + wave; seg < w.nseg;
-         seg += (int64_t)gridDim.x * kSegPerBlock4) {
+    const int64_t nb = w.bt[BT_CAP4][t + 1] - w.bt[BT_CAP4][t];
+    for (int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_CAP4][t]) * kSegPerBlock4 + wave; ls < d.nseg;
+         ls += nb * kSegPerBlock4) {
         for (int tile = 0; tile < kSegTiles; ++tile) {
             float x[4];
             uint32_t valid;
-            load_tile<ALIGNED>(vec, n, seg * kSeg + tile * 256 + 4 * lane, x, valid);
+            load_tile<ALIGNED>(vec, d.n, ls * kSeg + tile * 256 + 4 * lane, x, valid);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float a = fabsf(x[q]);
                 if (((valid >> q) & 1u) && a >= tmin) {
 #pragma unroll
-                    for (int j = 1; j <= kMaxLower; ++j) c[j] += (j <= m) && a >= t[j];
+                    for (int j = 1; j <= kMaxLower; ++j) c[j] += (j <= m) && a >= th[j];
                 }
             }
         }
@@ -575,17 +822,17 @@ k_lower_counts(const float* __restrict__ vec, int64_t n, SelWS w, dgc_select_par
         const uint64_t v = (uint64_t)part[0][j] + part[1][j] + part[2][j] + part[3][j];
         if (v) atomicAdd(&st->lower_cnt[j], (unsigned long long)v);
     }
-    if (!last_block_arrival(&st->tickets[0], gridDim.x)) return;
+    if (!last_block_arrival(&st->tickets[0], (uint32_t)nb)) return;
     if (threadIdx.x == 0) {
         int js = m;
         for (int j = 1; j <= m; ++j) {
             const long long nj = (long long)load_count(&st->lower_cnt[j]);
-            if (nj >= p.lower_count) {
+            if (nj >= d.lower_count) {
                 js = j;
                 break;
             }
         }
-        st->t_cur = t[js];
+        st->t_cur = th[js];
         st->iter = js;
         st->recounts = js;
         st->overflow = 0;
@@ -594,35 +841,43 @@ k_lower_counts(const float* __restrict__ vec, int64_t n, SelWS w, dgc_select_par
     }
 }
 
-// ------------------------------------------------------------------ resample
+// ------------------------------------------------------------------ resample (partial_sort path)
 // Candidate keys (|x| >= t_cur) for the resample radix select: the segment list
 // when complete, a re-read of vec when it spilled. One wave per segment.
 struct CandKeys {
-    const float* vec;
-    int64_t n;
     SelWS w;
+    const float* vec_flat;
+    __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_CAP4], w.T, b); }
+    __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_CAP4][t]; }
+    __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_CAP4][t + 1] - w.bt[BT_CAP4][t]; }
+    __device__ __forceinline__ bool active(int t) const { return w.st[t].resample_pending != 0; }
+    __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
+    __device__ __forceinline__ float* out(int t) const { return &w.st[t].tk; }
     template <class F>
-    __device__ __forceinline__ void visit(F&& f) const {
+    __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
+        const TDesc& d = w.td[t];
+        const float* vec = vec_flat + d.off;
         const int lane = threadIdx.x & 63;
-        const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-        const float t = w.st->t_cur;
-        for (int64_t seg = gw; seg < w.nseg; seg += nw) {
+        const int64_t gw = (lb * blockDim.x + threadIdx.x) >> 6;
+        const int64_t nw = (nb * blockDim.x) >> 6;
+        const float tc = w.st[t].t_cur;
+        for (int64_t ls = gw; ls < d.nseg; ls += nw) {
+            const int64_t seg = d.seg0 + ls;
             const uint32_t lc = w.seg_lcnt[seg];
             if (lc <= (uint32_t)kCap) {
                 if (lane < lc) {
                     const float a = fabsf(w.lst_val[seg * kCap + lane]);
-                    if (a >= t) f(abs_key(a));
+                    if (a >= tc) f(abs_key(a));
                 }
             } else {
                 for (int tile = 0; tile < kSegTiles; ++tile) {
                     float x[4];
                     uint32_t valid;
-                    load_tile<false>(vec, n, seg * kSeg + tile * 256 + 4 * lane, x, valid);
-                    const uint32_t p = ge_mask(x, valid, t);
+                    load_tile<false>(vec, d.n, ls * kSeg + tile * 256 + 4 * lane, x, valid);
+                    const uint32_t pm = ge_mask(x, valid, tc);
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (p & (1u << j)) f(abs_key(x[j]));
+                        if (pm & (1u << j)) f(abs_key(x[j]));
                 }
             }
         }
@@ -630,12 +885,15 @@ struct CandKeys {
 };
 
 // Per-segment counts of |x| > tk and |x| == tk (both imply |x| >= t_cur), one
-// thread per segment, spilled segments re-read by waves; the last workgroup scans
-// the group totals and sets the tie quota k - #greater.
+// thread per segment, spilled segments re-read by waves; the tensor's last
+// workgroup scans its group totals and sets the tie quota k - #greater.
 __global__ void __launch_bounds__(kBlock)
-k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w, int64_t k) {
-    SelState* st = w.st;
+k_count_gt_eq(const float* __restrict__ vec_flat, SelWS w) {
+    const int t = task(w, BT_SEG, blockIdx.x);
+    SelState* st = w.st + t;
     if (!st->resample_pending) return;
+    const TDesc& d = w.td[t];
+    const float* vec = vec_flat + d.off;
     const float tk = st->tk;
     __shared__ int spill[kBlock];
     __shared__ int nspill;
@@ -645,9 +903,11 @@ k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w, int64_t k) {
         bgt = beq = 0;
     }
     __syncthreads();
-    const int64_t seg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_SEG][t]) * kBlock;
+    const int64_t ls = lseg0 + threadIdx.x;
     uint32_t gt = 0, eq = 0;
-    if (seg < w.nseg) {
+    if (ls < d.nseg) {
+        const int64_t seg = d.seg0 + ls;
         const uint32_t lc = w.seg_lcnt[seg];
         if (lc <= (uint32_t)kCap) {
             for (uint32_t e = 0; e < lc; ++e) {
@@ -670,12 +930,12 @@ k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w, int64_t k) {
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int q = wave; q < nspill; q += kSegPerBlock4) {
-        const int64_t s2 = (int64_t)blockIdx.x * kBlock + spill[q];
+        const int64_t ls2 = lseg0 + spill[q];
         uint32_t g2 = 0, e2 = 0;
         for (int tile = 0; tile < kSegTiles; ++tile) {
             float x[4];
             uint32_t valid;
-            load_tile<false>(vec, n, s2 * kSeg + tile * 256 + 4 * lane, x, valid);
+            load_tile<false>(vec, d.n, ls2 * kSeg + tile * 256 + 4 * lane, x, valid);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float a = fabsf(x[j]);
@@ -687,34 +947,35 @@ k_count_gt_eq(const float* __restrict__ vec, int64_t n, SelWS w, int64_t k) {
         g2 = wave_sum(g2);
         e2 = wave_sum(e2);
         if (lane == 0) {
-            w.seg_gt[s2] = g2;
-            w.seg_eq[s2] = e2;
+            w.seg_gt[d.seg0 + ls2] = g2;
+            w.seg_eq[d.seg0 + ls2] = e2;
             if (g2) atomicAdd(&bgt, g2);
             if (e2) atomicAdd(&beq, e2);
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int64_t g = ((int64_t)blockIdx.x * kBlock) / kGroupSegs;
+        const int64_t g = d.grp0 + lseg0 / kGroupSegs;
         if (bgt) atomicAdd(&w.grp_gt[g], (unsigned long long)bgt);
         if (beq) atomicAdd(&w.grp_eq[g], (unsigned long long)beq);
     }
-    if (!last_block_arrival(&st->tickets[1], gridDim.x)) return;
+    const uint32_t nb = (uint32_t)(w.bt[BT_SEG][t + 1] - w.bt[BT_SEG][t]);
+    if (!last_block_arrival(&st->tickets[1], nb)) return;
     __shared__ uint64_t lds16[16];
-    const uint64_t G = block_scan_array(w.grp_gt, w.grp_gt_off, w.ngrp, lds16);
+    const uint64_t G = block_scan_array(w.grp_gt + d.grp0, w.grp_gt_off + d.grp0, d.ngrp, lds16);
     __syncthreads();
-    block_scan_array(w.grp_eq, w.grp_eq_off, w.ngrp, lds16);
+    block_scan_array(w.grp_eq + d.grp0, w.grp_eq_off + d.grp0, d.ngrp, lds16);
     if (threadIdx.x == 0) {
         st->n_greater = (long long)G;
-        st->tie_quota = k - (long long)G;
-        st->limit = k;
+        st->tie_quota = d.k - (long long)G;
+        st->limit = d.k;
     }
 }
 
 // ------------------------------------------------------------------ emit
 struct EmitOut {
-    float* vec;          // null: leave vec untouched (pure selection)
-    float* mmt;          // null: no momentum masking
+    float* vec;          // flat; null: leave vec untouched (pure selection)
+    float* mmt;          // flat; null: no momentum masking
     void* values;
     void* indices;
     int32_t vdtype, idtype;
@@ -722,40 +983,53 @@ struct EmitOut {
     int64_t* cand;
 };
 
-__device__ __forceinline__ void emit_one(const EmitOut& o, int64_t pos, int64_t gidx, float x) {
+// Entries a tensor emits: the first `limit` candidates, or k after a resample.
+__device__ __forceinline__ long long final_count(const SelState& s, int64_t k) {
+    return s.branch == DGC_BRANCH_RESAMPLE ? (long long)k : s.limit;
+}
+
+// Output position of a tensor's first entry: the entries of the tensors before it.
+__device__ __forceinline__ long long out_base(const SelWS& w, int t) {
+    long long b = 0;
+    for (int u = 0; u < t; ++u) b += final_count(w.st[u], w.td[u].k);
+    return b;
+}
+
+// pos: output slot; li: the element's index within its tensor (d.off + li in the flat buffers).
+__device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long long pos, int64_t li, float x) {
     if (o.queue) {
-        o.queue[pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
-        o.cand[pos] = gidx;
+        o.queue[d.cand_off + pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
+        o.cand[d.cand_off + pos] = li;
         return;
     }
     store_value(o.values, pos, x, o.vdtype);
-    store_index(o.indices, pos, gidx, o.idtype);
+    store_index(o.indices, pos, d.idx_base + li, o.idtype);
     // scattered 4-B writes, one per 128-B line: non-temporal (no L2 allocation)
-    if (o.vec) __builtin_nontemporal_store(0.f, o.vec + gidx);
-    if (o.mmt) __builtin_nontemporal_store(0.f, o.mmt + gidx);
+    if (o.vec) __builtin_nontemporal_store(0.f, o.vec + d.off + li);
+    if (o.mmt) __builtin_nontemporal_store(0.f, o.mmt + d.off + li);
 }
 
-// Wave-cooperative emit of one spilled segment by re-reading vec.
+// Wave-cooperative emit of one spilled segment (local ls) by re-reading vec.
 // FIRSTK: positions base + rank for |x| >= t, kept while < limit.
-__device__ void emit_reread_firstk(const float* __restrict__ vec_in, int64_t n, int64_t seg, long long base,
-                                   long long limit, float t, const EmitOut& o) {
+__device__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long base,
+                                   long long limit, long long obase, float t, const EmitOut& o) {
     const int lane = threadIdx.x & 63;
     uint32_t run = 0;
     for (int tile = 0; tile < kSegTiles; ++tile) {
         float x[4];
         uint32_t valid;
-        const int64_t e0 = seg * kSeg + tile * 256 + 4 * lane;
-        load_tile<false>(vec_in, n, e0, x, valid);
-        const uint32_t p = ge_mask(x, valid, t);
-        if (__ballot(p != 0)) {
+        const int64_t e0 = ls * kSeg + tile * 256 + 4 * lane;
+        load_tile<false>(vec, d.n, e0, x, valid);
+        const uint32_t pm = ge_mask(x, valid, t);
+        if (__ballot(pm != 0)) {
             uint32_t lb, tot;
-            wave_prefix4(p, lb, tot);
+            wave_prefix4(pm, lb, tot);
             uint32_t r = run + lb;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if (p & (1u << j)) {
+                if (pm & (1u << j)) {
                     const long long pos = base + r;
-                    if (pos < limit) emit_one(o, pos, e0 + j, x[j]);
+                    if (pos < limit) emit_one(o, d, obase + pos, e0 + j, x[j]);
                     ++r;
                 }
             run += tot;
@@ -763,16 +1037,16 @@ __device__ void emit_reread_firstk(const float* __restrict__ vec_in, int64_t n, 
     }
 }
 
-// RESAMPLE: |x| > tk always, |x| == tk while the running tie rank is below T.
-__device__ void emit_reread_resample(const float* __restrict__ vec_in, int64_t n, int64_t seg, long long bg,
-                                     long long bt, float tk, long long T, const EmitOut& o) {
+// RESAMPLE (partial_sort path): |x| > tk always, |x| == tk while the running tie rank is below T.
+__device__ void emit_reread_resample(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long bg,
+                                     long long bt, float tk, long long T, long long obase, const EmitOut& o) {
     const int lane = threadIdx.x & 63;
     uint32_t run_g = 0, run_t = 0;
     for (int tile = 0; tile < kSegTiles; ++tile) {
         float x[4];
         uint32_t valid;
-        const int64_t e0 = seg * kSeg + tile * 256 + 4 * lane;
-        load_tile<false>(vec_in, n, e0, x, valid);
+        const int64_t e0 = ls * kSeg + tile * 256 + 4 * lane;
+        load_tile<false>(vec, d.n, e0, x, valid);
         uint32_t pg = 0, pe = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -791,7 +1065,7 @@ __device__ void emit_reread_resample(const float* __restrict__ vec_in, int64_t n
             for (int j = 0; j < 4; ++j) {
                 const bool gt = (pg >> j) & 1u, eq = (pe >> j) & 1u;
                 const long long tb = bt + rt;
-                if (gt || (eq && tb < T)) emit_one(o, bg + rg + (tb < T ? tb : T), e0 + j, x[j]);
+                if (gt || (eq && tb < T)) emit_one(o, d, obase + bg + rg + (tb < T ? tb : T), e0 + j, x[j]);
                 rg += gt;
                 rt += eq;
             }
@@ -806,32 +1080,39 @@ __device__ void emit_reread_resample(const float* __restrict__ vec_in, int64_t n
 // lane l takes list entry l (one coalesced load per list) and ballot ranks give the
 // output positions. Each wave emits 64 consecutive segments, kEmitBatch lists in
 // flight; a spilled segment is re-read from vec by the same wave.
+// o.queue == null: the payload (every branch but a K5 resample, which k_emit_queue
+// writes). o.queue != null: K5's candidate gather — every element >= t_cur, ascending
+// (the reference's `indices` before its resample topk), only when K5 serves the tensor.
 constexpr int kEmitThreads = kGroupSegs;
 constexpr int kEmitBatch = 8;
 constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
 static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
 
-// o.queue == null: the payload (every branch but a K5 resample, which k_emit_queue
-// writes). o.queue != null: K5's candidate gather — every element >= t_cur, ascending
-// (the reference's `indices` before its resample topk), only when K5 serves the step.
 __global__ void __launch_bounds__(kEmitThreads)
-k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
-    const SelState* st = w.st;
+k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+    const int t = task(w, BT_GRP, blockIdx.x);
+    const SelState* st = w.st + t;
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth;
     if (k5 != (o.queue != nullptr)) return;
     const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
-    const int64_t g = blockIdx.x;
-    const int64_t seg0 = g * kGroupSegs;
+    const TDesc& d = w.td[t];
+    const float* vec = vec_flat + d.off;
+    const int64_t lg = (int64_t)blockIdx.x - w.bt[BT_GRP][t];   // group within the tensor
+    const int64_t g = d.grp0 + lg;
+    const int64_t lseg0 = lg * kGroupSegs;
     __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs], lcn[kGroupSegs];
     __shared__ uint64_t lds16[16];
+    __shared__ long long obase_s;
+    if (threadIdx.x == 0) obase_s = k5 ? 0 : out_base(w, t);
     const long long limit = k5 ? st->n_cur : st->limit;
     const long long T = st->tie_quota;
     const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
     const long long gb = rs ? w.grp_eq_off[g] : 0;
     {
-        const int64_t seg = seg0 + threadIdx.x;
+        const int64_t ls = lseg0 + threadIdx.x;
         uint32_t ca = 0, cb = 0, lc = 0;
-        if (seg < w.nseg) {
+        if (ls < d.nseg) {
+            const int64_t seg = d.seg0 + ls;
             ca = rs ? w.seg_gt[seg] : w.seg_cnt[seg];
             cb = rs ? w.seg_eq[seg] : 0;
             lc = w.seg_lcnt[seg];
@@ -846,7 +1127,8 @@ k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
         lcn[threadIdx.x] = work ? lc : kEmitSkip;
     }
     __syncthreads();
-    const float t = st->t_cur, tk = st->tk;
+    const long long obase = obase_s;
+    const float tc = st->t_cur, tk = st->tk;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt();
     for (int j0 = wv * 64; j0 < wv * 64 + 64; j0 += kEmitBatch) {
@@ -858,7 +1140,7 @@ k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
             x[q] = 0.f;
             e[q] = 0;
             if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
-                const int64_t slot = (seg0 + j0 + q) * kCap + lane;
+                const int64_t slot = (d.seg0 + lseg0 + j0 + q) * kCap + lane;
                 x[q] = w.lst_val[slot];
                 e[q] = w.lst_off[slot];
             }
@@ -867,80 +1149,102 @@ k_emit(const float* __restrict__ vec_in, int64_t n, SelWS w, EmitOut o) {
         for (int q = 0; q < kEmitBatch; ++q) {
             const uint32_t L = lcn[j0 + q];
             if (L == kEmitSkip) continue;
-            const int64_t seg = seg0 + j0 + q;
+            const int64_t ls = lseg0 + j0 + q;
             const long long ba = ga + off_a[j0 + q], bb = gb + off_b[j0 + q];
             if (L > (uint32_t)kCap) {
                 if (rs)
-                    emit_reread_resample(vec_in, n, seg, ba, bb, tk, T, o);
+                    emit_reread_resample(vec, d, ls, ba, bb, tk, T, obase, o);
                 else
-                    emit_reread_firstk(vec_in, n, seg, ba, limit, t, o);
+                    emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o);
                 continue;
             }
             const bool in = (uint32_t)lane < L;
             const float a = fabsf(x[q]);
-            const int64_t gidx = seg * kSeg + e[q];
+            const int64_t li = ls * kSeg + e[q];
             if (!rs) {
-                const bool sel = in && a >= t;
+                const bool sel = in && a >= tc;
                 const uint64_t m = __ballot(sel);
                 const long long pos = ba + __popcll(m & lt);
-                if (sel && pos < limit) emit_one(o, pos, gidx, x[q]);
+                if (sel && pos < limit) emit_one(o, d, obase + pos, li, x[q]);
             } else {
                 const bool gt = in && a > tk, eq = in && a == tk;
                 const uint64_t mg = __ballot(gt), me = __ballot(eq);
                 const long long tb = bb + __popcll(me & lt);
-                if (gt || (eq && tb < T)) emit_one(o, ba + __popcll(mg & lt) + (tb < T ? tb : T), gidx, x[q]);
+                if (gt || (eq && tb < T)) emit_one(o, d, obase + ba + __popcll(mg & lt) + (tb < T ? tb : T), li, x[q]);
             }
         }
     }
 }
 
-// K5: the reference's resample topk replayed on the gathered candidates (introselect.hpp).
-__global__ void __launch_bounds__(kNthThreads) k_nth_select(SelWS w, int64_t k) {
-    const SelState* st = w.st;
+// K5: the reference's resample topk replayed on the gathered candidates
+// (introselect.hpp), one workgroup per tensor.
+__global__ void __launch_bounds__(kNthThreads) k_nth_select(SelWS w) {
+    const int t = blockIdx.x;
+    const SelState* st = w.st + t;
     if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
-    nth_element_wg(w.queue, st->n_cur, k - 1, w.gpos_l, w.gpos_r);
+    const TDesc& d = w.td[t];
+    uint32_t* gl = w.gpos + d.gpos_off;
+    uint32_t* gr = gl + d.cand_cap / 2 + 1;
+    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr);
 }
 
 // K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
 // wire casts and the masking of DGCSGDMemory.update.
-__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_in, SelWS w, EmitOut o,
-                                                      int64_t k) {
-    const SelState* st = w.st;
+__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+    const int t = task(w, BT_QUEUE, blockIdx.x);
+    const SelState* st = w.st + t;
     if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
-    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < k; q += (int64_t)gridDim.x * kBlock) {
-        const uint32_t j = (uint32_t)w.queue[q];
-        const int64_t gidx = w.cand_idx[j];
-        emit_one(o, q, gidx, vec_in[gidx]);
-    }
+    const TDesc& d = w.td[t];
+    __shared__ long long obase_s;
+    if (threadIdx.x == 0) obase_s = out_base(w, t);
+    __syncthreads();
+    const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
+    if (q >= d.k) return;
+    const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
+    const int64_t li = w.cand_idx[d.cand_off + j];
+    emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
 }
 
-// Result record; and the next call's speculative list threshold, margin x t_cur.
-__global__ void k_sel_finish(SelState* st, int64_t k, int64_t* count_out, dgc_select_info* info,
-                             float* spec, float margin) {
-    if (threadIdx.x != 0) return;
-    st->epoch += 1;
-    const long long cnt = st->branch == DGC_BRANCH_RESAMPLE ? k : st->limit;
-    if (count_out) *count_out = cnt;
-    if (info) {
-        info->count = cnt;
-        info->candidates = st->n_cur;
-        info->threshold0 = st->t0;
-        info->threshold = st->t_cur;
-        info->branch = st->branch;
-        info->recounts = st->recounts;
-        info->overflow_segments = st->full_passes ? st->overflow : st->list_spills;
-        info->full_passes = st->full_passes;
-        info->tie_rule = st->tie_rule;
-        info->pad = 0;
+// Result records; the payload's total count; and every tensor's next speculative
+// list threshold, margin x t_cur x growth. One workgroup.
+__global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info, float margin) {
+    __shared__ unsigned long long total;
+    if (threadIdx.x == 0) total = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < w.T; t += blockDim.x) {
+        SelState* st = w.st + t;
+        st->epoch += 1;
+        const long long cnt = final_count(*st, w.td[t].k);
+        atomicAdd(&total, (unsigned long long)cnt);
+        if (info) {
+            dgc_select_info& r = info[t];
+            r.count = cnt;
+            r.candidates = st->n_cur;
+            r.threshold0 = st->t0;
+            r.threshold = st->t_cur;
+            r.branch = st->branch;
+            r.recounts = st->recounts;
+            r.overflow_segments = st->full_passes ? st->overflow : st->list_spills;
+            r.full_passes = st->full_passes;
+            r.tie_rule = st->tie_rule;
+            r.pad = 0;
+        }
+        if (w.spec) {
+            // spec[0]: next call's list threshold = margin * t * growth, growth = t / spec[1]
+            // (the previous final threshold) clamped to [1, 1.5]; spec[1] := t.
+            float* spec = w.spec + 2 * t;
+            const float tc = st->t_cur;
+            const float gr = fminf(fmaxf(tc / spec[1], 1.f), 1.5f);   // NaN (first call: inf/inf) -> 1
+            spec[0] = (tc == tc && tc > 0.f && tc < __builtin_huge_valf()) ? tc * margin * gr : __builtin_huge_valf();
+            spec[1] = tc;
+        }
     }
-    if (spec) {
-        // spec[0]: next call's list threshold = margin * t * growth, growth = t / spec[1]
-        // (the previous final threshold) clamped to [1, 1.5]; spec[1] := t.
-        const float t = st->t_cur;
-        const float g = fminf(fmaxf(t / spec[1], 1.f), 1.5f);   // NaN (first call: inf/inf) -> 1
-        spec[0] = (t == t && t > 0.f && t < __builtin_huge_valf()) ? t * margin * g : __builtin_huge_valf();
-        spec[1] = t;
-    }
+    __syncthreads();
+    if (threadIdx.x == 0 && count_out) *count_out = (int64_t)total;
+}
+
+__global__ void k_spec_reset(float* spec, int32_t T) {
+    for (int i = threadIdx.x; i < 2 * T; i += blockDim.x) spec[i] = __builtin_huge_valf();
 }
 
 // ------------------------------------------------------------------ host driver
@@ -961,59 +1265,56 @@ static int validate_select(const dgc_select_params* p, void* values, void* indic
     return DGC_OK;
 }
 
-// Selection on an already-carved workspace. keep_lists: the lists / seg_lcnt /
-// t_list in the workspace are valid (written by the listing K1).
-static int select_core(float* vec, float* mmt, const float* thr0, const dgc_select_params* p, void* values,
-                       void* indices, int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists,
-                       int sync_mode, float* spec, float margin, hipStream_t s) {
-    const int64_t n = p->numel;
-    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(kScanThreads), 0, s, w, thr0, keep_lists);
+static SelCfg cfg_of(const dgc_select_params& p) {
+    return SelCfg{p.upper, p.lower, p.max_iters, p.resample, p.masking, p.vdtype, p.idtype, p.update_memory};
+}
+
+// The selection of every tensor (its K1 lists kept or not), from k_sel_init to the
+// payload: stream-ordered, and in DGC_SYNC_DEVICE mode with no host synchronisation.
+static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
+                       int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists, int sync_mode,
+                       float margin, hipStream_t s) {
+    hipLaunchKernelGGL(k_sel_init, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, w, keep_lists);
     DGC_LAUNCHED();
-    const int64_t nsuper = ceil_div(w.nseg, (int64_t)kSuper);
-    const int grid_full = (int)ceil_div(nsuper, kSegPerBlock4);   // one-shot full pass
-    const int grid_gs = grid_for(nsuper, kSegPerBlock4);          // grid-stride (gated) kernels
-    const int grid_cl = (int)ceil_div(w.nseg, kBlock);           // list count: a thread per segment
     const bool al = aligned16(vec);
-    const bool adapt = p->numel > p->num_samples;
-    const bool lower_fast = p->resample && p->max_iters <= kMaxLower;
-    // One count pass at t_cur: k_count_lists serves t_cur >= t_list from the lists,
-    // k_select_pass re-reads vec (and re-lists) below it. Both are gated on the device;
-    // `need` says which may run: 1 = lists only, 2 = full pass only, 3 = either.
-    // The first pass of dgc_select (no K1 lists, t_list = inf) is always a full pass.
+    // resample=True with max_iters <= kMaxLower: one multi-threshold pass replaces the lowers
+    const bool lower_fast = p.resample && p.max_iters <= kMaxLower;
     auto pass = [&](int need, bool likely_lists) -> int {
+        // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
+        // (both gated per tensor on the device); need: 1 = lists, 2 = full, 3 = either
         if (need & 1) {
-            hipLaunchKernelGGL(k_count_lists, dim3(grid_cl), dim3(kBlock), 0, s, vec, n, w);
+            hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w);
             DGC_LAUNCHED();
         }
         if (need & 2) {
-            const int gf = likely_lists ? grid_gs : grid_full;
+            const int which = likely_lists ? BT_CAP16 : BT_FULL;
+            const unsigned grid = (unsigned)L.grid[which];
             if (al)
-                hipLaunchKernelGGL(k_select_pass<true>, dim3(gf), dim3(kBlock), 0, s, vec, n, w);
+                hipLaunchKernelGGL(k_select_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, which);
             else
-                hipLaunchKernelGGL(k_select_pass<false>, dim3(gf), dim3(kBlock), 0, s, vec, n, w);
+                hipLaunchKernelGGL(k_select_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, which);
             DGC_LAUNCHED();
         }
-        hipLaunchKernelGGL(k_decide, dim3(1), dim3(kScanThreads), 0, s, w, *p);
+        hipLaunchKernelGGL(k_decide, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, w, p);
         DGC_LAUNCHED();
         return DGC_OK;
     };
     auto lower = [&]() -> int {
+        const unsigned grid = (unsigned)L.grid[BT_CAP4];
         if (al)
-            hipLaunchKernelGGL(k_lower_counts<true>, dim3(grid_gs), dim3(kBlock), 0, s, vec, n, w, *p);
+            hipLaunchKernelGGL(k_lower_counts<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
         else
-            hipLaunchKernelGGL(k_lower_counts<false>, dim3(grid_gs), dim3(kBlock), 0, s, vec, n, w, *p);
+            hipLaunchKernelGGL(k_lower_counts<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    EmitOut o{p->update_memory ? vec : nullptr, (p->update_memory && p->masking) ? mmt : nullptr, values,
-              indices, p->vdtype, p->idtype, nullptr, nullptr};
+    EmitOut o{p.update_memory ? vec : nullptr, (p.update_memory && p.masking) ? mmt : nullptr, values, indices,
+              p.vdtype, p.idtype, nullptr, nullptr};
     auto resample_lowest = [&]() -> int {
         // partial_sort path (>= 64k candidates): radix k-th value, ties lowest index first.
         // rs state reset by k_decide when it chose this path
-        CandKeys src{vec, n, w};
-        DGC_TRY(radix_select_passes(src, grid_for(w.nseg, kSegPerBlock4), &w.st->tk, w.rs,
-                                    &w.st->resample_pending, s));
-        hipLaunchKernelGGL(k_count_gt_eq, dim3(grid_cl), dim3(kBlock), 0, s, vec, n, w, (int64_t)p->num_selects);
+        DGC_TRY(radix_select_passes(CandKeys{w, vec}, (int)L.grid[BT_CAP4], s));
+        hipLaunchKernelGGL(k_count_gt_eq, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w);
         DGC_LAUNCHED();
         return DGC_OK;
     };
@@ -1022,64 +1323,120 @@ static int select_core(float* vec, float* mmt, const float* thr0, const dgc_sele
         EmitOut g = o;
         g.queue = w.queue;
         g.cand = w.cand_idx;
-        hipLaunchKernelGGL(k_emit, dim3((unsigned)w.ngrp), dim3(kEmitThreads), 0, s, vec, n, w, g);
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitThreads), 0, s, vec, w, g);
         DGC_LAUNCHED();
-        hipLaunchKernelGGL(k_nth_select, dim3(1), dim3(kNthThreads), 0, s, w, (int64_t)p->num_selects);
+        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, w);
         DGC_LAUNCHED();
-        hipLaunchKernelGGL(k_emit_queue, dim3(grid_for(p->num_selects)), dim3(kBlock), 0, s, vec, w, o,
-                           (int64_t)p->num_selects);
+        hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
         DGC_LAUNCHED();
         return DGC_OK;
     };
     DGC_TRY(keep_lists ? pass(3, true) : pass(2, false));
     if (sync_mode == DGC_SYNC_HOST) {
-        // read each decision back and launch only what it needs
-        SelState hs{};
+        // read the decisions back and launch only what they need
+        std::vector<SelState> hs(L.T);
         for (;;) {
-            DGC_HIP(hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s));
+            DGC_HIP(hipMemcpyAsync(hs.data(), w.st, sizeof(SelState) * L.T, hipMemcpyDeviceToHost, s));
             DGC_HIP(hipStreamSynchronize(s));
-            if (hs.done) break;
-            if (hs.lower_pending) {
+            bool all_done = true, any_lower = false, any_full = false, any_list = false;
+            for (const SelState& h : hs) {
+                if (h.done) continue;
+                all_done = false;
+                if (h.lower_pending)
+                    any_lower = true;
+                else if (h.t_cur >= h.t_list)
+                    any_list = true;
+                else
+                    any_full = true;
+            }
+            if (all_done) break;
+            if (any_lower) {
                 DGC_TRY(lower());   // picks t_cur on the device: either pass may follow
                 DGC_TRY(pass(3, false));
             } else {
-                DGC_TRY(pass(hs.t_cur >= hs.t_list ? 1 : 2, false));
+                DGC_TRY(pass((any_list ? 1 : 0) | (any_full ? 2 : 0), false));
             }
         }
-        if (hs.branch == DGC_BRANCH_RESAMPLE) DGC_TRY(hs.rs_nth ? resample_exact() : resample_lowest());
-    } else if (adapt) {
+        bool any_nth = false, any_low = false;
+        for (const SelState& h : hs) {
+            if (h.branch != DGC_BRANCH_RESAMPLE) continue;
+            if (h.rs_nth)
+                any_nth = true;
+            else
+                any_low = true;
+        }
+        if (any_low) DGC_TRY(resample_lowest());
+        if (any_nth) DGC_TRY(resample_exact());
+    } else if (L.adapt_any) {
         // every kernel below early-exits on a device flag when it is not needed
         if (lower_fast) {
             DGC_TRY(lower());
             DGC_TRY(pass(3, true));
         } else {
-            for (int i = 0; i < p->max_iters; ++i) DGC_TRY(pass(3, true));
+            for (int i = 0; i < p.max_iters; ++i) DGC_TRY(pass(3, true));
         }
-        if (p->resample) {
+        if (p.resample) {
             DGC_TRY(resample_lowest());
             DGC_TRY(resample_exact());
         }
     }
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)w.ngrp), dim3(kEmitThreads), 0, s, vec, n, w, o);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitThreads), 0, s, vec, w, o);
     DGC_LAUNCHED();
-    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(64), 0, s, w.st, (int64_t)p->num_selects, count_out, info,
-                       spec, margin);
+    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, count_out, info, margin);
     DGC_LAUNCHED();
     return DGC_OK;
 }
 
-int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p, void* values,
-           void* indices, int64_t* count_out, dgc_select_info* info, void* ws, size_t ws_bytes,
-           int sync_mode, hipStream_t s) {
+// ------------------------------------------------------------------ one-tensor plumbing
+// Layout + table of one unpadded tensor. samples: reserve the strided-sample buffer.
+static void one_layout(const dgc_select_params& p, int64_t stride, int64_t ks, bool samples, Layout& L,
+                       OneTable& ot) {
+    TensorIn in{p.numel, 0, p.num_selects, p.num_samples, ks, stride, p.upper_count, p.lower_count, samples};
+    std::vector<TDesc> td;
+    std::vector<int32_t> bt[BT_COUNT];
+    std::vector<int32_t> small;
+    build_layout(&in, 1, false, L, td, bt, small);
+    ot.d = td[0];
+    for (int which = 0; which < BT_COUNT; ++which) {
+        ot.bt[which][0] = bt[which][0];
+        ot.bt[which][1] = bt[which][1];
+    }
+    ot.start = 0;
+}
+
+static size_t one_ws_bytes(int64_t numel, int64_t k, int64_t num_samples, bool samples) {
+    dgc_select_params p{};
+    p.numel = numel;
+    p.num_selects = k;
+    p.num_samples = num_samples;
+    Layout L;
+    OneTable ot{};
+    one_layout(p, 2, 1, samples, L, ot);
+    size_t b = 0;
+    carve_select(nullptr, L, &b);
+    return b;
+}
+
+static size_t select_ws_bytes(int64_t numel, int64_t k) { return one_ws_bytes(numel, k, numel, false); }
+
+int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p, void* values, void* indices,
+           int64_t* count_out, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
     DGC_TRY(validate_select(p, values, indices));
     if (!vec || !thr0 || (p->update_memory && p->masking && !mmt))
         DGC_FAIL(DGC_ERR_INVALID, "dgc_select: null vec/thr0/mmt");
-    const int64_t n = p->numel;
-    if (!ws || ws_bytes < select_ws_bytes(n, p->num_selects) || (reinterpret_cast<uintptr_t>(ws) & 255))
-        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_select: workspace needs %zu bytes, 256-B aligned",
-                 select_ws_bytes(n, p->num_selects));
-    SelWS w = carve_select(ws, n, p->num_selects);
-    return select_core(vec, mmt, thr0, p, values, indices, count_out, info, w, 0, sync_mode, nullptr, 1.f, s);
+    Layout L;
+    OneTable ot{};
+    one_layout(*p, 1, 1, false, L, ot);
+    size_t need = 0;
+    carve_select(nullptr, L, &need);
+    if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
+        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_select: workspace needs %zu bytes, 256-B aligned", need);
+    SelWS w = carve_select(ws, L);
+    w.spec = nullptr;
+    w.thr = const_cast<float*>(thr0);
+    hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
+    DGC_LAUNCHED();
+    return select_core(vec, mmt, cfg_of(*p), L, values, indices, count_out, info, w, 0, sync_mode, 1.f, s);
 }
 
 // ------------------------------------------------------------------ threshold
@@ -1096,121 +1453,105 @@ int kth_largest(const float* x, int64_t n, int64_t k, float* out, void* ws, size
     }
     if (!ws || ws_bytes < sizeof(RSState) || (reinterpret_cast<uintptr_t>(ws) & 255))
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_kth_largest: workspace needs %zu bytes", sizeof(RSState));
-    return radix_select_launch(DenseKeys{x, n}, n, (uint64_t)k, out, reinterpret_cast<RSState*>(ws), s);
+    RSState* st = reinterpret_cast<RSState*>(ws);
+    hipLaunchKernelGGL(k_rs_init, dim3(1), dim3(kBlock), 0, s, st, (uint64_t)k);
+    DGC_LAUNCHED();
+    return radix_select_passes(DenseKeys{x, n, st, out}, grid_for(n, kBlock * 16, 512), s);
 }
 
-// ------------------------------------------------------------------ fused compress
+// K3 of every tensor of the call: the small ones in one workgroup each, the rest in
+// three multi-block passes.
+static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStream_t s) {
+    if (L.nsmall) {
+        hipLaunchKernelGGL(k_rs_small_multi, dim3((unsigned)L.nsmall), dim3(kScanThreads), 0, s, w, vec);
+        DGC_LAUNCHED();
+    }
+    if (L.grid[BT_SAMP] > 0) {
+        hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w);
+        DGC_LAUNCHED();
+        DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
+    }
+    return DGC_OK;
+}
+
+// ------------------------------------------------------------------ fused compress (one tensor)
 int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n, float momentum,
                bool nesterov, bool accumulate, float* samples, int64_t s_start, int64_t s_stride,
                int64_t s_count, hipStream_t st);
 int sample_strided_launch(const float* vec, int64_t start, int64_t stride, int64_t count, float* out,
                           hipStream_t s);
 
-struct CompressWS {
-    float* thr;
-    float* samples;
-    RSState* rs;
-    void* sel;
-    size_t sel_bytes;
-};
-
-// sample_buf: floats reserved for the strided samples (0 when numel == num_samples)
-static CompressWS carve_compress(void* base, int64_t numel, int64_t k, int64_t sample_buf, size_t* bytes = nullptr) {
-    Carver c(base);
-    CompressWS w{};
-    w.thr = c.take<float>(64);
-    w.rs = c.take<RSState>(1);
-    w.samples = c.take<float>(sample_buf);
-    w.sel_bytes = select_ws_bytes(numel, k);
-    w.sel = c.take<char>(w.sel_bytes);
-    if (bytes) *bytes = c.bytes();
-    return w;
-}
-
-static size_t compress_ws_bytes(int64_t numel, int64_t k, int64_t sample_buf) {
-    size_t b = 0;
-    carve_compress(nullptr, numel, k, sample_buf, &b);
-    return b;
-}
-
-struct CompressArgs {
-    int64_t n, L, sbuf;
-    bool sampled;
-};
-
 static int compress_check(const dgc_select_params* p, void* values, void* indices, int64_t s_start,
-                          int64_t s_stride, int64_t top_k_samples, void* ws, size_t ws_bytes, CompressArgs* a,
-                          bool need_outputs) {
+                          int64_t s_stride, int64_t top_k_samples, bool need_outputs) {
     if (need_outputs) DGC_TRY(validate_select(p, values, indices));
     else if (!p) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: null params");
-    a->n = p->numel;
-    a->sampled = p->numel != p->num_samples;
-    if (a->sampled && (s_stride < 2 || s_start < 0 || s_start >= s_stride))
+    const bool sampled = p->numel != p->num_samples;
+    if (sampled && (s_stride < 2 || s_start < 0 || s_start >= s_stride))
         DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: sample_start must be in [0, stride)");
-    a->L = a->sampled ? ceil_div(a->n - s_start, s_stride) : a->n;
-    if (need_outputs && (top_k_samples < 1 || top_k_samples > a->L))
-        DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: top_k_samples %lld outside [1, %lld]",
-                 (long long)top_k_samples, (long long)a->L);
-    a->sbuf = a->sampled ? a->L : 0;
-    if (!ws || ws_bytes < compress_ws_bytes(a->n, p->num_selects, a->sbuf) || (reinterpret_cast<uintptr_t>(ws) & 255))
-        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_compress: workspace needs %zu bytes, 256-B aligned",
-                 compress_ws_bytes(a->n, p->num_selects, a->sbuf));
+    const int64_t cnt = sampled ? ceil_div(p->numel - s_start, s_stride) : p->numel;
+    if (need_outputs && (top_k_samples < 1 || top_k_samples > cnt))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: top_k_samples %lld outside [1, %lld]", (long long)top_k_samples,
+                 (long long)cnt);
     return DGC_OK;
 }
 
-// K1 (+ fused strided sample + speculative candidate lists at *spec).
+static int one_ws(const dgc_select_params* p, int64_t s_start, int64_t s_stride, int64_t ks, float* spec,
+                  void* ws, size_t ws_bytes, Layout& L, SelWS& w, OneTable& ot) {
+    one_layout(*p, s_stride, ks, true, L, ot);
+    ot.start = p->numel != p->num_samples ? s_start : 0;
+    size_t need = 0;
+    carve_select(nullptr, L, &need);
+    if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
+        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_compress: workspace needs %zu bytes, 256-B aligned", need);
+    w = carve_select(ws, L);
+    w.spec = spec;   // the caller's per-tensor float[2] (null: no speculative lists)
+    return DGC_OK;
+}
+
+// K1 (+ fused strided sample + speculative candidate lists at spec[0]).
 int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bool nesterov, int64_t s_start,
-                   int64_t s_stride, const dgc_select_params* p, const float* spec, void* ws, size_t ws_bytes,
+                   int64_t s_stride, const dgc_select_params* p, float* spec, void* ws, size_t ws_bytes,
                    hipStream_t s) {
-    CompressArgs a{};
-    DGC_TRY(compress_check(p, nullptr, nullptr, s_start, s_stride, 1, ws, ws_bytes, &a, false));
+    DGC_TRY(compress_check(p, nullptr, nullptr, s_start, s_stride, 1, false));
     if (!grad || !mmt || !vec) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: null grad/mmt/vec");
-    CompressWS cw = carve_compress(ws, a.n, p->num_selects, a.sbuf);
-    SelWS w = carve_select(cw.sel, a.n, p->num_selects);
+    Layout L;
+    SelWS w;
+    OneTable ot{};
+    DGC_TRY(one_ws(p, s_start, s_stride, 1, spec, ws, ws_bytes, L, w, ot));
+    hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
+    DGC_LAUNCHED();
+    const int64_t n = p->numel;
+    const bool sampled = n != p->num_samples;
+    const int64_t cnt = sampled ? ceil_div(n - s_start, s_stride) : 0;
     const bool list_path = aligned16(grad) && aligned16(mmt) && aligned16(vec) &&
-                           (!a.sampled || (s_stride >= 4 && s_stride < (1LL << 30)));
+                           (!sampled || (s_stride >= 4 && s_stride < (1LL << 30)));
     if (!list_path) {
-        DGC_TRY(compensate(grad, mmt, vec, nullptr, a.n, momentum, nesterov, true, a.sampled ? cw.samples : nullptr,
-                           s_start, s_stride, a.sampled ? a.L : 0, s));
+        DGC_TRY(compensate(grad, mmt, vec, nullptr, n, momentum, nesterov, true, sampled ? w.samples : nullptr,
+                           s_start, s_stride, cnt, s));
         hipLaunchKernelGGL(k_no_lists, dim3(1), dim3(64), 0, s, w);
         DGC_LAUNCHED();
         return DGC_OK;
     }
-    SampleSpec sp{a.sampled ? cw.samples : nullptr, s_start, s_stride, a.sampled ? a.L : 0,
-                  1.0 / (double)s_stride, 1.0f / (float)s_stride};
-    const int64_t grid = ceil_div(w.nseg, kSegPerBlock4);
-    if (grid > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: n too large");
-    auto g4 = reinterpret_cast<const float4*>(grad);
-    auto m4 = reinterpret_cast<float4*>(mmt);
-    auto v4 = reinterpret_cast<float4*>(vec);
-    if (nesterov) {
-        if (a.sampled)
-            hipLaunchKernelGGL((k_compensate_list<true, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, g4, m4, v4,
-                               a.n, momentum, sp, spec, w);
+    if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: n too large");
+    if (L.grid[BT_K1] > 0) {
+        if (nesterov)
+            hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
+                               vec, momentum, w);
         else
-            hipLaunchKernelGGL((k_compensate_list<true, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, g4, m4,
-                               v4, a.n, momentum, sp, spec, w);
-    } else {
-        if (a.sampled)
-            hipLaunchKernelGGL((k_compensate_list<false, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, g4, m4,
-                               v4, a.n, momentum, sp, spec, w);
-        else
-            hipLaunchKernelGGL((k_compensate_list<false, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, g4, m4,
-                               v4, a.n, momentum, sp, spec, w);
+            hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad,
+                               mmt, vec, momentum, w);
+        DGC_LAUNCHED();
     }
-    DGC_LAUNCHED();
-    if (a.n & 3) {   // scalar tail (< 4 elements) incl. its samples; its segment is marked spilled
-        const int64_t done = (a.n / 4) * 4;
-        DGC_TRY(compensate(grad + done, mmt + done, vec + done, nullptr, a.n - done, momentum, nesterov, true,
-                           nullptr, 0, 1, 0, s));
-        if (a.sampled) {
+    if (n & 3) {   // scalar tail (< 4 elements) incl. its samples; its segment is marked spilled
+        const int64_t done = (n / 4) * 4;
+        DGC_TRY(compensate(grad + done, mmt + done, vec + done, nullptr, n - done, momentum, nesterov, true, nullptr,
+                           0, 1, 0, s));
+        if (sampled) {
             // samples in the tail: start + q*stride >= done
             const int64_t q_first = done >= s_start ? ceil_div(done - s_start, s_stride) : 0;
-            const int64_t cnt = a.L - q_first;
-            if (cnt > 0) {
-                const int64_t st0 = s_start + q_first * s_stride;
-                DGC_TRY(sample_strided_launch(vec, st0, s_stride, cnt, cw.samples + q_first, s));
-            }
+            const int64_t c = cnt - q_first;
+            if (c > 0)
+                DGC_TRY(sample_strided_launch(vec, s_start + q_first * s_stride, s_stride, c, w.samples + q_first, s));
         }
     }
     return DGC_OK;
@@ -1221,16 +1562,140 @@ int compress_finish(float* vec, float* mmt, int64_t s_start, int64_t s_stride, i
                     const dgc_select_params* p, float* spec, float margin, void* values, void* indices,
                     int64_t* count_out, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode,
                     hipStream_t s) {
-    CompressArgs a{};
-    DGC_TRY(compress_check(p, values, indices, s_start, s_stride, top_k_samples, ws, ws_bytes, &a, true));
+    DGC_TRY(compress_check(p, values, indices, s_start, s_stride, top_k_samples, true));
     if (!vec || (p->masking && !mmt)) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: null vec/mmt");
-    CompressWS cw = carve_compress(ws, a.n, p->num_selects, a.sbuf);
-    const float* src = a.sampled ? cw.samples : vec;
-    DGC_TRY(kth_largest(src, a.L, top_k_samples, cw.thr, cw.rs, sizeof(RSState), s));
-    SelWS w = carve_select(cw.sel, a.n, p->num_selects);
+    Layout L;
+    SelWS w;
+    OneTable ot{};
+    DGC_TRY(one_ws(p, s_start, s_stride, top_k_samples, spec, ws, ws_bytes, L, w, ot));
+    hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);   // begin's table had no top_k_samples
+    DGC_LAUNCHED();
+    DGC_TRY(thresholds(w, L, vec, s));
     dgc_select_params q = *p;
     q.update_memory = 1;   // DGCSGDMemory.update fused into the emit
-    return select_core(vec, mmt, cw.thr, &q, values, indices, count_out, info, w, 1, sync_mode, spec, margin, s);
+    return select_core(vec, mmt, cfg_of(q), L, values, indices, count_out, info, w, 1, sync_mode, margin, s);
+}
+
+// ------------------------------------------------------------------ batch
+static int batch_layout(const dgc_batch_desc* b, Layout& L, std::vector<TDesc>& td,
+                        std::vector<int32_t> (&bt)[BT_COUNT], std::vector<int32_t>& small) {
+    if (!b || b->count < 1 || !b->numel || !b->offset || !b->num_selects || !b->num_samples || !b->top_k_samples ||
+        !b->sample_stride)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_batch: null or empty tensor table");
+    std::vector<TensorIn> in(b->count);
+    int64_t prev_end = 0;
+    for (int32_t t = 0; t < b->count; ++t) {
+        TensorIn& x = in[t];
+        x.n = b->numel[t];
+        x.off = b->offset[t];
+        x.k = b->num_selects[t];
+        x.S = b->num_samples[t];
+        x.ks = b->top_k_samples[t];
+        x.stride = b->sample_stride[t];
+        x.upper_count = (int64_t)std::floor((double)x.k * b->upper_bound);
+        x.lower_count = (int64_t)std::ceil(b->lower_bound * (double)x.k);
+        x.samples = true;
+        if (x.n < 1 || x.k < 1 || x.k > x.n || x.S < 1 || x.S > x.n || x.ks < 1 || x.ks > x.S)
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_batch: tensor %d: bad numel/num_selects/num_samples/top_k_samples", t);
+        if (x.n != x.S && (x.stride < 4 || x.stride >= (1LL << 30)))
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_batch: tensor %d: sample stride %lld outside [4, 2^30)", t,
+                     (long long)x.stride);
+        if (x.off % kSeg || x.off < prev_end)
+            DGC_FAIL(DGC_ERR_INVALID,
+                     "dgc_batch: tensor %d: offset %lld must be a multiple of %d, ascending, non-overlapping", t,
+                     (long long)x.off, kSeg);
+        prev_end = x.off + (int64_t)align_up((size_t)x.n, 4);
+        if (prev_end > b->flat_numel) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch: tensor %d past flat_numel", t);
+    }
+    if (b->int32_indices && b->flat_numel > 2147483647LL)
+        DGC_FAIL(DGC_ERR_OVERFLOW, "dgc_batch: int32 indices cannot address %lld elements", (long long)b->flat_numel);
+    build_layout(in.data(), b->count, true, L, td, bt, small);
+    return DGC_OK;
+}
+
+static SelCfg cfg_of_batch(const dgc_batch_desc* b) {
+    return SelCfg{(float)b->upper_bound, (float)b->lower_bound, b->max_iters, b->resample, b->momentum_masking,
+                  b->fp16_values ? DGC_F16 : DGC_F32, b->int32_indices ? DGC_I32 : DGC_I64, 1};
+}
+
+size_t batch_ws_bytes(const dgc_batch_desc* b) {
+    Layout L;
+    std::vector<TDesc> td;
+    std::vector<int32_t> bt[BT_COUNT];
+    std::vector<int32_t> small;
+    if (batch_layout(b, L, td, bt, small) != DGC_OK) return 0;
+    size_t n = 0;
+    carve_select(nullptr, L, &n);
+    return n;
+}
+
+int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s) {
+    Layout L;
+    std::vector<TDesc> td;
+    std::vector<int32_t> bt[BT_COUNT];
+    std::vector<int32_t> small;
+    DGC_TRY(batch_layout(b, L, td, bt, small));
+    size_t need = 0;
+    carve_select(nullptr, L, &need);
+    if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
+        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_batch_init: workspace needs %zu bytes, 256-B aligned", need);
+    SelWS w = carve_select(ws, L);
+    DGC_HIP(hipMemsetAsync(w.st, 0, sizeof(SelState) * L.T, s));
+    DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
+    for (int which = 0; which < BT_COUNT; ++which)
+        DGC_HIP(hipMemcpyAsync(w.bt[which], bt[which].data(), sizeof(int32_t) * (L.T + 1), hipMemcpyHostToDevice, s));
+    if (L.nsmall)
+        DGC_HIP(hipMemcpyAsync(w.small, small.data(), sizeof(int32_t) * L.nsmall, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_spec_reset, dim3(1), dim3(256), 0, s, w.spec, L.T);
+    DGC_LAUNCHED();
+    // the host tables are pageable and local: let the copies finish first
+    DGC_HIP(hipStreamSynchronize(s));
+    return DGC_OK;
+}
+
+int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
+                   void* payload, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
+    Layout L;
+    std::vector<TDesc> td;
+    std::vector<int32_t> bt[BT_COUNT];
+    std::vector<int32_t> small;
+    DGC_TRY(batch_layout(b, L, td, bt, small));
+    size_t need = 0;
+    carve_select(nullptr, L, &need);
+    if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
+        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_batch_compress: workspace needs %zu bytes, 256-B aligned", need);
+    if (!grad || !mmt || !vec || !payload || !starts) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
+    if (!aligned16(grad) || !aligned16(mmt) || !aligned16(vec))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: flat buffers must be 16-B aligned");
+    for (int32_t t = 0; t < L.T; ++t)
+        if (td[t].samp_off >= 0 && (starts[t] < 0 || starts[t] >= td[t].stride))
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: tensor %d: sample start outside [0, stride)", t);
+    SelWS w = carve_select(ws, L);
+    for (int32_t t0 = 0; t0 < L.T; t0 += 64) {
+        StartChunk c{};
+        c.first = t0;
+        c.count = std::min<int32_t>(64, L.T - t0);
+        for (int i = 0; i < c.count; ++i) c.start[i] = td[t0 + i].samp_off >= 0 ? starts[t0 + i] : 0;
+        hipLaunchKernelGGL(k_put_starts, dim3(1), dim3(64), 0, s, w, c);
+        DGC_LAUNCHED();
+    }
+    if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: too many segments");
+    if (b->nesterov)
+        hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt, vec,
+                           b->momentum, w);
+    else
+        hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
+                           vec, b->momentum, w);
+    DGC_LAUNCHED();
+    DGC_TRY(thresholds(w, L, vec, s));
+    int64_t cap = 0;
+    for (const TDesc& d : td) cap += d.k;
+    const SelCfg cfg = cfg_of_batch(b);
+    int64_t voff = 0, ioff = 0;
+    payload_layout(cap, cfg.vdtype, cfg.idtype, &voff, &ioff);
+    char* pl = static_cast<char*>(payload);
+    return select_core(vec, mmt, cfg, L, pl + voff, pl + ioff, reinterpret_cast<int64_t*>(pl), info, w, 1,
+                       sync_mode, b->spec_margin, s);
 }
 
 }  // namespace dgc
@@ -1256,15 +1721,15 @@ extern "C" int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_s
 }
 
 extern "C" size_t dgc_compress_workspace(int64_t numel, int64_t num_selects, int64_t num_samples) {
-    // the strided slice holds ceil((numel - start) / stride) <= num_samples + 1 samples
-    return dgc::compress_ws_bytes(numel, num_selects, numel == num_samples ? 0 : num_samples + 1);
+    return dgc::one_ws_bytes(numel, num_selects, num_samples, true);
 }
 
 extern "C" int dgc_compress_begin(const float* grad, float* mmt, float* vec, float momentum, int32_t nesterov,
                                   int64_t sample_start, int64_t sample_stride, const dgc_select_params* params,
                                   const float* spec_threshold, void* ws, size_t ws_bytes, void* stream) {
+    // begin only reads spec[0] (the list threshold); finish updates it
     return dgc::compress_begin(grad, mmt, vec, momentum, nesterov != 0, sample_start, sample_stride, params,
-                               spec_threshold, ws, ws_bytes, static_cast<hipStream_t>(stream));
+                               const_cast<float*>(spec_threshold), ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dgc_compress_finish(float* vec, float* mmt, int64_t sample_start, int64_t sample_stride,
@@ -1288,4 +1753,17 @@ extern "C" int dgc_compress(const float* grad, float* mmt, float* vec, float mom
     return dgc::compress_finish(vec, mmt, sample_start, sample_stride, top_k_samples, params, spec_threshold,
                                 spec_margin, values_out, indices_out, count_out, info_out, ws, ws_bytes,
                                 sync_mode, static_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t dgc_batch_workspace(const dgc_batch_desc* batch) { return dgc::batch_ws_bytes(batch); }
+
+extern "C" int dgc_batch_init(const dgc_batch_desc* batch, void* ws, size_t ws_bytes, void* stream) {
+    return dgc::batch_init(batch, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
+                                  const int64_t* sample_starts, void* payload, dgc_select_info* info_out, void* ws,
+                                  size_t ws_bytes, int32_t sync_mode, void* stream) {
+    return dgc::batch_compress(batch, grad, mmt, vec, sample_starts, payload, info_out, ws, ws_bytes, sync_mode,
+                               static_cast<hipStream_t>(stream));
 }

@@ -1,0 +1,206 @@
+"""Every compressed tensor of a training step through ONE set of launches.
+
+The reference compresses tensor by tensor, from one autograd hook per parameter,
+with two Horovod allgathers per tensor (dgc/horovod/optimizer.py:116-155,
+dgc/compression.py:155-212). ``DGCBatch`` keeps the per-tensor numerics exactly —
+the same attributes (dgc/compression.py:56-89), one ``random.randint(0, stride - 1)``
+per tensor and step in the tensors' order (dgc/compression.py:118), the same
+compensate / threshold / adaptation / resample / masking per tensor — but lays the
+tensors side by side in three flat fp32 buffers (gradients, momentums, velocities;
+each tensor at a 1024-element-aligned offset) and runs
+
+    dgc_batch_compress   K1 over all tensors, K3 for all thresholds, the selection
+                         chain with per-tensor state, one packed payload
+    one allgather        the packed payload, RCCL over xGMI (gloo stages via the host)
+    decompress           dgc_fill_zero + dgc_scatter_packed over the flat gradient
+
+with O(1) launches per phase and no host synchronisation. The payload carries flat
+indices (tensor offset + index in the tensor), tensor after tensor.
+
+``grad(name)`` / ``momentum(name)`` / ``velocity(name)`` / ``out(name)`` are views in
+the flat buffers (the parameter-shaped tensors the reference keeps per name).
+"""
+import ctypes
+import math
+import random
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from . import comm
+
+__all__ = ["DGCBatch", "BatchDesc"]
+
+SEG = 1024   # tensors start at multiples of this many elements (the kernels' segment)
+
+
+class BatchDesc(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int32), ("numel", ctypes.POINTER(ctypes.c_int64)),
+                ("offset", ctypes.POINTER(ctypes.c_int64)), ("num_selects", ctypes.POINTER(ctypes.c_int64)),
+                ("num_samples", ctypes.POINTER(ctypes.c_int64)), ("top_k_samples", ctypes.POINTER(ctypes.c_int64)),
+                ("sample_stride", ctypes.POINTER(ctypes.c_int64)), ("flat_numel", ctypes.c_int64),
+                ("upper_bound", ctypes.c_double), ("lower_bound", ctypes.c_double),
+                ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("momentum_masking", ctypes.c_int32),
+                ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
+                ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float)]
+
+
+def _attributes(numel, ratio, sample_ratio):
+    """(num_selects, num_samples, top_k_samples, sample_stride): dgc/compression.py:56-89."""
+    from .compression import DGCCompressor
+    stride, samples = DGCCompressor._stride_and_samples(numel, ratio, sample_ratio)
+    return int(math.ceil(numel * ratio)), samples, int(math.ceil(samples * ratio)), stride
+
+
+class DGCBatch:
+    def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
+                 sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
+                 resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None):
+        self.device = torch.device(device or "cuda")
+        self.names = [n for n, _ in named_shapes]
+        self.shapes = {n: tuple(s) for n, s in named_shapes}
+        self.numels = [math.prod(self.shapes[n]) for n in self.names]
+        self.momentum, self.nesterov, self.momentum_masking = float(momentum), bool(nesterov), bool(momentum_masking)
+        self.sample_ratio = min(max(sample_ratio, 0.01), 1.0)
+        self.upper, self.lower = float(compress_upper_bound), float(compress_lower_bound)
+        self.max_iters, self.resample = int(max_adaptation_iters), bool(resample)
+        self.vdtype = torch.float16 if fp16_values else torch.float32
+        self.idtype = torch.int32 if int32_indices else torch.int64
+        self.world = world_size or (dist.get_world_size() if dist.is_initialized() else 1)
+        self.rng = random.Random(seed) if seed is not None else random   # the reference draws from `random`
+        offs, end = [], 0
+        for n in self.numels:
+            offs.append(end)
+            end += -(-n // SEG) * SEG
+        self.offsets = offs
+        self.flat_numel = max(end, SEG)
+        dev = self.device
+        self.grad_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self.mmt_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self.vec_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self.out_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self._L = _lib.lib()
+        self.info = torch.zeros(len(self.names) * _lib.INFO_BYTES, dtype=torch.uint8, device=dev)
+        self.set_ratio(compress_ratio)
+
+    # ---------------------------------------------------------------- layout
+    def set_ratio(self, compress_ratio):
+        """(Re-)derive every tensor's attributes for a compress ratio and write the
+        device tables — ``DGCCompressor.initialize`` (dgc/compression.py:56-89), also
+        what ``warmup_compress_ratio`` re-runs on a ratio change (:91-107)."""
+        ratio = compress_ratio if compress_ratio <= 1.0 else 1.0 / compress_ratio
+        self.ratio = ratio
+        T = len(self.names)
+        self.attrs = [_attributes(n, ratio, self.sample_ratio) for n in self.numels]
+        arr = lambda xs: (ctypes.c_int64 * T)(*xs)   # noqa: E731
+        self._arrays = [arr(self.numels), arr(self.offsets), arr([a[0] for a in self.attrs]),
+                        arr([a[1] for a in self.attrs]), arr([a[2] for a in self.attrs]), arr([a[3] for a in self.attrs])]
+        d = BatchDesc()
+        d.count = T
+        d.numel, d.offset, d.num_selects, d.num_samples, d.top_k_samples, d.sample_stride = self._arrays
+        d.flat_numel = self.flat_numel
+        d.upper_bound, d.lower_bound = self.upper, self.lower
+        d.max_iters, d.resample, d.momentum_masking = self.max_iters, int(self.resample), int(self.momentum_masking)
+        d.fp16_values, d.int32_indices = int(self.vdtype == torch.float16), int(self.idtype == torch.int32)
+        d.nesterov, d.momentum, d.spec_margin = int(self.nesterov), self.momentum, _lib.SPEC_MARGIN
+        self.desc = d
+        L = self._L
+        wsz = L.dgc_batch_workspace(ctypes.byref(d))
+        if wsz == 0:
+            raise RuntimeError(f"dgc_batch_workspace: {L.dgc_last_error().decode()}")
+        self.ws = torch.empty(wsz, dtype=torch.uint8, device=self.device)
+        _lib.check(L.dgc_batch_init(ctypes.byref(d), self.ws.data_ptr(), wsz, _lib.stream_of(self.device)),
+                   "dgc_batch_init")
+        self.capacity = sum(a[0] for a in self.attrs)
+        from .compression import _layout
+        self.rank_stride, self.voff, self.ioff = _layout(self.capacity, self.vdtype, self.idtype)
+        self.payload = torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device)
+        self.gathered = (torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=self.device)
+                         if self.world > 1 else self.payload)
+        self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(self.flat_numel, self.world, self.capacity),
+                                  dtype=torch.uint8, device=self.device)
+
+    def _view(self, flat, name):
+        i = self.names.index(name)
+        return flat[self.offsets[i]: self.offsets[i] + self.numels[i]].view(self.shapes[name])
+
+    def grad(self, name):
+        return self._view(self.grad_flat, name)
+
+    def momentum_of(self, name):
+        return self._view(self.mmt_flat, name)
+
+    def velocity_of(self, name):
+        return self._view(self.vec_flat, name)
+
+    def out(self, name):
+        return self._view(self.out_flat, name)
+
+    # ---------------------------------------------------------------- phases
+    def draw_starts(self):
+        """random.randint(0, stride - 1) per sampled tensor, in the tensors' order (dgc/compression.py:118)."""
+        starts = []
+        for n, (k, S, ks, stride) in zip(self.numels, self.attrs):
+            starts.append(self.rng.randint(0, stride - 1) if n != S else 0)
+        return starts
+
+    def compress(self, starts=None):
+        """Every tensor: compensate -> sample -> threshold -> select -> pack -> masking."""
+        starts = self.draw_starts() if starts is None else starts
+        self.starts = starts
+        arr = (ctypes.c_int64 * len(starts))(*starts)
+        _lib.check(self._L.dgc_batch_compress(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
+                                              self.mmt_flat.data_ptr(), self.vec_flat.data_ptr(), arr,
+                                              self.payload.data_ptr(), self.info.data_ptr(), self.ws.data_ptr(),
+                                              self.ws.numel(), _lib.SYNC_DEVICE, _lib.stream_of(self.device)),
+                   "dgc_batch_compress")
+
+    def exchange(self):
+        if self.world > 1:
+            comm.allgather_packed_async(self.payload, out=self.gathered).wait()
+
+    def decompress(self, out_flat=None):
+        """out = the rank-order sum of the gathered entries / W, +0.0 elsewhere (every tensor)."""
+        out = self.out_flat if out_flat is None else out_flat
+        L = self._L
+        st = _lib.stream_of(self.device)
+        _lib.check(L.dgc_fill_zero(out.data_ptr(), self.flat_numel, st), "dgc_fill_zero")
+        _lib.check(L.dgc_scatter_packed(self.gathered.data_ptr(), self.world, self.rank_stride, self.capacity,
+                                        _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(), self.flat_numel,
+                                        1.0 / self.world, self.dec_ws.data_ptr(), self.dec_ws.numel(), st),
+                   "dgc_scatter_packed")
+        return out
+
+    def step(self, starts=None):
+        self.compress(starts)
+        self.exchange()
+        return self.decompress()
+
+    # ---------------------------------------------------------------- results
+    def infos(self):
+        raw = self.info.cpu().numpy().tobytes()
+        out = []
+        for t in range(len(self.names)):
+            i = _lib.SelectInfo.from_buffer_copy(raw[t * _lib.INFO_BYTES:(t + 1) * _lib.INFO_BYTES])
+            out.append(dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
+                            branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
+                            overflow_segments=i.overflow_segments, full_passes=i.full_passes,
+                            tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule)))
+        return out
+
+    def transmitted(self, rank_payload=None):
+        """{name: (values, indices)} of one rank's payload (this rank's by default), with
+        indices relative to the tensor — what the reference's compress returns."""
+        p = self.payload if rank_payload is None else rank_payload
+        total = int(p[:8].view(torch.int64).item())
+        vb = torch.empty(0, dtype=self.vdtype).element_size()
+        ib = torch.empty(0, dtype=self.idtype).element_size()
+        vals = p[self.voff: self.voff + total * vb].view(self.vdtype)
+        idxs = p[self.ioff: self.ioff + total * ib].view(self.idtype)
+        counts = [i["count"] for i in self.infos()]
+        res, pos = {}, 0
+        for name, off, c in zip(self.names, self.offsets, counts):
+            res[name] = (vals[pos: pos + c], idxs[pos: pos + c].to(torch.int64) - off)
+            pos += c
+        return res

@@ -181,6 +181,43 @@ int dgc_compress_finish(float* vec, float* mmt, int64_t sample_start, int64_t sa
                         dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
                         void* stream);
 
+/* ---- batch: every compressed tensor of a step in the same launches ----
+ * The reference compresses tensor by tensor from the optimizer's hooks
+ * (dgc/horovod/optimizer.py:116-155). A batch lays its `count` tensors at offsets of
+ * three flat fp32 buffers (grad, mmt, vec; offsets multiples of 1024, ascending,
+ * each tensor followed by zeros up to a multiple of 4) and runs compensate ->
+ * sample -> threshold -> select / adapt / resample -> pack -> masking for all of
+ * them with O(1) launches per phase and, in DGC_SYNC_DEVICE mode, no host sync.
+ * Per tensor the numerics are exactly dgc_compress's (same attributes, same
+ * sample start). The payload is ONE packed rank buffer (dgc_payload_layout with
+ * capacity = sum of num_selects): the tensors' entries one after the other, in
+ * tensor order, with FLAT indices (offset + index in the tensor); decompress it with
+ * dgc_decompress_packed / dgc_scatter_packed over flat_numel elements. */
+typedef struct dgc_batch_desc {
+    int32_t count;                  /* tensors                                        */
+    const int64_t* numel;           /* host arrays of `count`: attributes per tensor  */
+    const int64_t* offset;          /*   (dgc/compression.py:85)                      */
+    const int64_t* num_selects;
+    const int64_t* num_samples;
+    const int64_t* top_k_samples;
+    const int64_t* sample_stride;
+    int64_t flat_numel;             /* length of the flat buffers                     */
+    double upper_bound, lower_bound;/* compress_upper_bound / compress_lower_bound    */
+    int32_t max_iters, resample, momentum_masking, fp16_values, int32_indices, nesterov;
+    float momentum;
+    float spec_margin;              /* speculative list threshold margin (0.8)        */
+} dgc_batch_desc;
+
+size_t dgc_batch_workspace(const dgc_batch_desc* batch);
+/* Writes the batch's device tables into the workspace (synchronous). Re-run after any
+ * change of the tensors or their attributes (e.g. warmup_compress_ratio). */
+int dgc_batch_init(const dgc_batch_desc* batch, void* ws, size_t ws_bytes, void* stream);
+/* sample_starts: host array of `count` (random.randint(0, stride - 1) per tensor, in
+ * the tensors' order); info_out: device array of `count` records (may be NULL). */
+int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
+                       const int64_t* sample_starts, void* payload, dgc_select_info* info_out, void* ws,
+                       size_t ws_bytes, int32_t sync_mode, void* stream);
+
 /* ---- K6: deterministic decompress ----
  * grad[0..n) = scale * (rank-order sequential sum of the entries), every other
  * slot +0.0. dgc_decompress takes the concatenated (values, indices) of the

@@ -1,0 +1,115 @@
+"""The batched step: every compressed tensor of a model in one
+set of launches (dgc.batch.DGCBatch -> dgc_batch_compress), checked tensor by tensor
+against the oracle — the reference's per-hook compress (dgc/horovod/optimizer.py:116-155,
+dgc/compression.py:155-177) with one random.randint per tensor in the tensors' order."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dgc_oracle as O
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view({4: np.uint32, 2: np.uint16, 8: np.uint64}[a.dtype.itemsize])
+
+
+def _sets():
+    from dgc import workloads
+    r50, _ = workloads.split(workloads.resnet50())
+    vgg, _ = workloads.split(workloads.vgg16_bn())
+    mixed = [("tiny_direct", (1500,)), ("stride1", (2001,)), ("a", (64, 3, 7, 7)), ("odd", (1000003,)),
+             ("b", (300, 1000)), ("ties", (4099,)), ("c", (2048, 1024))]
+    return {"resnet50": (r50, False, False), "vgg16_bn": (vgg, True, True), "mixed": (mixed, False, False)}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("label", ["mixed", "resnet50", "vgg16_bn"])
+def test_batch_matches_per_tensor_oracle(label):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc.batch import DGCBatch
+    shapes, fp16, int32 = _sets()[label]
+    nest = label == "mixed"
+    b = DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, nesterov=nest, fp16_values=fp16,
+                 int32_indices=int32, device=DEV, seed=42)
+    ref_rng = random.Random(42)
+    state = {n: (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
+             for i, n in enumerate(b.names)}
+    branches = set()
+    for s in range(3 if label != "vgg16_bn" else 2):
+        grads = {}
+        for t, name in enumerate(b.names):
+            kind = "ties" if name == "ties" else ("layered" if t % 3 == 0 else "normal")
+            g = synth.gradient(1000 * s + t, b.numels[t], kind, 1e-3 * (1 + t % 7))
+            grads[name] = g
+            b.grad(name).copy_(torch.from_numpy(g).view(b.shapes[name]))
+        starts = b.draw_starts()
+        b.compress(starts)
+        out = b.decompress()
+        torch.cuda.synchronize()
+        sent = b.transmitted()
+        infos = b.infos()
+        for t, name in enumerate(b.names):
+            N = b.numels[t]
+            attrs = O.attributes(N, 0.001)
+            start = ref_rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
+            assert start == starts[t], (name, s)
+            m_o, v_o = state[name]
+            ov, oi, info = O.compress_step(grads[name], m_o, v_o, attrs, start, nesterov=nest)
+            wv, wi = O.wire_cast(ov, oi, fp16, int32)
+            key = f"{label}/s{s}/{name}"
+            branches.add(info["branch"])
+            assert infos[t]["branch"] == info["branch"], key
+            gv, gi = sent[name]
+            assert np.array_equal(gi.cpu().numpy(), oi), key
+            assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
+            assert np.array_equal(bits(b.momentum_of(name).reshape(-1).cpu().numpy()), bits(m_o)), key
+            assert np.array_equal(bits(b.velocity_of(name).reshape(-1).cpu().numpy()), bits(v_o)), key
+            dense = O.decompress([wv], [oi], N, 1)
+            assert np.array_equal(bits(b.out(name).reshape(-1).cpu().numpy()), bits(dense)), key
+        # padding between tensors stays zero (no tensor writes outside itself)
+        pad = torch.ones(b.flat_numel, dtype=torch.bool, device=DEV)
+        for off, n in zip(b.offsets, b.numels):
+            pad[off: off + n] = False
+        assert not bool(out[pad].any()) and not bool(b.vec_flat[pad].any())
+    if label == "mixed":
+        assert {"direct", "resample"} <= branches, branches
+
+
+def test_batch_warmup_ratio_change():
+    """warmup_compress_ratio re-initialises the attributes mid-run (dgc/compression.py:91-107)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc import workloads
+    from dgc.batch import DGCBatch
+    shapes, _ = workloads.split(workloads.resnet20())
+    b = DGCBatch(shapes, compress_ratio=0.316, momentum=0.9, fp16_values=True, int32_indices=True, device=DEV,
+                 seed=7)
+    ref_rng = random.Random(7)
+    state = {n: (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
+             for i, n in enumerate(b.names)}
+    for s, ratio in enumerate([0.316, 0.316, 0.1, 0.001, 0.001]):
+        if ratio != b.ratio:
+            b.set_ratio(ratio)
+        grads = {}
+        for t, name in enumerate(b.names):
+            grads[name] = synth.gradient(77 * s + t, b.numels[t], "normal", 0.01)
+            b.grad(name).copy_(torch.from_numpy(grads[name]).view(b.shapes[name]))
+        b.compress()
+        torch.cuda.synchronize()
+        sent = b.transmitted()
+        for t, name in enumerate(b.names):
+            attrs = O.attributes(b.numels[t], ratio)
+            start = ref_rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
+            m_o, v_o = state[name]
+            ov, oi, _ = O.compress_step(grads[name], m_o, v_o, attrs, start)
+            wv, wi = O.wire_cast(ov, oi, True, True)
+            assert np.array_equal(sent[name][1].cpu().numpy(), oi), (s, name)
+            assert np.array_equal(bits(sent[name][0].cpu().numpy()), bits(wv)), (s, name)
