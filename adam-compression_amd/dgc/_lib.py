@@ -9,7 +9,7 @@ import os
 import torch
 
 __all__ = ["lib", "check", "stream_of", "ptr", "SelectParams", "SelectInfo", "Workspace",
-           "VD", "ID", "BRANCHES", "LIB_PATH", "available"]
+           "VD", "ID", "BRANCHES", "LIB_PATH", "available", "BatchDesc"]
 
 LIB_PATH = os.environ.get(
     "DGC_HIP_LIB",
@@ -41,6 +41,18 @@ class SelectInfo(ctypes.Structure):
 
 
 INFO_BYTES = ctypes.sizeof(SelectInfo)
+
+
+class BatchDesc(ctypes.Structure):
+    """dgc_batch_desc (include/dgc_hip.h): a batch's tensors and shared settings."""
+    _fields_ = [("count", ctypes.c_int32), ("numel", ctypes.POINTER(ctypes.c_int64)),
+                ("offset", ctypes.POINTER(ctypes.c_int64)), ("num_selects", ctypes.POINTER(ctypes.c_int64)),
+                ("num_samples", ctypes.POINTER(ctypes.c_int64)), ("top_k_samples", ctypes.POINTER(ctypes.c_int64)),
+                ("sample_stride", ctypes.POINTER(ctypes.c_int64)), ("flat_numel", ctypes.c_int64),
+                ("upper_bound", ctypes.c_double), ("lower_bound", ctypes.c_double),
+                ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("momentum_masking", ctypes.c_int32),
+                ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
+                ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float)]
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -77,6 +89,10 @@ _SIGNATURES = {
     "dgc_scatter_packed": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
     "dgc_fill_zero": (ctypes.c_int, [_P, _I64, _P]),
     "dgc_decompress_status": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dgc_batch_workspace": (_SZ, [ctypes.POINTER(BatchDesc)]),
+    "dgc_batch_init": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _SZ, _P]),
+    "dgc_batch_compress": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, ctypes.POINTER(_I64), _P, _P, _P,
+                                          _SZ, _I32, _P]),
     "dgc_sgd_step": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                     ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _P]),
 }

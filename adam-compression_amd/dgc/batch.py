@@ -30,20 +30,9 @@ import torch.distributed as dist
 from . import _lib
 from . import comm
 
-__all__ = ["DGCBatch", "BatchDesc"]
+__all__ = ["DGCBatch"]
 
 SEG = 1024   # tensors start at multiples of this many elements (the kernels' segment)
-
-
-class BatchDesc(ctypes.Structure):
-    _fields_ = [("count", ctypes.c_int32), ("numel", ctypes.POINTER(ctypes.c_int64)),
-                ("offset", ctypes.POINTER(ctypes.c_int64)), ("num_selects", ctypes.POINTER(ctypes.c_int64)),
-                ("num_samples", ctypes.POINTER(ctypes.c_int64)), ("top_k_samples", ctypes.POINTER(ctypes.c_int64)),
-                ("sample_stride", ctypes.POINTER(ctypes.c_int64)), ("flat_numel", ctypes.c_int64),
-                ("upper_bound", ctypes.c_double), ("lower_bound", ctypes.c_double),
-                ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("momentum_masking", ctypes.c_int32),
-                ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
-                ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float)]
 
 
 def _attributes(numel, ratio, sample_ratio):
@@ -96,7 +85,7 @@ class DGCBatch:
         arr = lambda xs: (ctypes.c_int64 * T)(*xs)   # noqa: E731
         self._arrays = [arr(self.numels), arr(self.offsets), arr([a[0] for a in self.attrs]),
                         arr([a[1] for a in self.attrs]), arr([a[2] for a in self.attrs]), arr([a[3] for a in self.attrs])]
-        d = BatchDesc()
+        d = _lib.BatchDesc()
         d.count = T
         d.numel, d.offset, d.num_selects, d.num_samples, d.top_k_samples, d.sample_stride = self._arrays
         d.flat_numel = self.flat_numel

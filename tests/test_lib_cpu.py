@@ -70,3 +70,28 @@ def test_invalid_arguments_fail_without_gpu(L):
     rc = L.dgc_select(None, None, None, ctypes.byref(p), ctypes.c_void_p(16), ctypes.c_void_p(16), None,
                       None, None, 0, 0, None)
     assert rc == 3
+
+
+def test_batch_desc_validation_without_gpu(L):
+    """dgc_batch_workspace sizes a valid batch and refuses bad layouts (no GPU needed)."""
+    import ctypes
+    from dgc import _lib
+
+    def desc(numels, offsets, flat):
+        T = len(numels)
+        arr = lambda xs: (ctypes.c_int64 * T)(*xs)   # noqa: E731
+        keep = [arr(numels), arr(offsets), arr([max(1, n // 1000) for n in numels]), arr(numels),
+                arr([max(1, n // 1000) for n in numels]), arr([1] * T)]
+        d = _lib.BatchDesc()
+        d.count = T
+        d.numel, d.offset, d.num_selects, d.num_samples, d.top_k_samples, d.sample_stride = keep
+        d.flat_numel, d.upper_bound, d.lower_bound, d.max_iters, d.resample = flat, 1.3, 0.8, 10, 1
+        return d, keep
+
+    d, keep = desc([5000, 3000], [0, 5120], 8192)
+    assert L.dgc_batch_workspace(ctypes.byref(d)) > 0
+    d, keep = desc([5000, 3000], [0, 5000], 8192)          # offset not a multiple of 1024
+    assert L.dgc_batch_workspace(ctypes.byref(d)) == 0
+    assert b"multiple of 1024" in L.dgc_last_error()
+    d, keep = desc([5000, 3000], [0, 5120], 8000)          # past flat_numel
+    assert L.dgc_batch_workspace(ctypes.byref(d)) == 0
