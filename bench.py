@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
-"""DGC hot-path benchmark on MI355X: one flat fp32 gradient bucket per rank through
-compensate -> compress (sample, threshold, select, masking) -> RCCL allgather ->
-decompress, all on the device (BASELINE.json configs[3]: 1B elements, ratio 0.001,
-nesterov, momentum 0.9, fp32/int64 wire; 1/2/4/8 GPUs, weak scaling).
+"""DGC hot-path benchmark on MI355X: compensate -> compress (sample, threshold,
+select, adaptation, masking) -> RCCL allgather -> decompress, all on the device.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--numel 1e9] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--no-cpu]
     torchrun --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line. ``value`` = grad elements processed by all ranks per
-second (each rank compresses its own N-element gradient). ``roofline`` is for the
-dominant kernel, K1 (compensate + fused sample), timed with HIP events on the
-stream it runs on; the whole step's algorithmic HBM rate is reported beside it.
+Workloads (BASELINE.json configs; synthetic data of their shapes):
+  flat-1B       (default) 1e9-element fp32 bucket, ratio 0.001, nesterov, fp32/int64  [configs[3]]
+  flat-7B-bf16  7e9 elements, bf16-origin gradients, ratio 1e-4, int64 indices        [configs[4]]
+  resnet50      the 161 gradient tensors of ResNet-50 (54 compressed, 25.5M elements;
+                107 dense), ratio 0.001, fp32/int64, one batched step                  [configs[1]]
+  vgg16_bn      the 58 gradient tensors of VGG-16-BN (16 compressed, 138.3M elements),
+                ratio 0.001, fp16 values / int32 indices                               [configs[2]]
+
+Rank 0 prints ONE JSON line. ``value`` = gradient elements processed by all ranks per
+second (each rank compresses its own replica's gradients: weak scaling). ``roofline``
+is for the dominant kernel, K1 (compensate + fused sample + candidate lists), timed
+with HIP events on the stream it runs on; ``step_hbm`` is the whole step's algorithmic
+HBM rate. With ``--gpus N`` and no torchrun, N ranks are spawned on 127.0.0.1.
 """
 import argparse
 import json
@@ -31,68 +38,135 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_COPY_GBS = 6290.0            # measured float4 copy ceiling (same guide)
 XGMI_LINK_GBS = 153.0            # per link, per direction
 
+WORKLOADS = {
+    "flat-1B": dict(kind="flat", numel=10 ** 9, ratio=1e-3, grad="normal", nesterov=True,
+                    config="BASELINE configs[3]: synthetic 1B-element flat gradient bucket"),
+    "flat-7B-bf16": dict(kind="flat", numel=7 * 10 ** 9, ratio=1e-4, grad="bf16", nesterov=True,
+                         config="BASELINE configs[4]: synthetic 7B-element bf16-origin gradient"),
+    "resnet50": dict(kind="model", model="resnet50", ratio=1e-3, fp16=False, int32=False, nesterov=False,
+                     config="BASELINE configs[1]: ResNet-50 ImageNet gradient set"),
+    "vgg16_bn": dict(kind="model", model="vgg16_bn", ratio=1e-3, fp16=True, int32=True, nesterov=False,
+                     config="BASELINE configs[2]: VGG-16-BN gradient set"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--numel", type=float, default=1e9)
-    ap.add_argument("--ratio", type=float, default=0.001)
-    ap.add_argument("--cpu-numel", type=float, default=1e9, help="CPU-baseline sample size")
-    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--workload", default="flat-1B", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-numel", type=float, default=3e8, help="CPU-baseline sample (all cores), flat")
+    ap.add_argument("--cpu-numel-1t", type=float, default=5e7, help="CPU-baseline sample (1 thread), flat")
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
+    ap.add_argument("--fill", default="auto", choices=["auto", "inline", "allgather"])
     return ap.parse_args()
 
 
-def cpu_baseline(numel, ratio, steps):
-    """The reference op sequence restated on torch CPU (oracle/torch_cpu.py), timed on
-    this host's cores over a bounded sample of the workload (rank 0, N=1 only)."""
-    from oracle import torch_cpu
-    threads = torch.get_num_threads()
-    N = int(numel)
-    attrs = torch_cpu.attributes(N, ratio)
-    g = torch.randn(N, generator=torch.Generator().manual_seed(1))
-    mmt, vec, out = torch.zeros(N), torch.zeros(N), torch.empty(N)
-    import random
-    rng = random.Random(42)
-    torch_cpu.cpu_step(g, mmt, vec, out, attrs, rng.randint(0, attrs[4] - 1))   # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        torch_cpu.cpu_step(g, mmt, vec, out, attrs, rng.randint(0, attrs[4] - 1))
-    dt = (time.perf_counter() - t0) / steps
-    model = ""
+# ---------------------------------------------------------------------------- CPU baseline
+def cpu_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    return ""
+
+
+def cpu_baseline(wl, numel, steps, threads):
+    """The reference op sequence restated on torch CPU (oracle/torch_cpu.py, pinned to
+    the reference's golden fixtures), timed on this host over a bounded sample of the
+    workload (rank 0, N=1 only): the same per-element work, fewer elements."""
+    from oracle import torch_cpu
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    import random
+    rng = random.Random(42)
+    try:
+        if wl["kind"] == "model":
+            from dgc import workloads
+            comp, dense = workloads.split(getattr(workloads, wl["model"])())
+            tensors = []
+            for i, (name, shape) in enumerate(comp):
+                n = workloads.numel(shape)
+                attrs = torch_cpu.attributes(n, wl["ratio"])
+                g = torch.randn(n, generator=torch.Generator().manual_seed(i))
+                tensors.append((attrs, g, torch.zeros(n), torch.zeros(n), torch.empty(n)))
+            N = sum(t[0][0] for t in tensors)
+
+            def step():
+                for attrs, g, m, v, out in tensors:
+                    start = rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
+                    torch_cpu.cpu_step(g, m, v, out, attrs, start, nesterov=wl["nesterov"])
+            what = f"all {len(tensors)} compressed tensors ({N} elements) of {wl['model']}"
+        else:
+            N = int(numel)
+            attrs = torch_cpu.attributes(N, wl["ratio"])
+            g = torch.randn(N, generator=torch.Generator().manual_seed(1))
+            if wl["grad"] == "bf16":
+                g = g.to(torch.bfloat16).float()
+            m, v, out = torch.zeros(N), torch.zeros(N), torch.empty(N)
+
+            def step():
+                torch_cpu.cpu_step(g, m, v, out, attrs, rng.randint(0, attrs[4] - 1), nesterov=wl["nesterov"])
+            what = f"a {N}-element flat sample of the {wl['numel']}-element bucket at the same ratio"
+        step()   # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        torch.set_num_threads(prev)
     return {"value": N / dt, "unit": "grad elements/s", "cores": threads, "kind": "port",
-            "sample": f"{N} elements x {steps} steps (compensate+sparsify+update+decompress, W=1, "
-                      f"torch {torch.__version__} CPU ops as the reference issues them), "
-                      f"{dt * 1e3:.1f} ms/step on {threads} threads; {model}"}
+            "sample": f"{what} x {steps} steps (compensate+sparsify+update+decompress, W=1, torch "
+                      f"{torch.__version__} CPU ops as the reference issues them): {dt * 1e3:.1f} ms/step on "
+                      f"{threads} thread(s); {cpu_model()}"}
 
 
-def pmc_traffic(kernel_key="k_compensate_list"):
+# ---------------------------------------------------------------------------- profiles
+def pmc_traffic(workload, kernel_key="k_compensate_list"):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC profile
-    of this bench (tools/gpu_check.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    passes; FETCH_SIZE x2 for gfx950's half count of wide reads, KB x 1024)."""
+    of this exact bench command (tools/pmc_json.py over separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x2 for gfx950's half count of wide reads)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", "pmc.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", f"pmc_{workload}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for k, v in d.get("kernels", {}).items():
+        if kernel_key in k:
+            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], REPO)
+    return None, None
+
+
+def rocprof_k1_ms(workload, kernel_key="k_compensate_list"):
+    """The dominant kernel's average duration in the committed rocprofv3 kernel-trace
+    stats of this exact bench command (profiles/round*/kstats_<workload>.json)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", f"kstats_{workload}.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
     for k, v in d.items():
         if kernel_key in k:
-            return v["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], REPO)
+            return v["avg_ms"], os.path.relpath(files[-1], REPO)
     return None, None
 
 
+# ---------------------------------------------------------------------------- launcher
 def free_port():
     import socket
     with socket.socket() as s:
@@ -130,11 +204,146 @@ def spawn(envs):
     return next((c for c in codes if c != 0), 0)
 
 
+# ---------------------------------------------------------------------------- workloads
+class FlatRun:
+    """One flat bucket per rank through dgc.bucket.DGCBucket."""
+
+    def __init__(self, wl, rank, world, dev, fill):
+        from dgc.bucket import DGCBucket
+        N = wl["numel"]
+        self.N = N
+        self.b = DGCBucket(N, compress_ratio=wl["ratio"], momentum=0.9, nesterov=wl["nesterov"], device=dev,
+                           world_size=world, fill=fill)
+        gen = torch.Generator(device=dev)
+        self.grads = []
+        for s in range(2):   # two alternating gradients per rank, generated before timing
+            gen.manual_seed(0xD6C + 1000 * rank + s)
+            g = torch.empty(N, device=dev)
+            for c0 in range(0, N, 1 << 30):
+                c1 = min(N, c0 + (1 << 30))
+                x = torch.randn(c1 - c0, generator=gen, device=dev)
+                g[c0:c1] = x.to(torch.bfloat16).float() if wl["grad"] == "bf16" else x
+                del x
+            self.grads.append(g)
+        self.out = torch.empty(N, device=dev)
+        self.elements = N
+        self.k, self.S = self.b.k, self.b.num_samples
+        self.payload = self.b.rank_stride
+        self.vbytes, self.ibytes = 4, 8
+
+    def step(self, i, ev=None):
+        self.b.step(self.grads[i % 2], self.out, ev)
+
+    def k1_bytes(self):
+        return 20 * self.N + 4 * self.b.cnt    # read g, mmt, vec; write mmt, vec; write the samples
+
+    def info(self):
+        return self.b.last_info()
+
+    def config(self):
+        b = self.b
+        return {"numel": self.N, "num_selects": b.k, "num_samples": b.num_samples, "sample_stride": b.stride,
+                "fill": b.fill}
+
+
+class ModelRun:
+    """A model's gradient set per rank: the compressed tensors through one DGCBatch
+    step, the dense (dim <= 1) tensors as one flat allreduce + compensate(accumulate=False)
+    (dgc/compression.py:173-177, 195-198)."""
+
+    def __init__(self, wl, rank, world, dev):
+        from dgc import workloads
+        from dgc.batch import DGCBatch
+        comp, dense = workloads.split(getattr(workloads, wl["model"])())
+        self.b = DGCBatch(comp, compress_ratio=wl["ratio"], momentum=0.9, nesterov=wl["nesterov"],
+                          fp16_values=wl["fp16"], int32_indices=wl["int32"], device=dev, world_size=world, seed=42)
+        self.n_comp = sum(self.b.numels)
+        self.n_dense = sum(workloads.numel(s) for _, s in dense)
+        self.world = world
+        gen = torch.Generator(device=dev)
+        self.grads = []
+        for s in range(2):
+            gen.manual_seed(0xD6C + 1000 * rank + s)
+            g = torch.zeros(self.b.flat_numel, device=dev)
+            for off, n in zip(self.b.offsets, self.b.numels):
+                g[off: off + n] = torch.randn(n, generator=gen, device=dev) * 1e-3
+            self.grads.append((g, torch.randn(self.n_dense, generator=gen, device=dev) * 1e-3))
+        self.dense_mmt = torch.zeros(self.n_dense, device=dev)
+        self.dense_out = torch.empty(self.n_dense, device=dev)
+        self.dense_wire = torch.empty(self.n_dense, dtype=torch.float16 if wl["fp16"] else torch.float32, device=dev)
+        self.elements = self.n_comp + self.n_dense
+        self.k, self.S = self.b.capacity, sum(a[1] for a in self.b.attrs)
+        self.payload = self.b.rank_stride
+        self.vbytes, self.ibytes = (2 if wl["fp16"] else 4), (4 if wl["int32"] else 8)
+        self.nesterov = wl["nesterov"]
+        from dgc import _lib
+        self._lib = _lib
+
+    def step(self, i, ev=None):
+        g, gd = self.grads[i % 2]
+        ev = ev or {}
+        L, b = self._lib.lib(), self.b
+        b.grad_flat = g   # the model's gradients live in the batch's flat buffer (p.grad views)
+        for name, fn in (("compensate", lambda: b.compress()), ("allgather", b.exchange),
+                         ("decompress", b.decompress)):
+            pair = ev.get(name)
+            if pair:
+                pair[0].record()
+            fn()
+            if pair:
+                pair[1].record()
+        # dense tensors: (fp16 wire cast) -> allreduce Average -> compensate(accumulate=False)
+        self.dense_wire.copy_(gd)
+        if self.world > 1:
+            from dgc import comm
+            comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Average))
+        src = self.dense_wire if self.dense_wire.dtype == torch.float32 else self.dense_wire.float()
+        self._lib.check(L.dgc_compensate(src.data_ptr(), self.dense_mmt.data_ptr(), None, self.dense_out.data_ptr(),
+                                         self.n_dense, 0.9, int(self.nesterov), 0, None, 0, 1, 0,
+                                         self._lib.stream_of(g.device)), "dgc_compensate")
+
+    def k1_bytes(self):
+        # every compressed tensor: read g, mmt, vec; write mmt, vec; plus the samples written
+        return 20 * self.n_comp + 4 * sum(a[1] + 1 for a in self.b.attrs if a[1] != 0)
+
+    def info(self):
+        infos = self.b.infos()
+        branches = {}
+        for i in infos:
+            branches[i["branch"]] = branches.get(i["branch"], 0) + 1
+        return {"tensors": len(infos), "count": sum(i["count"] for i in infos), "branches": branches,
+                "full_passes": sum(i["full_passes"] for i in infos),
+                "exact_resamples": sum(i["tie_rule"] == "exact" for i in infos)}
+
+    def config(self):
+        return {"compressed_tensors": len(self.b.names), "compressed_elements": self.n_comp,
+                "dense_elements": self.n_dense, "num_selects_total": self.b.capacity}
+
+
+def step_bytes(run, world, full_passes):
+    """Bytes one rank must move per step (per compressed element):
+    compensate 20 + select re-read 4 (0 when the K1 candidate lists serve the
+    selection) + dense decompress write 4, the samples 4S, masking 8k, payload written
+    k(vb+ib) + gathered W*k(vb+ib) read, scatter RMW 8Wk. `contract` keeps the 28 B
+    of SURVEY.md §8d; `required` is what this step's path actually needs."""
+    n = run.n_comp if isinstance(run, ModelRun) else run.N
+    k, S = run.k, run.S
+    sparse = 4 * S + 8 * k + (1 + world) * k * (run.vbytes + run.ibytes) + 8 * world * k
+    contract = 28 * n + sparse
+    required = (24 if full_passes == 0 else 28) * n + sparse
+    if isinstance(run, ModelRun):   # dense tensors: read g, mmt; write mmt, out
+        contract += 16 * run.n_dense
+        required += 16 * run.n_dense
+    return contract, required
+
+
+# ---------------------------------------------------------------------------- main
 def main():
     args = parse()
     envs = launch_plan(args.gpus, os.environ)
     if envs is not None:
         sys.exit(spawn(envs))
+    wl = WORKLOADS[args.workload]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -142,22 +351,15 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    from dgc.bucket import DGCBucket, algorithmic_bytes
-
-    N = int(args.numel)
-    bucket = DGCBucket(N, compress_ratio=args.ratio, momentum=0.9, nesterov=True, device=dev, world_size=world)
-    gen = torch.Generator(device=dev)
-    grads = []
-    for s in range(2):
-        gen.manual_seed(0xD6C + 1000 * rank + s)
-        grads.append(torch.randn(N, generator=gen, device=dev))
-    out = torch.empty(N, device=dev)
+    run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev)
 
     phases = ("compensate", "select", "allgather", "decompress")
     for i in range(args.warmup):
-        bucket.step(grads[i % 2], out)
+        run.step(i)
     torch.cuda.synchronize()
     timed = phases if args.phases else ("compensate", "allgather")
+    if wl["kind"] == "model":
+        timed = ("compensate", "allgather", "decompress")   # compensate = the whole batched compress
     evs = [{p: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for p in timed}
            for _ in range(args.steps)]
     if world > 1:
@@ -165,7 +367,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        bucket.step(grads[i % 2], out, evs[i])
+        run.step(i, evs[i])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -174,21 +376,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ms = {p: sum(e[p][0].elapsed_time(e[p][1]) for e in evs) / args.steps for p in timed}
-    info = bucket.last_info()
+    info = run.info()
     ms_step = elapsed * 1e3 / args.steps
-    k, S = bucket.k, bucket.num_samples
-    step_bytes = algorithmic_bytes(N, k, S, world)
-    k1_bytes = 20 * N + 4 * bucket.cnt            # read g, mmt, vec; write mmt, vec; write samples
-    k1_gbs = k1_bytes / (ms["compensate"] * 1e-3) / 1e9
-    payload = bucket.rank_stride
-    traffic, traffic_src = pmc_traffic()
+    full_passes = info.get("full_passes", 0)
+    contract, required = step_bytes(run, world, full_passes)
+    k1_bytes = run.k1_bytes()
+    traffic, traffic_src = pmc_traffic(args.workload)
+    prof_ms, prof_src = rocprof_k1_ms(args.workload)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
+    if wl["kind"] == "flat":
+        k1_ms = ms["compensate"]
+        k1_name = "K1 compensate + fused sample + speculative lists (k_compensate_list)"
+    else:
+        # the batched compress phase holds K1 and the selection: K1's share comes from rocprof
+        k1_ms = prof_ms if prof_ms else ms["compensate"]
+        k1_name = "K1 over all compressed tensors (k_compensate_list, one launch)"
+    k1_gbs = k1_bytes / (k1_ms * 1e-3) / 1e9
+    wire = f"{'fp16' if run.vbytes == 2 else 'fp32'} values / {'int32' if run.ibytes == 4 else 'int64'} indices"
     res = {
         "metric": METRIC,
-        "value": world * N / (ms_step * 1e-3),
+        "value": world * run.elements / (ms_step * 1e-3),
         "unit": "grad elements/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -198,32 +408,32 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: torch.randn N(0,1) fp32 gradients, 2 alternating buffers per rank "
-                "(seed 0xD6C + 1000*rank + buffer); momentum/velocity state evolves across steps",
-        "config": {"workload": "flat-1B-bucket (BASELINE configs[3])" if N == 10 ** 9 else f"flat-{N}-bucket",
-                   "numel": N, "compress_ratio": args.ratio, "num_selects": k, "num_samples": S,
-                   "sample_stride": bucket.stride, "nesterov": True, "momentum": 0.9, "momentum_masking": True,
-                   "wire": "fp32 values / int64 indices", "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "K1 compensate + fused sample + speculative lists (k_compensate_list)",
-                     "bound": "hbm",
-                     "achieved": k1_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k1_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": k1_bytes,
-                     "avg_launch_ms": ms["compensate"]},
-        "step_hbm": {"algorithmic_bytes_per_rank": step_bytes,
-                     "achieved_GBs": step_bytes / (ms_step * 1e-3) / 1e9,
-                     "frac_of_8TBs": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "frac_of_measured_copy": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_COPY_GBS},
+        "data": "synthetic: torch.randn N(0,1) gradients (bf16-rounded for flat-7B-bf16; x1e-3 for the model "
+                "sets), 2 alternating buffers per rank (seed 0xD6C + 1000*rank + buffer); momentum/velocity "
+                "state evolves across steps",
+        "config": dict({"workload": f"{args.workload} ({wl['config']})", "compress_ratio": wl["ratio"],
+                        "nesterov": wl["nesterov"], "momentum": 0.9, "momentum_masking": True, "wire": wire,
+                        "parallelism": f"dp{world}"}, **run.config()),
+        "roofline": {"kernel": k1_name, "bound": "hbm", "achieved": k1_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": k1_gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": k1_bytes, "avg_launch_ms": k1_ms,
+                     "rocprof_avg_launch_ms": prof_ms, "rocprof_source": prof_src},
+        "step_hbm": {"required_bytes_per_rank": required, "contract_bytes_per_rank": contract,
+                     "achieved_GBs": required / (ms_step * 1e-3) / 1e9,
+                     "frac_of_8TBs": required / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "contract_frac_of_8TBs": contract / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "frac_of_measured_copy": required / (ms_step * 1e-3) / 1e9 / HBM_COPY_GBS},
         "phase_ms": {p: round(v, 4) for p, v in ms.items()},
         "selection": info,
     }
-    if world > 1 and ms["allgather"] > 0:
-        bus = (world - 1) * payload / (ms["allgather"] * 1e-3) / 1e9
-        res["allgather"] = {"payload_bytes_per_rank": payload, "bus_GBs": bus,
-                            "peak_GBs": (world - 1) * XGMI_LINK_GBS,
-                            "frac": bus / ((world - 1) * XGMI_LINK_GBS)}
+    if world > 1 and ms.get("allgather", 0) > 0:
+        bus = (world - 1) * run.payload / (ms["allgather"] * 1e-3) / 1e9
+        res["allgather"] = {"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
+                            "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS)}
     if world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(args.cpu_numel, args.ratio, args.cpu_steps)
+        cores = cpu_cores()
+        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_numel, args.cpu_steps, cores)
+        res["cpu_baseline_1thread"] = cpu_baseline(wl, args.cpu_numel_1t, 2, 1)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

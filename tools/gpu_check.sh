@@ -1,25 +1,22 @@
 #!/bin/bash
-# One GPU session: parity tests, ablations, a rocprofv3 kernel-trace of the bench, the bench.
-#   tools/gpu_check.sh TAG [bench args...]
-# Outputs under gpurun_out/: pytest_gpu.log, ablate.json, prof_TAG/, bench.json
-TAG=${1:-x}
-shift
+# Profile exactly one bench command on the GPU box: the bench itself, a rocprofv3
+# kernel-trace + --stats run of the same command, and one --pmc pass per counter.
+#   tools/gpu_check.sh WORKLOAD STEPS WARMUP [extra bench args...]
+# Outputs under gpurun_out/: bench_WL.json, prof_WL/, pmc_WL/ (then tools/profile_summary.py).
+set -o pipefail
+WL=${1:-flat-1B}
+STEPS=${2:-20}
+WARM=${3:-5}
+shift 3
 mkdir -p gpurun_out
-rm -rf gpurun_out/prof_$TAG gpurun_out/bench.json gpurun_out/ablate.json
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python tools/ablate.py > gpurun_out/ablate.json 2> gpurun_out/ablate.err || exit $?
+rm -rf "gpurun_out/prof_$WL" "gpurun_out/pmc_$WL"
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run \
-    --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu "$@" \
-    > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
-# HBM traffic counters, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950)
-if [ "${DGC_PMC:-1}" = "1" ]; then
-  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG" -o fetch --output-format csv \
-      -- python bench.py --steps 3 --warmup 1 --no-cpu "$@" > /dev/null 2> gpurun_out/pmc_fetch.err || exit $?
-  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG" -o write --output-format csv \
-      -- python bench.py --steps 3 --warmup 1 --no-cpu "$@" > /dev/null 2> gpurun_out/pmc_write.err || exit $?
-fi
+CMD="bench.py --gpus 1 --steps $STEPS --warmup $WARM --workload $WL $*"
+timeout -k 10 400 python $CMD > "gpurun_out/bench_$WL.json" 2> "gpurun_out/bench_$WL.err" || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$WL" -o run \
+    --output-format csv -- python $CMD --no-cpu > "gpurun_out/bench_prof_$WL.json" 2> "gpurun_out/prof_$WL.err" || exit $?
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$WL" -o fetch \
+    --output-format csv -- python $CMD --no-cpu > /dev/null 2> "gpurun_out/pmc_fetch_$WL.err" || exit $?
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$WL" -o write \
+    --output-format csv -- python $CMD --no-cpu > /dev/null 2> "gpurun_out/pmc_write_$WL.err" || exit $?
+echo "done $WL"
