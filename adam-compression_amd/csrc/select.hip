@@ -308,7 +308,7 @@ __global__ void k_put_starts(SelWS w, StartChunk c) {
     const int i = threadIdx.x;
     if (i >= c.count) return;
     const int t = c.first + i;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     w.starts[t] = c.start[i];
     w.scnt[t] = d.samp_off < 0 ? d.n : ceil_div(d.n - c.start[i], d.stride);
 }
@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(kBlock)
 k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat, float* __restrict__ vec_flat,
                   float mom, SelWS w) {
     const int t = task(w, BT_K1, blockIdx.x);
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_K1][t]) * kSegPerBlock4 + wave;   // local segment
     const float4* g = reinterpret_cast<const float4*>(g_flat + d.off);
@@ -481,7 +481,7 @@ struct SampleKeys {
     __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
     template <class F>
     __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
-        const TDesc& d = w.td[t];
+        const TDesc d = w.td[t];   // by value: stores below cannot alias it
         const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
         visit_dense(x, w.scnt[t], lb, nb, f);
     }
@@ -497,7 +497,7 @@ __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
 // One workgroup per small tensor: all three passes from LDS.
 __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat) {
     const int t = w.small[blockIdx.x];
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
     rs_small_wg(x, w.scnt[t], (uint64_t)d.ks, w.thr + t);
 }
@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const 
 // One workgroup per tensor: reset the tensor's state for this call.
 __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lists) {
     const int t = blockIdx.x;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     SelState* st = w.st + t;
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
@@ -555,7 +555,7 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
     const int t = task(w, BT_SEG, blockIdx.x);
     const SelState* st = w.st + t;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
     __shared__ int spill[kBlock];
@@ -616,7 +616,7 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
     const int t = task(w, which, blockIdx.x);
     const SelState* st = w.st + t;
     if (!st->active || st->t_cur >= st->t_list) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -696,7 +696,7 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
     const int t = blockIdx.x;
     SelState* st = w.st + t;
     if (!st->active) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     __shared__ uint64_t lds16[16];
     __shared__ int finished, reset_rs;
     uint64_t local = 0;
@@ -781,7 +781,7 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     const int t = task(w, BT_CAP4, blockIdx.x);
     SelState* st = w.st + t;
     if (!st->lower_pending) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const int m = p.max_iters;
     float th[kMaxLower + 1];
@@ -855,7 +855,7 @@ struct CandKeys {
     __device__ __forceinline__ float* out(int t) const { return &w.st[t].tk; }
     template <class F>
     __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
-        const TDesc& d = w.td[t];
+        const TDesc d = w.td[t];   // by value: stores below cannot alias it
         const float* vec = vec_flat + d.off;
         const int lane = threadIdx.x & 63;
         const int64_t gw = (lb * blockDim.x + threadIdx.x) >> 6;
@@ -892,7 +892,7 @@ k_count_gt_eq(const float* __restrict__ vec_flat, SelWS w) {
     const int t = task(w, BT_SEG, blockIdx.x);
     SelState* st = w.st + t;
     if (!st->resample_pending) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tk = st->tk;
     __shared__ int spill[kBlock];
@@ -1095,7 +1095,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth;
     if (k5 != (o.queue != nullptr)) return;
     const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const int64_t lg = (int64_t)blockIdx.x - w.bt[BT_GRP][t];   // group within the tensor
     const int64_t g = d.grp0 + lg;
@@ -1182,7 +1182,7 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(SelWS w) {
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
     if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     uint32_t* gl = w.gpos + d.gpos_off;
     uint32_t* gr = gl + d.cand_cap / 2 + 1;
     nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr);
@@ -1194,7 +1194,7 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
     const int t = task(w, BT_QUEUE, blockIdx.x);
     const SelState* st = w.st + t;
     if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
-    const TDesc& d = w.td[t];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
     __shared__ long long obase_s;
     if (threadIdx.x == 0) obase_s = out_base(w, t);
     __syncthreads();

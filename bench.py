@@ -67,10 +67,19 @@ def parse():
 
 # ---------------------------------------------------------------------------- CPU baseline
 def cpu_cores():
+    """The host cores this process may use: its affinity set, capped by OMP_NUM_THREADS
+    when the host sets it (the GPU box exposes every CPU of the machine to affinity but
+    grants each job a share, 16, through OMP_NUM_THREADS)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def cpu_model():
@@ -353,6 +362,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev)
 
+    log(f"{args.workload}: rank {rank}/{world} set up")
     phases = ("compensate", "select", "allgather", "decompress")
     for i in range(args.warmup):
         run.step(i)
@@ -430,8 +440,10 @@ def main():
         bus = (world - 1) * run.payload / (ms["allgather"] * 1e-3) / 1e9
         res["allgather"] = {"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
                             "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS)}
+    log(f"{args.workload}: {ms_step:.3f} ms/step on the GPU")
     if world == 1 and not args.no_cpu:
         cores = cpu_cores()
+        log(f"CPU baseline on {cores} threads, then 1 thread")
         res["cpu_baseline"] = cpu_baseline(wl, args.cpu_numel, args.cpu_steps, cores)
         res["cpu_baseline_1thread"] = cpu_baseline(wl, args.cpu_numel_1t, 2, 1)
     print(json.dumps(res), flush=True)
