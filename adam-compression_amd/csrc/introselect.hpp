@@ -6,7 +6,7 @@
 // std::nth_element(queue, queue + k - 1, queue + n, comp) with comp = "value greater"
 // (NaN above everything); queue[0..k) IS the output, in that order — which boundary
 // ties survive and the order of the transmitted (values, indices) both come from it.
-// This file replays that introselect exactly, on one 1024-thread workgroup:
+// This file replays that introselect exactly, on one 512-thread workgroup:
 //
 //   while (last - first > 3):                     (depth limit 2*lg(n) -> heap select)
 //     median of (first+1, mid, last-1) -> first   (std::__move_median_to_first)
@@ -26,20 +26,31 @@
 // positions, the next pass swaps. oracle/introselect.py is the same algorithm in
 // numpy, checked against torch.topk itself.
 //
-// Ranges above kNthLds entries are partitioned in global memory (L2-resident; 16
-// waves, each over a contiguous stretch, 4 entries per lane per step); the rest of
-// the selection runs out of LDS. Entries are (key << 32 | j), key = |x| bits.
+// Phases, by the size of the range still being partitioned:
+//   > kNthLds entries   in global memory (L2 / Infinity-Cache resident), 8 waves, each
+//                       over a contiguous stretch, 4 tiles of loads in flight per lane;
+//   > kNthWave entries  in LDS, same 8-wave step (four barriers per step);
+//   <= kNthWave         one wave, wave-synchronous (no workgroup barrier at all).
+// Entries are (key << 32 | j), key = |x| bits.
 #pragma once
 
 #include "dgc_common.hpp"
 
 namespace dgc {
 
-constexpr int kNthThreads = 1024;
+constexpr int kNthThreads = 512;    // 8 waves: 256 VGPRs per lane for the batched loads
 constexpr int kNthWaves = kNthThreads / kWave;
 constexpr int kNthLds = 12288;   // entries partitioned in LDS (96 KB + 48 KB of pair slots)
+constexpr int kNthWave = 1024;   // entries finished by a single wave
+constexpr int kNthBatch = 4;     // 256-entry tiles loaded per lane before use
 
 __device__ __forceinline__ uint32_t qkey(uint64_t e) { return (uint32_t)(e >> 32); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ---------------------------------------------------------------- heaps (depth limit)
 // std::__adjust_heap + std::__push_heap on q[0..n) with comp = key greater (the
@@ -88,18 +99,7 @@ __device__ void nth_heap_select(uint64_t* q, int64_t mid, int64_t n, int64_t nth
     q[nth] = t;
 }
 
-// ---------------------------------------------------------------- one partition
-struct NthShared {
-    int64_t f, l, depth, cut;
-    uint32_t wl[kNthWaves], wr[kNthWaves];   // per-wave stopper counts
-    uint32_t wlo[kNthWaves], wro[kNthWaves]; // their exclusive prefixes
-    uint32_t TR;                             // right stoppers in [f+1, l)
-    uint32_t s;                              // swaps
-    unsigned long long l_next, r_min;
-    int heap_exit;
-};
-
-// std::__move_median_to_first(f, f+1, mid, l-1) with comp = key greater. Thread 0.
+// std::__move_median_to_first(f, f+1, mid, l-1) with comp = key greater. One thread.
 __device__ __forceinline__ void nth_median(uint64_t* q, int64_t f, int64_t l) {
     const int64_t a = f + 1, b = f + (l - f) / 2, c = l - 1;
     const uint32_t ka = qkey(q[a]), kb = qkey(q[b]), kc = qkey(q[c]);
@@ -113,176 +113,7 @@ __device__ __forceinline__ void nth_median(uint64_t* q, int64_t f, int64_t l) {
     q[m] = t;
 }
 
-// Lane's 4 consecutive entries of the 256-entry tile at `base` (positions < end).
-__device__ __forceinline__ void nth_load4(const uint64_t* q, int64_t e0, int64_t end, uint64_t (&x)[4],
-                                          uint32_t& valid) {
-    valid = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const bool ok = e0 + j < end;
-        x[j] = ok ? q[e0 + j] : 0ull;
-        valid |= (uint32_t)ok << j;
-    }
-}
-
-// Partition q[f+1, l) around the pivot q[f] (after nth_median); sets sh.cut. All
-// threads of the workgroup call it; lpos/rpos hold >= (l - f) / 2 + 1 slots each.
-__device__ void nth_partition(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh) {
-    const int64_t f = sh.f, l = sh.l;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t P = qkey(q[f]);
-    const int64_t a0 = f + 1, R = l - a0;
-    const int64_t per = ceil_div(ceil_div(R, (int64_t)kNthWaves), (int64_t)256) * 256;
-    const int64_t wb = a0 + wv * per, we = wb + per < l ? wb + per : l;
-    // pass 1: stopper counts per wave
-    uint32_t cl = 0, cr = 0;
-    for (int64_t t0 = wb; t0 < we; t0 += 256) {
-        uint64_t x[4];
-        uint32_t valid;
-        nth_load4(q, t0 + 4 * lane, we, x, valid);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if ((valid >> j) & 1u) {
-                const uint32_t k = qkey(x[j]);
-                cl += k <= P;
-                cr += k >= P;
-            }
-        }
-    }
-    cl = wave_sum(cl);
-    cr = wave_sum(cr);
-    if (lane == 0) {
-        sh.wl[wv] = cl;
-        sh.wr[wv] = cr;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t sl = 0, sr = 0;
-        for (int i = 0; i < kNthWaves; ++i) {
-            sh.wlo[i] = sl;
-            sh.wro[i] = sr;
-            sl += sh.wl[i];
-            sr += sh.wr[i];
-        }
-        sh.TR = sr;
-        sh.s = 0;
-        sh.l_next = ~0ull;
-        sh.r_min = ~0ull;
-    }
-    __syncthreads();
-    // pass 2: ranks, pairing, paired positions
-    const uint32_t TR = sh.TR;
-    uint32_t runl = sh.wlo[wv], runr = sh.wro[wv];
-    uint32_t paired = 0;
-    unsigned long long lnext = ~0ull, rmin = ~0ull;
-    for (int64_t t0 = wb; t0 < we; t0 += 256) {
-        const int64_t e0 = t0 + 4 * lane;
-        uint64_t x[4];
-        uint32_t valid;
-        nth_load4(q, e0, we, x, valid);
-        uint32_t pl = 0, pr = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k = qkey(x[j]);
-            pl |= (uint32_t)(k <= P) << j;
-            pr |= (uint32_t)(k >= P) << j;
-        }
-        pl &= valid;
-        pr &= valid;
-        uint32_t bl, tl, br, tr;
-        wave_prefix4(pl, bl, tl);
-        wave_prefix4(pr, br, tr);
-        uint32_t rl = runl + bl;   // left stoppers before this element
-        uint32_t rr = runr + br;   // right stoppers in [f+1, this element)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool isl = (pl >> j) & 1u, isr = (pr >> j) & 1u;
-            const int64_t i = e0 + j;
-            const uint32_t rr_incl = rr + (isr ? 1u : 0u);
-            if (isl) {
-                // L_{rl+1} = i is swapped iff #(key >= P in (i, l)) >= rl + 1
-                if (TR - rr_incl >= rl + 1) {
-                    lpos[rl] = (uint32_t)(i - f);
-                    ++paired;
-                } else if ((unsigned long long)i < lnext) {
-                    lnext = (unsigned long long)i;
-                }
-            }
-            if (isr) {
-                // R_{u+1} = i with u = #(key >= P in (i, l)); swapped iff #(key <= P in [f+1, i)) >= u + 1
-                const uint32_t u = TR - rr_incl;
-                if (rl >= u + 1) {
-                    rpos[u] = (uint32_t)(i - f);
-                    if ((unsigned long long)i < rmin) rmin = (unsigned long long)i;
-                }
-            }
-            rl += isl;
-            rr = rr_incl;
-        }
-        runl += tl;
-        runr += tr;
-    }
-    paired = wave_sum(paired);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long a = __shfl_xor(lnext, o), b = __shfl_xor(rmin, o);
-        lnext = a < lnext ? a : lnext;
-        rmin = b < rmin ? b : rmin;
-    }
-    if (lane == 0) {
-        if (paired) atomicAdd(&sh.s, paired);
-        if (lnext != ~0ull) atomicMin(&sh.l_next, lnext);
-        if (rmin != ~0ull) atomicMin(&sh.r_min, rmin);
-    }
-    __syncthreads();
-    // pass 3: the swaps L_t <-> R_t, t < s (disjoint positions)
-    const uint32_t s = sh.s;
-    for (uint32_t t = threadIdx.x; t < s; t += kNthThreads) {
-        const int64_t li = f + lpos[t], ri = f + rpos[t];
-        const uint64_t a = q[li], b = q[ri];
-        q[li] = b;
-        q[ri] = a;
-    }
-    if (threadIdx.x == 0) {
-        const int64_t rs = s ? (int64_t)sh.r_min : l;
-        const int64_t ln = sh.l_next == ~0ull ? INT64_MAX : (int64_t)sh.l_next;
-        sh.cut = ln < rs ? ln : rs;
-    }
-    __syncthreads();
-}
-
-// The introselect loop over q[f, l) while the range exceeds `stop` entries; returns
-// with sh.f/sh.l/sh.depth updated, or sh.heap_exit = 1 after a depth-limit exit.
-__device__ void nth_loop(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth, int64_t stop) {
-    for (;;) {
-        if (sh.l - sh.f <= stop || sh.heap_exit) return;   // uniform: read after a barrier
-        if (sh.depth == 0) {
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                nth_heap_select(q + sh.f, nth + 1 - sh.f, sh.l - sh.f, nth - sh.f);
-                sh.heap_exit = 1;
-            }
-            __syncthreads();
-            return;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            sh.depth -= 1;
-            nth_median(q, sh.f, sh.l);
-        }
-        __syncthreads();
-        nth_partition(q, lpos, rpos, sh);
-        if (threadIdx.x == 0) {
-            if (sh.cut <= nth)
-                sh.f = sh.cut;
-            else
-                sh.l = sh.cut;
-        }
-        __syncthreads();
-    }
-}
-
-// std::__insertion_sort of q[f, l) (<= 3 entries after the loop). Thread 0.
+// std::__insertion_sort of q[f, l) (<= 3 entries after the loop). One thread.
 __device__ void nth_insertion_sort(uint64_t* q, int64_t f, int64_t l) {
     for (int64_t i = f + 1; i < l; ++i) {
         const uint64_t v = q[i];
@@ -300,7 +131,272 @@ __device__ void nth_insertion_sort(uint64_t* q, int64_t f, int64_t l) {
     }
 }
 
-// std::nth_element(q, q + nth, q + n, comp) in place, by the calling 1024-thread
+// Lane's 4 consecutive entries of a 256-entry tile (positions < end).
+__device__ __forceinline__ void nth_load4(const uint64_t* q, int64_t e0, int64_t end, uint64_t (&x)[4],
+                                          uint32_t& valid) {
+    valid = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool ok = e0 + j < end;
+        x[j] = ok ? q[e0 + j] : 0ull;
+        valid |= (uint32_t)ok << j;
+    }
+}
+
+__device__ __forceinline__ void stopper_masks(const uint64_t (&x)[4], uint32_t valid, uint32_t P, uint32_t& pl,
+                                              uint32_t& pr) {
+    pl = pr = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t k = qkey(x[j]);
+        pl |= (uint32_t)(k <= P) << j;
+        pr |= (uint32_t)(k >= P) << j;
+    }
+    pl &= valid;
+    pr &= valid;
+}
+
+// Pass 2 on one tile: ranks, pairing and the paired positions. rl / rr: the left and
+// right stoppers before the tile (uniform over the wave); lpos/rpos hold positions
+// relative to f. Returns via the accumulators.
+__device__ __forceinline__ void pair_tile(const uint64_t (&x)[4], uint32_t valid, uint32_t P, int64_t e0, int64_t f,
+                                          uint32_t TR, uint32_t& runl, uint32_t& runr, uint32_t* lpos, uint32_t* rpos,
+                                          uint32_t& paired, unsigned long long& lnext, unsigned long long& rmin) {
+    uint32_t pl, pr;
+    stopper_masks(x, valid, P, pl, pr);
+    uint32_t bl, tl, br, tr;
+    wave_prefix4(pl, bl, tl);
+    wave_prefix4(pr, br, tr);
+    uint32_t rl = runl + bl;   // left stoppers before this element
+    uint32_t rr = runr + br;   // right stoppers in [f+1, this element)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool isl = (pl >> j) & 1u, isr = (pr >> j) & 1u;
+        const int64_t i = e0 + j;
+        const uint32_t rr_incl = rr + (isr ? 1u : 0u);
+        if (isl) {
+            // L_{rl+1} = i is swapped iff #(key >= P in (i, l)) >= rl + 1
+            if (TR - rr_incl >= rl + 1) {
+                lpos[rl] = (uint32_t)(i - f);
+                ++paired;
+            } else if ((unsigned long long)i < lnext) {
+                lnext = (unsigned long long)i;
+            }
+        }
+        if (isr) {
+            // R_{u+1} = i with u = #(key >= P in (i, l)); swapped iff #(key <= P in [f+1, i)) >= u + 1
+            const uint32_t u = TR - rr_incl;
+            if (rl >= u + 1) {
+                rpos[u] = (uint32_t)(i - f);
+                if ((unsigned long long)i < rmin) rmin = (unsigned long long)i;
+            }
+        }
+        rl += isl;
+        rr = rr_incl;
+    }
+    runl += tl;
+    runr += tr;
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long a = __shfl_xor(v, o);
+        v = a < v ? a : v;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------- workgroup step
+struct NthShared {
+    int64_t f, l, depth;
+    uint32_t wl[kNthWaves], wr[kNthWaves];   // per-wave stopper counts
+    uint32_t s;                              // swaps
+    unsigned long long l_next, r_min;
+    int heap_exit;
+};
+
+// One partition step over q[f, l) by the whole workgroup; the pivot is already at
+// q[f] and sh.s / l_next / r_min are reset. On return (after the last barrier) the
+// step's swaps are done and sh.s / l_next / r_min hold its result.
+__device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh) {
+    const int64_t f = sh.f, l = sh.l;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t P = qkey(q[f]);
+    const int64_t a0 = f + 1, R = l - a0;
+    const int64_t per = ceil_div(ceil_div(R, (int64_t)kNthWaves), (int64_t)256) * 256;
+    const int64_t wb = a0 + wv * per, we = wb + per < l ? wb + per : l;
+    // pass 1: stopper counts per wave, kNthBatch tiles of loads in flight per lane
+    uint32_t cl = 0, cr = 0;
+    for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
+        uint64_t x[kNthBatch][4];
+        uint32_t valid[kNthBatch];
+#pragma unroll
+        for (int b = 0; b < kNthBatch; ++b) nth_load4(q, t0 + b * 256 + 4 * lane, we, x[b], valid[b]);
+#pragma unroll
+        for (int b = 0; b < kNthBatch; ++b) {
+            uint32_t pl, pr;
+            stopper_masks(x[b], valid[b], P, pl, pr);
+            cl += __popc(pl);
+            cr += __popc(pr);
+        }
+    }
+    cl = wave_sum(cl);
+    cr = wave_sum(cr);
+    if (lane == 0) {
+        sh.wl[wv] = cl;
+        sh.wr[wv] = cr;
+    }
+    __syncthreads();
+    // every wave derives its own prefix and the total from the 16 wave counts
+    uint32_t runl = 0, runr = 0, TR = 0;
+#pragma unroll
+    for (int i = 0; i < kNthWaves; ++i) {
+        const uint32_t a = sh.wl[i], b = sh.wr[i];
+        runl += i < wv ? a : 0u;
+        runr += i < wv ? b : 0u;
+        TR += b;
+    }
+    // pass 2: ranks, pairing, paired positions
+    uint32_t paired = 0;
+    unsigned long long lnext = ~0ull, rmin = ~0ull;
+    for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
+        uint64_t x[kNthBatch][4];
+        uint32_t valid[kNthBatch];
+#pragma unroll
+        for (int b = 0; b < kNthBatch; ++b) nth_load4(q, t0 + b * 256 + 4 * lane, we, x[b], valid[b]);
+#pragma unroll
+        for (int b = 0; b < kNthBatch; ++b)
+            pair_tile(x[b], valid[b], P, t0 + b * 256 + 4 * lane, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+    }
+    paired = wave_sum(paired);
+    lnext = wave_min_u64(lnext);
+    rmin = wave_min_u64(rmin);
+    if (lane == 0) {
+        if (paired) atomicAdd(&sh.s, paired);
+        if (lnext != ~0ull) atomicMin(&sh.l_next, lnext);
+        if (rmin != ~0ull) atomicMin(&sh.r_min, rmin);
+    }
+    __syncthreads();
+    // pass 3: the swaps L_t <-> R_t, t < s (disjoint positions)
+    const uint32_t s = sh.s;
+    for (uint32_t t = threadIdx.x; t < s; t += kNthThreads) {
+        const int64_t li = f + lpos[t], ri = f + rpos[t];
+        const uint64_t a = q[li], b = q[ri];
+        q[li] = b;
+        q[ri] = a;
+    }
+    __syncthreads();
+}
+
+// Thread 0, after a step: the cut, the next range, and either the next step's
+// median (returns 1), a depth-limit heap exit, or the end of this phase (returns 0).
+__device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop) {
+    const int64_t rs = sh.s ? (int64_t)sh.r_min : sh.l;
+    const int64_t ln = sh.l_next == ~0ull ? INT64_MAX : (int64_t)sh.l_next;
+    const int64_t cut = ln < rs ? ln : rs;
+    if (cut <= nth)
+        sh.f = cut;
+    else
+        sh.l = cut;
+    return 0;
+}
+
+// The introselect loop on q[f, l) by the whole workgroup while the range exceeds
+// `stop` entries; ends with a barrier, sh.f/l/depth updated or sh.heap_exit set.
+__device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth,
+                            int64_t stop) {
+    // thread 0 prepares a step: depth check, median, reset of the step's results
+    auto prepare = [&]() -> bool {
+        if (sh.l - sh.f <= stop) return false;
+        if (sh.depth == 0) {
+            nth_heap_select(q + sh.f, nth + 1 - sh.f, sh.l - sh.f, nth - sh.f);
+            sh.heap_exit = 1;
+            return false;
+        }
+        sh.depth -= 1;
+        nth_median(q, sh.f, sh.l);
+        sh.s = 0;
+        sh.l_next = ~0ull;
+        sh.r_min = ~0ull;
+        return true;
+    };
+    __shared__ int go;
+    if (threadIdx.x == 0) go = !sh.heap_exit && prepare();
+    __syncthreads();
+    while (go) {
+        nth_step_wg(q, lpos, rpos, sh);
+        if (threadIdx.x == 0) {
+            nth_advance(q, sh, nth, stop);
+            go = prepare();
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- single-wave tail
+// The same step by one wave on an LDS range of <= kNthWave entries: no workgroup barrier.
+__device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, int64_t f, int64_t l) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t P = qkey(q[f]);
+    const int64_t a0 = f + 1;
+    uint32_t cr = 0;
+    for (int64_t t0 = a0; t0 < l; t0 += 256) {
+        uint64_t x[4];
+        uint32_t valid, pl, pr;
+        nth_load4(q, t0 + 4 * lane, l, x, valid);
+        stopper_masks(x, valid, P, pl, pr);
+        cr += __popc(pr);
+    }
+    const uint32_t TR = wave_sum(cr);
+    uint32_t runl = 0, runr = 0, paired = 0;
+    unsigned long long lnext = ~0ull, rmin = ~0ull;
+    for (int64_t t0 = a0; t0 < l; t0 += 256) {
+        uint64_t x[4];
+        uint32_t valid;
+        nth_load4(q, t0 + 4 * lane, l, x, valid);
+        pair_tile(x, valid, P, t0 + 4 * lane, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+    }
+    const uint32_t s = wave_sum(paired);
+    lnext = wave_min_u64(lnext);
+    rmin = wave_min_u64(rmin);
+    wave_sync();   // the pair slots are written
+    for (uint32_t t = lane; t < s; t += kWave) {
+        const int64_t li = f + lpos[t], ri = f + rpos[t];
+        const uint64_t a = q[li], b = q[ri];
+        q[li] = b;
+        q[ri] = a;
+    }
+    wave_sync();   // the swaps are done
+    const int64_t rs = s ? (int64_t)rmin : l;
+    const int64_t ln = lnext == ~0ull ? INT64_MAX : (int64_t)lnext;
+    return ln < rs ? ln : rs;
+}
+
+// Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
+__device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth) {
+    int64_t f = sh.f, l = sh.l, depth = sh.depth;
+    const int lane = threadIdx.x & 63;
+    while (l - f > 3) {
+        if (depth == 0) {
+            if (lane == 0) nth_heap_select(q + f, nth + 1 - f, l - f, nth - f);
+            wave_sync();
+            return;
+        }
+        depth -= 1;
+        if (lane == 0) nth_median(q, f, l);
+        wave_sync();
+        const int64_t cut = nth_step_wave(q, lpos, rpos, f, l);
+        if (cut <= nth)
+            f = cut;
+        else
+            l = cut;
+    }
+    if (lane == 0) nth_insertion_sort(q, f, l);
+    wave_sync();
+}
+
+// std::nth_element(q, q + nth, q + n, comp) in place, by the calling 512-thread
 // workgroup. gpos_l/gpos_r: global pair slots (>= n / 2 + 1 each) for the ranges
 // above kNthLds. Returns after a final barrier.
 __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r) {
@@ -315,9 +411,9 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     }
     __syncthreads();
     if (n <= 0 || nth >= n) return;
-    nth_loop(q, gpos_l, gpos_r, sh, nth, kNthLds);            // global phase
+    nth_loop_wg(q, gpos_l, gpos_r, sh, nth, kNthLds);                 // global phase
     if (sh.heap_exit) return;
-    const int64_t f = sh.f, m = sh.l - sh.f;                  // <= kNthLds entries left
+    const int64_t f = sh.f, m = sh.l - sh.f;                          // <= kNthLds entries left
     for (int64_t i = threadIdx.x; i < m; i += kNthThreads) lq[i] = q[f + i];
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -325,8 +421,8 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
         sh.l = m;
     }
     __syncthreads();
-    nth_loop(lq, llp, lrp, sh, nth - f, 3);                   // LDS phase
-    if (threadIdx.x == 0 && !sh.heap_exit) nth_insertion_sort(lq, sh.f, sh.l);
+    nth_loop_wg(lq, llp, lrp, sh, nth - f, kNthWave);                  // LDS phase, all waves
+    if (!sh.heap_exit && threadIdx.x < kWave) nth_tail_wave(lq, llp, lrp, sh, nth - f);   // one wave
     __syncthreads();
     for (int64_t i = threadIdx.x; i < m; i += kNthThreads) q[f + i] = lq[i];
     __syncthreads();

@@ -434,6 +434,7 @@ def main():
                      "contract_frac_of_8TBs": contract / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "frac_of_measured_copy": required / (ms_step * 1e-3) / 1e9 / HBM_COPY_GBS},
         "phase_ms": {p: round(v, 4) for p, v in ms.items()},
+        "compensate_ms_per_step": [round(e["compensate"][0].elapsed_time(e["compensate"][1]), 3) for e in evs],
         "selection": info,
     }
     if world > 1 and ms.get("allgather", 0) > 0:
