@@ -94,7 +94,13 @@ struct SelState {
     int32_t full_passes, list_spills, epoch;
     int32_t rs_nth;        // RESAMPLE served by the exact nth_element replay (K5)
     int32_t tie_rule;      // DGC_TIES_*: how the resample chose among boundary ties
+    // Deferred momentum masking (DGCSGDMemory.update, dgc/memory.py:72-77): the last
+    // call emitted "the first def_limit elements >= def_t" without zeroing them; the
+    // next K1, which streams vec and mmt anyway, zeroes them before compensating.
+    int32_t def_mode, def_mask_mmt;
+    float def_t;
     int32_t pad;
+    long long def_limit;
     uint32_t tickets[4];
     // Segments whose K1 list overflowed, counted by K1 into slot [epoch & 1] (64
     // shards against atomic contention); k_sel_init reads it and zeroes the other
@@ -106,7 +112,8 @@ struct SelState {
 // Per-call settings shared by the tensors.
 struct SelCfg {
     float upper, lower;         // fl32(compress_upper_bound), fl32(compress_lower_bound)
-    int32_t max_iters, resample, masking, vdtype, idtype, update_memory;
+    int32_t max_iters, resample, masking, vdtype, idtype;
+    int32_t update_memory;      // 0: none, 1: zero the emitted slots now, 2: deferred to the next K1
 };
 
 // Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
@@ -128,6 +135,7 @@ struct SelWS {
     uint32_t* seg_cnt;
     uint32_t* seg_gt;
     uint32_t* seg_eq;
+    uint32_t* seg_off;         // in-group output offset of each segment's first emitted entry
     uint16_t* lst_off;
     float* lst_val;
     unsigned long long* grp_cnt;   // grp_cnt, grp_gt, grp_eq: contiguous
@@ -268,6 +276,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.seg_cnt = c.take<uint32_t>(L.nseg);
     w.seg_gt = c.take<uint32_t>(L.nseg);
     w.seg_eq = c.take<uint32_t>(L.nseg);
+    w.seg_off = c.take<uint32_t>(L.nseg);
     w.lst_off = c.take<uint16_t>(L.nseg * kCap);
     w.lst_val = c.take<float>(L.nseg * kCap);
     w.queue = c.take<uint64_t>(L.ncand);
@@ -366,20 +375,123 @@ __device__ __forceinline__ void list_append(uint32_t p, const float (&x)[4], int
     }
 }
 
-// Count of |x| >= t over local segment ls of a tensor (elements v[0..n)), re-read by the calling wave.
-__device__ uint32_t wave_count_segment(const float* __restrict__ v, int64_t n, int64_t ls, float t) {
+// The calling wave's view of local segment ls of a tensor (elements v[0..n)):
+// tile u holds elements ls*1024 + 256u + 4*lane + j. All loads are issued before
+// any use; 16-B loads when the tensor base is 16-B aligned (a uniform branch).
+__device__ __forceinline__ void load_segment(const float* __restrict__ v, int64_t n, int64_t ls,
+                                             float (&x)[kSegTiles][4], uint32_t (&valid)[kSegTiles]) {
     const int lane = threadIdx.x & 63;
-    uint32_t c = 0;
-    for (int tile = 0; tile < kSegTiles; ++tile) {
-        float x[4];
-        uint32_t valid;
-        load_tile<false>(v, n, ls * kSeg + tile * 256 + 4 * lane, x, valid);
-        c += __popc(ge_mask(x, valid, t));
+    if (aligned16(v)) {
+#pragma unroll
+        for (int u = 0; u < kSegTiles; ++u) load_tile<true>(v, n, ls * kSeg + u * 256 + 4 * lane, x[u], valid[u]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < kSegTiles; ++u) load_tile<false>(v, n, ls * kSeg + u * 256 + 4 * lane, x[u], valid[u]);
     }
+}
+
+// Count of |x| >= t over local segment ls of a tensor, re-read by the calling wave.
+__device__ uint32_t wave_count_segment(const float* __restrict__ v, int64_t n, int64_t ls, float t) {
+    float x[kSegTiles][4];
+    uint32_t valid[kSegTiles];
+    load_segment(v, n, ls, x, valid);
+    uint32_t c = 0;
+#pragma unroll
+    for (int u = 0; u < kSegTiles; ++u) c += __popc(ge_mask(x[u], valid[u], t));
     return wave_sum(c);
 }
 
 __device__ __forceinline__ int task(const SelWS& w, int which, int b) { return task_of_block(w.bt[which], w.T, b); }
+
+// The last call's deferred masking for one segment (one wave): zero, in the loaded
+// tiles, the elements that call emitted — the first def_limit elements (flat
+// order) with |vec| >= def_t, ranked by grp_off + seg_off + in-segment rank. vec is
+// unchanged since that emit, so the recount reproduces its choice exactly.
+__device__ __forceinline__ void apply_deferred_mask(const SelState& st, const SelWS& w, const TDesc& d,
+                                                    int64_t ls, int lane, float4 (&vv)[kSegTiles],
+                                                    float4 (&mv)[kSegTiles]) {
+    const float dt = st.def_t;
+    const long long dlim = st.def_limit;
+    const bool mm = st.def_mask_mmt != 0;
+    long long rank = w.grp_off[d.grp0 + ls / kGroupSegs] + w.seg_off[d.seg0 + ls];
+#pragma unroll
+    for (int u = 0; u < kSegTiles; ++u) {
+        if (rank >= dlim) break;   // wave-uniform
+        const int64_t v = ls * (kSeg / 4) + u * 64 + lane;
+        const float xo[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+        const uint32_t pm = ge_mask(xo, v < d.nv4 ? 0xFu : 0u, dt);
+        uint32_t lb, tot;
+        wave_prefix4(pm, lb, tot);
+        long long r = rank + lb;
+        float* vf = reinterpret_cast<float*>(&vv[u]);
+        float* mf = reinterpret_cast<float*>(&mv[u]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (pm & (1u << j)) {
+                if (r < dlim) {
+                    vf[j] = 0.f;
+                    if (mm) mf[j] = 0.f;
+                }
+                ++r;
+            }
+        rank += tot;
+    }
+}
+
+// Applies a pending deferred masking without compensating (flush before anyone reads
+// vec/mmt, and the non-list K1 fallback). One wave per segment.
+__global__ void __launch_bounds__(kBlock) k_mask_flush(float* __restrict__ vec_flat, float* __restrict__ mmt_flat,
+                                                       SelWS w) {
+    const int t = task(w, BT_K1, blockIdx.x);
+    const SelState* st = w.st + t;
+    if (!st->def_mode) return;
+    const TDesc d = w.td[t];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_K1][t]) * kSegPerBlock4 + wave;
+    if (ls >= d.nseg) return;
+    float* vec = vec_flat + d.off;
+    float* mmt = st->def_mask_mmt ? mmt_flat + d.off : nullptr;
+    const float dt = st->def_t;
+    const long long dlim = st->def_limit;
+    long long rank = w.grp_off[d.grp0 + ls / kGroupSegs] + w.seg_off[d.seg0 + ls];
+    if (rank >= dlim) return;
+    float x[kSegTiles][4];
+    uint32_t valid[kSegTiles];
+    load_segment(vec, d.n, ls, x, valid);
+#pragma unroll
+    for (int u = 0; u < kSegTiles; ++u) {
+        const uint32_t pm = ge_mask(x[u], valid[u], dt);
+        uint32_t lb, tot;
+        wave_prefix4(pm, lb, tot);
+        long long r = rank + lb;
+        const int64_t e0 = ls * kSeg + u * 256 + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (pm & (1u << j)) {
+                if (r < dlim) {
+                    vec[e0 + j] = 0.f;
+                    if (mmt) mmt[e0 + j] = 0.f;
+                }
+                ++r;
+            }
+        rank += tot;
+    }
+}
+
+__global__ void k_def_clear(SelWS w) {
+    for (int t = threadIdx.x; t < w.T; t += blockDim.x) w.st[t].def_mode = 0;
+}
+
+static int mask_flush(float* vec, float* mmt, const Layout& L, const SelWS& w, hipStream_t s) {
+    if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: n too large");
+    if (L.grid[BT_K1] > 0) {
+        hipLaunchKernelGGL(k_mask_flush, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, vec, mmt, w);
+        DGC_LAUNCHED();
+    }
+    hipLaunchKernelGGL(k_def_clear, dim3(1), dim3(256), 0, s, w);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
 
 // ------------------------------------------------------------------ K1 with lists
 // K1 (compensate + strided sample, see compensate.hip) that also lists every
@@ -423,6 +535,7 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     const int64_t seg = d.seg0 + ls;
     uint16_t* lo = w.lst_off + seg * kCap;
     float* lv = w.lst_val + seg * kCap;
+    if (st->def_mode && ls < d.nseg) apply_deferred_mask(*st, w, d, ls, lane, vv, mv);
 #pragma unroll
     for (int u = 0; u < kSegTiles; ++u) {
         const int64_t v = ls * (kSeg / 4) + u * 64 + lane;
@@ -870,14 +983,15 @@ struct CandKeys {
                     if (a >= tc) f(abs_key(a));
                 }
             } else {
-                for (int tile = 0; tile < kSegTiles; ++tile) {
-                    float x[4];
-                    uint32_t valid;
-                    load_tile<false>(vec, d.n, ls * kSeg + tile * 256 + 4 * lane, x, valid);
-                    const uint32_t pm = ge_mask(x, valid, tc);
+                float x[kSegTiles][4];
+                uint32_t valid[kSegTiles];
+                load_segment(vec, d.n, ls, x, valid);
+#pragma unroll
+                for (int u = 0; u < kSegTiles; ++u) {
+                    const uint32_t pm = ge_mask(x[u], valid[u], tc);
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (pm & (1u << j)) f(abs_key(x[j]));
+                        if (pm & (1u << j)) f(abs_key(x[u][j]));
                 }
             }
         }
@@ -932,14 +1046,15 @@ k_count_gt_eq(const float* __restrict__ vec_flat, SelWS w) {
     for (int q = wave; q < nspill; q += kSegPerBlock4) {
         const int64_t ls2 = lseg0 + spill[q];
         uint32_t g2 = 0, e2 = 0;
-        for (int tile = 0; tile < kSegTiles; ++tile) {
-            float x[4];
-            uint32_t valid;
-            load_tile<false>(vec, d.n, ls2 * kSeg + tile * 256 + 4 * lane, x, valid);
+        float x[kSegTiles][4];
+        uint32_t valid[kSegTiles];
+        load_segment(vec, d.n, ls2, x, valid);
+#pragma unroll
+        for (int u = 0; u < kSegTiles; ++u) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float a = fabsf(x[j]);
-                const bool ok = (valid >> j) & 1u;
+                const float a = fabsf(x[u][j]);
+                const bool ok = (valid[u] >> j) & 1u;
                 g2 += ok && a > tk;
                 e2 += ok && a == tk;
             }
@@ -981,6 +1096,7 @@ struct EmitOut {
     int32_t vdtype, idtype;
     uint64_t* queue;     // non-null: K5 candidate gather (queue[pos] = key << 32 | pos, cand[pos] = index)
     int64_t* cand;
+    int32_t defer;       // first-k branches: leave vec/mmt to the next K1 (record seg_off instead)
 };
 
 // Entries a tensor emits: the first `limit` candidates, or k after a resample.
@@ -996,7 +1112,8 @@ __device__ __forceinline__ long long out_base(const SelWS& w, int t) {
 }
 
 // pos: output slot; li: the element's index within its tensor (d.off + li in the flat buffers).
-__device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long long pos, int64_t li, float x) {
+__device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long long pos, int64_t li, float x,
+                                         bool mask_now = true) {
     if (o.queue) {
         o.queue[d.cand_off + pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
         o.cand[d.cand_off + pos] = li;
@@ -1004,6 +1121,7 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long 
     }
     store_value(o.values, pos, x, o.vdtype);
     store_index(o.indices, pos, d.idx_base + li, o.idtype);
+    if (!mask_now) return;
     // scattered 4-B writes, one per 128-B line: non-temporal (no L2 allocation)
     if (o.vec) __builtin_nontemporal_store(0.f, o.vec + d.off + li);
     if (o.mmt) __builtin_nontemporal_store(0.f, o.mmt + d.off + li);
@@ -1012,15 +1130,17 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long 
 // Wave-cooperative emit of one spilled segment (local ls) by re-reading vec.
 // FIRSTK: positions base + rank for |x| >= t, kept while < limit.
 __device__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long base,
-                                   long long limit, long long obase, float t, const EmitOut& o) {
+                                   long long limit, long long obase, float t, const EmitOut& o, bool mask_now) {
     const int lane = threadIdx.x & 63;
     uint32_t run = 0;
+    float xs[kSegTiles][4];
+    uint32_t vs[kSegTiles];
+    load_segment(vec, d.n, ls, xs, vs);
+#pragma unroll
     for (int tile = 0; tile < kSegTiles; ++tile) {
-        float x[4];
-        uint32_t valid;
+        const float(&x)[4] = xs[tile];
         const int64_t e0 = ls * kSeg + tile * 256 + 4 * lane;
-        load_tile<false>(vec, d.n, e0, x, valid);
-        const uint32_t pm = ge_mask(x, valid, t);
+        const uint32_t pm = ge_mask(x, vs[tile], t);
         if (__ballot(pm != 0)) {
             uint32_t lb, tot;
             wave_prefix4(pm, lb, tot);
@@ -1029,7 +1149,7 @@ __device__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d
             for (int j = 0; j < 4; ++j)
                 if (pm & (1u << j)) {
                     const long long pos = base + r;
-                    if (pos < limit) emit_one(o, d, obase + pos, e0 + j, x[j]);
+                    if (pos < limit) emit_one(o, d, obase + pos, e0 + j, x[j], mask_now);
                     ++r;
                 }
             run += tot;
@@ -1042,11 +1162,14 @@ __device__ void emit_reread_resample(const float* __restrict__ vec, const TDesc&
                                      long long bt, float tk, long long T, long long obase, const EmitOut& o) {
     const int lane = threadIdx.x & 63;
     uint32_t run_g = 0, run_t = 0;
+    float xs[kSegTiles][4];
+    uint32_t vs[kSegTiles];
+    load_segment(vec, d.n, ls, xs, vs);
+#pragma unroll
     for (int tile = 0; tile < kSegTiles; ++tile) {
-        float x[4];
-        uint32_t valid;
+        const float(&x)[4] = xs[tile];
+        const uint32_t valid = vs[tile];
         const int64_t e0 = ls * kSeg + tile * 256 + 4 * lane;
-        load_tile<false>(vec, d.n, e0, x, valid);
         uint32_t pg = 0, pe = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1096,6 +1219,8 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     if (k5 != (o.queue != nullptr)) return;
     const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    // first-k branches of an engine that defers: the next K1 zeroes what this emits
+    const bool defer_here = o.defer && !rs && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
     const int64_t lg = (int64_t)blockIdx.x - w.bt[BT_GRP][t];   // group within the tensor
     const int64_t g = d.grp0 + lg;
@@ -1122,6 +1247,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         __syncthreads();
         const uint32_t ob = rs ? (uint32_t)block_exclusive_scan((uint64_t)cb, lds16, &tot) : 0u;
         const bool work = rs ? (ca > 0 || (cb > 0 && gb + ob < T)) : (ca > 0 && ga + oa < limit);
+        if (defer_here && ls < d.nseg) w.seg_off[d.seg0 + ls] = oa;
         off_a[threadIdx.x] = oa;
         off_b[threadIdx.x] = ob;
         lcn[threadIdx.x] = work ? lc : kEmitSkip;
@@ -1155,7 +1281,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
                 if (rs)
                     emit_reread_resample(vec, d, ls, ba, bb, tk, T, obase, o);
                 else
-                    emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o);
+                    emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o, !defer_here);
                 continue;
             }
             const bool in = (uint32_t)lane < L;
@@ -1165,7 +1291,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
                 const bool sel = in && a >= tc;
                 const uint64_t m = __ballot(sel);
                 const long long pos = ba + __popcll(m & lt);
-                if (sel && pos < limit) emit_one(o, d, obase + pos, li, x[q]);
+                if (sel && pos < limit) emit_one(o, d, obase + pos, li, x[q], !defer_here);
             } else {
                 const bool gt = in && a > tk, eq = in && a == tk;
                 const uint64_t mg = __ballot(gt), me = __ballot(eq);
@@ -1207,7 +1333,8 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
 
 // Result records; the payload's total count; and every tensor's next speculative
 // list threshold, margin x t_cur x growth. One workgroup.
-__global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info, float margin) {
+__global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info, float margin, int defer,
+                             int mask_mmt) {
     __shared__ unsigned long long total;
     if (threadIdx.x == 0) total = 0;
     __syncthreads();
@@ -1215,6 +1342,11 @@ __global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info,
         SelState* st = w.st + t;
         st->epoch += 1;
         const long long cnt = final_count(*st, w.td[t].k);
+        // what the next K1 must zero (first-k branches of a deferring engine only)
+        st->def_mode = (defer && st->branch != DGC_BRANCH_RESAMPLE && !w.td[t].tail && cnt > 0) ? 1 : 0;
+        st->def_t = st->t_cur;
+        st->def_limit = st->limit;
+        st->def_mask_mmt = mask_mmt;
         atomicAdd(&total, (unsigned long long)cnt);
         if (info) {
             dgc_select_info& r = info[t];
@@ -1309,7 +1441,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         return DGC_OK;
     };
     EmitOut o{p.update_memory ? vec : nullptr, (p.update_memory && p.masking) ? mmt : nullptr, values, indices,
-              p.vdtype, p.idtype, nullptr, nullptr};
+              p.vdtype, p.idtype, nullptr, nullptr, (int32_t)(p.update_memory == 2)};
     auto resample_lowest = [&]() -> int {
         // partial_sort path (>= 64k candidates): radix k-th value, ties lowest index first.
         // rs state reset by k_decide when it chose this path
@@ -1382,7 +1514,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     }
     hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitThreads), 0, s, vec, w, o);
     DGC_LAUNCHED();
-    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, count_out, info, margin);
+    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, count_out, info, margin,
+                       (int)(p.update_memory == 2), (int)(p.masking != 0));
     DGC_LAUNCHED();
     return DGC_OK;
 }
@@ -1526,6 +1659,7 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
     const bool list_path = aligned16(grad) && aligned16(mmt) && aligned16(vec) &&
                            (!sampled || (s_stride >= 4 && s_stride < (1LL << 30)));
     if (!list_path) {
+        DGC_TRY(mask_flush(vec, mmt, L, w, s));   // a deferring finish left its masking to K1
         DGC_TRY(compensate(grad, mmt, vec, nullptr, n, momentum, nesterov, true, sampled ? w.samples : nullptr,
                            s_start, s_stride, cnt, s));
         hipLaunchKernelGGL(k_no_lists, dim3(1), dim3(64), 0, s, w);
@@ -1572,7 +1706,8 @@ int compress_finish(float* vec, float* mmt, int64_t s_start, int64_t s_stride, i
     DGC_LAUNCHED();
     DGC_TRY(thresholds(w, L, vec, s));
     dgc_select_params q = *p;
-    q.update_memory = 1;   // DGCSGDMemory.update fused into the emit
+    // DGCSGDMemory.update fused into the emit (1), or deferred into the next K1 (2)
+    q.update_memory = p->update_memory == 2 ? 2 : 1;
     return select_core(vec, mmt, cfg_of(q), L, values, indices, count_out, info, w, 1, sync_mode, margin, s);
 }
 
@@ -1615,7 +1750,8 @@ static int batch_layout(const dgc_batch_desc* b, Layout& L, std::vector<TDesc>& 
 
 static SelCfg cfg_of_batch(const dgc_batch_desc* b) {
     return SelCfg{(float)b->upper_bound, (float)b->lower_bound, b->max_iters, b->resample, b->momentum_masking,
-                  b->fp16_values ? DGC_F16 : DGC_F32, b->int32_indices ? DGC_I32 : DGC_I64, 1};
+                  b->fp16_values ? DGC_F16 : DGC_F32, b->int32_indices ? DGC_I32 : DGC_I64,
+                  b->deferred_masking ? 2 : 1};
 }
 
 size_t batch_ws_bytes(const dgc_batch_desc* b) {
@@ -1698,6 +1834,29 @@ int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float
                        sync_mode, b->spec_margin, s);
 }
 
+int compress_flush(float* vec, float* mmt, int64_t s_stride, const dgc_select_params* p, void* ws, size_t ws_bytes,
+                   hipStream_t s) {
+    if (!p || !vec) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress_flush: null params/vec");
+    Layout L;
+    SelWS w;
+    OneTable ot{};
+    DGC_TRY(one_ws(p, 0, s_stride, 1, nullptr, ws, ws_bytes, L, w, ot));   // tables as the last call left them
+    return mask_flush(vec, mmt, L, w, s);
+}
+
+int batch_flush(const dgc_batch_desc* b, float* mmt, float* vec, void* ws, size_t ws_bytes, hipStream_t s) {
+    Layout L;
+    std::vector<TDesc> td;
+    std::vector<int32_t> bt[BT_COUNT];
+    std::vector<int32_t> small;
+    DGC_TRY(batch_layout(b, L, td, bt, small));
+    size_t need = 0;
+    carve_select(nullptr, L, &need);
+    if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255) || !vec || !mmt)
+        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_batch_flush: workspace needs %zu bytes, 256-B aligned", need);
+    return mask_flush(vec, mmt, L, carve_select(ws, L), s);
+}
+
 }  // namespace dgc
 
 // ------------------------------------------------------------------ C ABI
@@ -1766,4 +1925,14 @@ extern "C" int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad
                                   size_t ws_bytes, int32_t sync_mode, void* stream) {
     return dgc::batch_compress(batch, grad, mmt, vec, sample_starts, payload, info_out, ws, ws_bytes, sync_mode,
                                static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_compress_flush(float* vec, float* mmt, int64_t sample_stride, const dgc_select_params* params,
+                                  void* ws, size_t ws_bytes, void* stream) {
+    return dgc::compress_flush(vec, mmt, sample_stride, params, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_batch_flush(const dgc_batch_desc* batch, float* mmt, float* vec, void* ws, size_t ws_bytes,
+                               void* stream) {
+    return dgc::batch_flush(batch, mmt, vec, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }

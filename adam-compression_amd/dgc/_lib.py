@@ -52,7 +52,8 @@ class BatchDesc(ctypes.Structure):
                 ("upper_bound", ctypes.c_double), ("lower_bound", ctypes.c_double),
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("momentum_masking", ctypes.c_int32),
                 ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
-                ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float)]
+                ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float),
+                ("deferred_masking", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -79,6 +80,7 @@ _SIGNATURES = {
                                           _SZ, _P]),
     "dgc_compress_finish": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, ctypes.POINTER(SelectParams), _P, _F, _P, _P,
                                            _P, _P, _P, _SZ, _I32, _P]),
+    "dgc_compress_flush": (ctypes.c_int, [_P, _P, _I64, ctypes.POINTER(SelectParams), _P, _SZ, _P]),
     "dgc_decompress_workspace": (_SZ, [_I64, _I32]),
     "dgc_decompress_packed_workspace": (_SZ, [_I64, _I32, _I64]),
     "dgc_decompress": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, ctypes.POINTER(ctypes.c_int64), _I32, _P,
@@ -93,6 +95,7 @@ _SIGNATURES = {
     "dgc_batch_init": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _SZ, _P]),
     "dgc_batch_compress": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, ctypes.POINTER(_I64), _P, _P, _P,
                                           _SZ, _I32, _P]),
+    "dgc_batch_flush": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _SZ, _P]),
     "dgc_sgd_step": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                     ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _P]),
 }

@@ -45,7 +45,8 @@ def _attributes(numel, ratio, sample_ratio):
 class DGCBatch:
     def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
-                 resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None):
+                 resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
+                 deferred_masking=True):
         self.device = torch.device(device or "cuda")
         self.names = [n for n, _ in named_shapes]
         self.shapes = {n: tuple(s) for n, s in named_shapes}
@@ -66,8 +67,10 @@ class DGCBatch:
         self.flat_numel = max(end, SEG)
         dev = self.device
         self.grad_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
-        self.mmt_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
-        self.vec_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self._mmt_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self._vec_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self.deferred_masking = bool(deferred_masking)
+        self._pending = False
         self.out_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
         self._L = _lib.lib()
         self.info = torch.zeros(len(self.names) * _lib.INFO_BYTES, dtype=torch.uint8, device=dev)
@@ -79,6 +82,7 @@ class DGCBatch:
         device tables — ``DGCCompressor.initialize`` (dgc/compression.py:56-89), also
         what ``warmup_compress_ratio`` re-runs on a ratio change (:91-107)."""
         ratio = compress_ratio if compress_ratio <= 1.0 else 1.0 / compress_ratio
+        self.flush()   # a pending masking lives in the old workspace
         self.ratio = ratio
         T = len(self.names)
         self.attrs = [_attributes(n, ratio, self.sample_ratio) for n in self.numels]
@@ -93,6 +97,7 @@ class DGCBatch:
         d.max_iters, d.resample, d.momentum_masking = self.max_iters, int(self.resample), int(self.momentum_masking)
         d.fp16_values, d.int32_indices = int(self.vdtype == torch.float16), int(self.idtype == torch.int32)
         d.nesterov, d.momentum, d.spec_margin = int(self.nesterov), self.momentum, _lib.SPEC_MARGIN
+        d.deferred_masking = int(self.deferred_masking)
         self.desc = d
         L = self._L
         wsz = L.dgc_batch_workspace(ctypes.byref(d))
@@ -109,6 +114,26 @@ class DGCBatch:
                          if self.world > 1 else self.payload)
         self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(self.flat_numel, self.world, self.capacity),
                                   dtype=torch.uint8, device=self.device)
+
+    def flush(self):
+        """Applies a deferred masking now (no-op when none is pending)."""
+        if self._pending:
+            _lib.check(self._L.dgc_batch_flush(ctypes.byref(self.desc), self._mmt_flat.data_ptr(),
+                                               self._vec_flat.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                               _lib.stream_of(self.device)), "dgc_batch_flush")
+            self._pending = False
+
+    @property
+    def mmt_flat(self):
+        """Flat momentum buffer, masking applied."""
+        self.flush()
+        return self._mmt_flat
+
+    @property
+    def vec_flat(self):
+        """Flat velocity buffer, masking applied."""
+        self.flush()
+        return self._vec_flat
 
     def _view(self, flat, name):
         i = self.names.index(name)
@@ -140,10 +165,11 @@ class DGCBatch:
         self.starts = starts
         arr = (ctypes.c_int64 * len(starts))(*starts)
         _lib.check(self._L.dgc_batch_compress(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
-                                              self.mmt_flat.data_ptr(), self.vec_flat.data_ptr(), arr,
+                                              self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
                                               self.payload.data_ptr(), self.info.data_ptr(), self.ws.data_ptr(),
                                               self.ws.numel(), _lib.SYNC_DEVICE, _lib.stream_of(self.device)),
                    "dgc_batch_compress")
+        self._pending = self.deferred_masking
 
     def exchange(self):
         if self.world > 1:

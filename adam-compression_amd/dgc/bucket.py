@@ -50,7 +50,7 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42, fill="auto"):
+                 device=None, world_size=None, seed=42, fill="auto", deferred_masking=True):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)
@@ -71,12 +71,16 @@ class DGCBucket:
         p.lower_count = math.ceil(compress_lower_bound * self.k)
         p.upper, p.lower = float(compress_upper_bound), float(compress_lower_bound)
         p.max_iters, p.resample, p.masking = int(max_adaptation_iters), int(bool(resample)), int(bool(momentum_masking))
-        p.vdtype, p.idtype, p.update_memory = _lib.VD[self.vdtype], _lib.ID[self.idtype], 1
+        # update_memory 2: the first-k branches' DGCSGDMemory.update zeroing rides in the
+        # next step's K1, which streams vec/mmt anyway (mmt/vec below flush it on read)
+        p.vdtype, p.idtype = _lib.VD[self.vdtype], _lib.ID[self.idtype]
+        p.update_memory = 2 if deferred_masking else 1
         self.params = p
 
         dev = self.device
-        self.mmt = torch.zeros(N, dtype=torch.float32, device=dev)
-        self.vec = torch.zeros(N, dtype=torch.float32, device=dev)
+        self._mmt = torch.zeros(N, dtype=torch.float32, device=dev)
+        self._vec = torch.zeros(N, dtype=torch.float32, device=dev)
+        self._pending = False
         L = _lib.lib()
         self.sampled = N != self.num_samples
         self.ws = torch.empty(L.dgc_compress_workspace(N, self.k, self.num_samples), dtype=torch.uint8,
@@ -100,22 +104,45 @@ class DGCBucket:
             self._ev_go = torch.cuda.Event()
             self._ev_filled = torch.cuda.Event()
 
+    # ---------------------------------------------------------------- state
+    def flush(self):
+        """Applies a deferred masking now (no-op when none is pending)."""
+        if self._pending:
+            _lib.check(self._L.dgc_compress_flush(self._vec.data_ptr(), self._mmt.data_ptr(), self.stride,
+                                                  ctypes.byref(self.params), self.ws.data_ptr(), self.ws.numel(),
+                                                  _lib.stream_of(self.device)), "dgc_compress_flush")
+            self._pending = False
+
+    @property
+    def mmt(self):
+        """Momentum (DGCSGDMemory.momentums), masking applied."""
+        self.flush()
+        return self._mmt
+
+    @property
+    def vec(self):
+        """Velocity (DGCSGDMemory.velocities), masking applied."""
+        self.flush()
+        return self._vec
+
     # ---------------------------------------------------------------- phases
     def compensate(self, grad):
         """K1: compensate + fused strided sample + speculative candidate lists."""
         L = self._L
         self.start = self.rng.randint(0, self.stride - 1) if self.sampled else 0
-        _lib.check(L.dgc_compress_begin(grad.data_ptr(), self.mmt.data_ptr(), self.vec.data_ptr(), self.momentum,
+        _lib.check(L.dgc_compress_begin(grad.data_ptr(), self._mmt.data_ptr(), self._vec.data_ptr(), self.momentum,
                                         int(self.nesterov), self.start, self.stride, ctypes.byref(self.params),
                                         self.spec.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
                                         _lib.stream_of(self.device)), "dgc_compress_begin")
         self.cnt = (self.numel - self.start + self.stride - 1) // self.stride if self.sampled else self.numel
+        self._pending = False   # K1 applied it
 
     def select(self):
         """K3 threshold + K4 selection / adaptation / resample / emit + masking, into the payload."""
         L = self._L
         base = self.payload.data_ptr()
-        _lib.check(L.dgc_compress_finish(self.vec.data_ptr(), self.mmt.data_ptr(), self.start, self.stride,
+        self._pending = self.params.update_memory == 2
+        _lib.check(L.dgc_compress_finish(self._vec.data_ptr(), self._mmt.data_ptr(), self.start, self.stride,
                                          self.top_k_samples, ctypes.byref(self.params), self.spec.data_ptr(),
                                          _lib.SPEC_MARGIN, base + self.voff, base + self.ioff, base,
                                          self.info.data_ptr(), self.ws.data_ptr(), self.ws.numel(),

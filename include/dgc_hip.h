@@ -97,6 +97,10 @@ typedef struct dgc_select_params {
     int32_t idtype;           /* enum dgc_idtype of indices_out             */
     int32_t update_memory;    /* 1: zero the emitted slots of vec (and of   */
                               /*    mmt when masking) = DGCSGDMemory.update */
+                              /* 2 (dgc_compress only): deferred — the next */
+                              /*    dgc_compress_begin on this workspace    */
+                              /*    zeroes them while it streams vec/mmt;   */
+                              /*    dgc_compress_flush applies it on demand */
                               /* 0: pure selection, vec/mmt untouched       */
 } dgc_select_params;
 
@@ -180,6 +184,12 @@ int dgc_compress_finish(float* vec, float* mmt, int64_t sample_start, int64_t sa
                         float spec_margin, void* values_out, void* indices_out, int64_t* count_out,
                         dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
                         void* stream);
+/* Applies a masking that a dgc_compress_finish with params.update_memory == 2 left
+ * pending on this workspace (no-op when none is). Call before reading vec/mmt (state
+ * dict, checkpoint) between a dgc_compress_finish and the next dgc_compress_begin
+ * (which applies it by itself; a flush after that begin would zero the new values). */
+int dgc_compress_flush(float* vec, float* mmt, int64_t sample_stride, const dgc_select_params* params,
+                       void* ws, size_t ws_bytes, void* stream);
 
 /* ---- batch: every compressed tensor of a step in the same launches ----
  * The reference compresses tensor by tensor from the optimizer's hooks
@@ -206,6 +216,11 @@ typedef struct dgc_batch_desc {
     int32_t max_iters, resample, momentum_masking, fp16_values, int32_indices, nesterov;
     float momentum;
     float spec_margin;              /* speculative list threshold margin (0.8)        */
+    int32_t deferred_masking;       /* 1: first-k branches leave DGCSGDMemory.update's */
+                                    /*   zeroing to the next compress's K1 (which    */
+                                    /*   streams vec/mmt anyway); dgc_batch_flush    */
+                                    /*   applies it before vec/mmt are read elsewhere */
+    int32_t pad;
 } dgc_batch_desc;
 
 size_t dgc_batch_workspace(const dgc_batch_desc* batch);
@@ -217,6 +232,8 @@ int dgc_batch_init(const dgc_batch_desc* batch, void* ws, size_t ws_bytes, void*
 int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
                        const int64_t* sample_starts, void* payload, dgc_select_info* info_out, void* ws,
                        size_t ws_bytes, int32_t sync_mode, void* stream);
+/* Pending deferred masking (deferred_masking = 1) applied now; no-op when none is. */
+int dgc_batch_flush(const dgc_batch_desc* batch, float* mmt, float* vec, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- K6: deterministic decompress ----
  * grad[0..n) = scale * (rank-order sequential sum of the entries), every other

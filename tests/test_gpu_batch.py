@@ -43,7 +43,11 @@ def test_batch_matches_per_tensor_oracle(label):
     state = {n: (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
              for i, n in enumerate(b.names)}
     branches = set()
-    for s in range(3 if label != "vgg16_bn" else 2):
+    steps = 3 if label != "vgg16_bn" else 2
+    for s in range(steps):
+        # state read on odd and last steps only: reading flushes the deferred masking, so the
+        # other steps leave it to the next K1 (the bench's path)
+        check_state = s % 2 == 1 or s == steps - 1
         grads = {}
         for t, name in enumerate(b.names):
             kind = "ties" if name == "ties" else ("layered" if t % 3 == 0 else "normal")
@@ -70,15 +74,18 @@ def test_batch_matches_per_tensor_oracle(label):
             gv, gi = sent[name]
             assert np.array_equal(gi.cpu().numpy(), oi), key
             assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
-            assert np.array_equal(bits(b.momentum_of(name).reshape(-1).cpu().numpy()), bits(m_o)), key
-            assert np.array_equal(bits(b.velocity_of(name).reshape(-1).cpu().numpy()), bits(v_o)), key
+            if check_state:
+                assert np.array_equal(bits(b.momentum_of(name).reshape(-1).cpu().numpy()), bits(m_o)), key
+                assert np.array_equal(bits(b.velocity_of(name).reshape(-1).cpu().numpy()), bits(v_o)), key
             dense = O.decompress([wv], [oi], N, 1)
             assert np.array_equal(bits(b.out(name).reshape(-1).cpu().numpy()), bits(dense)), key
         # padding between tensors stays zero (no tensor writes outside itself)
         pad = torch.ones(b.flat_numel, dtype=torch.bool, device=DEV)
         for off, n in zip(b.offsets, b.numels):
             pad[off: off + n] = False
-        assert not bool(out[pad].any()) and not bool(b.vec_flat[pad].any())
+        assert not bool(out[pad].any())
+        if check_state:
+            assert not bool(b.vec_flat[pad].any())
     if label == "mixed":
         assert {"direct", "resample"} <= branches, branches
 

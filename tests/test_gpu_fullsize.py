@@ -62,7 +62,8 @@ def test_flat_1b_bucket_steps_match_oracle():
         assert info["branch"] == oinfo["branch"], (s, info)
         assert np.array_equal(gi, oi), (s, info)
         assert np.array_equal(gv.view(np.uint32), ov.view(np.uint32)), s
-        assert _equal_bits(b.vec, v_o) and _equal_bits(b.mmt, m_o), s
+        if s % 3 == 2 or s == steps - 1:   # reading flushes the deferred masking: most steps leave it to K1
+            assert _equal_bits(b.vec, v_o) and _equal_bits(b.mmt, m_o), s
         dense = np.zeros(N, np.float32)
         dense[oi] = ov    # W = 1: unique indices, scale 1
         assert _equal_bits(out, dense), s
