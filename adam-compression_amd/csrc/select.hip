@@ -502,7 +502,7 @@ static int mask_flush(float* vec, float* mmt, const Layout& L, const SelWS& w, h
 template <bool NEST>
 __global__ void __launch_bounds__(kBlock)
 k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat, float* __restrict__ vec_flat,
-                  float mom, SelWS w) {
+                  float mom, SelWS w, StartChunk sc) {
     const int t = task(w, BT_K1, blockIdx.x);
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -515,7 +515,14 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     SelState* st = w.st + t;
     if (blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) st->t_list = tl;
     const bool sample = d.samp_off >= 0;
-    const int64_t start = sample ? w.starts[t] : 0, scount = sample ? w.scnt[t] : 0;
+    // sample starts of the first sc.count tensors ride in the arguments (no k_put_starts)
+    const bool arg_start = t < sc.count;
+    const int64_t start = !sample ? 0 : (arg_start ? sc.start[t] : w.starts[t]);
+    const int64_t scount = !sample ? 0 : (arg_start ? ceil_div(d.n - start, d.stride) : w.scnt[t]);
+    if (arg_start && blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) {
+        w.starts[t] = sc.start[t];
+        w.scnt[t] = sample ? scount : d.n;
+    }
     float* sout = sample ? w.samples + d.samp_off : nullptr;
     // waves past the tensor's last segment load nothing and list nothing, but stay for
     // the block barrier of the spill count
@@ -1668,12 +1675,13 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
     }
     if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: n too large");
     if (L.grid[BT_K1] > 0) {
+        const StartChunk none{};   // k_put_one wrote the start
         if (nesterov)
             hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
-                               vec, momentum, w);
+                               vec, momentum, w, none);
         else
             hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad,
-                               mmt, vec, momentum, w);
+                               mmt, vec, momentum, w, none);
         DGC_LAUNCHED();
     }
     if (n & 3) {   // scalar tail (< 4 elements) incl. its samples; its segment is marked spilled
@@ -1789,40 +1797,67 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
     return DGC_OK;
 }
 
-int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
-                   void* payload, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
-    Layout L;
-    std::vector<TDesc> td;
+// Host layout + workspace check shared by the batch entry points.
+static int batch_ws(const dgc_batch_desc* b, void* ws, size_t ws_bytes, const char* who, Layout& L,
+                    std::vector<TDesc>& td, SelWS& w) {
     std::vector<int32_t> bt[BT_COUNT];
     std::vector<int32_t> small;
     DGC_TRY(batch_layout(b, L, td, bt, small));
     size_t need = 0;
     carve_select(nullptr, L, &need);
     if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
-        DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_batch_compress: workspace needs %zu bytes, 256-B aligned", need);
-    if (!grad || !mmt || !vec || !payload || !starts) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
+        DGC_FAIL(DGC_ERR_WORKSPACE, "%s: workspace needs %zu bytes, 256-B aligned", who, need);
+    w = carve_select(ws, L);
+    return DGC_OK;
+}
+
+// K1 over every tensor (+ fused strided samples + speculative candidate lists).
+int batch_compress_begin(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
+                         void* ws, size_t ws_bytes, hipStream_t s) {
+    Layout L;
+    std::vector<TDesc> td;
+    SelWS w;
+    DGC_TRY(batch_ws(b, ws, ws_bytes, "dgc_batch_compress", L, td, w));
+    if (!grad || !mmt || !vec || !starts) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
     if (!aligned16(grad) || !aligned16(mmt) || !aligned16(vec))
         DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: flat buffers must be 16-B aligned");
     for (int32_t t = 0; t < L.T; ++t)
         if (td[t].samp_off >= 0 && (starts[t] < 0 || starts[t] >= td[t].stride))
             DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: tensor %d: sample start outside [0, stride)", t);
-    SelWS w = carve_select(ws, L);
-    for (int32_t t0 = 0; t0 < L.T; t0 += 64) {
-        StartChunk c{};
-        c.first = t0;
-        c.count = std::min<int32_t>(64, L.T - t0);
-        for (int i = 0; i < c.count; ++i) c.start[i] = td[t0 + i].samp_off >= 0 ? starts[t0 + i] : 0;
-        hipLaunchKernelGGL(k_put_starts, dim3(1), dim3(64), 0, s, w, c);
-        DGC_LAUNCHED();
+    // up to 64 starts go to K1 in its arguments; a larger batch puts them first
+    StartChunk arg{};
+    if (L.T <= 64) {
+        arg.count = L.T;
+        for (int i = 0; i < L.T; ++i) arg.start[i] = td[i].samp_off >= 0 ? starts[i] : 0;
+    } else {
+        for (int32_t t0 = 0; t0 < L.T; t0 += 64) {
+            StartChunk c{};
+            c.first = t0;
+            c.count = std::min<int32_t>(64, L.T - t0);
+            for (int i = 0; i < c.count; ++i) c.start[i] = td[t0 + i].samp_off >= 0 ? starts[t0 + i] : 0;
+            hipLaunchKernelGGL(k_put_starts, dim3(1), dim3(64), 0, s, w, c);
+            DGC_LAUNCHED();
+        }
     }
     if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: too many segments");
     if (b->nesterov)
         hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt, vec,
-                           b->momentum, w);
+                           b->momentum, w, arg);
     else
         hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
-                           vec, b->momentum, w);
+                           vec, b->momentum, w, arg);
     DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+// K3 thresholds, then the selection of every tensor into the one packed payload.
+int batch_compress_finish(const dgc_batch_desc* b, float* mmt, float* vec, void* payload, dgc_select_info* info,
+                          void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
+    Layout L;
+    std::vector<TDesc> td;
+    SelWS w;
+    DGC_TRY(batch_ws(b, ws, ws_bytes, "dgc_batch_compress", L, td, w));
+    if (!mmt || !vec || !payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
     DGC_TRY(thresholds(w, L, vec, s));
     int64_t cap = 0;
     for (const TDesc& d : td) cap += d.k;
@@ -1832,6 +1867,13 @@ int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float
     char* pl = static_cast<char*>(payload);
     return select_core(vec, mmt, cfg, L, pl + voff, pl + ioff, reinterpret_cast<int64_t*>(pl), info, w, 1,
                        sync_mode, b->spec_margin, s);
+}
+
+int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
+                   void* payload, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
+    if (!payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
+    DGC_TRY(batch_compress_begin(b, grad, mmt, vec, starts, ws, ws_bytes, s));
+    return batch_compress_finish(b, mmt, vec, payload, info, ws, ws_bytes, sync_mode, s);
 }
 
 int compress_flush(float* vec, float* mmt, int64_t s_stride, const dgc_select_params* p, void* ws, size_t ws_bytes,
@@ -1925,6 +1967,19 @@ extern "C" int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad
                                   size_t ws_bytes, int32_t sync_mode, void* stream) {
     return dgc::batch_compress(batch, grad, mmt, vec, sample_starts, payload, info_out, ws, ws_bytes, sync_mode,
                                static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_batch_compress_begin(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
+                                        const int64_t* sample_starts, void* ws, size_t ws_bytes, void* stream) {
+    return dgc::batch_compress_begin(batch, grad, mmt, vec, sample_starts, ws, ws_bytes,
+                                     static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt, float* vec, void* payload,
+                                         dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
+                                         void* stream) {
+    return dgc::batch_compress_finish(batch, mmt, vec, payload, info_out, ws, ws_bytes, sync_mode,
+                                      static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dgc_compress_flush(float* vec, float* mmt, int64_t sample_stride, const dgc_select_params* params,

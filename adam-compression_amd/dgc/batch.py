@@ -159,17 +159,31 @@ class DGCBatch:
             starts.append(self.rng.randint(0, stride - 1) if n != S else 0)
         return starts
 
-    def compress(self, starts=None):
-        """Every tensor: compensate -> sample -> threshold -> select -> pack -> masking."""
+    def compensate(self, starts=None):
+        """K1 over every tensor: compensate + strided samples + candidate lists (and any
+        masking the previous select left pending)."""
         starts = self.draw_starts() if starts is None else starts
         self.starts = starts
         arr = (ctypes.c_int64 * len(starts))(*starts)
-        _lib.check(self._L.dgc_batch_compress(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
-                                              self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
-                                              self.payload.data_ptr(), self.info.data_ptr(), self.ws.data_ptr(),
-                                              self.ws.numel(), _lib.SYNC_DEVICE, _lib.stream_of(self.device)),
-                   "dgc_batch_compress")
+        _lib.check(self._L.dgc_batch_compress_begin(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
+                                                    self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
+                                                    self.ws.data_ptr(), self.ws.numel(),
+                                                    _lib.stream_of(self.device)), "dgc_batch_compress_begin")
+        self._pending = False
+
+    def select(self):
+        """K3 thresholds + selection / adaptation / resample / pack / masking of every tensor."""
+        _lib.check(self._L.dgc_batch_compress_finish(ctypes.byref(self.desc), self._mmt_flat.data_ptr(),
+                                                     self._vec_flat.data_ptr(), self.payload.data_ptr(),
+                                                     self.info.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                                     _lib.SYNC_DEVICE, _lib.stream_of(self.device)),
+                   "dgc_batch_compress_finish")
         self._pending = self.deferred_masking
+
+    def compress(self, starts=None):
+        """Every tensor: compensate -> sample -> threshold -> select -> pack -> masking."""
+        self.compensate(starts)
+        self.select()
 
     def exchange(self):
         if self.world > 1:

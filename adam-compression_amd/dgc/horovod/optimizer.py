@@ -25,9 +25,12 @@ from dgc.horovod.compression import Compression
 
 __all__ = ["DistributedOptimizer"]
 
+_BATCHED = "batched"   # hook handle of a gradient left to the grouped exchange
+
 
 class _DistributedOptimizer(torch.optim.Optimizer):
-    def __init__(self, params, named_parameters, compression, backward_passes_per_step=1, op=Average):
+    def __init__(self, params, named_parameters, compression, backward_passes_per_step=1, op=Average,
+                 batch=False):
         super(self.__class__, self).__init__(params)
         self._compression = compression
         self._communicate_ = getattr(compression, "communicate", None) or \
@@ -62,6 +65,14 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._requires_update = set()
         self._synchronized = False
         self._should_synchronize = True
+        self._batched = None
+        self._order = []
+        if batch:
+            from dgc.horovod import batched
+            if not batched.supported(compression):
+                raise ValueError("batch=True needs a DGCCompressor driving a DGCSGDMemory with strided sampling "
+                                 "and no gradient clipping")
+            self._batched = batched.BatchedStep(compression, named_parameters)
         if comm.size() > 1 or os.environ.get("HOROVOD_ELASTIC") == "1":
             self._register_hooks()
 
@@ -106,11 +117,25 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             handle, ctx = None, None
             self._allreduce_delay[p] -= 1
             if self._allreduce_delay[p] == 0:
-                handle, ctx = self._allreduce_grad_async(p)
+                if self._batched is not None:   # exchanged with all the others in synchronize()
+                    self._order.append(self._parameter_names.get(p))
+                    handle = _BATCHED
+                else:
+                    handle, ctx = self._allreduce_grad_async(p)
             self._handles[p] = (handle, ctx)
         return hook
 
     def synchronize(self):
+        if self._batched is not None:
+            if self._requires_update:
+                # one grouped compress -> allgather -> decompress (+ one dense allreduce)
+                self._batched.step(self._order)
+                for p in self._requires_update:
+                    self._allreduce_delay[p] = self.backward_passes_per_step
+            self._order.clear()
+            self._handles.clear()
+            self._synchronized = True
+            return
         for p in self._requires_update - set(self._handles.keys()):
             self._handles[p] = self._allreduce_grad_async(p)
         for p, (handle, ctx) in list(self._handles.items()):
@@ -148,14 +173,26 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             raise AssertionError("optimizer.zero_grad() was called after loss.backward() but before "
                                  "optimizer.step() or optimizer.synchronize(). This is prohibited as it "
                                  "can cause a race condition.")
+        if self._batched is not None and not args and not kwargs.get("set_to_none", False):
+            # keep the gradients as views of the flat buffers: zero them in place
+            if self._batched.zero_grads():
+                return None
         return super(self.__class__, self).zero_grad(*args, **kwargs)
 
 
 def DistributedOptimizer(optimizer, named_parameters=None, compression=Compression.none,
-                         backward_passes_per_step=1, op=Average):
+                         backward_passes_per_step=1, op=Average, batch=False):
     """Wrap ``optimizer`` so gradients are compressed, exchanged across ranks and
-    decompressed before it steps (dgc/horovod/optimizer.py:370-417)."""
+    decompressed before it steps (dgc/horovod/optimizer.py:370-417).
+
+    ``batch=True`` (not in the reference; DGCCompressor + DGCSGDMemory only) exchanges
+    every gradient of a step at once in ``synchronize()``: one K1 launch, one packed
+    allgather and one decompress for all compressed tensors, one allreduce for the
+    dense ones, no host synchronisation (dgc/horovod/batched.py). The numerics, the
+    sample-start draws and so the weights are those of the per-tensor path."""
     if op == Adasum and comm.size() > 1:
         raise NotImplementedError("Adasum is not part of the DGC path (dgc/horovod/optimizer.py:197-367)")
+    if batch and op != Average:
+        raise NotImplementedError("batch=True exchanges with Average (dgc/compression.py:23)")
     cls = type(optimizer.__class__.__name__, (optimizer.__class__,), dict(_DistributedOptimizer.__dict__))
-    return cls(optimizer.param_groups, named_parameters, compression, backward_passes_per_step, op)
+    return cls(optimizer.param_groups, named_parameters, compression, backward_passes_per_step, op, batch)

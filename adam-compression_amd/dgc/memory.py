@@ -55,11 +55,19 @@ class DGCSGDMemory(Memory):
         self.momentums = {}
         self.velocities = {}
         self._bad = {}
+        # callables run before the state is read or replaced: a batched step
+        # (dgc/horovod/batched.py) applies a deferred momentum masking there
+        self._before_read = []
+
+    def _sync(self):
+        for fn in self._before_read:
+            fn()
 
     def initialize(self, named_parameters):
         """zeros_like per parameter (dgc/memory.py:43-48)."""
         if comm.rank() == 0:
             print("=> initializing dgc sgd memory")
+        self._sync()
         for name, param in named_parameters:
             self.momentums[name] = torch.zeros_like(param.data)
             self.velocities[name] = torch.zeros_like(param.data)
@@ -73,6 +81,7 @@ class DGCSGDMemory(Memory):
 
         accumulate=True returns ``velocities[name]`` itself (updated in place);
         accumulate=False (dense tensors) returns a new tensor."""
+        self._sync()
         grad = self._clip(grad)
         mmt = self.momentums[name]
         _lib.require_cuda_f32(grad, "DGCSGDMemory.compensate")
@@ -94,6 +103,7 @@ class DGCSGDMemory(Memory):
 
     def update(self, name, ctx):
         """Zero the transmitted slots (dgc/memory.py:72-77)."""
+        self._sync()
         indices = ctx[0]
         vec = self.velocities[name]
         mmt = self.momentums[name]
@@ -111,9 +121,11 @@ class DGCSGDMemory(Memory):
                                       _lib.ptr(bad), _lib.stream_of(vec.device)), "dgc_mask_indices")
 
     def state_dict(self):
+        self._sync()
         return dict(momentums=self.momentums, velocities=self.velocities)
 
     def load_state_dict(self, state_dict):
+        self._sync()
         momentums = state_dict["momentums"]
         velocities = state_dict["velocities"]
         for name in self.momentums.keys():

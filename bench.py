@@ -293,7 +293,7 @@ class ModelRun:
         ev = ev or {}
         L, b = self._lib.lib(), self.b
         b.grad_flat = g   # the model's gradients live in the batch's flat buffer (p.grad views)
-        for name, fn in (("compensate", lambda: b.compress()), ("allgather", b.exchange),
+        for name, fn in (("compensate", b.compensate), ("select", b.select), ("allgather", b.exchange),
                          ("decompress", b.decompress)):
             pair = ev.get(name)
             if pair:
@@ -369,7 +369,7 @@ def main():
     torch.cuda.synchronize()
     timed = phases if args.phases else ("compensate", "allgather")
     if wl["kind"] == "model":
-        timed = ("compensate", "allgather", "decompress")   # compensate = the whole batched compress
+        timed = phases   # K1 (compensate) timed live on its own, as for the flat bucket
     evs = [{p: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for p in timed}
            for _ in range(args.steps)]
     if world > 1:
@@ -397,12 +397,10 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    k1_ms = ms["compensate"]   # HIP events around K1's launch on the stream it runs on
     if wl["kind"] == "flat":
-        k1_ms = ms["compensate"]
         k1_name = "K1 compensate + fused sample + speculative lists (k_compensate_list)"
     else:
-        # the batched compress phase holds K1 and the selection: K1's share comes from rocprof
-        k1_ms = prof_ms if prof_ms else ms["compensate"]
         k1_name = "K1 over all compressed tensors (k_compensate_list, one launch)"
     k1_gbs = k1_bytes / (k1_ms * 1e-3) / 1e9
     wire = f"{'fp16' if run.vbytes == 2 else 'fp32'} values / {'int32' if run.ibytes == 4 else 'int64'} indices"

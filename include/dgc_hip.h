@@ -232,6 +232,15 @@ int dgc_batch_init(const dgc_batch_desc* batch, void* ws, size_t ws_bytes, void*
 int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
                        const int64_t* sample_starts, void* payload, dgc_select_info* info_out, void* ws,
                        size_t ws_bytes, int32_t sync_mode, void* stream);
+/* dgc_batch_compress in its two phases (same arguments): begin = K1 over every tensor
+ * (compensate + strided samples + speculative candidate lists, and any masking a
+ * deferring finish left pending); finish = K3 thresholds + the selection into the
+ * payload. Nothing may touch grad/mmt/vec between them. */
+int dgc_batch_compress_begin(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
+                             const int64_t* sample_starts, void* ws, size_t ws_bytes, void* stream);
+int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt, float* vec, void* payload,
+                              dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
+                              void* stream);
 /* Pending deferred masking (deferred_masking = 1) applied now; no-op when none is. */
 int dgc_batch_flush(const dgc_batch_desc* batch, float* mmt, float* vec, void* ws, size_t ws_bytes, void* stream);
 

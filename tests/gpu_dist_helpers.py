@@ -69,10 +69,11 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def optimizer_replay_worker(rank, world, port, label, queue):
+def optimizer_replay_worker(rank, world, port, label, batch, queue):
     """label "tinynet": optimizer.npz (3 steps, nesterov DGCSGD, fp32/int64, ratio 0.01);
     label "resnet20": BASELINE configs[0] (ResNet-20, ratio 0.001 with the 5-epoch warmup
-    0.316 -> 0.1 -> 0.001 re-initialising mid-run, fp16 values, int32 indices)."""
+    0.316 -> 0.1 -> 0.001 re-initialising mid-run, fp16 values, int32 indices).
+    batch: DistributedOptimizer(batch=True) — one grouped exchange per step."""
     import torch.distributed as dist
     _init(rank, world, port)
     problems = []
@@ -113,7 +114,7 @@ def optimizer_replay_worker(rank, world, port, label, queue):
             mem.initialize(model.named_parameters())
             comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
         dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
-                                    backward_passes_per_step=1, op=Average)
+                                    backward_passes_per_step=1, op=Average, batch=batch)
         params = dict(model.named_parameters())
         random.seed(cfg["random_seed"])
         calls = []
@@ -133,8 +134,10 @@ def optimizer_replay_worker(rank, world, port, label, queue):
             grads = [trace[f"{key}/{j}"] for j in range(len(order))]
             calls.clear()
             replay_backward(params, order, grads, dev)
-            if calls != order:
+            if (list(dopt._order) if batch else calls) != order:
                 problems.append(("hook order", s))
+            if batch and calls:
+                problems.append(("per-tensor compress in batch mode", s))
             dopt.step()
             dopt.zero_grad()
             torch.cuda.synchronize()

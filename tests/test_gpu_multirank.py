@@ -6,7 +6,9 @@ its regrouping of topk-ordered runs, DGCSGD's fused step.
 * The reference's DistributedOptimizer runs (optimizer.npz: 3 steps; ResNet-20 =
   BASELINE configs[0]: 6 steps over the 0.316 -> 0.1 -> 0.001 warmup with
   re-initialisation, fp16 values / int32 indices) are replayed from the recorded
-  per-step gradients and hook order; the weights must equal the reference's bit for bit.
+  per-step gradients and hook order; the weights must equal the reference's bit for
+  bit — per tensor as the reference runs, and with batch=True (one grouped K1 /
+  allgather / decompress and one dense allreduce per step).
 * DGCBucket at W=2, both fill modes, against the oracle over both ranks' payloads.
 """
 import pytest
@@ -42,9 +44,10 @@ def run(fn, world, *args):
 
 
 @pytest.mark.timeout(200)
+@pytest.mark.parametrize("batch", [False, True], ids=["per-tensor", "batched"])
 @pytest.mark.parametrize("label", ["tinynet", "resnet20"])
-def test_distributed_optimizer_w2_reproduces_reference_weights(label):
-    out = run(G.optimizer_replay_worker, 2, label)
+def test_distributed_optimizer_w2_reproduces_reference_weights(label, batch):
+    out = run(G.optimizer_replay_worker, 2, label, batch)
     for rank, problems in out.items():
         assert problems == [], (rank, problems)
 
