@@ -42,9 +42,32 @@ constexpr int kNthThreads = 512;    // 8 waves: 256 VGPRs per lane for the batch
 constexpr int kNthWaves = kNthThreads / kWave;
 constexpr int kNthLds = 12288;   // entries partitioned in LDS (96 KB + 48 KB of pair slots)
 constexpr int kNthWave = 1024;   // entries finished by a single wave
-constexpr int kNthBatch = 4;     // 256-entry tiles loaded per lane before use
 
 __device__ __forceinline__ uint32_t qkey(uint64_t e) { return (uint32_t)(e >> 32); }
+
+#ifdef DGC_K5_PROF
+// tools/k5_prof: phase timestamps (wall clock, 100 MHz) and step counts of the last
+// K5 run by workgroup 0 — a profiling build only (make k5prof).
+struct K5Prof {
+    unsigned long long t[8];
+    unsigned int steps[4];
+    unsigned long long sub[8];   // global-phase step parts, summed over steps
+};
+__device__ K5Prof g_k5prof;
+#define K5_STAMP(i) \
+    do { if (blockIdx.x == 0 && threadIdx.x == 0) g_k5prof.t[i] = wall_clock64(); } while (0)
+#define K5_STEP(i) \
+    do { if (blockIdx.x == 0 && threadIdx.x == 0) g_k5prof.steps[i] += 1; } while (0)
+#define K5_SUB_BEGIN() unsigned long long k5_t0 = wall_clock64()
+#define K5_SUB(i, global) \
+    do { if ((global) && blockIdx.x == 0 && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
+         g_k5prof.sub[i] += t_ - k5_t0; k5_t0 = t_; } } while (0)
+#else
+#define K5_SUB_BEGIN() do { } while (0)
+#define K5_SUB(i, global) do { } while (0)
+#define K5_STAMP(i) do { } while (0)
+#define K5_STEP(i) do { } while (0)
+#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -99,18 +122,25 @@ __device__ void nth_heap_select(uint64_t* q, int64_t mid, int64_t n, int64_t nth
     q[nth] = t;
 }
 
-// std::__move_median_to_first(f, f+1, mid, l-1) with comp = key greater. One thread.
-__device__ __forceinline__ void nth_median(uint64_t* q, int64_t f, int64_t l) {
+// std::__move_median_to_first(f, f+1, mid, l-1) with comp = key greater. One thread;
+// the four entries are loaded together (one round trip when q is in global memory).
+// Returns the pivot key.
+__device__ __forceinline__ uint32_t nth_median(uint64_t* q, int64_t f, int64_t l) {
     const int64_t a = f + 1, b = f + (l - f) / 2, c = l - 1;
-    const uint32_t ka = qkey(q[a]), kb = qkey(q[b]), kc = qkey(q[c]);
+    const uint64_t ea = q[a], eb = q[b], ec = q[c], ef = q[f];
+    const uint32_t ka = qkey(ea), kb = qkey(eb), kc = qkey(ec);
     int64_t m;
-    if (ka > kb)
-        m = kb > kc ? b : (ka > kc ? c : a);
-    else
-        m = ka > kc ? a : (kb > kc ? c : b);
-    const uint64_t t = q[f];
-    q[f] = q[m];
-    q[m] = t;
+    uint64_t em;
+    if (ka > kb) {
+        if (kb > kc) { m = b; em = eb; }
+        else if (ka > kc) { m = c; em = ec; }
+        else { m = a; em = ea; }
+    } else if (ka > kc) { m = a; em = ea; }
+    else if (kb > kc) { m = c; em = ec; }
+    else { m = b; em = eb; }
+    q[m] = ef;   // m != f (a, b, c > f)
+    q[f] = em;
+    return qkey(em);
 }
 
 // std::__insertion_sort of q[f, l) (<= 3 entries after the loop). One thread.
@@ -131,15 +161,64 @@ __device__ void nth_insertion_sort(uint64_t* q, int64_t f, int64_t l) {
     }
 }
 
-// Lane's 4 consecutive entries of a 256-entry tile (positions < end).
-__device__ __forceinline__ void nth_load4(const uint64_t* q, int64_t e0, int64_t end, uint64_t (&x)[4],
-                                          uint32_t& valid) {
+// Lane's 4 consecutive entries of a 256-entry tile, positions in [begin, end). Tiles
+// are laid from a 16-B-aligned base (nth_base), so a lane whose 4 entries are all in
+// range reads them with two 16-B loads.
+__device__ __forceinline__ void nth_load4(const uint64_t* q, int64_t e0, int64_t begin, int64_t end,
+                                          uint64_t (&x)[4], uint32_t& valid) {
+    if (e0 >= begin && e0 + 3 < end) {
+        const uint4 a = *reinterpret_cast<const uint4*>(q + e0);
+        const uint4 b = *reinterpret_cast<const uint4*>(q + e0 + 2);
+        x[0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        x[1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
+        x[2] = (uint64_t)b.x | ((uint64_t)b.y << 32);
+        x[3] = (uint64_t)b.z | ((uint64_t)b.w << 32);
+        valid = 0xFu;
+        return;
+    }
     valid = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const bool ok = e0 + j < end;
+        const bool ok = e0 + j >= begin && e0 + j < end;
         x[j] = ok ? q[e0 + j] : 0ull;
         valid |= (uint32_t)ok << j;
+    }
+}
+
+// The first tile position at or below a0 whose address is 16-B aligned.
+__device__ __forceinline__ int64_t nth_base(const uint64_t* q, int64_t a0) {
+    return a0 - (int64_t)((reinterpret_cast<uintptr_t>(q + a0) >> 3) & 1u);
+}
+
+// The step's swaps L_t <-> R_t, t < s (disjoint positions), by threads tid of nt:
+// kNthSwapBatch pairs per thread with all their loads in flight before any store
+// (8 for the global-memory phase, 2 in LDS where latency is short and registers count).
+template <int kNthSwapBatch>
+__device__ __forceinline__ void nth_swaps(uint64_t* q, const uint32_t* lpos, const uint32_t* rpos, int64_t f,
+                                          uint32_t s, uint32_t tid, uint32_t nt) {
+    for (uint32_t t0 = tid; t0 < s; t0 += nt * kNthSwapBatch) {
+        uint32_t li[kNthSwapBatch], ri[kNthSwapBatch];
+#pragma unroll
+        for (int j = 0; j < kNthSwapBatch; ++j) {
+            const uint32_t t = t0 + j * nt;
+            li[j] = t < s ? lpos[t] : 0u;
+            ri[j] = t < s ? rpos[t] : 0u;
+        }
+        uint64_t a[kNthSwapBatch], b[kNthSwapBatch];
+#pragma unroll
+        for (int j = 0; j < kNthSwapBatch; ++j) {
+            if (t0 + j * nt < s) {
+                a[j] = q[f + li[j]];
+                b[j] = q[f + ri[j]];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kNthSwapBatch; ++j) {
+            if (t0 + j * nt < s) {
+                q[f + li[j]] = b[j];
+                q[f + ri[j]] = a[j];
+            }
+        }
     }
 }
 
@@ -156,52 +235,100 @@ __device__ __forceinline__ void stopper_masks(const uint64_t (&x)[4], uint32_t v
     pr &= valid;
 }
 
-// Pass 2 on one tile: ranks, pairing and the paired positions. rl / rr: the left and
-// right stoppers before the tile (uniform over the wave); lpos/rpos hold positions
-// relative to f. Returns via the accumulators.
-__device__ __forceinline__ void pair_tile(const uint64_t (&x)[4], uint32_t valid, uint32_t P, int64_t e0, int64_t f,
-                                          uint32_t TR, uint32_t& runl, uint32_t& runr, uint32_t* lpos, uint32_t* rpos,
-                                          uint32_t& paired, unsigned long long& lnext, unsigned long long& rmin) {
-    uint32_t pl, pr;
-    stopper_masks(x, valid, P, pl, pr);
+// Wave total of 4 predicate bits per lane (ballots: scalar, no cross-lane shuffles).
+__device__ __forceinline__ uint32_t wave_count4(uint32_t p) {
+    return (uint32_t)(__popcll(__ballot(p & 1u)) + __popcll(__ballot(p & 2u)) + __popcll(__ballot(p & 4u)) +
+                      __popcll(__ballot(p & 8u)));
+}
+
+// The first element, in tile order 4 * lane + j, set in the per-j ballots m; 256 if none.
+__device__ __forceinline__ uint32_t first_in_tile(const uint64_t (&m)[4]) {
+    uint32_t best = 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (m[j]) {
+            const uint32_t e = 4u * (uint32_t)__builtin_ctzll(m[j]) + (uint32_t)j;
+            best = e < best ? e : best;
+        }
+    }
+    return best;
+}
+
+// Pass 2 on one tile (elements tile + 4 * lane + j, stopper bits pl / pr from
+// stopper_masks): ranks, pairing and the paired positions. runl / runr: the left and right stoppers before the tile; lpos/rpos
+// hold positions relative to f. The step's results: paired (swaps), lnext (first
+// unswapped left stopper), rmin (smallest swapped right stopper); INT64_MAX = none.
+// BALLOT: accumulated wave-uniformly from ballots (a few tiles: no reduction after);
+// else per lane, for the caller to reduce once after many tiles.
+// STAGE (pair slots in global memory): the tile's swapped left stoppers have the
+// consecutive ranks runl.. and its swapped right stoppers the consecutive ranks from
+// TR - runr - tr up, so they go through the wave's LDS area stg (2 x 256 slots) and
+// leave in coalesced stores — ~2 per tile instead of 8 exec-masked scattered ones
+// (which held the pass on the vector-memory counter).
+template <bool BALLOT, bool STAGE = false>
+__device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile, int64_t f, uint32_t TR,
+                                          uint32_t& runl, uint32_t& runr, uint32_t* lpos, uint32_t* rpos,
+                                          uint32_t& paired, int64_t& lnext, int64_t& rmin, uint32_t* stg = nullptr) {
+    const int lane = threadIdx.x & 63;
     uint32_t bl, tl, br, tr;
     wave_prefix4(pl, bl, tl);
     wave_prefix4(pr, br, tr);
     uint32_t rl = runl + bl;   // left stoppers before this element
     uint32_t rr = runr + br;   // right stoppers in [f+1, this element)
+    const uint32_t ulow = TR - runr - tr;   // the tile's smallest right-stopper rank
+    uint64_t msl[4], mln[4], msr[4];
+    uint32_t nsl = 0, nsr = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const bool isl = (pl >> j) & 1u, isr = (pr >> j) & 1u;
-        const int64_t i = e0 + j;
+        const int64_t i = tile + 4 * lane + j;
         const uint32_t rr_incl = rr + (isr ? 1u : 0u);
-        if (isl) {
-            // L_{rl+1} = i is swapped iff #(key >= P in (i, l)) >= rl + 1
-            if (TR - rr_incl >= rl + 1) {
-                lpos[rl] = (uint32_t)(i - f);
-                ++paired;
-            } else if ((unsigned long long)i < lnext) {
-                lnext = (unsigned long long)i;
-            }
+        // L_{rl+1} = i is swapped iff #(key >= P in (i, l)) >= rl + 1
+        const bool swl = isl && TR - rr_incl >= rl + 1;
+        // R_{u+1} = i with u = #(key >= P in (i, l)); swapped iff #(key <= P in [f+1, i)) >= u + 1
+        const uint32_t u = TR - rr_incl;
+        const bool swr = isr && rl >= u + 1;
+        if (STAGE) {
+            if (swl) stg[rl - runl] = (uint32_t)(i - f);
+            if (swr) stg[256 + (u - ulow)] = (uint32_t)(i - f);
+            nsl += (uint32_t)__popcll(__ballot(swl));
+            nsr += (uint32_t)__popcll(__ballot(swr));
+        } else {
+            if (swl) lpos[rl] = (uint32_t)(i - f);
+            if (swr) rpos[u] = (uint32_t)(i - f);
         }
-        if (isr) {
-            // R_{u+1} = i with u = #(key >= P in (i, l)); swapped iff #(key <= P in [f+1, i)) >= u + 1
-            const uint32_t u = TR - rr_incl;
-            if (rl >= u + 1) {
-                rpos[u] = (uint32_t)(i - f);
-                if ((unsigned long long)i < rmin) rmin = (unsigned long long)i;
-            }
+        if (BALLOT) {
+            msl[j] = __ballot(swl);
+            mln[j] = __ballot(isl && !swl);
+            msr[j] = __ballot(swr);
+        } else {
+            paired += swl;
+            if (isl && !swl && i < lnext) lnext = i;
+            if (swr && i < rmin) rmin = i;
         }
         rl += isl;
         rr = rr_incl;
+    }
+    if (BALLOT) {
+        paired += (uint32_t)(__popcll(msl[0]) + __popcll(msl[1]) + __popcll(msl[2]) + __popcll(msl[3]));
+        const uint32_t el = first_in_tile(mln), er = first_in_tile(msr);
+        if (el < 256 && tile + el < lnext) lnext = tile + el;
+        if (er < 256 && tile + er < rmin) rmin = tile + er;
+    }
+    if (STAGE && (nsl | nsr)) {
+        wave_sync();
+        for (uint32_t k = lane; k < nsl; k += 64) lpos[runl + k] = stg[k];
+        for (uint32_t k = lane; k < nsr; k += 64) rpos[ulow + k] = stg[256 + k];
+        wave_sync();   // the next tile may overwrite stg
     }
     runl += tl;
     runr += tr;
 }
 
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long a = __shfl_xor(v, o);
+        const int64_t a = __shfl_xor(v, o);
         v = a < v ? a : v;
     }
     return v;
@@ -210,6 +337,7 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // ---------------------------------------------------------------- workgroup step
 struct NthShared {
     int64_t f, l, depth;
+    uint32_t pivot;                          // the step's pivot key (set by nth_median)
     uint32_t wl[kNthWaves], wr[kNthWaves];   // per-wave stopper counts
     uint32_t s;                              // swaps
     unsigned long long l_next, r_min;
@@ -218,27 +346,34 @@ struct NthShared {
 
 // One partition step over q[f, l) by the whole workgroup; the pivot is already at
 // q[f] and sh.s / l_next / r_min are reset. On return (after the last barrier) the
-// step's swaps are done and sh.s / l_next / r_min hold its result.
-__device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh) {
+// step's swaps are done and sh.s / l_next / r_min hold its result. Pass 1 keeps each
+// lane's stopper bits of each tile in mk (one byte, LDS) when the step's tiles fit
+// mk_tiles, so pass 2 reads bytes instead of the entries; otherwise it reloads them.
+template <int kNthBatch, int kSwapBatch>
+__device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, uint8_t* mk,
+                            int64_t mk_tiles, uint32_t* stage) {
     const int64_t f = sh.f, l = sh.l;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t P = qkey(q[f]);
-    const int64_t a0 = f + 1, R = l - a0;
+    const uint32_t P = sh.pivot;
+    const int64_t a0 = f + 1, base = nth_base(q, a0), R = l - base;
     const int64_t per = ceil_div(ceil_div(R, (int64_t)kNthWaves), (int64_t)256) * 256;
-    const int64_t wb = a0 + wv * per, we = wb + per < l ? wb + per : l;
+    const int64_t wb = base + wv * per, we = wb + per < l ? wb + per : l;
+    const bool keep = ceil_div(R, (int64_t)256) <= mk_tiles;
+    K5_SUB_BEGIN();
     // pass 1: stopper counts per wave, kNthBatch tiles of loads in flight per lane
     uint32_t cl = 0, cr = 0;
     for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
         uint64_t x[kNthBatch][4];
         uint32_t valid[kNthBatch];
 #pragma unroll
-        for (int b = 0; b < kNthBatch; ++b) nth_load4(q, t0 + b * 256 + 4 * lane, we, x[b], valid[b]);
+        for (int b = 0; b < kNthBatch; ++b) nth_load4(q, t0 + b * 256 + 4 * lane, a0, we, x[b], valid[b]);
 #pragma unroll
         for (int b = 0; b < kNthBatch; ++b) {
             uint32_t pl, pr;
             stopper_masks(x[b], valid[b], P, pl, pr);
             cl += __popc(pl);
             cr += __popc(pr);
+            if (keep && t0 + b * 256 < we) mk[((t0 + b * 256 - base) >> 8) * 64 + lane] = (uint8_t)(pl | (pr << 4));
         }
     }
     cl = wave_sum(cl);
@@ -248,6 +383,7 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
         sh.wr[wv] = cr;
     }
     __syncthreads();
+    K5_SUB(0, kNthBatch == 8);
     // every wave derives its own prefix and the total from the 16 wave counts
     uint32_t runl = 0, runr = 0, TR = 0;
 #pragma unroll
@@ -259,34 +395,50 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     }
     // pass 2: ranks, pairing, paired positions
     uint32_t paired = 0;
-    unsigned long long lnext = ~0ull, rmin = ~0ull;
-    for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
-        uint64_t x[kNthBatch][4];
-        uint32_t valid[kNthBatch];
+    int64_t lnext = INT64_MAX, rmin = INT64_MAX;
+    uint32_t* stg = stage ? stage + wv * 512 : nullptr;
+    if (keep && stg) {
+        for (int64_t t0 = wb; t0 < we; t0 += 256) {
+            const uint32_t m = mk[((t0 - base) >> 8) * 64 + lane];
+            pair_tile<false, true>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin, stg);
+        }
+    } else if (keep) {
+        for (int64_t t0 = wb; t0 < we; t0 += 256) {
+            const uint32_t m = mk[((t0 - base) >> 8) * 64 + lane];
+            pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+        }
+    } else {
+        for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
+            uint64_t x[kNthBatch][4];
+            uint32_t valid[kNthBatch];
 #pragma unroll
-        for (int b = 0; b < kNthBatch; ++b) nth_load4(q, t0 + b * 256 + 4 * lane, we, x[b], valid[b]);
+            for (int b = 0; b < kNthBatch; ++b) nth_load4(q, t0 + b * 256 + 4 * lane, a0, we, x[b], valid[b]);
 #pragma unroll
-        for (int b = 0; b < kNthBatch; ++b)
-            pair_tile(x[b], valid[b], P, t0 + b * 256 + 4 * lane, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+            for (int b = 0; b < kNthBatch; ++b) {
+                uint32_t pl, pr;
+                stopper_masks(x[b], valid[b], P, pl, pr);
+                if (stg)
+                    pair_tile<false, true>(pl, pr, t0 + b * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin,
+                                           stg);
+                else
+                    pair_tile<false>(pl, pr, t0 + b * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+            }
+        }
     }
     paired = wave_sum(paired);
-    lnext = wave_min_u64(lnext);
-    rmin = wave_min_u64(rmin);
+    lnext = wave_min_i64(lnext);
+    rmin = wave_min_i64(rmin);
     if (lane == 0) {
         if (paired) atomicAdd(&sh.s, paired);
-        if (lnext != ~0ull) atomicMin(&sh.l_next, lnext);
-        if (rmin != ~0ull) atomicMin(&sh.r_min, rmin);
+        if (lnext != INT64_MAX) atomicMin(&sh.l_next, (unsigned long long)lnext);
+        if (rmin != INT64_MAX) atomicMin(&sh.r_min, (unsigned long long)rmin);
     }
     __syncthreads();
+    K5_SUB(1, kNthBatch == 8);
     // pass 3: the swaps L_t <-> R_t, t < s (disjoint positions)
-    const uint32_t s = sh.s;
-    for (uint32_t t = threadIdx.x; t < s; t += kNthThreads) {
-        const int64_t li = f + lpos[t], ri = f + rpos[t];
-        const uint64_t a = q[li], b = q[ri];
-        q[li] = b;
-        q[ri] = a;
-    }
+    nth_swaps<kSwapBatch>(q, lpos, rpos, f, sh.s, threadIdx.x, kNthThreads);
     __syncthreads();
+    K5_SUB(2, kNthBatch == 8);
 }
 
 // Thread 0, after a step: the cut, the next range, and either the next step's
@@ -304,8 +456,9 @@ __device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop
 
 // The introselect loop on q[f, l) by the whole workgroup while the range exceeds
 // `stop` entries; ends with a barrier, sh.f/l/depth updated or sh.heap_exit set.
+template <int kNthBatch, int kSwapBatch>
 __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth,
-                            int64_t stop) {
+                            int64_t stop, uint8_t* mk, int64_t mk_tiles, uint32_t* stage) {
     // thread 0 prepares a step: depth check, median, reset of the step's results
     auto prepare = [&]() -> bool {
         if (sh.l - sh.f <= stop) return false;
@@ -315,7 +468,7 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
             return false;
         }
         sh.depth -= 1;
-        nth_median(q, sh.f, sh.l);
+        sh.pivot = nth_median(q, sh.f, sh.l);
         sh.s = 0;
         sh.l_next = ~0ull;
         sh.r_min = ~0ull;
@@ -325,52 +478,51 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     if (threadIdx.x == 0) go = !sh.heap_exit && prepare();
     __syncthreads();
     while (go) {
-        nth_step_wg(q, lpos, rpos, sh);
+        K5_STEP(stop == kNthLds ? 0 : 1);
+        nth_step_wg<kNthBatch, kSwapBatch>(q, lpos, rpos, sh, mk, mk_tiles, stage);
+        K5_SUB_BEGIN();
         if (threadIdx.x == 0) {
             nth_advance(q, sh, nth, stop);
             go = prepare();
         }
         __syncthreads();
+        K5_SUB(3, kNthBatch == 8);
     }
 }
 
 // ---------------------------------------------------------------- single-wave tail
 // The same step by one wave on an LDS range of <= kNthWave entries: no workgroup barrier.
 __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, int64_t f, int64_t l) {
+    constexpr int kTiles = kNthWave / 256 + 1;   // the range <= kNthWave, from a base <= a0
     const int lane = threadIdx.x & 63;
     const uint32_t P = qkey(q[f]);
-    const int64_t a0 = f + 1;
-    uint32_t cr = 0;
-    for (int64_t t0 = a0; t0 < l; t0 += 256) {
-        uint64_t x[4];
-        uint32_t valid, pl, pr;
-        nth_load4(q, t0 + 4 * lane, l, x, valid);
-        stopper_masks(x, valid, P, pl, pr);
-        cr += __popc(pr);
+    const int64_t a0 = f + 1, base = nth_base(q, a0);
+    uint32_t TR = 0, m[kTiles];
+#pragma unroll
+    for (int u = 0; u < kTiles; ++u) {
+        const int64_t t0 = base + 256 * u;
+        m[u] = 0;
+        if (t0 < l) {
+            uint64_t x[4];
+            uint32_t valid, pl, pr;
+            nth_load4(q, t0 + 4 * lane, a0, l, x, valid);
+            stopper_masks(x, valid, P, pl, pr);
+            TR += wave_count4(pr);
+            m[u] = pl | (pr << 4);
+        }
     }
-    const uint32_t TR = wave_sum(cr);
-    uint32_t runl = 0, runr = 0, paired = 0;
-    unsigned long long lnext = ~0ull, rmin = ~0ull;
-    for (int64_t t0 = a0; t0 < l; t0 += 256) {
-        uint64_t x[4];
-        uint32_t valid;
-        nth_load4(q, t0 + 4 * lane, l, x, valid);
-        pair_tile(x, valid, P, t0 + 4 * lane, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+    uint32_t runl = 0, runr = 0, s = 0;
+    int64_t lnext = INT64_MAX, rmin = INT64_MAX;
+#pragma unroll
+    for (int u = 0; u < kTiles; ++u) {
+        const int64_t t0 = base + 256 * u;
+        if (t0 < l) pair_tile<true>(m[u] & 15u, m[u] >> 4, t0, f, TR, runl, runr, lpos, rpos, s, lnext, rmin);
     }
-    const uint32_t s = wave_sum(paired);
-    lnext = wave_min_u64(lnext);
-    rmin = wave_min_u64(rmin);
     wave_sync();   // the pair slots are written
-    for (uint32_t t = lane; t < s; t += kWave) {
-        const int64_t li = f + lpos[t], ri = f + rpos[t];
-        const uint64_t a = q[li], b = q[ri];
-        q[li] = b;
-        q[ri] = a;
-    }
+    nth_swaps<2>(q, lpos, rpos, f, s, lane, kWave);
     wave_sync();   // the swaps are done
-    const int64_t rs = s ? (int64_t)rmin : l;
-    const int64_t ln = lnext == ~0ull ? INT64_MAX : (int64_t)lnext;
-    return ln < rs ? ln : rs;
+    const int64_t rs = s ? rmin : l;
+    return lnext < rs ? lnext : rs;
 }
 
 // Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
@@ -384,7 +536,8 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
             return;
         }
         depth -= 1;
-        if (lane == 0) nth_median(q, f, l);
+        K5_STEP(2);
+        if (lane == 0) (void)nth_median(q, f, l);
         wave_sync();
         const int64_t cut = nth_step_wave(q, lpos, rpos, f, l);
         if (cut <= nth)
@@ -401,8 +554,9 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
 // above kNthLds. Returns after a final barrier.
 __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r) {
     __shared__ NthShared sh;
-    __shared__ uint64_t lq[kNthLds];
+    __shared__ __align__(16) uint64_t lq[kNthLds];
     __shared__ uint32_t llp[kNthLds / 2 + 1], lrp[kNthLds / 2 + 1];
+    __shared__ uint8_t lmk[(kNthLds / 256 + 1) * 64];   // LDS phase stopper bytes
     if (threadIdx.x == 0) {
         sh.f = 0;
         sh.l = n;
@@ -411,7 +565,15 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     }
     __syncthreads();
     if (n <= 0 || nth >= n) return;
-    nth_loop_wg(q, gpos_l, gpos_r, sh, nth, kNthLds);                 // global phase
+    K5_STAMP(0);
+    // global phase: lq (unused until the LDS phase) holds the stopper bytes and, in its
+    // last 16 KB, the waves' pair-slot staging areas
+    constexpr int64_t kStageBytes = kNthWaves * 512 * 4;
+    static_assert(sizeof(lq) > kStageBytes, "K5: LDS staging");
+    nth_loop_wg<8, 8>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<uint8_t*>(lq),
+                      (int64_t)((sizeof(lq) - kStageBytes) / 64),
+                      reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lq) + sizeof(lq) - kStageBytes));
+    K5_STAMP(1);
     if (sh.heap_exit) return;
     const int64_t f = sh.f, m = sh.l - sh.f;                          // <= kNthLds entries left
     for (int64_t i = threadIdx.x; i < m; i += kNthThreads) lq[i] = q[f + i];
@@ -421,11 +583,15 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
         sh.l = m;
     }
     __syncthreads();
-    nth_loop_wg(lq, llp, lrp, sh, nth - f, kNthWave);                  // LDS phase, all waves
+    K5_STAMP(2);
+    nth_loop_wg<1, 2>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthLds / 256 + 1, nullptr);   // LDS phase
+    K5_STAMP(3);
     if (!sh.heap_exit && threadIdx.x < kWave) nth_tail_wave(lq, llp, lrp, sh, nth - f);   // one wave
     __syncthreads();
+    K5_STAMP(4);
     for (int64_t i = threadIdx.x; i < m; i += kNthThreads) q[f + i] = lq[i];
     __syncthreads();
+    K5_STAMP(5);
 }
 
 }  // namespace dgc

@@ -1982,6 +1982,18 @@ extern "C" int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt
                                       static_cast<hipStream_t>(stream));
 }
 
+#ifdef DGC_K5_PROF
+extern "C" int dgc_k5_prof(void* out, int reset) {
+    if (reset) {
+        dgc::K5Prof z{};
+        DGC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dgc::g_k5prof), &z, sizeof(z)));
+        return DGC_OK;
+    }
+    DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_k5prof), sizeof(dgc::K5Prof)));
+    return DGC_OK;
+}
+#endif
+
 extern "C" int dgc_compress_flush(float* vec, float* mmt, int64_t sample_stride, const dgc_select_params* params,
                                   void* ws, size_t ws_bytes, void* stream) {
     return dgc::compress_flush(vec, mmt, sample_stride, params, ws, ws_bytes, static_cast<hipStream_t>(stream));
