@@ -260,43 +260,32 @@ __device__ __forceinline__ uint32_t first_in_tile(const uint64_t (&m)[4]) {
 // unswapped left stopper), rmin (smallest swapped right stopper); INT64_MAX = none.
 // BALLOT: accumulated wave-uniformly from ballots (a few tiles: no reduction after);
 // else per lane, for the caller to reduce once after many tiles.
-// STAGE (pair slots in global memory): the tile's swapped left stoppers have the
-// consecutive ranks runl.. and its swapped right stoppers the consecutive ranks from
-// TR - runr - tr up, so they go through the wave's LDS area stg (2 x 256 slots) and
-// leave in coalesced stores — ~2 per tile instead of 8 exec-masked scattered ones
-// (which held the pass on the vector-memory counter).
-template <bool BALLOT, bool STAGE = false>
+template <bool BALLOT>
 __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile, int64_t f, uint32_t TR,
                                           uint32_t& runl, uint32_t& runr, uint32_t* lpos, uint32_t* rpos,
-                                          uint32_t& paired, int64_t& lnext, int64_t& rmin, uint32_t* stg = nullptr) {
+                                          uint32_t& paired, uint32_t& lnext, uint32_t& rmin) {
+    // positions relative to f (32-bit: a range is < 2^32 entries); lnext / rmin too,
+    // UINT32_MAX = none
     const int lane = threadIdx.x & 63;
+    const uint32_t rel0 = (uint32_t)(tile - f) + 4u * (uint32_t)lane;
     uint32_t bl, tl, br, tr;
     wave_prefix4(pl, bl, tl);
     wave_prefix4(pr, br, tr);
     uint32_t rl = runl + bl;   // left stoppers before this element
     uint32_t rr = runr + br;   // right stoppers in [f+1, this element)
-    const uint32_t ulow = TR - runr - tr;   // the tile's smallest right-stopper rank
     uint64_t msl[4], mln[4], msr[4];
-    uint32_t nsl = 0, nsr = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const bool isl = (pl >> j) & 1u, isr = (pr >> j) & 1u;
-        const int64_t i = tile + 4 * lane + j;
+        const uint32_t i = rel0 + (uint32_t)j;
         const uint32_t rr_incl = rr + (isr ? 1u : 0u);
         // L_{rl+1} = i is swapped iff #(key >= P in (i, l)) >= rl + 1
         const bool swl = isl && TR - rr_incl >= rl + 1;
         // R_{u+1} = i with u = #(key >= P in (i, l)); swapped iff #(key <= P in [f+1, i)) >= u + 1
         const uint32_t u = TR - rr_incl;
         const bool swr = isr && rl >= u + 1;
-        if (STAGE) {
-            if (swl) stg[rl - runl] = (uint32_t)(i - f);
-            if (swr) stg[256 + (u - ulow)] = (uint32_t)(i - f);
-            nsl += (uint32_t)__popcll(__ballot(swl));
-            nsr += (uint32_t)__popcll(__ballot(swr));
-        } else {
-            if (swl) lpos[rl] = (uint32_t)(i - f);
-            if (swr) rpos[u] = (uint32_t)(i - f);
-        }
+        if (swl) lpos[rl] = i;
+        if (swr) rpos[u] = i;
         if (BALLOT) {
             msl[j] = __ballot(swl);
             mln[j] = __ballot(isl && !swl);
@@ -312,23 +301,18 @@ __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile
     if (BALLOT) {
         paired += (uint32_t)(__popcll(msl[0]) + __popcll(msl[1]) + __popcll(msl[2]) + __popcll(msl[3]));
         const uint32_t el = first_in_tile(mln), er = first_in_tile(msr);
-        if (el < 256 && tile + el < lnext) lnext = tile + el;
-        if (er < 256 && tile + er < rmin) rmin = tile + er;
-    }
-    if (STAGE && (nsl | nsr)) {
-        wave_sync();
-        for (uint32_t k = lane; k < nsl; k += 64) lpos[runl + k] = stg[k];
-        for (uint32_t k = lane; k < nsr; k += 64) rpos[ulow + k] = stg[256 + k];
-        wave_sync();   // the next tile may overwrite stg
+        const uint32_t t32 = (uint32_t)(tile - f);
+        if (el < 256 && t32 + el < lnext) lnext = t32 + el;
+        if (er < 256 && t32 + er < rmin) rmin = t32 + er;
     }
     runl += tl;
     runr += tr;
 }
 
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const int64_t a = __shfl_xor(v, o);
+        const uint32_t a = __shfl_xor(v, o);
         v = a < v ? a : v;
     }
     return v;
@@ -351,7 +335,7 @@ struct NthShared {
 // mk_tiles, so pass 2 reads bytes instead of the entries; otherwise it reloads them.
 template <int kNthBatch, int kSwapBatch>
 __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, uint8_t* mk,
-                            int64_t mk_tiles, uint32_t* stage) {
+                            int64_t mk_tiles) {
     const int64_t f = sh.f, l = sh.l;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t P = sh.pivot;
@@ -394,15 +378,8 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
         TR += b;
     }
     // pass 2: ranks, pairing, paired positions
-    uint32_t paired = 0;
-    int64_t lnext = INT64_MAX, rmin = INT64_MAX;
-    uint32_t* stg = stage ? stage + wv * 512 : nullptr;
-    if (keep && stg) {
-        for (int64_t t0 = wb; t0 < we; t0 += 256) {
-            const uint32_t m = mk[((t0 - base) >> 8) * 64 + lane];
-            pair_tile<false, true>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin, stg);
-        }
-    } else if (keep) {
+    uint32_t paired = 0, lnext = UINT32_MAX, rmin = UINT32_MAX;
+    if (keep) {
         for (int64_t t0 = wb; t0 < we; t0 += 256) {
             const uint32_t m = mk[((t0 - base) >> 8) * 64 + lane];
             pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
@@ -417,21 +394,17 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
             for (int b = 0; b < kNthBatch; ++b) {
                 uint32_t pl, pr;
                 stopper_masks(x[b], valid[b], P, pl, pr);
-                if (stg)
-                    pair_tile<false, true>(pl, pr, t0 + b * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin,
-                                           stg);
-                else
-                    pair_tile<false>(pl, pr, t0 + b * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+                pair_tile<false>(pl, pr, t0 + b * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
             }
         }
     }
     paired = wave_sum(paired);
-    lnext = wave_min_i64(lnext);
-    rmin = wave_min_i64(rmin);
+    lnext = wave_min_u32(lnext);
+    rmin = wave_min_u32(rmin);
     if (lane == 0) {
         if (paired) atomicAdd(&sh.s, paired);
-        if (lnext != INT64_MAX) atomicMin(&sh.l_next, (unsigned long long)lnext);
-        if (rmin != INT64_MAX) atomicMin(&sh.r_min, (unsigned long long)rmin);
+        if (lnext != UINT32_MAX) atomicMin(&sh.l_next, (unsigned long long)(f + lnext));
+        if (rmin != UINT32_MAX) atomicMin(&sh.r_min, (unsigned long long)(f + rmin));
     }
     __syncthreads();
     K5_SUB(1, kNthBatch == 8);
@@ -458,7 +431,7 @@ __device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop
 // `stop` entries; ends with a barrier, sh.f/l/depth updated or sh.heap_exit set.
 template <int kNthBatch, int kSwapBatch>
 __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth,
-                            int64_t stop, uint8_t* mk, int64_t mk_tiles, uint32_t* stage) {
+                            int64_t stop, uint8_t* mk, int64_t mk_tiles) {
     // thread 0 prepares a step: depth check, median, reset of the step's results
     auto prepare = [&]() -> bool {
         if (sh.l - sh.f <= stop) return false;
@@ -479,7 +452,7 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     __syncthreads();
     while (go) {
         K5_STEP(stop == kNthLds ? 0 : 1);
-        nth_step_wg<kNthBatch, kSwapBatch>(q, lpos, rpos, sh, mk, mk_tiles, stage);
+        nth_step_wg<kNthBatch, kSwapBatch>(q, lpos, rpos, sh, mk, mk_tiles);
         K5_SUB_BEGIN();
         if (threadIdx.x == 0) {
             nth_advance(q, sh, nth, stop);
@@ -511,8 +484,7 @@ __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, in
             m[u] = pl | (pr << 4);
         }
     }
-    uint32_t runl = 0, runr = 0, s = 0;
-    int64_t lnext = INT64_MAX, rmin = INT64_MAX;
+    uint32_t runl = 0, runr = 0, s = 0, lnext = UINT32_MAX, rmin = UINT32_MAX;
 #pragma unroll
     for (int u = 0; u < kTiles; ++u) {
         const int64_t t0 = base + 256 * u;
@@ -521,8 +493,9 @@ __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, in
     wave_sync();   // the pair slots are written
     nth_swaps<2>(q, lpos, rpos, f, s, lane, kWave);
     wave_sync();   // the swaps are done
-    const int64_t rs = s ? rmin : l;
-    return lnext < rs ? lnext : rs;
+    const int64_t rs = s ? f + (int64_t)rmin : l;
+    const int64_t ln = lnext == UINT32_MAX ? INT64_MAX : f + (int64_t)lnext;
+    return ln < rs ? ln : rs;
 }
 
 // Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
@@ -566,13 +539,9 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     __syncthreads();
     if (n <= 0 || nth >= n) return;
     K5_STAMP(0);
-    // global phase: lq (unused until the LDS phase) holds the stopper bytes and, in its
-    // last 16 KB, the waves' pair-slot staging areas
-    constexpr int64_t kStageBytes = kNthWaves * 512 * 4;
-    static_assert(sizeof(lq) > kStageBytes, "K5: LDS staging");
+    // global phase: lq (unused until the LDS phase) holds the stopper bytes
     nth_loop_wg<8, 8>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<uint8_t*>(lq),
-                      (int64_t)((sizeof(lq) - kStageBytes) / 64),
-                      reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lq) + sizeof(lq) - kStageBytes));
+                      (int64_t)(sizeof(lq) / 64));
     K5_STAMP(1);
     if (sh.heap_exit) return;
     const int64_t f = sh.f, m = sh.l - sh.f;                          // <= kNthLds entries left
@@ -584,7 +553,7 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     }
     __syncthreads();
     K5_STAMP(2);
-    nth_loop_wg<1, 2>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthLds / 256 + 1, nullptr);   // LDS phase
+    nth_loop_wg<1, 2>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthLds / 256 + 1);   // LDS phase
     K5_STAMP(3);
     if (!sh.heap_exit && threadIdx.x < kWave) nth_tail_wave(lq, llp, lrp, sh, nth - f);   // one wave
     __syncthreads();
