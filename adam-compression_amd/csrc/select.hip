@@ -961,6 +961,111 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     }
 }
 
+// The "lower" recounts served by the K1 candidate lists: the counts at the first
+// kLowerLists thresholds t_j that are >= t_list, from the complete lists (a spilled
+// segment is re-read by a wave). When one of them reaches lower*k, the first such j
+// is the reference's j* and k_lower_counts' pass over vec is skipped; otherwise the
+// counts are cleared and k_lower_counts recounts every t_j over vec. One thread per
+// segment, like k_count_lists.
+constexpr int kLowerLists = 4;
+
+__global__ void __launch_bounds__(kBlock)
+k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
+    const int t = task(w, BT_SEG, blockIdx.x);
+    SelState* st = w.st + t;
+    if (!st->lower_pending) return;
+    float th[kLowerLists + 1];
+    th[0] = st->t_cur;
+#pragma unroll
+    for (int j = 1; j <= kLowerLists; ++j) th[j] = __fmul_rn(th[j - 1], p.lower);
+    const float tl = st->t_list;
+    int ms = 0;   // thresholds t_1..t_ms are served by the lists (uniform per tensor)
+#pragma unroll
+    for (int j = 1; j <= kLowerLists; ++j)
+        if (j <= p.max_iters && th[j] >= tl) ms = j;
+    if (ms == 0) return;
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const float* vec = vec_flat + d.off;
+    __shared__ int spill[kBlock];
+    __shared__ int nspill;
+    __shared__ uint32_t bsum[kLowerLists + 1];
+    if (threadIdx.x == 0) nspill = 0;
+    if (threadIdx.x <= kLowerLists) bsum[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_SEG][t]) * kBlock;
+    const int64_t ls = lseg0 + threadIdx.x;
+    uint32_t c[kLowerLists + 1];
+#pragma unroll
+    for (int j = 0; j <= kLowerLists; ++j) c[j] = 0;
+    if (ls < d.nseg) {
+        const int64_t seg = d.seg0 + ls;
+        const uint32_t lc = w.seg_lcnt[seg];
+        if (lc <= (uint32_t)kCap) {
+            const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
+            float4 v[kCap / 4];
+#pragma unroll
+            for (int q = 0; q < kCap / 4; ++q)   // all loads issued before any use
+                if ((uint32_t)(4 * q) < lc) v[q] = l4[q];
+#pragma unroll
+            for (int q = 0; q < kCap / 4; ++q) {
+                const uint32_t e = 4 * q;
+                const float a[4] = {fabsf(v[q].x), fabsf(v[q].y), fabsf(v[q].z), fabsf(v[q].w)};
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (e + r < lc) {
+#pragma unroll
+                        for (int j = 1; j <= kLowerLists; ++j) c[j] += (j <= ms) && a[r] >= th[j];
+                    }
+            }
+        } else {
+            spill[atomicAdd(&nspill, 1)] = threadIdx.x;
+        }
+    }
+#pragma unroll
+    for (int j = 1; j <= kLowerLists; ++j) {
+        const uint32_t v = wave_sum(c[j]);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&bsum[j], v);
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    for (int q = wave; q < nspill; q += kSegPerBlock4) {
+        float x[kSegTiles][4];
+        uint32_t valid[kSegTiles];
+        load_segment(vec, d.n, lseg0 + spill[q], x, valid);
+        for (int j = 1; j <= ms; ++j) {
+            uint32_t cs = 0;
+#pragma unroll
+            for (int u = 0; u < kSegTiles; ++u) cs += __popc(ge_mask(x[u], valid[u], th[j]));
+            cs = wave_sum(cs);
+            if ((threadIdx.x & 63) == 0 && cs) atomicAdd(&bsum[j], cs);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x >= 1 && threadIdx.x <= ms && bsum[threadIdx.x])
+        atomicAdd(&st->lower_cnt[threadIdx.x], (unsigned long long)bsum[threadIdx.x]);
+    const uint32_t nb = (uint32_t)(w.bt[BT_SEG][t + 1] - w.bt[BT_SEG][t]);
+    if (!last_block_arrival(&st->tickets[2], nb)) return;
+    if (threadIdx.x == 0) {
+        int js = 0;
+        for (int j = 1; j <= ms; ++j) {
+            if ((long long)load_count(&st->lower_cnt[j]) >= d.lower_count) {
+                js = j;
+                break;
+            }
+        }
+        if (js) {
+            st->t_cur = th[js];
+            st->iter = js;
+            st->recounts = js;
+            st->overflow = 0;
+            st->lower_pending = 0;
+            st->active = 1;   // count pass + decide at t_{j*}
+        } else {
+            for (int j = 1; j <= ms; ++j) st->lower_cnt[j] = 0;   // k_lower_counts recounts every t_j
+        }
+    }
+}
+
 // ------------------------------------------------------------------ resample (partial_sort path)
 // Candidate keys (|x| >= t_cur) for the resample radix select: the segment list
 // when complete, a re-read of vec when it spilled. One wave per segment.
@@ -1214,7 +1319,7 @@ __device__ void emit_reread_resample(const float* __restrict__ vec, const TDesc&
 // writes). o.queue != null: K5's candidate gather — every element >= t_cur, ascending
 // (the reference's `indices` before its resample topk), only when K5 serves the tensor.
 constexpr int kEmitThreads = kGroupSegs;
-constexpr int kEmitBatch = 8;
+constexpr int kEmitBatch = 16;
 constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
 static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
 
@@ -1439,6 +1544,9 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         return DGC_OK;
     };
     auto lower = [&]() -> int {
+        // the lists first (most lowers end within their range), then vec if needed
+        hipLaunchKernelGGL(k_lower_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w, p);
+        DGC_LAUNCHED();
         const unsigned grid = (unsigned)L.grid[BT_CAP4];
         if (al)
             hipLaunchKernelGGL(k_lower_counts<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
