@@ -206,6 +206,35 @@ int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n,
 
 }  // namespace dgc
 
+// Ceiling probe for K1's access mix: three 16-B non-temporal reads and two 16-B
+// non-temporal writes per float4, one-shot 256-thread blocks — K1's memory shape
+// with no arithmetic to speak of. The bench runs it on its own buffers after the
+// timed steps to measure what the box it landed on streams (boxes differ by ~10 %).
+__global__ void __launch_bounds__(dgc::kBlock)
+k_probe_3r2w(const float4* __restrict__ a, const float4* __restrict__ b, const float4* __restrict__ c,
+             float4* __restrict__ d, float4* __restrict__ e, int64_t n4) {
+    const int64_t v = (int64_t)blockIdx.x * dgc::kBlock + threadIdx.x;
+    if (v >= n4) return;
+    const float4 x = dgc::ld_nt(a + v), y = dgc::ld_nt(b + v), z = dgc::ld_nt(c + v);
+    dgc::st_nt(d + v, make_float4(x.x + z.x, x.y + z.y, x.z + z.z, x.w + z.w));
+    dgc::st_nt(e + v, make_float4(y.x + z.x, y.y + z.y, y.z + z.z, y.w + z.w));
+}
+
+extern "C" int dgc_hbm_probe(const float* a, const float* b, const float* c, float* d, float* e, int64_t n,
+                             void* stream) {
+    if (!a || !b || !c || !d || !e || n < 4) DGC_FAIL(DGC_ERR_INVALID, "dgc_hbm_probe: bad arguments");
+    if (!dgc::aligned16(a) || !dgc::aligned16(b) || !dgc::aligned16(c) || !dgc::aligned16(d) || !dgc::aligned16(e))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_hbm_probe: buffers must be 16-B aligned");
+    const int64_t n4 = n / 4;
+    if (dgc::ceil_div(n4, (int64_t)dgc::kBlock) > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_hbm_probe: n too large");
+    hipLaunchKernelGGL(k_probe_3r2w, dim3((unsigned)dgc::ceil_div(n4, (int64_t)dgc::kBlock)), dim3(dgc::kBlock), 0,
+                       static_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(a),
+                       reinterpret_cast<const float4*>(b), reinterpret_cast<const float4*>(c),
+                       reinterpret_cast<float4*>(d), reinterpret_cast<float4*>(e), n4);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
 extern "C" int dgc_compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n,
                               float momentum, int32_t nesterov, int32_t accumulate, float* samples,
                               int64_t sample_start, int64_t sample_stride, int64_t num_samples,

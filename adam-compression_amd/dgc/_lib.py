@@ -99,6 +99,7 @@ _SIGNATURES = {
                                                 _SZ, _P]),
     "dgc_batch_compress_finish": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _P, _P, _SZ, _I32, _P]),
     "dgc_batch_flush": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _SZ, _P]),
+    "dgc_hbm_probe": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),
     "dgc_sgd_step": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                     ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _P]),
 }

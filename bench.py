@@ -246,6 +246,9 @@ class FlatRun:
     def k1_bytes(self):
         return 20 * self.N + 4 * self.b.cnt    # read g, mmt, vec; write mmt, vec; write the samples
 
+    def probe_buffers(self):
+        return [self.grads[0], self.grads[1], self.out], [self.b._mmt, self.b._vec]
+
     def info(self):
         return self.b.last_info()
 
@@ -311,6 +314,10 @@ class ModelRun:
                                          self.n_dense, 0.9, int(self.nesterov), 0, None, 0, 1, 0,
                                          self._lib.stream_of(g.device)), "dgc_compensate")
 
+    def probe_buffers(self):
+        b = self.b
+        return [self.grads[0][0], self.grads[1][0], b.out_flat], [b._mmt_flat, b._vec_flat]
+
     def k1_bytes(self):
         # every compressed tensor: read g, mmt, vec; write mmt, vec; plus the samples written
         return 20 * self.n_comp + 4 * sum(a[1] + 1 for a in self.b.attrs if a[1] != 0)
@@ -327,6 +334,32 @@ class ModelRun:
     def config(self):
         return {"compressed_tensors": len(self.b.names), "compressed_elements": self.n_comp,
                 "dense_elements": self.n_dense, "num_selects_total": self.b.capacity}
+
+
+def hbm_probe(reads, writes, reps=5):
+    """This box's streaming rate for K1's access mix, measured in the same run:
+    dgc_hbm_probe (3 non-temporal 16-B reads + 2 writes per float4, one-shot blocks,
+    K1's shape without its arithmetic) over the workload's own buffers after the timed
+    steps, HIP events on the stream it runs on, best of ``reps``. MI355X boxes differ
+    by ~10 % (the same library ran K1 in 3.29 and 3.68 ms on two boxes,
+    tools/ab_k1.py), so K1 is also reported as a fraction of this."""
+    from dgc import _lib
+    L = _lib.lib()
+    n = min(t.numel() for t in reads + writes)
+    dev = reads[0].device
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.check(L.dgc_hbm_probe(*(t.data_ptr() for t in reads), *(t.data_ptr() for t in writes), n,
+                                   _lib.stream_of(dev)), "dgc_hbm_probe")
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1)
+        best = t if best is None else min(best, t)
+    nbytes = 20 * (n // 4) * 4
+    return {"kind": "dgc_hbm_probe: K1's access shape, 3 reads + 2 writes of 16 B per float4", "bytes": nbytes,
+            "ms": best, "GBs": nbytes / (best * 1e-3) / 1e9}
 
 
 def step_bytes(run, world, full_passes):
@@ -387,6 +420,7 @@ def main():
         elapsed = t.item()
     ms = {p: sum(e[p][0].elapsed_time(e[p][1]) for e in evs) / args.steps for p in timed}
     info = run.info()
+    probe = hbm_probe(*run.probe_buffers())   # after the timed steps: overwrites the state
     ms_step = elapsed * 1e3 / args.steps
     full_passes = info.get("full_passes", 0)
     contract, required = step_bytes(run, world, full_passes)
@@ -431,6 +465,8 @@ def main():
                      "frac_of_8TBs": required / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "contract_frac_of_8TBs": contract / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "frac_of_measured_copy": required / (ms_step * 1e-3) / 1e9 / HBM_COPY_GBS},
+        "hbm_probe": dict(probe, k1_frac_of_probe=k1_gbs / probe["GBs"],
+                          step_frac_of_probe=required / (ms_step * 1e-3) / 1e9 / probe["GBs"]),
         "phase_ms": {p: round(v, 4) for p, v in ms.items()},
         "compensate_ms_per_step": [round(e["compensate"][0].elapsed_time(e["compensate"][1]), 3) for e in evs],
         "selection": info,

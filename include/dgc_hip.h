@@ -284,6 +284,12 @@ int dgc_fill_zero(float* grad, int64_t n, void* stream);
  * Reads 4 bytes from the workspace (synchronous). */
 int dgc_decompress_status(const void* ws, int32_t* status, void* stream);
 
+/* Measurement only (bench.py): K1's memory shape — d = a + c, e = b + c over n
+ * floats (n/4 float4; 16-B aligned buffers), three non-temporal 16-B reads and two
+ * non-temporal 16-B writes per float4 — to measure the streaming rate of the box at
+ * hand next to K1. Not part of the reference's interface. */
+int dgc_hbm_probe(const float* a, const float* b, const float* c, float* d, float* e, int64_t n, void* stream);
+
 /* ---- K7: DGCSGD.step over `count` parameters of one group (dgc/optim/sgd.py:42-68) ----
  * params[i], grads[i] (and bufs[i], the momentum_buffer, when weight_decay != 0 and
  * momentum != 0) are fp32 device arrays of numels[i] elements; first[i] = 1 when the
