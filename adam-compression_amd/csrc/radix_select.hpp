@@ -47,17 +47,21 @@ __host__ __device__ constexpr uint32_t rs_pmask(int pass) {
 __host__ __device__ constexpr int rs_bins(int pass) { return pass == 2 ? 1024 : 2048; }
 
 // The task served by block b, from an ascending prefix table blk[0..T] of block counts
-// (blk[T] = grid): the largest t with blk[t] <= b. Every thread computes the same t.
+// (blk[T] = grid, blk[0] = 0): the largest t with blk[t] <= b = (#entries <= b) - 1.
+// Each wave counts 64 entries per load with a ballot — one round trip for T <= 64
+// where a binary search is log2(T) dependent ones, paid at the start of every block
+// of every batched launch. Call from whole waves; every lane gets the same t.
 __device__ __forceinline__ int task_of_block(const int32_t* blk, int T, int b) {
-    int lo = 0, hi = T - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (blk[mid] <= b)
-            lo = mid;
-        else
-            hi = mid - 1;
+    if (T <= 1) return 0;
+    const int lane = threadIdx.x & 63;
+    int cnt = 0;
+    for (int i0 = 0; i0 < T; i0 += 64) {
+        const int i = i0 + lane;
+        const uint64_t m = __ballot(i < T && blk[i] <= b);
+        cnt += __popcll(m);
+        if (m != ~0ull) break;   // ascending table: every later entry is > b
     }
-    return lo;
+    return __builtin_amdgcn_readfirstlane(cnt - 1);
 }
 
 // Strided visit of n floats' keys by the `nb` blocks of one task (lb = block index in the task).

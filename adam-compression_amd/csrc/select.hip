@@ -1217,10 +1217,16 @@ __device__ __forceinline__ long long final_count(const SelState& s, int64_t k) {
 }
 
 // Output position of a tensor's first entry: the entries of the tensors before it.
+// The payload position of tensor t's first entry: the final counts of the tensors
+// before it, summed by one wave (all loads in flight at once — a serial loop over 50
+// tensors was 50 dependent round trips). Call from a whole wave; every lane gets it.
 __device__ __forceinline__ long long out_base(const SelWS& w, int t) {
     long long b = 0;
-    for (int u = 0; u < t; ++u) b += final_count(w.st[u], w.td[u].k);
-    return b;
+    for (int u0 = 0; u0 < t; u0 += kWave) {
+        const int u = u0 + (int)(threadIdx.x & 63);
+        b += u < t ? final_count(w.st[u], w.td[u].k) : 0;
+    }
+    return wave_sum(b);
 }
 
 // pos: output slot; li: the element's index within its tensor (d.off + li in the flat buffers).
@@ -1340,7 +1346,10 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs], lcn[kGroupSegs];
     __shared__ uint64_t lds16[16];
     __shared__ long long obase_s;
-    if (threadIdx.x == 0) obase_s = k5 ? 0 : out_base(w, t);
+    if (threadIdx.x < kWave) {
+        const long long b = k5 ? 0 : out_base(w, t);
+        if (threadIdx.x == 0) obase_s = b;
+    }
     const long long limit = k5 ? st->n_cur : st->limit;
     const long long T = st->tie_quota;
     const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
@@ -1434,7 +1443,10 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
     if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     __shared__ long long obase_s;
-    if (threadIdx.x == 0) obase_s = out_base(w, t);
+    if (threadIdx.x < kWave) {
+        const long long b = out_base(w, t);
+        if (threadIdx.x == 0) obase_s = b;
+    }
     __syncthreads();
     const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
     if (q >= d.k) return;

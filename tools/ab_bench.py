@@ -1,0 +1,31 @@
+"""Same-box A/B of whole bench steps: `python tools/ab_bench.py WORKLOAD LIB_A LIB_B [reps]`
+runs `bench.py --workload WORKLOAD --no-cpu` with DGC_HIP_LIB = each library in turn,
+alternating `reps` times, and prints ms/step, K1 ms and the phase times per run (MI355X
+boxes differ by ~10 %, so only same-box comparisons mean anything). Both libraries must
+export the symbols dgc/_lib.py binds (build the other one from a nearby revision:
+`make -C <old csrc> OUT_DIR=<repo>/adam-compression_amd/lib/ab_old`)."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    wl, libs = sys.argv[1], sys.argv[2:4]
+    reps = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    for _ in range(reps):
+        for lib in libs:
+            env = dict(os.environ, DGC_HIP_LIB=os.path.abspath(lib))
+            out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--workload", wl, "--no-cpu",
+                                  "--steps", "20", "--warmup", "5"], env=env, check=True, capture_output=True,
+                                 text=True).stdout
+            d = json.loads(out.strip().splitlines()[-1])
+            print(json.dumps({"lib": lib, "ms_per_step": round(d["ms_per_step"], 4),
+                              "k1_ms": round(d["roofline"]["avg_launch_ms"], 4), "phase_ms": d["phase_ms"]}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
