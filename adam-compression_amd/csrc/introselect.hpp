@@ -525,9 +525,11 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
 // std::nth_element(q, q + nth, q + n, comp) in place, by the calling 512-thread
 // workgroup. gpos_l/gpos_r: global pair slots (>= n / 2 + 1 each) for the ranges
 // above kNthLds. Returns after a final barrier.
-__device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r) {
+// lq: the caller's LDS area of kNthLds entries (16-B aligned): the partition range
+// in the LDS phase, the stopper bytes in the global phase.
+__device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r,
+                               uint64_t* lq) {
     __shared__ NthShared sh;
-    __shared__ __align__(16) uint64_t lq[kNthLds];
     __shared__ uint32_t llp[kNthLds / 2 + 1], lrp[kNthLds / 2 + 1];
     __shared__ uint8_t lmk[(kNthLds / 256 + 1) * 64];   // LDS phase stopper bytes
     if (threadIdx.x == 0) {
@@ -541,7 +543,7 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     K5_STAMP(0);
     // global phase: lq (unused until the LDS phase) holds the stopper bytes
     nth_loop_wg<8, 8>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<uint8_t*>(lq),
-                      (int64_t)(sizeof(lq) / 64));
+                      (int64_t)(kNthLds * sizeof(uint64_t) / 64));
     K5_STAMP(1);
     if (sh.heap_exit) return;
     const int64_t f = sh.f, m = sh.l - sh.f;                          // <= kNthLds entries left

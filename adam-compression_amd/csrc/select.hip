@@ -62,6 +62,9 @@ constexpr int kSpillShards = 64;
 constexpr int kSpillDiv = 32;                   // lists dropped when > nseg/32 segments spill
 constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgroup
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole batch
+constexpr int kHeapMax = 4096;                  // K5b: exact partial_sort replay up to this k (heap in LDS)
+constexpr int kHeapThreads = 512;                // = kNthThreads: K5b runs inside k_nth_select
+constexpr int kHeapPer = 16;                    // K5b: consecutive elements per thread per chunk
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
 
@@ -92,7 +95,8 @@ struct SelState {
     long long tie_quota;   // RESAMPLE: k - n_greater ties, lowest index first
     int32_t resample_pending, overflow, done, lower_pending;
     int32_t full_passes, list_spills, epoch;
-    int32_t rs_nth;        // RESAMPLE served by the exact nth_element replay (K5)
+    int32_t rs_nth;        // RESAMPLE: 1 = exact nth_element replay (K5), 2 = exact
+                           // partial_sort replay (K5b), 0 = radix + lowest-index ties
     int32_t tie_rule;      // DGC_TIES_*: how the resample chose among boundary ties
     // Deferred momentum masking (DGCSGDMemory.update, dgc/memory.py:72-77): the last
     // call emitted "the first def_limit elements >= def_t" without zeroing them; the
@@ -846,7 +850,10 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
                     if (cnt < 64 * k && cnt <= d.cand_cap) {   // torch's nth_element path: replayed
                         st->rs_nth = 1;
                         st->tie_rule = DGC_TIES_EXACT;
-                    } else {                                    // partial_sort path: lowest-index ties
+                    } else if (k <= kHeapMax && d.n <= 0xFFFFFFFFLL) {   // partial_sort path: replayed
+                        st->rs_nth = 2;
+                        st->tie_rule = DGC_TIES_EXACT;
+                    } else {                                    // partial_sort path, large k: lowest-index ties
                         st->resample_pending = 1;
                         st->tie_rule = DGC_TIES_LOWEST_INDEX;
                         reset_rs = 1;
@@ -1333,7 +1340,8 @@ __global__ void __launch_bounds__(kEmitThreads)
 k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const int t = task(w, BT_GRP, blockIdx.x);
     const SelState* st = w.st + t;
-    const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth;
+    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
+    const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
     if (k5 != (o.queue != nullptr)) return;
     const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -1423,24 +1431,14 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     }
 }
 
-// K5: the reference's resample topk replayed on the gathered candidates
-// (introselect.hpp), one workgroup per tensor.
-__global__ void __launch_bounds__(kNthThreads) k_nth_select(SelWS w) {
-    const int t = blockIdx.x;
-    const SelState* st = w.st + t;
-    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    uint32_t* gl = w.gpos + d.gpos_off;
-    uint32_t* gr = gl + d.cand_cap / 2 + 1;
-    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr);
-}
+
 
 // K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
 // wire casts and the masking of DGCSGDMemory.update.
 __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const int t = task(w, BT_QUEUE, blockIdx.x);
     const SelState* st = w.st + t;
-    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth)) return;
+    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1)) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     __shared__ long long obase_s;
     if (threadIdx.x < kWave) {
@@ -1453,6 +1451,126 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
     const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
     const int64_t li = w.cand_idx[d.cand_off + j];
     emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
+}
+
+// K5b: torch's CPU topk on its partial_sort path (k * 64 <= candidates, i.e. a sampled
+// threshold >= 64x too low), replayed exactly for k <= kHeapMax:
+// std::partial_sort(queue, queue + k, queue + n, greater) = heap select over the
+// candidates in index order — make_heap of the first k, then every later candidate
+// whose key beats the heap's top replaces it (pop_heap) — and sort_heap; queue[0..k)
+// is the output in that order (dgc/compression.py:134-137). The heap lives in LDS
+// and is worked by one thread (the order of ties depends on its exact layout); the
+// other threads stream vec in chunks, compact each chunk's candidates in index order
+// and pre-filter those that cannot beat the top (the top only rises). Then the emit
+// (values, wire casts, DGCSGDMemory.update's masking) in parallel.
+__device__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o, int t,
+                               uint64_t* heap, uint64_t* hot) {
+    const SelState* st = w.st + t;
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const float* vec = vec_flat + d.off;
+    const float tc = st->t_cur;
+    const int64_t k = d.k;
+    constexpr int64_t kChunkElems = (int64_t)kHeapThreads * kHeapPer;
+    __shared__ uint64_t lds16[16];
+    __shared__ long long obase_s;
+    const int tid = threadIdx.x;
+    int64_t filled = 0;   // candidates seen so far (uniform)
+    for (int64_t c0 = 0; c0 < d.n; c0 += kChunkElems) {
+        const int64_t e0 = c0 + (int64_t)tid * kHeapPer;
+        float x[kHeapPer];
+        uint32_t cm = 0;
+#pragma unroll
+        for (int j = 0; j < kHeapPer; ++j) {
+            const bool ok = e0 + j < d.n;
+            x[j] = ok ? vec[e0 + j] : 0.f;
+            cm |= (uint32_t)(ok && fabsf(x[j]) >= tc) << j;
+        }
+        uint64_t total;
+        const uint64_t base = block_exclusive_scan((uint64_t)__popc(cm), lds16, &total);
+        const int64_t fnew = filled + (int64_t)total;
+        if (filled < k) {   // the first k candidates fill the heap in index order
+            uint64_t r = base;
+#pragma unroll
+            for (int j = 0; j < kHeapPer; ++j) {
+                if ((cm >> j) & 1u) {
+                    const int64_t g = filled + (int64_t)r++;
+                    if (g < k) heap[g] = ((uint64_t)abs_key(x[j]) << 32) | (uint64_t)(uint32_t)(e0 + j);
+                }
+            }
+            __syncthreads();
+            if (fnew >= k && tid == 0 && k >= 2) {   // std::__make_heap
+                for (int64_t parent = (k - 2) / 2;; --parent) {
+                    nth_adjust_heap(heap, parent, k, heap[parent]);
+                    if (parent == 0) break;
+                }
+            }
+            __syncthreads();
+        }
+        if (fnew > k) {   // candidates past the first k: the heap-select loop
+            const uint32_t top = qkey(heap[0]);
+            uint32_t hm = 0;
+            uint64_t r = base;
+#pragma unroll
+            for (int j = 0; j < kHeapPer; ++j) {
+                if ((cm >> j) & 1u) {
+                    const int64_t g = filled + (int64_t)r++;
+                    if (g >= k && abs_key(x[j]) > top) hm |= 1u << j;
+                }
+            }
+            uint64_t htot;
+            const uint64_t hb = block_exclusive_scan((uint64_t)__popc(hm), lds16, &htot);
+            uint64_t q = hb;
+#pragma unroll
+            for (int j = 0; j < kHeapPer; ++j)
+                if ((hm >> j) & 1u) hot[q++] = ((uint64_t)abs_key(x[j]) << 32) | (uint64_t)(uint32_t)(e0 + j);
+            __syncthreads();
+            if (tid == 0) {
+                for (uint64_t h = 0; h < htot; ++h) {   // comp(candidate, top): strictly greater
+                    const uint64_t v = hot[h];
+                    if (qkey(v) > qkey(heap[0])) nth_adjust_heap(heap, 0, k, v);
+                }
+            }
+            __syncthreads();
+        }
+        filled = fnew;
+    }
+    if (tid == 0) {   // std::__sort_heap
+        for (int64_t last = k; last > 1;) {
+            --last;
+            const uint64_t v = heap[last];
+            heap[last] = heap[0];
+            nth_adjust_heap(heap, 0, last, v);
+        }
+    }
+    if (tid < kWave) {
+        const long long b = out_base(w, t);
+        if (tid == 0) obase_s = b;
+    }
+    __syncthreads();
+    for (int64_t p = tid; p < k; p += kHeapThreads) {
+        const int64_t li = (int64_t)(uint32_t)heap[p];
+        emit_one(o, d, obase_s + p, li, vec[li]);
+    }
+}
+
+// K5 / K5b, one workgroup per tensor: the reference's resample topk replayed on the
+// gathered candidates (introselect.hpp: nth_element), or — partial_sort path, k <=
+// kHeapMax — heap select + sort_heap over vec, which also emits. They share one LDS area.
+static_assert(kHeapMax + (int64_t)kHeapThreads * kHeapPer <= kNthLds, "K5b: heap + chunk fit K5's LDS");
+__global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
+                                                            EmitOut o) {
+    const int t = blockIdx.x;
+    const SelState* st = w.st + t;
+    if (st->branch != DGC_BRANCH_RESAMPLE || !st->rs_nth) return;
+    __shared__ __align__(16) uint64_t lq[kNthLds];
+    if (st->rs_nth == 2) {
+        heap_select_wg(vec_flat, w, o, t, lq, lq + kHeapMax);
+        return;
+    }
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    uint32_t* gl = w.gpos + d.gpos_off;
+    uint32_t* gr = gl + d.cand_cap / 2 + 1;
+    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, lq);
 }
 
 // Result records; the payload's total count; and every tensor's next speculative
@@ -1584,7 +1702,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         g.cand = w.cand_idx;
         hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitThreads), 0, s, vec, w, g);
         DGC_LAUNCHED();
-        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, w);
+        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o);
         DGC_LAUNCHED();
         hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
         DGC_LAUNCHED();
@@ -1616,16 +1734,18 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
                 DGC_TRY(pass((any_list ? 1 : 0) | (any_full ? 2 : 0), false));
             }
         }
-        bool any_nth = false, any_low = false;
+        bool any_nth = false, any_low = false, any_heap = false;
         for (const SelState& h : hs) {
             if (h.branch != DGC_BRANCH_RESAMPLE) continue;
-            if (h.rs_nth)
+            if (h.rs_nth == 1)
                 any_nth = true;
+            else if (h.rs_nth == 2)
+                any_heap = true;
             else
                 any_low = true;
         }
         if (any_low) DGC_TRY(resample_lowest());
-        if (any_nth) DGC_TRY(resample_exact());
+        if (any_nth || any_heap) DGC_TRY(resample_exact());   // k_nth_select serves both
     } else if (L.adapt_any) {
         // every kernel below early-exits on a device flag when it is not needed
         if (lower_fast) {
