@@ -72,3 +72,106 @@ def test_flat_1b_bucket_steps_match_oracle():
         print(f"step {s}: {info}", file=sys.stderr, flush=True)
     # the bench's steady state was exercised: selections served by the K1 lists
     assert any(fp == 0 for _, fp, _ in seen[1:]), seen
+
+
+def _ref_compensate_(g, mmt, vec, chunk=1 << 28):
+    """DGCSGDMemory.compensate, nesterov (dgc/memory.py:58-61), as the reference's own
+    torch ops — separate add_/mul_ kernels, one rounding each — chunk by chunk."""
+    for c0 in range(0, g.numel(), chunk):
+        s = slice(c0, min(g.numel(), c0 + chunk))
+        mmt[s].add_(g[s]).mul_(0.9)
+        vec[s].add_(mmt[s]).add_(g[s])
+
+
+def _count_ge(vec, t, chunk=1 << 28):
+    return sum(int((vec[c0:c0 + chunk].abs() >= t).sum()) for c0 in range(0, vec.numel(), chunk))
+
+
+def _first_ge(vec, t, limit, chunk=1 << 28):
+    """nonzero(|vec| >= t)[:limit] in index order, chunk by chunk (int64)."""
+    parts, got = [], 0
+    for c0 in range(0, vec.numel(), chunk):
+        idx = torch.nonzero(vec[c0:c0 + chunk].abs() >= t).view(-1) + c0
+        parts.append(idx[: limit - got])
+        got += parts[-1].numel()
+        if got >= limit:
+            break
+    return torch.cat(parts)
+
+
+@pytest.mark.timeout(900)
+def test_flat_7b_bf16_steps_match_reference_ops():
+    """BASELINE configs[4] at full size: N = 7e9 (> 2^32, so indices past 32 bits),
+    bf16-origin gradients (dense ties), ratio 1e-4, nesterov, two steps through
+    DGCBucket as bench.py runs it. Checked against the reference's algorithm re-run
+    with torch ops on the GPU, chunked (the numpy oracle is too slow at 7e9): compensate
+    (bit-exact momentum/velocity), the sampled threshold (topk of the strided samples),
+    the adaptation loop on exact counts, the transmitted indices in order and values,
+    the masking, and the decompressed output."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    free, _ = torch.cuda.mem_get_info()
+    if free < 200 * 2 ** 30:
+        pytest.skip("needs ~200 GiB of free HBM")
+    from dgc.bucket import DGCBucket
+    N, ratio = 7 * 10 ** 9, 1e-4
+    b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=42)
+    numel, k, S, ks, stride = O.attributes(N, ratio)
+    assert (b.k, b.stride, b.top_k_samples) == (k, stride, ks)
+    g = torch.empty(N, device=DEV)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(0xD6C)
+    for c0 in range(0, N, 1 << 30):
+        c1 = min(N, c0 + (1 << 30))
+        g[c0:c1] = torch.randn(c1 - c0, generator=gen, device=DEV).to(torch.bfloat16).float()
+    mmt_e = torch.zeros(N, device=DEV)
+    vec_e = torch.zeros(N, device=DEV)
+    out = torch.empty(N, device=DEV)
+    rng = random.Random(42)
+    U, Lc = O.adapt_bounds(k)
+    for s in range(2):
+        start = rng.randint(0, stride - 1)
+        b.step(g, out)
+        torch.cuda.synchronize()
+        info = b.last_info()
+        _ref_compensate_(g, mmt_e, vec_e)
+        samples = vec_e[start::stride].abs()
+        t = torch.topk(samples, ks).values.min()
+        assert t.view(torch.int32).item() == torch.tensor([info["threshold0"]]).view(torch.int32).item(), s
+        del samples
+        n = _count_ge(vec_e, t)
+        branch = "exhausted"
+        for _ in range(10):                                   # dgc/compression.py:128-149
+            if n > k:
+                branch = "resample" if n > U else "trunc"
+                break
+            if n < Lc:
+                t = t * torch.tensor(0.8, device=DEV)
+                n = _count_ge(vec_e, t)
+            else:
+                branch = "ok"
+                break
+        assert (branch, n) == (info["branch"], info["candidates"]), (s, info, branch, n)
+        if branch == "resample":
+            cand = _first_ge(vec_e, t, n)
+            order = torch.topk(vec_e[cand].abs().cpu(), k, sorted=False)[1]   # the reference's CPU topk
+            want = cand.cpu()[order]
+        else:
+            want = _first_ge(vec_e, t, min(n, k)).cpu()
+        cnt = info["count"]
+        gi = b.payload[b.ioff: b.ioff + 8 * cnt].view(torch.int64).cpu()
+        gv = b.payload[b.voff: b.voff + 4 * cnt].view(torch.float32).cpu()
+        assert torch.equal(gi, want), s
+        assert int(gi.max()) >= 2 ** 32 or int(want.max()) < 2 ** 32
+        wv = vec_e[want.to(DEV)].cpu()
+        assert torch.equal(gv.view(torch.int32), wv.view(torch.int32)), s
+        vec_e[want.to(DEV)] = 0.0                             # DGCSGDMemory.update (dgc/memory.py:72-77)
+        mmt_e[want.to(DEV)] = 0.0
+        for c0 in range(0, N, 1 << 28):                       # state after masking, bit for bit
+            c1 = min(N, c0 + (1 << 28))
+            assert torch.equal(b.vec[c0:c1].view(torch.int32), vec_e[c0:c1].view(torch.int32)), (s, c0)
+            assert torch.equal(b.mmt[c0:c1].view(torch.int32), mmt_e[c0:c1].view(torch.int32)), (s, c0)
+        assert torch.equal(out[want.to(DEV)].cpu().view(torch.int32), wv.view(torch.int32))
+        assert sum(int(torch.count_nonzero(out[c0:c0 + (1 << 28)])) for c0 in range(0, N, 1 << 28)) == \
+            int(torch.count_nonzero(wv))
+        print(f"7B step {s}: {info}, max index {int(gi.max())}", file=sys.stderr, flush=True)
