@@ -32,6 +32,7 @@ def _equal_bits(gpu, host):
 def test_flat_1b_bucket_steps_match_oracle():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    torch.cuda.empty_cache()   # what earlier tests left cached
     free, _ = torch.cuda.mem_get_info()
     if free < 40 * 2 ** 30:
         pytest.skip("needs ~40 GiB of free HBM")
@@ -110,6 +111,7 @@ def test_flat_7b_bf16_steps_match_reference_ops():
     the masking, and the decompressed output."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    torch.cuda.empty_cache()   # what earlier tests left cached
     free, _ = torch.cuda.mem_get_info()
     if free < 200 * 2 ** 30:
         pytest.skip("needs ~200 GiB of free HBM")
