@@ -174,6 +174,7 @@ struct Layout {
     int64_t nseg = 0, ngrp = 0, nsamp = 0, ncand = 0, ngpos = 0;
     int32_t nsmall = 0;
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
+    bool lowest_any = false;    // some tensor can take the approximate partial_sort resample
     int64_t grid[BT_COUNT] = {};
 };
 
@@ -220,6 +221,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.lower_count = in[t].lower_count;
         const bool sampled = d.n != d.S;
         L.adapt_any |= sampled;
+        L.lowest_any |= sampled && (d.k > kHeapMax || d.n > 0xFFFFFFFFLL);   // see k_decide
         d.samp_off = (sampled && in[t].samples) ? samp : -1;
         if (d.samp_off >= 0) samp += (int64_t)align_up((size_t)(d.S + 1), 64);
         d.cand_off = cand;
@@ -1755,7 +1757,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
             for (int i = 0; i < p.max_iters; ++i) DGC_TRY(pass(3, true));
         }
         if (p.resample) {
-            DGC_TRY(resample_lowest());
+            if (L.lowest_any) DGC_TRY(resample_lowest());   // 4 gated launches no tensor here can need
             DGC_TRY(resample_exact());
         }
     }
