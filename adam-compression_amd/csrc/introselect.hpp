@@ -273,6 +273,40 @@ __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile
     wave_prefix4(pr, br, tr);
     uint32_t rl = runl + bl;   // left stoppers before this element
     uint32_t rr = runr + br;   // right stoppers in [f+1, this element)
+    if (!BALLOT) {
+        // Whole-tile cases (wave-uniform): with every right stopper after the tile
+        // outnumbering the left stoppers up to its end, all its left stoppers are
+        // swapped and none of its right ones; with the left stoppers before it
+        // outnumbering every right stopper from its start, the reverse. Only the tile(s)
+        // where the two counts cross need the per-element test below. (Measured: a
+        // third off the pairing pass; no gain in the few-tile single-wave tail.)
+        const int64_t after = (int64_t)TR - runr - tr, from = (int64_t)TR - runr;
+        if (after >= (int64_t)runl + tl) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if ((pl >> j) & 1u) lpos[rl++] = rel0 + (uint32_t)j;
+            }
+            paired += (uint32_t)__popc(pl);
+            runl += tl;
+            runr += tr;
+            return;
+        }
+        if ((int64_t)runl >= from) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t i = rel0 + (uint32_t)j;
+                if ((pr >> j) & 1u) {
+                    rr += 1;
+                    rpos[TR - rr] = i;
+                    rmin = i < rmin ? i : rmin;
+                }
+                if (((pl >> j) & 1u) && i < lnext) lnext = i;
+            }
+            runl += tl;
+            runr += tr;
+            return;
+        }
+    }
     uint64_t msl[4], mln[4], msr[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
