@@ -61,3 +61,14 @@ def test_bucket_w2_matches_oracle(fill, kind):
         assert problems == [], (rank, res)
     if kind == "layered":
         assert "resample" in dict(out[0])["branches"]
+
+
+@pytest.mark.timeout(240)
+def test_bucket_w4_matches_oracle():
+    """4 ranks (processes) on one MI355X: the 4-run decompress (bounds + wave scatter +
+    crowded-chunk path) and the side-stream zero fill under the exchange, against the
+    oracle over all four ranks' payloads."""
+    out = run(G.bucket_worker, 4, "allgather", "normal")
+    for rank, res in out.items():
+        problems = [r for r in res if r[0] != "branches"]
+        assert problems == [], (rank, res)
