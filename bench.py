@@ -400,9 +400,10 @@ def main():
     for i in range(args.warmup):
         run.step(i)
     torch.cuda.synchronize()
-    timed = phases if args.phases else ("compensate", "allgather")
-    if wl["kind"] == "model":
-        timed = phases   # K1 (compensate) timed live on its own, as for the flat bucket
+    # HIP events in the timed steps: K1 (the roofline kernel) always; the allgather when
+    # there is one (its bus bandwidth); every phase only with --phases — each event pair
+    # costs the GPU a few µs of idle time, ~7 % of a ResNet-50 step with all four phases
+    timed = phases if args.phases else (("compensate", "allgather") if world > 1 else ("compensate",))
     evs = [{p: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for p in timed}
            for _ in range(args.steps)]
     if world > 1:
