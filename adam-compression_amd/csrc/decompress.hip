@@ -554,7 +554,12 @@ k_scatter_overflow(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, floa
 static int vbytes(int vd) { return vd == DGC_F16 ? 2 : 4; }
 static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
 
-int fill_zero(float* x, int64_t n, hipStream_t s);
+// words zeroed by the dense fill's first block (a null pointer with a zero count skips)
+struct ZeroWords {
+    int32_t* p[3];
+    int32_t n[3];
+};
+int fill_zero(float* x, int64_t n, hipStream_t s, const ZeroWords& z);
 
 // Decompress schedule. `entries` is a host-side upper bound on the total entries,
 // `run_cap` on the entries of one run, and `runs` the number of runs when the host
@@ -569,10 +574,17 @@ template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
                        bool dense, int64_t entries, int64_t run_cap, int runs, hipStream_t s) {
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
-    if (dense) DGC_TRY(fill_zero(grad, n, s));
-    if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
-    if (runs == 1) {   // a thread per entry
+    // status, the overflow queue count and the unsorted flags are reset before any
+    // kernel of this call can set them: by the dense fill's first block, or memsets
+    if (dense) {
+        ZeroWords z{{w.status, w.ovf_cnt, w.unsorted}, {1, 1, w.sort_cap ? kMaxRuns : 0}};
+        DGC_TRY(fill_zero(grad, n, s, z));
+    } else {
+        if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
         DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
+        DGC_HIP(hipMemsetAsync(w.ovf_cnt, 0, sizeof(int32_t), s));
+    }
+    if (runs == 1) {   // a thread per entry
         if (entries > 0) {
             hipLaunchKernelGGL((k_scatter_single<VD, ID>), dim3((unsigned)ceil_div(entries, (int64_t)kBlock)),
                                dim3(kBlock), 0, s, w, rs, grad, n, scale);
@@ -581,10 +593,6 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
         return DGC_OK;
     }
     const unsigned bx = (unsigned)grid_for(run_cap + 1, kBlock, kMaxGrid / 2);
-    // status, the overflow queue and the unsorted flags are reset before any kernel of
-    // this call can set them
-    DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
-    DGC_HIP(hipMemsetAsync(w.ovf_cnt, 0, sizeof(int32_t), s));
     hipLaunchKernelGGL(k_bounds<ID>, dim3(bx, (unsigned)max_runs), dim3(kBlock), 0, s, w, rs, n, run_cap);
     DGC_LAUNCHED();
     if (w.sort_cap) {
@@ -702,10 +710,16 @@ int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, i
 
 // Zero fill (the sparse scatter's precondition): one-shot workgroups, one 16-B
 // plain store per lane — measured 7.0 TB/s on MI355X at 4 GB, vs 5.2-6.2 for
-// grid-stride or non-temporal forms (tools/membench.hip).
-__global__ void __launch_bounds__(kBlock) k_fill_zero(float4* __restrict__ x, int64_t n4) {
+// grid-stride or non-temporal forms (tools/membench.hip). Block 0 also zeroes the
+// decompress's status words (ZeroWords), which saves the scatter two memset packets.
+__global__ void __launch_bounds__(kBlock) k_fill_zero(float4* __restrict__ x, int64_t n4, ZeroWords z) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n4) x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (blockIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            for (int j = threadIdx.x; j < z.n[q]; j += kBlock) z.p[q][j] = 0;
+    }
 }
 
 __global__ void k_fill_zero1(float* __restrict__ x, int64_t begin, int64_t n) {
@@ -713,9 +727,15 @@ __global__ void k_fill_zero1(float* __restrict__ x, int64_t begin, int64_t n) {
     if (i < n) x[i] = 0.f;
 }
 
-int fill_zero(float* x, int64_t n, hipStream_t s) {
+// z: words to zero in the same launch (or their memsets when x gets no vector kernel).
+int fill_zero(float* x, int64_t n, hipStream_t s, const ZeroWords& z) {
     if (!x || n < 0) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: null buffer or n < 0");
-    if (n == 0) return DGC_OK;
+    bool zeroed = false;
+    if (n == 0) {
+        for (int q = 0; q < 3; ++q)
+            if (z.n[q]) DGC_HIP(hipMemsetAsync(z.p[q], 0, sizeof(int32_t) * z.n[q], s));
+        return DGC_OK;
+    }
     if (reinterpret_cast<uintptr_t>(x) & 3) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: buffer must be 4-B aligned");
     // scalar head up to the first 16-B boundary (a grad that is an offset view), then 16-B stores
     const int64_t lead = std::min<int64_t>(n, (int64_t)((16 - (reinterpret_cast<uintptr_t>(x) & 15)) & 15) / 4);
@@ -729,9 +749,13 @@ int fill_zero(float* x, int64_t n, hipStream_t s) {
     if (n4 > 0) {
         if (ceil_div(n4, (int64_t)kBlock) > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: n too large");
         hipLaunchKernelGGL(k_fill_zero, dim3((unsigned)ceil_div(n4, (int64_t)kBlock)), dim3(kBlock), 0, s,
-                           reinterpret_cast<float4*>(x), n4);
+                           reinterpret_cast<float4*>(x), n4, z);
         DGC_LAUNCHED();
+        zeroed = true;
     }
+    if (!zeroed)
+        for (int q = 0; q < 3; ++q)
+            if (z.n[q]) DGC_HIP(hipMemsetAsync(z.p[q], 0, sizeof(int32_t) * z.n[q], s));
     const int64_t head = n4 * 4;
     if (head < n) {
         hipLaunchKernelGGL(k_fill_zero1, dim3(1), dim3(64), 0, s, x, head, n);
@@ -763,7 +787,7 @@ extern "C" int dgc_decompress(const void* values, int32_t vdtype, const void* in
 }
 
 extern "C" int dgc_fill_zero(float* x, int64_t n, void* stream) {
-    return dgc::fill_zero(x, n, static_cast<hipStream_t>(stream));
+    return dgc::fill_zero(x, n, static_cast<hipStream_t>(stream), dgc::ZeroWords{});
 }
 
 extern "C" int64_t dgc_payload_layout(int64_t capacity, int32_t vdtype, int32_t idtype,

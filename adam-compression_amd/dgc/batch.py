@@ -12,7 +12,7 @@ each tensor at a 1024-element-aligned offset) and runs
     dgc_batch_compress   K1 over all tensors, K3 for all thresholds, the selection
                          chain with per-tensor state, one packed payload
     one allgather        the packed payload, RCCL over xGMI (gloo stages via the host)
-    decompress           dgc_fill_zero + dgc_scatter_packed over the flat gradient
+    decompress           dgc_decompress_packed (zero fill + scatter) over the flat gradient
 
 with O(1) launches per phase and no host synchronisation. The payload carries flat
 indices (tensor offset + index in the tensor), tensor after tensor.
@@ -194,11 +194,11 @@ class DGCBatch:
         out = self.out_flat if out_flat is None else out_flat
         L = self._L
         st = _lib.stream_of(self.device)
-        _lib.check(L.dgc_fill_zero(out.data_ptr(), self.flat_numel, st), "dgc_fill_zero")
-        _lib.check(L.dgc_scatter_packed(self.gathered.data_ptr(), self.world, self.rank_stride, self.capacity,
-                                        _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(), self.flat_numel,
-                                        1.0 / self.world, self.dec_ws.data_ptr(), self.dec_ws.numel(), st),
-                   "dgc_scatter_packed")
+        # the zero fill and the scatter in one call: the fill also resets the scatter's status words
+        _lib.check(L.dgc_decompress_packed(self.gathered.data_ptr(), self.world, self.rank_stride, self.capacity,
+                                           _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
+                                           self.flat_numel, 1.0 / self.world, self.dec_ws.data_ptr(),
+                                           self.dec_ws.numel(), st), "dgc_decompress_packed")
         return out
 
     def step(self, starts=None):
