@@ -561,6 +561,26 @@ struct ZeroWords {
 };
 int fill_zero(float* x, int64_t n, hipStream_t s, const ZeroWords& z);
 
+// Sparse re-zero, the zero_() of a persistent output (dgc_decompress_packed_over):
+// grad holds exactly the previous call's result over `prev`, so +0.0 everywhere but at
+// prev's indices — zeroing those W*k slots is the whole-bucket fill for a fraction
+// W*k/n of its traffic. Block (0, 0) also resets the scatter's status words.
+template <int ID>
+__global__ void __launch_bounds__(kBlock) k_clear_packed(RunSrc prev, float* __restrict__ grad, int64_t n,
+                                                         ZeroWords z) {
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            for (int j = threadIdx.x; j < z.n[q]; j += kBlock) z.p[q][j] = 0;
+    }
+    const Run run = prev.get_raw((int)blockIdx.y);
+    for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < run.count;
+         e += (long long)gridDim.x * kBlock) {
+        const long long i = load_idx<ID>(run.idx, e);
+        if (i >= 0 && i < n) grad[i] = 0.f;
+    }
+}
+
 // Decompress schedule. `entries` is a host-side upper bound on the total entries,
 // `run_cap` on the entries of one run, and `runs` the number of runs when the host
 // knows it (0 otherwise). dense: grad is first zeroed by dgc_fill_zero (one-shot
@@ -570,14 +590,22 @@ int fill_zero(float* x, int64_t n, hipStream_t s, const ZeroWords& z);
 //   one run          a thread per entry
 //   several runs     bounds + a wave per kSCB super-chunks + the workgroup path for
 //                    crowded super-chunks
+// prev (packed mode, null otherwise): grad holds the result of the previous call over
+// that payload; its entries are re-zeroed instead of the dense fill.
 template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
-                       bool dense, int64_t entries, int64_t run_cap, int runs, hipStream_t s) {
+                       bool dense, int64_t entries, int64_t run_cap, int runs, hipStream_t s,
+                       const RunSrc* prev = nullptr) {
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
     // status, the overflow queue count and the unsorted flags are reset before any
-    // kernel of this call can set them: by the dense fill's first block, or memsets
-    if (dense) {
-        ZeroWords z{{w.status, w.ovf_cnt, w.unsorted}, {1, 1, w.sort_cap ? kMaxRuns : 0}};
+    // kernel of this call can set them: by the dense fill's (or the sparse re-zero's)
+    // first block, or memsets
+    const ZeroWords z{{w.status, w.ovf_cnt, w.unsorted}, {1, 1, w.sort_cap ? kMaxRuns : 0}};
+    if (prev) {
+        const dim3 grid((unsigned)grid_for(prev->capacity, kBlock, kMaxGrid / 2), (unsigned)prev->world);
+        hipLaunchKernelGGL(k_clear_packed<ID>, grid, dim3(kBlock), 0, s, *prev, grad, n, z);
+        DGC_LAUNCHED();
+    } else if (dense) {
         DGC_TRY(fill_zero(grad, n, s, z));
     } else {
         if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
@@ -615,15 +643,15 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
 
 static int dispatch_scatter(int vd, int id, const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
                             float scale, int max_runs, bool dense, int64_t entries, int64_t run_cap, int runs,
-                            hipStream_t s) {
+                            hipStream_t s, const RunSrc* prev = nullptr) {
     if (vd == DGC_F32 && id == DGC_I64)
-        return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
+        return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s, prev);
     if (vd == DGC_F32 && id == DGC_I32)
-        return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
+        return run_scatter<DGC_F32, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s, prev);
     if (vd == DGC_F16 && id == DGC_I64)
-        return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
+        return run_scatter<DGC_F16, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s, prev);
     if (vd == DGC_F16 && id == DGC_I32)
-        return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s);
+        return run_scatter<DGC_F16, DGC_I32>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s, prev);
     DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress: unsupported value/index dtype (%d, %d)", vd, id);
 }
 
@@ -694,7 +722,7 @@ int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t*
 
 int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity, int vd,
                       int id, float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, hipStream_t s,
-                      bool dense) {
+                      bool dense, const void* prev = nullptr) {
     DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world, capacity));
     int64_t voff, ioff;
     const int64_t min_stride = payload_layout(capacity, vd, id, &voff, &ioff);
@@ -704,6 +732,13 @@ int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, i
     DecWS w = carve_dec(ws, n, world, capacity);
     RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world,
               w.unsorted, w.sorted};
+    if (prev) {
+        if (prev == payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed_over: prev must be another buffer");
+        const RunSrc pr{nullptr, nullptr, static_cast<const char*>(prev), rank_stride, voff, ioff, capacity, world,
+                        nullptr, nullptr};
+        return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, false, (int64_t)world * capacity, capacity,
+                                world, s, &pr);
+    }
     return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, dense, (int64_t)world * capacity, capacity,
                             world, s);
 }
@@ -800,6 +835,15 @@ extern "C" int dgc_decompress_packed(const void* payload, int32_t world, int64_t
                                      int64_t n, float scale, void* ws, size_t ws_bytes, void* stream) {
     return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
                                   ws_bytes, static_cast<hipStream_t>(stream), true);
+}
+
+extern "C" int dgc_decompress_packed_over(const void* payload, const void* prev_payload, int32_t world,
+                                          int64_t rank_stride, int64_t capacity, int32_t vdtype, int32_t idtype,
+                                          float* grad, int64_t n, float scale, void* ws, size_t ws_bytes,
+                                          void* stream) {
+    if (!prev_payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed_over: null prev_payload");
+    return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
+                                  ws_bytes, static_cast<hipStream_t>(stream), false, prev_payload);
 }
 
 extern "C" int dgc_scatter_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,

@@ -16,11 +16,16 @@ every decision kept on the device:
   ``fill="allgather"`` issues the fill on a side stream right after the RCCL
   allgather is enqueued (ordered after the selection), so at W > 1 the 4 B/elem
   zero fill runs under the xGMI transfer instead of after it; the decompress then
-  only scatters. ``"inline"`` runs fill + scatter after the allgather. ``"auto"``
-  (default) picks ``"allgather"`` at W > 1 and ``"inline"`` at W = 1, where there
-  is no transfer to hide under (measured on one MI355X, overlapping the fill with
-  the selection kernels instead loses: they are latency-bound and slow down under
-  a concurrent 7 TB/s write stream).
+  only scatters. ``"inline"`` runs fill + scatter after the allgather.
+  ``"sparse"`` (and ``"auto"``, the default) treats ``out`` as a persistent output
+  bucket: when it is the tensor the previous step decompressed into and nobody has
+  written it since (same storage, same torch version counter), it is +0.0 except at
+  the previous step's W*k gathered indices, so ``zero_()`` is a sparse re-zero of
+  those slots (``dgc_decompress_packed_over``) — W*k scattered stores instead of a
+  4 B/elem stream; the dense result is the same, bit for bit. Any other ``out``
+  (first step, a new tensor, one modified in place) gets the dense fill. The
+  payload (W = 1) / gather buffer (W > 1) alternates between two buffers so the
+  previous step's indices survive the current step.
 
 The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
 kernels); the sample start is drawn from a ``random.Random`` seeded identically on
@@ -88,23 +93,37 @@ class DGCBucket:
         self.spec = torch.full((2,), float("inf"), dtype=torch.float32, device=dev)
         self.info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
         self.rank_stride, self.voff, self.ioff = _layout(self.k, self.vdtype, self.idtype)
-        self.payload = torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev)
-        self.gathered = (torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=dev)
-                         if self.world > 1 else self.payload)
+        if fill not in ("auto", "inline", "allgather", "sparse"):
+            raise ValueError(f"fill must be 'auto', 'inline', 'allgather' or 'sparse', not {fill!r}")
+        if fill == "auto":
+            fill = "sparse"
+        self.fill = fill
+        nbuf = 2 if fill == "sparse" else 1   # the previous step's gathered indices stay readable
+        self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=dev)
+                          for _ in range(nbuf)] if self.world > 1 else self._payloads)
+        self._par = 0
+        self._last_out = None   # (data_ptr, numel, _version) of the output after the last decompress
+        self._last_gathered = None
         self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(N, self.world, self.k), dtype=torch.uint8, device=dev)
         self.scale = 1.0 / self.world
         self._L = L
-        if fill not in ("auto", "inline", "allgather"):
-            raise ValueError(f"fill must be 'auto', 'inline' or 'allgather', not {fill!r}")
-        if fill == "auto":
-            fill = "allgather" if self.world > 1 else "inline"
-        self.fill = fill
         if fill == "allgather":
             self.side = torch.cuda.Stream(device=dev)
             self._ev_go = torch.cuda.Event()
             self._ev_filled = torch.cuda.Event()
 
     # ---------------------------------------------------------------- state
+    @property
+    def payload(self):
+        """This rank's packed payload of the current step."""
+        return self._payloads[self._par % len(self._payloads)]
+
+    @property
+    def gathered(self):
+        """The allgather buffer of the current step (the payload itself at W = 1)."""
+        return self._gathers[self._par % len(self._gathers)]
+
     def flush(self):
         """Applies a deferred masking now (no-op when none is pending)."""
         if self._pending:
@@ -129,6 +148,7 @@ class DGCBucket:
     def compensate(self, grad):
         """K1: compensate + fused strided sample + speculative candidate lists."""
         L = self._L
+        self._par += 1   # a step starts: the other payload / gather buffer
         self.start = self.rng.randint(0, self.stride - 1) if self.sampled else 0
         _lib.check(L.dgc_compress_begin(grad.data_ptr(), self._mmt.data_ptr(), self._vec.data_ptr(), self.momentum,
                                         int(self.nesterov), self.start, self.stride, ctypes.byref(self.params),
@@ -155,13 +175,24 @@ class DGCBucket:
 
     def decompress(self, out, dense=True):
         """dense: out = scale * (rank-order sum of the gathered entries), zeros elsewhere.
-        dense=False: out already holds +0.0 (see fill_zero); only the entries are written."""
+        dense=False: out already holds +0.0 (see fill_zero); only the entries are written.
+        fill="sparse": a dense decompress into the previous step's untouched output
+        re-zeroes only the previous entries (see the module docstring)."""
         L = self._L
-        fn = L.dgc_decompress_packed if dense else L.dgc_scatter_packed
-        _lib.check(fn(self.gathered.data_ptr(), self.world, self.rank_stride, self.k, _lib.VD[self.vdtype],
-                      _lib.ID[self.idtype], out.data_ptr(), self.numel, self.scale, self.dec_ws.data_ptr(),
-                      self.dec_ws.numel(), _lib.stream_of(self.device)),
-                   "dgc_decompress_packed" if dense else "dgc_scatter_packed")
+        cur = self.gathered
+        args = (self.world, self.rank_stride, self.k, _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
+                self.numel, self.scale, self.dec_ws.data_ptr(), self.dec_ws.numel(), _lib.stream_of(self.device))
+        if (dense and self.fill == "sparse" and self._last_gathered is not None and self._last_gathered is not cur
+                and self._last_out == (out.data_ptr(), out.numel(), out._version)):
+            _lib.check(L.dgc_decompress_packed_over(cur.data_ptr(), self._last_gathered.data_ptr(), *args),
+                       "dgc_decompress_packed_over")
+        else:
+            fn = L.dgc_decompress_packed if dense else L.dgc_scatter_packed
+            _lib.check(fn(cur.data_ptr(), *args), "dgc_decompress_packed" if dense else "dgc_scatter_packed")
+        # the raw-pointer writes leave torch's version counter alone: any later in-place
+        # write to out (or a view of it) changes it, and the next step fills densely
+        self._last_out = (out.data_ptr(), out.numel(), out._version)
+        self._last_gathered = cur
 
     def _fill_on_side(self, out):
         """zero_() of the output on the side stream, ordered after the event recorded
@@ -177,7 +208,7 @@ class DGCBucket:
         ev = events or {}
 
         def decompress():
-            if self.fill == "inline":
+            if self.fill != "allgather":
                 self.decompress(out)
             else:
                 torch.cuda.current_stream(self.device).wait_event(self._ev_filled)

@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
-    ap.add_argument("--fill", default="auto", choices=["auto", "inline", "allgather"])
+    ap.add_argument("--fill", default="auto", choices=["auto", "inline", "allgather", "sparse"],
+                    help="flat bucket's zero_(): auto = sparse re-zero of the persistent output (dgc/bucket.py)")
     return ap.parse_args()
 
 
@@ -367,12 +368,15 @@ def step_bytes(run, world, full_passes):
     compensate 20 + select re-read 4 (0 when the K1 candidate lists serve the
     selection) + dense decompress write 4, the samples 4S, masking 8k, payload written
     k(vb+ib) + gathered W*k(vb+ib) read, scatter RMW 8Wk. `contract` keeps the 28 B
-    of SURVEY.md §8d; `required` is what this step's path actually needs."""
+    of SURVEY.md §8d; `required` is what this step's path actually needs: no re-read
+    when the lists serve, and for the flat bucket's persistent output (fill "sparse")
+    a re-zero of the previous step's W*k slots (4 B each) instead of the dense 4 B/elem."""
     n = run.n_comp if isinstance(run, ModelRun) else run.N
     k, S = run.k, run.S
     sparse = 4 * S + 8 * k + (1 + world) * k * (run.vbytes + run.ibytes) + 8 * world * k
     contract = 28 * n + sparse
-    required = (24 if full_passes == 0 else 28) * n + sparse
+    rezero = isinstance(run, FlatRun) and run.b.fill == "sparse"
+    required = (20 + (0 if full_passes == 0 else 4) + (0 if rezero else 4)) * n + sparse + (4 * world * k if rezero else 0)
     if isinstance(run, ModelRun):   # dense tensors: read g, mmt; write mmt, out
         contract += 16 * run.n_dense
         required += 16 * run.n_dense

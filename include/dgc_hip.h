@@ -20,6 +20,8 @@
  *                         concatenation of the allgather     dgc/compression.py:200-212
  *   dgc_decompress_packed the same, straight from the padded RCCL allgather buffer
  *   dgc_scatter_packed    its sparse form (zero_() done earlier by dgc_fill_zero)
+ *   dgc_decompress_packed_over  the same into a persistent output that holds the
+ *                         previous call's result (zero_() as a sparse re-zero)
  *   dgc_sgd_step          DGCSGD.step (weight-decay momentum + update) dgc/optim/sgd.py:42-68
  *
  * Conventions
@@ -274,7 +276,20 @@ int dgc_decompress_packed(const void* payload, int32_t world, int64_t rank_strid
 int dgc_scatter_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
                        int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, void* ws,
                        size_t ws_bytes, void* stream);
-/* grad[0..n) = +0.0 with 16-B non-temporal stores (16-B aligned buffer). */
+/* dgc_decompress_packed into a PERSISTENT output: grad must hold exactly the result
+ * of the previous decompress over `prev_payload` (same world / rank_stride / capacity /
+ * dtypes / n, a different buffer than `payload`) and nothing else since, so it is +0.0
+ * everywhere but at prev's indices. Those W*k slots are re-zeroed (the reference's
+ * zero_(), dgc/compression.py:191, for W*k/n of the dense fill's traffic), then the
+ * entries of `payload` are written as dgc_decompress_packed writes them: the dense
+ * result is identical. The caller owns the precondition (dgc.bucket.DGCBucket checks
+ * the output tensor's identity and version counter and falls back to the dense fill). */
+int dgc_decompress_packed_over(const void* payload, const void* prev_payload, int32_t world,
+                               int64_t rank_stride, int64_t capacity, int32_t vdtype, int32_t idtype,
+                               float* grad, int64_t n, float scale, void* ws, size_t ws_bytes,
+                               void* stream);
+/* grad[0..n) = +0.0 with one-shot 16-B stores (4-B aligned buffer; a scalar head up to
+ * the first 16-B boundary). */
 int dgc_fill_zero(float* grad, int64_t n, void* stream);
 
 /* Status word written by the decompress kernels: bit 0 = an index was out of

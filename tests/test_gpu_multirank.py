@@ -9,7 +9,7 @@ its regrouping of topk-ordered runs, DGCSGD's fused step.
   per-step gradients and hook order; the weights must equal the reference's bit for
   bit — per tensor as the reference runs, and with batch=True (one grouped K1 /
   allgather / decompress and one dense allreduce per step).
-* DGCBucket at W=2, both fill modes, against the oracle over both ranks' payloads.
+* DGCBucket at W=2, every fill mode, against the oracle over both ranks' payloads.
 """
 import pytest
 import torch
@@ -53,7 +53,8 @@ def test_distributed_optimizer_w2_reproduces_reference_weights(label, batch):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("fill,kind", [("inline", "normal"), ("allgather", "normal"), ("allgather", "layered")])
+@pytest.mark.parametrize("fill,kind", [("inline", "normal"), ("allgather", "normal"), ("allgather", "layered"),
+                                       ("sparse", "normal"), ("sparse", "layered")])
 def test_bucket_w2_matches_oracle(fill, kind):
     out = run(G.bucket_worker, 2, fill, kind)
     for rank, res in out.items():
@@ -64,11 +65,12 @@ def test_bucket_w2_matches_oracle(fill, kind):
 
 
 @pytest.mark.timeout(240)
-def test_bucket_w4_matches_oracle():
+@pytest.mark.parametrize("fill", ["allgather", "sparse"])
+def test_bucket_w4_matches_oracle(fill):
     """4 ranks (processes) on one MI355X: the 4-run decompress (bounds + wave scatter +
-    crowded-chunk path) and the side-stream zero fill under the exchange, against the
-    oracle over all four ranks' payloads."""
-    out = run(G.bucket_worker, 4, "allgather", "normal")
+    crowded-chunk path) with the side-stream zero fill under the exchange or the sparse
+    re-zero of the persistent output, against the oracle over all four ranks' payloads."""
+    out = run(G.bucket_worker, 4, fill, "normal")
     for rank, res in out.items():
         problems = [r for r in res if r[0] != "branches"]
         assert problems == [], (rank, res)

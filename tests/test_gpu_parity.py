@@ -528,6 +528,51 @@ def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, in
     assert np.array_equal(bits(sparse.cpu().numpy()), bits(want))
 
 
+@pytest.mark.parametrize("N,W,cap,fp16,int32,shuffled", [
+    (1_000_003, 1, 1000, False, False, 0),
+    (500_000, 4, 3000, True, True, 1),
+    (300_000, 8, 30000, False, False, 2),
+])
+def test_decompress_over_previous_output(L, N, W, cap, fp16, int32, shuffled):
+    """dgc_decompress_packed_over: a persistent output that holds the previous payload's
+    decompress is re-zeroed at those indices only; the result equals the dense
+    decompress of the new payload bit for bit, over overlapping / disjoint / shuffled
+    runs and three steps."""
+    rng = np.random.default_rng(N + 7 * W)
+    wsz = L.dgc_decompress_packed_workspace(N, W, cap)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    out = torch.full((N,), float("nan"), device=DEV)
+    prev = None
+    for step in range(3):
+        runs = []
+        for r in range(W):
+            c = int(rng.integers(cap // 2, cap + 1))
+            idx = np.sort(rng.choice(N if step != 1 else N // 3, c, replace=False))   # step 1: a crowded prefix
+            v = rng.standard_normal(idx.size).astype(np.float32)
+            if shuffled == 2 or (shuffled == 1 and r == 0):
+                o = rng.permutation(idx.size)
+                v, idx = v[o], idx[o]
+            runs.append((v, idx.astype(np.int64)))
+        payload, stride, vd, idt = _packed(L, runs, cap, fp16, int32)
+        tp = to_dev(payload)
+        wv = [v.astype(np.float16).astype(np.float32) if fp16 else v for v, _ in runs]
+        want = O.decompress(wv, [i for _, i in runs], N, W)
+        if prev is None:
+            check(L, L.dgc_decompress_packed(P(tp), W, stride, cap, vd, idt, P(out), N, 1.0 / W, P(ws), wsz,
+                                             stream()))
+        else:
+            check(L, L.dgc_decompress_packed_over(P(tp), P(prev), W, stride, cap, vd, idt, P(out), N, 1.0 / W,
+                                                  P(ws), wsz, stream()))
+        st = ctypes.c_int32(-1)
+        check(L, L.dgc_decompress_status(P(ws), ctypes.byref(st), stream()))
+        torch.cuda.synchronize()
+        assert st.value == (2 if shuffled else 0), step
+        assert np.array_equal(bits(out.cpu().numpy()), bits(want)), step
+        prev = tp
+    assert L.dgc_decompress_packed_over(P(prev), P(prev), W, stride, cap, vd, idt, P(out), N, 1.0, P(ws), wsz,
+                                        stream()) != 0
+
+
 def test_sparse_scatter_flags_out_of_range(L):
     N, cap = 10_000, 8
     for W in (1, 3):
@@ -655,10 +700,16 @@ def test_large_bucket_properties(L, N):
     (1_048_576, 0.05, "layered", [1, 1, 1], "inline"),         # dense candidates: lists spill, re-reads
     (500_000, 0.01, "bf16", [1, 1, 1, 1], "inline"),
     (1_000_000, 0.001, "normal", [1, 3, 9, 27], "inline"),     # fast growth: K1 lists overflow -> dropped
+    (3_000_003, 0.001, "normal", [1, 1, 1, 1, 1], "sparse"),  # persistent output: sparse re-zero
+    (1_048_576, 0.05, "layered", [1, 1, 1, 0.1], "sparse"),
+    (1_000_000, 0.001, "normal", [1, 3, 9, 27, 1], "sparse+poke"),   # out written in place: dense fallback
 ])
 def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill):
     """DGCBucket (speculative K1 lists, DGC_SYNC_DEVICE, side-stream zero fill + sparse
-    scatter or the dense decompress) vs the oracle, step by step."""
+    scatter, the dense decompress, or the sparse re-zero of a persistent output) vs the
+    oracle, step by step."""
+    poke = fill.endswith("+poke")
+    fill = fill.split("+")[0]
     from dgc.bucket import DGCBucket
     b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=7, fill=fill)
     attrs = O.attributes(N, ratio)
@@ -684,6 +735,8 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill):
             assert np.array_equal(bits(b.mmt.cpu().numpy()), bits(m_o)), s
         assert np.array_equal(bits(out.cpu().numpy()), bits(O.decompress([ov], [oi], N, 1))), s
         served_by_lists += info["full_passes"] == 0
+        if poke and s % 2 == 0:
+            out[s:: 97].fill_(7.0)   # an in-place write the next step must not build on
     if scales == [1, 1, 1, 1, 1]:
         assert served_by_lists >= 3        # the steady state skips the re-read of vec
 
