@@ -168,8 +168,10 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
  * >= spec[0] and few segment lists overflowed, every count and selection is served
  * from the lists and the separate re-read of vec is skipped; otherwise one full pass
  * runs. Results are identical either way (spec only chooses the work).
- * On return spec[1] = the final threshold t and spec[0] = spec_margin x t x growth,
- * growth = t / (previous t) clamped to [1, 1.5] (0.8 is a good margin).
+ * On return spec[1] = the final threshold t and spec[0] = m x t x growth, growth =
+ * t / (previous t) clamped to [1, 1.5]; m = spec_margin (0.8 is a good one) after a
+ * call whose t fell below its list threshold, else 1.05 x (list threshold / t) of
+ * that call, within [spec_margin, 0.95]: the lists shrink while t moves predictably.
  * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
  * one workspace and must see the same sample_start/stride/params. */
 size_t dgc_compress_workspace(int64_t numel, int64_t num_selects, int64_t num_samples);
