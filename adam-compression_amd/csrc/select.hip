@@ -64,6 +64,7 @@ constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgrou
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole batch
 constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
 constexpr int kHeapMax = 4096;                  // K5b: exact partial_sort replay up to this k (heap in LDS)
+constexpr int kEmitSplit = 4;                   // k_emit workgroups per group when split (a wave emits 16 lists)
 constexpr int kHeapThreads = 512;                // = kNthThreads: K5b runs inside k_nth_select
 constexpr int kHeapPer = 16;                    // K5b: consecutive elements per thread per chunk
 
@@ -153,6 +154,7 @@ struct SelWS {
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     int64_t nseg, ngrp;
+    int32_t emit_split;        // k_emit workgroups per group (Layout::emit_split)
 };
 
 // Candidates the exact resample replays: torch's CPU topk runs nth_element while
@@ -176,10 +178,12 @@ struct Layout {
     int32_t nsmall = 0;
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool lowest_any = false;    // some tensor can take the approximate partial_sort resample
+    int32_t emit_split = 1;     // k_emit workgroups per group: kEmitSplit when the groups alone
+                                // give fewer workgroups than CUs (model gradient sets), else 1
     int64_t grid[BT_COUNT] = {};
 };
 
-static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg) {
+static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, int emit_split) {
     const int64_t cap = std::max<int64_t>(1, ceil_div((int64_t)kCapBlocks * d.nseg, std::max<int64_t>(1, total_seg)));
     switch (which) {
         case BT_K1: return ceil_div(d.nseg, (int64_t)kSegPerBlock4);
@@ -187,7 +191,7 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg) {
         case BT_CAP16: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock16), cap);
         case BT_CAP4: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock4), cap);
         case BT_SEG: return ceil_div(d.nseg, (int64_t)kBlock);
-        case BT_GRP: return d.ngrp;
+        case BT_GRP: return ceil_div(d.nseg, (int64_t)(kGroupSegs / emit_split));
         case BT_QUEUE: return ceil_div(d.k, (int64_t)kQueuePerBlock);
         case BT_SAMP: {
             const int64_t cnt = d.samp_off < 0 ? d.n : d.S + 1;
@@ -245,12 +249,13 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
     L.ncand = cand;
     L.ngpos = gpos;
     L.nsmall = (int32_t)small.size();
+    L.emit_split = grp < 256 ? kEmitSplit : 1;
     for (int which = 0; which < BT_COUNT; ++which) {
         bt[which].assign(T + 1, 0);
         int64_t acc = 0;
         for (int32_t t = 0; t < T; ++t) {
             bt[which][t] = (int32_t)acc;
-            acc += bt_blocks(which, td[t], L.nseg);
+            acc += bt_blocks(which, td[t], L.nseg, L.emit_split);
         }
         bt[which][T] = (int32_t)acc;
         L.grid[which] = acc;
@@ -260,6 +265,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
 static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) {
     SelWS w{};
     w.T = L.T;
+    w.emit_split = L.emit_split;
     w.nseg = L.nseg;
     w.ngrp = L.ngrp;
     Carver c(base);
@@ -1326,11 +1332,12 @@ __device__ void emit_reread_resample(const float* __restrict__ vec, const TDesc&
     }
 }
 
-// One workgroup per group of kGroupSegs segments, one thread per segment for the
-// in-group offset scan; then wave-per-segment emission: kCap == 64 list slots, so
-// lane l takes list entry l (one coalesced load per list) and ballot ranks give the
-// output positions. Each wave emits 64 consecutive segments, kEmitBatch lists in
-// flight; a spilled segment is re-read from vec by the same wave.
+// w.emit_split (1 or kEmitSplit) workgroups per group of kGroupSegs segments. Each
+// scans the whole group's segment counts (one thread per segment: the in-group
+// offsets), then emits its share (64 or 16 lists per wave), wave per segment: kCap == 64 list slots, so lane l takes list entry l
+// (one coalesced load per list) and ballot ranks give the output positions. Each
+// wave emits kEmitBatch consecutive segments with all their list loads in flight
+// (one round trip); a spilled segment is re-read from vec by the same wave.
 // o.queue == null: the payload (every branch but a K5 resample, which k_emit_queue
 // writes). o.queue != null: K5's candidate gather — every element >= t_cur, ascending
 // (the reference's `indices` before its resample topk), only when K5 serves the tensor.
@@ -1351,7 +1358,10 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
     const bool defer_here = o.defer && !rs && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
-    const int64_t lg = (int64_t)blockIdx.x - w.bt[BT_GRP][t];   // group within the tensor
+    const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
+    const int split = w.emit_split;
+    const int64_t lg = lb / split;                           // group within the tensor
+    const int sub = (int)(lb % split);                       // its share this workgroup emits
     const int64_t g = d.grp0 + lg;
     const int64_t lseg0 = lg * kGroupSegs;
     __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs], lcn[kGroupSegs];
@@ -1379,7 +1389,8 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         __syncthreads();
         const uint32_t ob = rs ? (uint32_t)block_exclusive_scan((uint64_t)cb, lds16, &tot) : 0u;
         const bool work = rs ? (ca > 0 || (cb > 0 && gb + ob < T)) : (ca > 0 && ga + oa < limit);
-        if (defer_here && ls < d.nseg) w.seg_off[d.seg0 + ls] = oa;
+        if (defer_here && ls < d.nseg && (int)threadIdx.x / (kGroupSegs / split) == sub)
+            w.seg_off[d.seg0 + ls] = oa;
         off_a[threadIdx.x] = oa;
         off_b[threadIdx.x] = ob;
         lcn[threadIdx.x] = work ? lc : kEmitSkip;
@@ -1389,7 +1400,10 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const float tc = st->t_cur, tk = st->tk;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt();
-    for (int j0 = wv * 64; j0 < wv * 64 + 64; j0 += kEmitBatch) {
+    static_assert(kGroupSegs / kEmitSplit / (kEmitThreads / kWave) % kEmitBatch == 0, "whole batches per wave");
+    const int wave_segs = kGroupSegs / split / (kEmitThreads / kWave);
+    const int jw = sub * (kGroupSegs / split) + wv * wave_segs;
+    for (int j0 = jw; j0 < jw + wave_segs; j0 += kEmitBatch) {
         float x[kEmitBatch];
         uint32_t e[kEmitBatch];
 #pragma unroll
