@@ -70,14 +70,24 @@ __device__ __forceinline__ void visit_dense(const float* x, int64_t n, int64_t l
     const int64_t tid = lb * blockDim.x + threadIdx.x;
     const int64_t G = nb * blockDim.x;
     if (aligned16(x)) {
+        // kVisitBatch float4 loads in flight per lane before any key is used: the
+        // histogram's LDS atomics would otherwise serialise one load round trip each
+        constexpr int kVisitBatch = 8;
         const int64_t n4 = n / 4;
         const float4* x4 = reinterpret_cast<const float4*>(x);
-        for (int64_t i = tid; i < n4; i += G) {
-            const float4 v = x4[i];
-            f(abs_key(v.x));
-            f(abs_key(v.y));
-            f(abs_key(v.z));
-            f(abs_key(v.w));
+        for (int64_t i0 = tid; i0 < n4; i0 += kVisitBatch * G) {
+            float4 v[kVisitBatch];
+#pragma unroll
+            for (int u = 0; u < kVisitBatch; ++u)
+                if (i0 + u * G < n4) v[u] = x4[i0 + u * G];
+#pragma unroll
+            for (int u = 0; u < kVisitBatch; ++u)
+                if (i0 + u * G < n4) {
+                    f(abs_key(v[u].x));
+                    f(abs_key(v[u].y));
+                    f(abs_key(v[u].z));
+                    f(abs_key(v[u].w));
+                }
         }
         for (int64_t i = n4 * 4 + tid; i < n; i += G) f(abs_key(x[i]));
     } else {

@@ -42,6 +42,8 @@
 // Everything is stream-ordered; in DGC_SYNC_DEVICE mode kernels that turn out to
 // be unneeded early-exit on a device flag, so no host synchronisation happens.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <vector>
 
@@ -64,7 +66,7 @@ constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgrou
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole batch
 constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
 constexpr int kHeapMax = 4096;                  // K5b: exact partial_sort replay up to this k (heap in LDS)
-constexpr int kEmitSplit = 4;                   // k_emit workgroups per group when split (a wave emits 16 lists)
+constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
 constexpr int kHeapThreads = 512;                // = kNthThreads: K5b runs inside k_nth_select
 constexpr int kHeapPer = 16;                    // K5b: consecutive elements per thread per chunk
 
@@ -154,7 +156,6 @@ struct SelWS {
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     int64_t nseg, ngrp;
-    int32_t emit_split;        // k_emit workgroups per group (Layout::emit_split)
 };
 
 // Candidates the exact resample replays: torch's CPU topk runs nth_element while
@@ -178,12 +179,10 @@ struct Layout {
     int32_t nsmall = 0;
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool lowest_any = false;    // some tensor can take the approximate partial_sort resample
-    int32_t emit_split = 1;     // k_emit workgroups per group: kEmitSplit when the groups alone
-                                // give fewer workgroups than CUs (model gradient sets), else 1
     int64_t grid[BT_COUNT] = {};
 };
 
-static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, int emit_split) {
+static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg) {
     const int64_t cap = std::max<int64_t>(1, ceil_div((int64_t)kCapBlocks * d.nseg, std::max<int64_t>(1, total_seg)));
     switch (which) {
         case BT_K1: return ceil_div(d.nseg, (int64_t)kSegPerBlock4);
@@ -191,7 +190,7 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, in
         case BT_CAP16: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock16), cap);
         case BT_CAP4: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock4), cap);
         case BT_SEG: return ceil_div(d.nseg, (int64_t)kBlock);
-        case BT_GRP: return ceil_div(d.nseg, (int64_t)(kGroupSegs / emit_split));
+        case BT_GRP: return ceil_div(d.nseg, (int64_t)(kGroupSegs / kEmitSplit));
         case BT_QUEUE: return ceil_div(d.k, (int64_t)kQueuePerBlock);
         case BT_SAMP: {
             const int64_t cnt = d.samp_off < 0 ? d.n : d.S + 1;
@@ -249,13 +248,12 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
     L.ncand = cand;
     L.ngpos = gpos;
     L.nsmall = (int32_t)small.size();
-    L.emit_split = grp < 256 ? kEmitSplit : 1;
     for (int which = 0; which < BT_COUNT; ++which) {
         bt[which].assign(T + 1, 0);
         int64_t acc = 0;
         for (int32_t t = 0; t < T; ++t) {
             bt[which][t] = (int32_t)acc;
-            acc += bt_blocks(which, td[t], L.nseg, L.emit_split);
+            acc += bt_blocks(which, td[t], L.nseg);
         }
         bt[which][T] = (int32_t)acc;
         L.grid[which] = acc;
@@ -265,7 +263,6 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
 static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) {
     SelWS w{};
     w.T = L.T;
-    w.emit_split = L.emit_split;
     w.nseg = L.nseg;
     w.ngrp = L.ngrp;
     Carver c(base);
@@ -1332,21 +1329,27 @@ __device__ void emit_reread_resample(const float* __restrict__ vec, const TDesc&
     }
 }
 
-// w.emit_split (1 or kEmitSplit) workgroups per group of kGroupSegs segments. Each
-// scans the whole group's segment counts (one thread per segment: the in-group
-// offsets), then emits its share (64 or 16 lists per wave), wave per segment: kCap == 64 list slots, so lane l takes list entry l
-// (one coalesced load per list) and ballot ranks give the output positions. Each
-// wave emits kEmitBatch consecutive segments with all their list loads in flight
-// (one round trip); a spilled segment is re-read from vec by the same wave.
+// kEmitSplit workgroups of kEmitSegs threads per group of kGroupSegs segments, one
+// thread per segment of its quarter. In-group offsets: the quarter's exclusive scan
+// plus the counts of the group's earlier quarters (read by the same threads, packed
+// into the high half of the one 64-bit scan). Then
+//   short lists (<= kEmitShort entries, the common case once the list threshold
+//   tracks the selection): the thread emits its own segment, sequentially — its list
+//   loads go out before the scan;
+//   longer lists: wave per segment — kCap == 64 list slots, lane l takes entry l (one
+//   coalesced load per list), ballot ranks give the positions, kEmitBatch lists in
+//   flight per wave;
+//   spilled segments (> kCap entries): one wave re-reads the 1024 elements.
 // o.queue == null: the payload (every branch but a K5 resample, which k_emit_queue
 // writes). o.queue != null: K5's candidate gather — every element >= t_cur, ascending
 // (the reference's `indices` before its resample topk), only when K5 serves the tensor.
-constexpr int kEmitThreads = kGroupSegs;
+constexpr int kEmitSegs = kGroupSegs / kEmitSplit;   // segments per workgroup (a quarter group)
 constexpr int kEmitBatch = 16;
+constexpr int kEmitShort = 16;                  // lists up to this long: a thread emits its segment
 constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
 static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
 
-__global__ void __launch_bounds__(kEmitThreads)
+__global__ void __launch_bounds__(kEmitSegs)
 k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const int t = task(w, BT_GRP, blockIdx.x);
     const SelState* st = w.st + t;
@@ -1359,7 +1362,181 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const bool defer_here = o.defer && !rs && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
     const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
-    const int split = w.emit_split;
+    const int64_t lg = lb / kEmitSplit;                      // group within the tensor
+    const int sub = (int)(lb % kEmitSplit);                  // its quarter
+    const int64_t g = d.grp0 + lg;
+    const int64_t lseg0 = lg * kGroupSegs + (int64_t)sub * kEmitSegs;   // first segment of the quarter
+    __shared__ uint32_t off_a[kEmitSegs], off_b[kEmitSegs], lcn[kEmitSegs];
+    __shared__ uint64_t lds16[16];
+    __shared__ long long obase_s;
+    if (threadIdx.x < kWave) {
+        const long long b = k5 ? 0 : out_base(w, t);
+        if (threadIdx.x == 0) obase_s = b;
+    }
+    const long long limit = k5 ? st->n_cur : st->limit;
+    const long long T = st->tie_quota;
+    const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
+    const long long gb = rs ? w.grp_eq_off[g] : 0;
+    const float tc = st->t_cur, tk = st->tk;
+    {
+        // thread jq <-> segment jq of the quarter, plus the earlier quarters' counts at
+        // the same position
+        const int jq = (int)threadIdx.x;
+        const int64_t ls = lseg0 + jq;
+        const uint32_t* ca_src = rs ? w.seg_gt : w.seg_cnt;
+        uint32_t ca = 0, cb = 0, lc = 0, pa = 0, pb = 0;
+        if (ls < d.nseg) {
+            const int64_t seg = d.seg0 + ls;
+            ca = ca_src[seg];
+            if (rs) cb = w.seg_eq[seg];
+            lc = w.seg_lcnt[seg];
+        }
+        for (int q = 0; q < sub; ++q) {   // the same position in the group's earlier quarters
+            const int64_t seg = d.seg0 + lg * kGroupSegs + (int64_t)q * kEmitSegs + threadIdx.x;
+            pa += ca_src[seg];
+            if (rs) pb += w.seg_eq[seg];
+        }
+        const bool short_list = ls < d.nseg && lc > 0 && lc <= (uint32_t)kEmitShort;
+        float4 sv[kEmitShort / 4];
+        uint4 so[kEmitShort / 8];
+        if (short_list) {
+            const int64_t slot = (d.seg0 + ls) * kCap;
+            const float4* v4 = reinterpret_cast<const float4*>(w.lst_val + slot);
+            const uint4* o4 = reinterpret_cast<const uint4*>(w.lst_off + slot);
+#pragma unroll
+            for (int q = 0; q < kEmitShort / 4; ++q)
+                if ((uint32_t)(4 * q) < lc) sv[q] = v4[q];
+#pragma unroll
+            for (int q = 0; q < kEmitShort / 8; ++q)
+                if ((uint32_t)(8 * q) < lc) so[q] = o4[q];
+        }
+        // (earlier quarters' total << 32) | this quarter's counts: one scan gives both
+        uint64_t tot;
+        const uint64_t ra = block_exclusive_scan(((uint64_t)pa << 32) | ca, lds16, &tot);
+        const uint32_t oa = (uint32_t)(tot >> 32) + (uint32_t)ra;
+        uint32_t ob = 0;
+        if (rs) {
+            __syncthreads();
+            const uint64_t rb = block_exclusive_scan(((uint64_t)pb << 32) | cb, lds16, &tot);
+            ob = (uint32_t)(tot >> 32) + (uint32_t)rb;
+        }
+        const bool work = rs ? (ca > 0 || (cb > 0 && gb + ob < T)) : (ca > 0 && ga + oa < limit);
+        if (defer_here && ls < d.nseg) w.seg_off[d.seg0 + ls] = oa;
+        off_a[jq] = oa;
+        off_b[jq] = ob;
+        lcn[jq] = (work && !short_list) ? lc : kEmitSkip;
+        __syncthreads();   // obase_s
+        if (work && short_list) {
+            const long long ob0 = obase_s;
+            const float* v = reinterpret_cast<const float*>(sv);
+            const uint16_t* e = reinterpret_cast<const uint16_t*>(so);
+            if (!rs) {   // the first `limit` entries >= tc, in index order
+                long long pos = ga + oa;
+#pragma unroll
+                for (int j = 0; j < kEmitShort; ++j)
+                    if ((uint32_t)j < lc && fabsf(v[j]) >= tc) {
+                        if (pos < limit) emit_one(o, d, ob0 + pos, ls * kSeg + e[j], v[j], !defer_here);
+                        ++pos;
+                    }
+            } else {     // every entry > tk, and entries == tk while the tie rank is below T
+                long long rg = ga + oa, rt = gb + ob;
+#pragma unroll
+                for (int j = 0; j < kEmitShort; ++j) {
+                    if ((uint32_t)j >= lc) continue;
+                    const float a = fabsf(v[j]);
+                    if (a > tk) {
+                        emit_one(o, d, ob0 + rg + (rt < T ? rt : T), ls * kSeg + e[j], v[j]);
+                        ++rg;
+                    } else if (a == tk) {
+                        if (rt < T) emit_one(o, d, ob0 + rg + rt, ls * kSeg + e[j], v[j]);
+                        ++rt;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const long long obase = obase_s;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt();
+    // which of the wave's segments are left to it (longer lists) and which spilled:
+    // one LDS read and two ballots, so a wave with nothing left skips
+    constexpr int kWaveSegs = kEmitSegs / (kEmitSegs / kWave);   // 64: one ballot covers them
+    const int jw = wv * kWaveSegs;
+    const uint32_t Lme = lane < kWaveSegs ? lcn[jw + lane] : kEmitSkip;
+    uint64_t todo = __ballot(Lme != kEmitSkip && Lme <= (uint32_t)kCap);
+    uint64_t spilled = __ballot(Lme != kEmitSkip && Lme > (uint32_t)kCap);
+    for (int b0 = 0; b0 < kWaveSegs; b0 += kEmitBatch) {
+        if (!((todo >> b0) & ((1ull << kEmitBatch) - 1))) continue;   // nothing in this batch
+        const int j0 = jw + b0;
+        float x[kEmitBatch];
+        uint32_t e[kEmitBatch];
+#pragma unroll
+        for (int q = 0; q < kEmitBatch; ++q) {   // all list loads issued first
+            const uint32_t L = lcn[j0 + q];
+            x[q] = 0.f;
+            e[q] = 0;
+            if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
+                const int64_t slot = (d.seg0 + lseg0 + j0 + q) * kCap + lane;
+                x[q] = w.lst_val[slot];
+                e[q] = w.lst_off[slot];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kEmitBatch; ++q) {
+            const uint32_t L = lcn[j0 + q];
+            if (L == kEmitSkip || L > (uint32_t)kCap) continue;
+            const int64_t ls = lseg0 + j0 + q;
+            const long long ba = ga + off_a[j0 + q], bb = gb + off_b[j0 + q];
+            const bool in = (uint32_t)lane < L;
+            const float a = fabsf(x[q]);
+            const int64_t li = ls * kSeg + e[q];
+            if (!rs) {
+                const bool sel = in && a >= tc;
+                const uint64_t m = __ballot(sel);
+                const long long pos = ba + __popcll(m & lt);
+                if (sel && pos < limit) emit_one(o, d, obase + pos, li, x[q], !defer_here);
+            } else {
+                const bool gt = in && a > tk, eq = in && a == tk;
+                const uint64_t mg = __ballot(gt), me = __ballot(eq);
+                const long long tb = bb + __popcll(me & lt);
+                if (gt || (eq && tb < T)) emit_one(o, d, obase + ba + __popcll(mg & lt) + (tb < T ? tb : T), li, x[q]);
+            }
+        }
+    }
+    while (spilled) {   // rare: one wave re-reads the segment's 1024 elements
+        const int j = jw + __builtin_ctzll(spilled);
+        spilled &= spilled - 1;
+        const int64_t ls = lseg0 + j;
+        const long long ba = ga + off_a[j], bb = gb + off_b[j];
+        if (rs)
+            emit_reread_resample(vec, d, ls, ba, bb, tk, T, obase, o);
+        else
+            emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o, !defer_here);
+    }
+}
+
+
+
+// The few groups of a model gradient set: kEmitSplit workgroups of kGroupSegs threads
+// per group, each scanning the whole group (thread per segment) and emitting its
+// quarter with 16 waves of 16 segments — one list batch per wave, every list by a
+// wave. More waves per quarter beat k_emit's short-list threads there (measured on
+// ResNet-50: 12 vs 15 us per launch).
+__global__ void __launch_bounds__(kGroupSegs)
+k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+    const int t = task(w, BT_GRP, blockIdx.x);
+    const SelState* st = w.st + t;
+    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
+    const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
+    if (k5 != (o.queue != nullptr)) return;
+    const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    // first-k branches of an engine that defers: the next K1 zeroes what this emits
+    const bool defer_here = o.defer && !rs && !k5 && !d.tail;
+    const float* vec = vec_flat + d.off;
+    const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
+    constexpr int split = kEmitSplit;
     const int64_t lg = lb / split;                           // group within the tensor
     const int sub = (int)(lb % split);                       // its share this workgroup emits
     const int64_t g = d.grp0 + lg;
@@ -1400,8 +1577,8 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const float tc = st->t_cur, tk = st->tk;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt();
-    static_assert(kGroupSegs / kEmitSplit / (kEmitThreads / kWave) % kEmitBatch == 0, "whole batches per wave");
-    const int wave_segs = kGroupSegs / split / (kEmitThreads / kWave);
+    constexpr int wave_segs = kGroupSegs / split / (kGroupSegs / kWave);
+    static_assert(wave_segs % kEmitBatch == 0, "whole batches per wave");
     const int jw = sub * (kGroupSegs / split) + wv * wave_segs;
     for (int j0 = jw; j0 < jw + wave_segs; j0 += kEmitBatch) {
         float x[kEmitBatch];
@@ -1447,8 +1624,6 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         }
     }
 }
-
-
 
 // K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
 // wire casts and the masking of DGCSGDMemory.update.
@@ -1671,6 +1846,19 @@ static SelCfg cfg_of(const dgc_select_params& p) {
 
 // The selection of every tensor (its K1 lists kept or not), from k_sel_init to the
 // payload: stream-ordered, and in DGC_SYNC_DEVICE mode with no host synchronisation.
+// k_emit for many groups (flat buckets), k_emit_wide for few (model gradient sets).
+// DGC_EMIT_SHAPE=quarter|wide forces one (the parity tests run both at small sizes).
+static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const EmitOut& o, hipStream_t s) {
+    const char* force = std::getenv("DGC_EMIT_SHAPE");
+    const bool wide = force ? std::strcmp(force, "wide") == 0 : L.ngrp < 256;
+    if (wide)
+        hipLaunchKernelGGL(k_emit_wide, dim3((unsigned)L.grid[BT_GRP]), dim3(kGroupSegs), 0, s, vec, w, o);
+    else
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitSegs), 0, s, vec, w, o);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
                        int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists, int sync_mode,
                        float margin, hipStream_t s) {
@@ -1726,8 +1914,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         EmitOut g = o;
         g.queue = w.queue;
         g.cand = w.cand_idx;
-        hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitThreads), 0, s, vec, w, g);
-        DGC_LAUNCHED();
+        DGC_TRY(launch_emit(L, vec, w, g, s));
         hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o);
         DGC_LAUNCHED();
         hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
@@ -1785,8 +1972,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
             DGC_TRY(resample_exact());
         }
     }
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitThreads), 0, s, vec, w, o);
-    DGC_LAUNCHED();
+    DGC_TRY(launch_emit(L, vec, w, o, s));
     hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, count_out, info, margin,
                        (int)(p.update_memory == 2), (int)(p.masking != 0));
     DGC_LAUNCHED();

@@ -30,10 +30,15 @@ def _sets():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("label", ["mixed", "resnet50", "vgg16_bn"])
-def test_batch_matches_per_tensor_oracle(label):
+@pytest.mark.parametrize("label,shape", [("mixed", None), ("resnet50", None), ("vgg16_bn", None),
+                                         ("mixed", "quarter"), ("resnet50", "quarter")])
+def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
+    """shape: the emit kernel (None: the library's choice — k_emit_wide for these few
+    groups; "quarter": k_emit, the flat buckets' kernel, forced)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if shape:
+        monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
     from dgc.batch import DGCBatch
     shapes, fp16, int32 = _sets()[label]
     nest = label == "mixed"

@@ -704,10 +704,13 @@ def test_large_bucket_properties(L, N):
     (1_048_576, 0.05, "layered", [1, 1, 1, 0.1], "sparse"),
     (1_000_000, 0.001, "normal", [1, 3, 9, 27, 1], "sparse+poke"),   # out written in place: dense fallback
 ])
-def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill):
+@pytest.mark.parametrize("shape", [None, "quarter"])
+def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monkeypatch):
     """DGCBucket (speculative K1 lists, DGC_SYNC_DEVICE, side-stream zero fill + sparse
     scatter, the dense decompress, or the sparse re-zero of a persistent output) vs the
     oracle, step by step."""
+    if shape:   # the emit kernel of >= 256 groups (k_emit), forced at these sizes
+        monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
     poke = fill.endswith("+poke")
     fill = fill.split("+")[0]
     from dgc.bucket import DGCBucket
