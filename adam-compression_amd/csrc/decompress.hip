@@ -590,24 +590,40 @@ __global__ void __launch_bounds__(kBlock) k_clear_packed(RunSrc prev, float* __r
 //   one run          a thread per entry
 //   several runs     bounds + a wave per kSCB super-chunks + the workgroup path for
 //                    crowded super-chunks
-// prev (packed mode, null otherwise): grad holds the result of the previous call over
-// that payload; its entries are re-zeroed instead of the dense fill.
+// How grad is zeroed before the scatter (the reference's zero_()):
+enum ZeroMode {
+    kZeroNone,    // grad already +0.0 (dgc_fill_zero issued earlier): memset the status words
+    kZeroDense,   // dense fill; its first block resets the status words
+    kZeroPrev,    // re-zero the entries of `prev` (grad holds its result) + status words
+    kZeroDone,    // dgc_clear_packed already did kZeroPrev's work on this workspace
+};
+
+static ZeroWords status_words(const DecWS& w) {
+    return ZeroWords{{w.status, w.ovf_cnt, w.unsorted}, {1, 1, w.sort_cap ? kMaxRuns : 0}};
+}
+
+template <int ID>
+static int launch_clear(const RunSrc& prev, const DecWS& w, float* grad, int64_t n, hipStream_t s) {
+    const dim3 grid((unsigned)grid_for(prev.capacity, kBlock, kMaxGrid / 2), (unsigned)prev.world);
+    hipLaunchKernelGGL(k_clear_packed<ID>, grid, dim3(kBlock), 0, s, prev, grad, n, status_words(w));
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+// prev: the previous payload (kZeroPrev only).
 template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
-                       bool dense, int64_t entries, int64_t run_cap, int runs, hipStream_t s,
+                       int zmode, int64_t entries, int64_t run_cap, int runs, hipStream_t s,
                        const RunSrc* prev = nullptr) {
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
     // status, the overflow queue count and the unsorted flags are reset before any
     // kernel of this call can set them: by the dense fill's (or the sparse re-zero's)
     // first block, or memsets
-    const ZeroWords z{{w.status, w.ovf_cnt, w.unsorted}, {1, 1, w.sort_cap ? kMaxRuns : 0}};
-    if (prev) {
-        const dim3 grid((unsigned)grid_for(prev->capacity, kBlock, kMaxGrid / 2), (unsigned)prev->world);
-        hipLaunchKernelGGL(k_clear_packed<ID>, grid, dim3(kBlock), 0, s, *prev, grad, n, z);
-        DGC_LAUNCHED();
-    } else if (dense) {
-        DGC_TRY(fill_zero(grad, n, s, z));
-    } else {
+    if (zmode == kZeroPrev) {
+        DGC_TRY(launch_clear<ID>(*prev, w, grad, n, s));
+    } else if (zmode == kZeroDense) {
+        DGC_TRY(fill_zero(grad, n, s, status_words(w)));
+    } else if (zmode == kZeroNone) {
         if (w.sort_cap) DGC_HIP(hipMemsetAsync(w.unsorted, 0, kMaxRuns * sizeof(int32_t), s));
         DGC_HIP(hipMemsetAsync(w.status, 0, sizeof(int32_t), s));
         DGC_HIP(hipMemsetAsync(w.ovf_cnt, 0, sizeof(int32_t), s));
@@ -642,7 +658,7 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
 }
 
 static int dispatch_scatter(int vd, int id, const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
-                            float scale, int max_runs, bool dense, int64_t entries, int64_t run_cap, int runs,
+                            float scale, int max_runs, int dense, int64_t entries, int64_t run_cap, int runs,
                             hipStream_t s, const RunSrc* prev = nullptr) {
     if (vd == DGC_F32 && id == DGC_I64)
         return run_scatter<DGC_F32, DGC_I64>(w, rs, grad, n, scale, max_runs, dense, entries, run_cap, runs, s, prev);
@@ -709,7 +725,7 @@ int decompress(const void* values, int vd, const void* indices, int id, int64_t 
         known_runs = nr;
     }
     RunSrc rs{w.runs, w.nruns, nullptr, 0, 0, 0, 0, 0, nullptr, nullptr};
-    return dispatch_scatter(vd, id, w, rs, grad, n, scale, max_runs, true, total, total, known_runs, s);
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, max_runs, kZeroDense, total, total, known_runs, s);
 }
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff) {
@@ -722,7 +738,7 @@ int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t*
 
 int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity, int vd,
                       int id, float* grad, int64_t n, float scale, void* ws, size_t ws_bytes, hipStream_t s,
-                      bool dense, const void* prev = nullptr) {
+                      int zmode, const void* prev = nullptr) {
     DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world, capacity));
     int64_t voff, ioff;
     const int64_t min_stride = payload_layout(capacity, vd, id, &voff, &ioff);
@@ -732,15 +748,30 @@ int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, i
     DecWS w = carve_dec(ws, n, world, capacity);
     RunSrc rs{nullptr, nullptr, static_cast<const char*>(payload), rank_stride, voff, ioff, capacity, world,
               w.unsorted, w.sorted};
-    if (prev) {
+    if (zmode == kZeroPrev) {
         if (prev == payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed_over: prev must be another buffer");
         const RunSrc pr{nullptr, nullptr, static_cast<const char*>(prev), rank_stride, voff, ioff, capacity, world,
                         nullptr, nullptr};
-        return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, false, (int64_t)world * capacity, capacity,
+        return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, zmode, (int64_t)world * capacity, capacity,
                                 world, s, &pr);
     }
-    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, dense, (int64_t)world * capacity, capacity,
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world, zmode, (int64_t)world * capacity, capacity,
                             world, s);
+}
+
+// dgc_clear_packed: kZeroPrev's re-zero alone (see dgc_hip.h).
+int clear_packed(const void* prev, int32_t world, int64_t rank_stride, int64_t capacity, int vd, int id,
+                 float* grad, int64_t n, void* ws, size_t ws_bytes, hipStream_t s) {
+    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world, capacity));
+    int64_t voff, ioff;
+    const int64_t min_stride = payload_layout(capacity, vd, id, &voff, &ioff);
+    if (!prev || rank_stride < min_stride || capacity < 0)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_clear_packed: null payload or rank_stride %lld < layout %lld",
+                 (long long)rank_stride, (long long)min_stride);
+    DecWS w = carve_dec(ws, n, world, capacity);
+    const RunSrc pr{nullptr, nullptr, static_cast<const char*>(prev), rank_stride, voff, ioff, capacity, world,
+                    nullptr, nullptr};
+    return id == DGC_I32 ? launch_clear<DGC_I32>(pr, w, grad, n, s) : launch_clear<DGC_I64>(pr, w, grad, n, s);
 }
 
 // Zero fill (the sparse scatter's precondition): one-shot workgroups, one 16-B
@@ -834,7 +865,7 @@ extern "C" int dgc_decompress_packed(const void* payload, int32_t world, int64_t
                                      int64_t capacity, int32_t vdtype, int32_t idtype, float* grad,
                                      int64_t n, float scale, void* ws, size_t ws_bytes, void* stream) {
     return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
-                                  ws_bytes, static_cast<hipStream_t>(stream), true);
+                                  ws_bytes, static_cast<hipStream_t>(stream), dgc::kZeroDense);
 }
 
 extern "C" int dgc_decompress_packed_over(const void* payload, const void* prev_payload, int32_t world,
@@ -843,14 +874,28 @@ extern "C" int dgc_decompress_packed_over(const void* payload, const void* prev_
                                           void* stream) {
     if (!prev_payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed_over: null prev_payload");
     return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
-                                  ws_bytes, static_cast<hipStream_t>(stream), false, prev_payload);
+                                  ws_bytes, static_cast<hipStream_t>(stream), dgc::kZeroPrev, prev_payload);
+}
+
+extern "C" int dgc_clear_packed(const void* prev_payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                                int32_t vdtype, int32_t idtype, float* grad, int64_t n, void* ws, size_t ws_bytes,
+                                void* stream) {
+    return dgc::clear_packed(prev_payload, world, rank_stride, capacity, vdtype, idtype, grad, n, ws, ws_bytes,
+                             static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_scatter_packed_cleared(const void* payload, int32_t world, int64_t rank_stride,
+                                          int64_t capacity, int32_t vdtype, int32_t idtype, float* grad, int64_t n,
+                                          float scale, void* ws, size_t ws_bytes, void* stream) {
+    return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
+                                  ws_bytes, static_cast<hipStream_t>(stream), dgc::kZeroDone);
 }
 
 extern "C" int dgc_scatter_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
                                   int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, void* ws,
                                   size_t ws_bytes, void* stream) {
     return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
-                                  ws_bytes, static_cast<hipStream_t>(stream), false);
+                                  ws_bytes, static_cast<hipStream_t>(stream), dgc::kZeroNone);
 }
 
 extern "C" int dgc_decompress_status(const void* ws, int32_t* status, void* stream) {

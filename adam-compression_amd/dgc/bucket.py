@@ -21,8 +21,10 @@ every decision kept on the device:
   bucket: when it is the tensor the previous step decompressed into and nobody has
   written it since (same storage, same torch version counter), it is +0.0 except at
   the previous step's W*k gathered indices, so ``zero_()`` is a sparse re-zero of
-  those slots (``dgc_decompress_packed_over``) — W*k scattered stores instead of a
-  4 B/elem stream; the dense result is the same, bit for bit. Any other ``out``
+  those slots — W*k scattered stores instead of a 4 B/elem stream, issued on a side
+  stream at the start of the step so they run under K1 (``dgc_clear_packed``, then
+  ``dgc_scatter_packed_cleared``; ``decompress`` alone does both in one call,
+  ``dgc_decompress_packed_over``); the dense result is the same, bit for bit. Any other ``out``
   (first step, a new tensor, one modified in place) gets the dense fill. The
   payload (W = 1) / gather buffer (W > 1) alternates between two buffers so the
   previous step's indices survive the current step.
@@ -108,7 +110,7 @@ class DGCBucket:
         self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(N, self.world, self.k), dtype=torch.uint8, device=dev)
         self.scale = 1.0 / self.world
         self._L = L
-        if fill == "allgather":
+        if fill in ("allgather", "sparse"):
             self.side = torch.cuda.Stream(device=dev)
             self._ev_go = torch.cuda.Event()
             self._ev_filled = torch.cuda.Event()
@@ -180,19 +182,38 @@ class DGCBucket:
         re-zeroes only the previous entries (see the module docstring)."""
         L = self._L
         cur = self.gathered
-        args = (self.world, self.rank_stride, self.k, _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
-                self.numel, self.scale, self.dec_ws.data_ptr(), self.dec_ws.numel(), _lib.stream_of(self.device))
-        if (dense and self.fill == "sparse" and self._last_gathered is not None and self._last_gathered is not cur
-                and self._last_out == (out.data_ptr(), out.numel(), out._version)):
+        args = self._dec_args(out)
+        if dense and self.fill == "sparse" and self._reusable(out) and self._last_gathered is not cur:
             _lib.check(L.dgc_decompress_packed_over(cur.data_ptr(), self._last_gathered.data_ptr(), *args),
                        "dgc_decompress_packed_over")
         else:
             fn = L.dgc_decompress_packed if dense else L.dgc_scatter_packed
             _lib.check(fn(cur.data_ptr(), *args), "dgc_decompress_packed" if dense else "dgc_scatter_packed")
-        # the raw-pointer writes leave torch's version counter alone: any later in-place
-        # write to out (or a view of it) changes it, and the next step fills densely
+        self._remember(out, cur)
+
+    def _dec_args(self, out):
+        return (self.world, self.rank_stride, self.k, _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
+                self.numel, self.scale, self.dec_ws.data_ptr(), self.dec_ws.numel(), _lib.stream_of(self.device))
+
+    def _reusable(self, out):
+        """out still holds exactly the last decompress's result: same storage, and no
+        in-place write since (torch's version counter; ours are raw-pointer writes)."""
+        return self._last_gathered is not None and self._last_out == (out.data_ptr(), out.numel(), out._version)
+
+    def _remember(self, out, cur):
         self._last_out = (out.data_ptr(), out.numel(), out._version)
         self._last_gathered = cur
+
+    def _clear_on_side(self, out):
+        """The sparse re-zero of the previous step's entries, on the side stream at the
+        start of the step (ordered after everything already issued, e.g. an optimizer
+        reading out), so it runs under K1 instead of before the scatter."""
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        _lib.check(self._L.dgc_clear_packed(self._last_gathered.data_ptr(), self.world, self.rank_stride, self.k,
+                                            _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(), self.numel,
+                                            self.dec_ws.data_ptr(), self.dec_ws.numel(), self.side.cuda_stream),
+                   "dgc_clear_packed")
+        self._ev_filled.record(self.side)
 
     def _fill_on_side(self, out):
         """zero_() of the output on the side stream, ordered after the event recorded
@@ -206,9 +227,18 @@ class DGCBucket:
         ``events`` maps a phase name to a (start, end) pair of torch.cuda.Event recorded
         around it on the current stream."""
         ev = events or {}
+        cleared = self.fill == "sparse" and self._reusable(out)
+        if cleared:
+            self._clear_on_side(out)
 
         def decompress():
-            if self.fill != "allgather":
+            if cleared:   # the entries onto the re-zeroed output
+                torch.cuda.current_stream(self.device).wait_event(self._ev_filled)
+                cur = self.gathered
+                _lib.check(self._L.dgc_scatter_packed_cleared(cur.data_ptr(), *self._dec_args(out)),
+                           "dgc_scatter_packed_cleared")
+                self._remember(out, cur)
+            elif self.fill != "allgather":
                 self.decompress(out)
             else:
                 torch.cuda.current_stream(self.device).wait_event(self._ev_filled)

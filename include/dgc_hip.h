@@ -21,7 +21,8 @@
  *   dgc_decompress_packed the same, straight from the padded RCCL allgather buffer
  *   dgc_scatter_packed    its sparse form (zero_() done earlier by dgc_fill_zero)
  *   dgc_decompress_packed_over  the same into a persistent output that holds the
- *                         previous call's result (zero_() as a sparse re-zero)
+ *                         previous call's result (zero_() as a sparse re-zero);
+ *                         dgc_clear_packed + dgc_scatter_packed_cleared: its two halves
  *   dgc_sgd_step          DGCSGD.step (weight-decay momentum + update) dgc/optim/sgd.py:42-68
  *
  * Conventions
@@ -290,6 +291,18 @@ int dgc_decompress_packed_over(const void* payload, const void* prev_payload, in
                                int64_t rank_stride, int64_t capacity, int32_t vdtype, int32_t idtype,
                                float* grad, int64_t n, float scale, void* ws, size_t ws_bytes,
                                void* stream);
+/* dgc_decompress_packed_over in two calls, so the re-zero can run on another stream
+ * while the compress and the allgather run: dgc_clear_packed re-zeroes prev_payload's
+ * entries in grad (same precondition) and resets the status words of `ws` (the
+ * dgc_decompress_packed_workspace of the scatter to come); dgc_scatter_packed_cleared
+ * then writes the new payload's entries, ordered after the clear by the caller, with
+ * that workspace untouched in between. */
+int dgc_clear_packed(const void* prev_payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                     int32_t vdtype, int32_t idtype, float* grad, int64_t n, void* ws, size_t ws_bytes,
+                     void* stream);
+int dgc_scatter_packed_cleared(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                               int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, void* ws,
+                               size_t ws_bytes, void* stream);
 /* grad[0..n) = +0.0 with one-shot 16-B stores (4-B aligned buffer; a scalar head up to
  * the first 16-B boundary). */
 int dgc_fill_zero(float* grad, int64_t n, void* stream);

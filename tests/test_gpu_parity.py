@@ -534,7 +534,8 @@ def test_sparse_scatter_matches_dense_decompress(L, N, W, cap, overlap, fp16, in
     (300_000, 8, 30000, False, False, 2),
 ])
 def test_decompress_over_previous_output(L, N, W, cap, fp16, int32, shuffled):
-    """dgc_decompress_packed_over: a persistent output that holds the previous payload's
+    """dgc_decompress_packed_over (and its two halves, dgc_clear_packed +
+    dgc_scatter_packed_cleared): a persistent output that holds the previous payload's
     decompress is re-zeroed at those indices only; the result equals the dense
     decompress of the new payload bit for bit, over overlapping / disjoint / shuffled
     runs and three steps."""
@@ -560,9 +561,13 @@ def test_decompress_over_previous_output(L, N, W, cap, fp16, int32, shuffled):
         if prev is None:
             check(L, L.dgc_decompress_packed(P(tp), W, stride, cap, vd, idt, P(out), N, 1.0 / W, P(ws), wsz,
                                              stream()))
-        else:
+        elif step == 1:
             check(L, L.dgc_decompress_packed_over(P(tp), P(prev), W, stride, cap, vd, idt, P(out), N, 1.0 / W,
                                                   P(ws), wsz, stream()))
+        else:   # the same in two calls (the engine issues the clear on a side stream)
+            check(L, L.dgc_clear_packed(P(prev), W, stride, cap, vd, idt, P(out), N, P(ws), wsz, stream()))
+            check(L, L.dgc_scatter_packed_cleared(P(tp), W, stride, cap, vd, idt, P(out), N, 1.0 / W, P(ws), wsz,
+                                                  stream()))
         st = ctypes.c_int32(-1)
         check(L, L.dgc_decompress_status(P(ws), ctypes.byref(st), stream()))
         torch.cuda.synchronize()

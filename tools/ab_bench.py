@@ -1,9 +1,11 @@
-"""Same-box A/B of whole bench steps: `python tools/ab_bench.py WORKLOAD LIB_A LIB_B [reps]`
-runs `bench.py --workload WORKLOAD --no-cpu` with DGC_HIP_LIB = each library in turn,
-alternating `reps` times, and prints ms/step, K1 ms and the phase times per run (MI355X
-boxes differ by ~10 %, so only same-box comparisons mean anything). Both libraries must
-export the symbols dgc/_lib.py binds (build the other one from a nearby revision:
-`make -C <old csrc> OUT_DIR=<repo>/adam-compression_amd/lib/ab_old`)."""
+"""Same-box A/B of whole bench steps: `python tools/ab_bench.py WORKLOAD A B [reps]`
+runs `bench.py --workload WORKLOAD --no-cpu` for A and B in turn, alternating `reps`
+times, and prints ms/step, K1 ms and the phase times per run (MI355X boxes differ by
+~10 %, so only same-box comparisons mean anything). A / B: a library (this tree's
+bench.py with DGC_HIP_LIB = it; it must export the symbols dgc/_lib.py binds — build it
+from a nearby revision: `make -C <old csrc> OUT_DIR=<repo>/adam-compression_amd/lib/ab_old`)
+or a directory holding a whole tree with its built library (`git worktree add .ab_head
+HEAD` + make), whose own bench.py runs — for changes above the library."""
 import json
 import os
 import subprocess
@@ -17,8 +19,12 @@ def main():
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     for _ in range(reps):
         for lib in libs:
-            env = dict(os.environ, DGC_HIP_LIB=os.path.abspath(lib))
-            out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--workload", wl, "--no-cpu",
+            if os.path.isdir(lib):
+                env, root = dict(os.environ), os.path.abspath(lib)
+                env.pop("DGC_HIP_LIB", None)
+            else:
+                env, root = dict(os.environ, DGC_HIP_LIB=os.path.abspath(lib)), REPO
+            out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--workload", wl, "--no-cpu",
                                   "--steps", "20", "--warmup", "5"], env=env, check=True, capture_output=True,
                                  text=True).stdout
             d = json.loads(out.strip().splitlines()[-1])

@@ -3,9 +3,11 @@
   python tools/dec_bench.py [--W 8] [--numel 1e9] [--reps 10]
 
 Builds W synthetic packed payloads of k = N/1000 ascending random indices each (the
-shape of the 1B-bucket allgather output) and times dgc_fill_zero, dgc_scatter_packed
-(sparse, onto a zeroed buffer) and dgc_decompress_packed (dense), `reps` times each;
-prints the average ms of each (HIP events on the current stream).
+shape of the 1B-bucket allgather output), twice (this step's and the previous one's),
+and times dgc_fill_zero, dgc_scatter_packed (sparse, onto a zeroed buffer),
+dgc_decompress_packed (dense) and dgc_decompress_packed_over (the sparse re-zero of
+the previous payload's entries + the scatter), `reps` times each; prints the average
+ms of each (HIP events on the current stream).
 """
 import argparse
 import json
@@ -44,15 +46,20 @@ def main():
     dev = torch.device("cuda:0")
     L = _lib.lib()
     stride, voff, ioff = _layout(k, torch.float32, torch.int64)
-    pay = torch.zeros(W * stride, dtype=torch.uint8, device=dev)
     gen = torch.Generator(device=dev).manual_seed(3)
-    for r in range(W):
-        idx = torch.sort(torch.randperm(N, device=dev, generator=gen)[:k]).values
-        row = pay[r * stride:(r + 1) * stride]
-        row[:8].view(torch.int64).fill_(k)
-        row[voff:voff + 4 * k].view(torch.float32).copy_(torch.randn(k, device=dev, generator=gen))
-        row[ioff:ioff + 8 * k].view(torch.int64).copy_(idx)
-        del idx
+
+    def payload():
+        pay = torch.zeros(W * stride, dtype=torch.uint8, device=dev)
+        for r in range(W):
+            idx = torch.sort(torch.randperm(N, device=dev, generator=gen)[:k]).values
+            row = pay[r * stride:(r + 1) * stride]
+            row[:8].view(torch.int64).fill_(k)
+            row[voff:voff + 4 * k].view(torch.float32).copy_(torch.randn(k, device=dev, generator=gen))
+            row[ioff:ioff + 8 * k].view(torch.int64).copy_(idx)
+            del idx
+        return pay
+
+    pay, prev = payload(), payload()
     out = torch.empty(N, device=dev)
     ws = torch.empty(L.dgc_decompress_packed_workspace(N, W, k), dtype=torch.uint8, device=dev)
     s = _lib.stream_of(dev)
@@ -68,9 +75,14 @@ def main():
         _lib.check(L.dgc_decompress_packed(pay.data_ptr(), W, stride, k, 0, 0, out.data_ptr(), N, 1.0 / W,
                                            ws.data_ptr(), ws.numel(), s), "dgc_decompress_packed")
 
+    def over():
+        _lib.check(L.dgc_decompress_packed_over(pay.data_ptr(), prev.data_ptr(), W, stride, k, 0, 0, out.data_ptr(),
+                                                N, 1.0 / W, ws.data_ptr(), ws.numel(), s),
+                   "dgc_decompress_packed_over")
+
     res = {"W": W, "numel": N, "k": k,
            "fill_ms": timeit(fill, args.reps), "scatter_ms": timeit(scatter, args.reps),
-           "dense_ms": timeit(dense, args.reps)}
+           "dense_ms": timeit(dense, args.reps), "over_ms": timeit(over, args.reps)}
     print(json.dumps(res), flush=True)
 
 
