@@ -1396,7 +1396,8 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
             pa += ca_src[seg];
             if (rs) pb += w.seg_eq[seg];
         }
-        const bool short_list = ls < d.nseg && lc > 0 && lc <= (uint32_t)kEmitShort;
+        // (a list with nothing at the current threshold is not read: most of them at 1e-4)
+        const bool short_list = ls < d.nseg && (ca > 0 || cb > 0) && lc <= (uint32_t)kEmitShort;
         float4 sv[kEmitShort / 4];
         uint4 so[kEmitShort / 8];
         if (short_list) {

@@ -227,7 +227,12 @@ class DGCBucket:
         ``events`` maps a phase name to a (start, end) pair of torch.cuda.Event recorded
         around it on the current stream."""
         ev = events or {}
-        cleared = self.fill == "sparse" and self._reusable(out)
+        # an output that shares storage with the gradient (the reference's in-place
+        # layout) is rewritten with each new gradient: always the dense fill there
+        aliased = out.untyped_storage().data_ptr() == grad.untyped_storage().data_ptr()
+        if aliased:
+            self._last_out = None
+        cleared = self.fill == "sparse" and not aliased and self._reusable(out)
         if cleared:
             self._clear_on_side(out)
 
@@ -240,6 +245,8 @@ class DGCBucket:
                 self._remember(out, cur)
             elif self.fill != "allgather":
                 self.decompress(out)
+                if aliased:
+                    self._last_out = None
             else:
                 torch.cuda.current_stream(self.device).wait_event(self._ev_filled)
                 self.decompress(out, dense=False)

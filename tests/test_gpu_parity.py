@@ -708,6 +708,7 @@ def test_large_bucket_properties(L, N):
     (3_000_003, 0.001, "normal", [1, 1, 1, 1, 1], "sparse"),  # persistent output: sparse re-zero
     (1_048_576, 0.05, "layered", [1, 1, 1, 0.1], "sparse"),
     (1_000_000, 0.001, "normal", [1, 3, 9, 27, 1], "sparse+poke"),   # out written in place: dense fallback
+    (1_000_000, 0.001, "normal", [1, 1, 1, 1], "sparse+alias"),      # out is the gradient buffer itself
 ])
 @pytest.mark.parametrize("shape", [None, "quarter"])
 def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monkeypatch):
@@ -717,6 +718,7 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monke
     if shape:   # the emit kernel of >= 256 groups (k_emit), forced at these sizes
         monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
     poke = fill.endswith("+poke")
+    alias = fill.endswith("+alias")
     fill = fill.split("+")[0]
     from dgc.bucket import DGCBucket
     b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=7, fill=fill)
@@ -728,7 +730,13 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monke
     for s, sc in enumerate(scales):
         g = synth.gradient(300 + s, N, kind, float(sc))
         start = rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
-        b.step(to_dev(g), out)
+        if alias:   # the reference's in-place layout: decompress into the gradient compressed;
+            # written through .data, which leaves out's version counter alone, so only the
+            # storage-aliasing guard keeps the sparse re-zero off
+            out.data.copy_(to_dev(g))
+            b.step(out, out)
+        else:
+            b.step(to_dev(g), out)
         torch.cuda.synchronize()
         info = b.last_info()
         ov, oi, oinfo = O.compress_step(g, m_o, v_o, attrs, start, nesterov=True)

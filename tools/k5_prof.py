@@ -31,7 +31,8 @@ def main():
     L.dgc_k5_prof.restype = ctypes.c_int
     L.dgc_k5_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
     cases = [(400_000, 400, 2_000), (1_000_000, 1000, 6_000), (2_000_000, 2000, 12_000),
-             (4_000_000, 2360, 30_000), (10_000_000, 10_000, 100_000), (100_000_000, 102_761, 1_000_000)]
+             (4_000_000, 2360, 30_000), (4_000_000, 2360, 57_000), (10_000_000, 10_000, 100_000),
+             (100_000_000, 102_761, 1_000_000)]
     for n, k, target in cases:
         select_case(L, n, k, target, reps=1)
         best = None
