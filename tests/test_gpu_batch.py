@@ -20,6 +20,13 @@ def bits(a):
     return a.view({4: np.uint32, 2: np.uint16, 8: np.uint64}[a.dtype.itemsize])
 
 
+def _same_or_nan(a, b):
+    """Bitwise equal, except that NaN matches NaN (numpy and the GPU may carry different
+    NaN payloads through the momentum arithmetic)."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return bool(np.all((np.isnan(a) & np.isnan(b)) | (bits(a) == bits(b))))
+
+
 def _sets():
     from dgc import workloads
     r50, _ = workloads.split(workloads.resnet50())
@@ -31,15 +38,20 @@ def _sets():
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("label,shape", [("mixed", None), ("resnet50", None), ("vgg16_bn", None),
-                                         ("mixed", "quarter"), ("resnet50", "quarter")])
+                                         ("mixed", "quarter"), ("resnet50", "quarter"), ("mixed+naninf", None)])
 def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
     """shape: the emit kernel (None: the library's choice — k_emit_wide for these few
-    groups; "quarter": k_emit, the flat buckets' kernel, forced)."""
+    groups; "quarter": k_emit, the flat buckets' kernel, forced). "+naninf": tensor "b"
+    gets a NaN at one of its samples on step 1 (its threshold turns NaN, nothing of it
+    is selected), "odd" a NaN that is never sampled and "c" +-inf — the other tensors'
+    selections must not notice."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if shape:
         monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
     from dgc.batch import DGCBatch
+    naninf = label.endswith("+naninf")
+    label = label.split("+")[0]
     shapes, fp16, int32 = _sets()[label]
     nest = label == "mixed"
     b = DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, nesterov=nest, fp16_values=fp16,
@@ -54,12 +66,20 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
         # other steps leave it to the next K1 (the bench's path)
         check_state = s % 2 == 1 or s == steps - 1
         grads = {}
+        starts = b.draw_starts()
         for t, name in enumerate(b.names):
             kind = "ties" if name == "ties" else ("layered" if t % 3 == 0 else "normal")
             g = synth.gradient(1000 * s + t, b.numels[t], kind, 1e-3 * (1 + t % 7))
+            if naninf:
+                stride = b.attrs[t][3]
+                if name == "b" and s == 1:
+                    g[7 * stride + starts[t]] = np.nan                       # sampled this step
+                if name == "odd" and s == 0:
+                    g[5 * stride + (starts[t] + 1) % stride] = np.nan      # a residue not sampled at s=0
+                if name == "c":
+                    g[[11 + s, 5000 + s]] = [np.inf, -np.inf]
             grads[name] = g
             b.grad(name).copy_(torch.from_numpy(g).view(b.shapes[name]))
-        starts = b.draw_starts()
         b.compress(starts)
         out = b.decompress()
         torch.cuda.synchronize()
@@ -80,8 +100,10 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
             assert np.array_equal(gi.cpu().numpy(), oi), key
             assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
             if check_state:
-                assert np.array_equal(bits(b.momentum_of(name).reshape(-1).cpu().numpy()), bits(m_o)), key
-                assert np.array_equal(bits(b.velocity_of(name).reshape(-1).cpu().numpy()), bits(v_o)), key
+                assert _same_or_nan(b.momentum_of(name).reshape(-1).cpu().numpy(), m_o), key
+                assert _same_or_nan(b.velocity_of(name).reshape(-1).cpu().numpy(), v_o), key
+            if naninf and name == "b" and s == 1:
+                assert np.isnan(infos[t]["threshold0"]) and infos[t]["count"] == 0, (key, infos[t])
             dense = O.decompress([wv], [oi], N, 1)
             assert np.array_equal(bits(b.out(name).reshape(-1).cpu().numpy()), bits(dense)), key
         # padding between tensors stays zero (no tensor writes outside itself)

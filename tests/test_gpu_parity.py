@@ -757,6 +757,62 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monke
         assert served_by_lists >= 3        # the steady state skips the re-read of vec
 
 
+def _same_bits_or_nan(a, b):
+    """Bitwise equal, except that any NaN matches any NaN (numpy and the GPU may carry
+    different NaN payloads through the momentum arithmetic)."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all(both_nan | (bits(a) == bits(b))))
+
+
+@pytest.mark.parametrize("case", ["nan_unsampled", "nan_sampled"])
+def test_bucket_nan_inf_gradients_match_oracle(L, case):
+    """NaN and +-inf gradients through DGCBucket against the oracle: an inf is selected
+    like any large value; a NaN is never selected (|NaN| >= t is false) and stays in
+    the velocity; a NaN among the strided samples makes the threshold NaN (topk ranks
+    it first, min propagates it, dgc/compression.py:123) and nothing is selected,
+    through the whole adaptation loop. (NaN inputs: parity against the oracle's
+    restatement of torch's NaN ordering; the reference's goldens hold no NaN.)"""
+    from dgc.bucket import DGCBucket
+    N, ratio = 1_000_003, 0.001
+    attrs = O.attributes(N, ratio)
+    stride = attrs[4]
+    rng = random.Random(11)
+    starts = [rng.randint(0, stride - 1) for _ in range(4)]
+    free = [r for r in range(stride) if r not in starts]   # residues no step samples
+    b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=11)
+    m_o, v_o = np.zeros(N, np.float32), np.zeros(N, np.float32)
+    out = torch.empty(N, device=DEV)
+    nan_thresholds, inf_sent = 0, 0
+    for s, start in enumerate(starts):
+        g = synth.gradient(700 + s, N, "normal")
+        g[[(1000 + s) * stride + free[0], (2000 + s) * stride + free[1]]] = [np.inf, -np.inf]
+        if case == "nan_unsampled":
+            g[(500 + s) * stride + free[2]] = np.nan
+        elif s in (1, 3):
+            g[(300 + s) * stride + start] = np.nan                 # sampled at this step
+        b.step(to_dev(g), out)
+        torch.cuda.synchronize()
+        info = b.last_info()
+        ov, oi, oinfo = O.compress_step(g, m_o, v_o, attrs, start, nesterov=True)
+        n = int(b.payload[:8].view(torch.int64).item())
+        gi = b.payload[b.ioff: b.ioff + 8 * n].view(torch.int64).cpu().numpy()
+        gv = b.payload[b.voff: b.voff + 4 * n].view(torch.float32).cpu().numpy()
+        assert info["branch"] == oinfo["branch"], (s, info, oinfo)
+        assert np.array_equal(gi, oi), (s, info)
+        assert _same_bits_or_nan(gv, ov), s
+        assert _same_bits_or_nan(np.float32(info["threshold0"]), oinfo["thresholds"][0]), (s, info)
+        nan_thresholds += bool(np.isnan(info["threshold0"]))
+        inf_sent += int(np.isinf(gv).sum())
+        if np.isnan(info["threshold0"]):
+            assert n == 0, info
+        assert _same_bits_or_nan(b.vec.cpu().numpy(), v_o), s
+        assert _same_bits_or_nan(b.mmt.cpu().numpy(), m_o), s
+        assert np.array_equal(bits(out.cpu().numpy()), bits(O.decompress([ov], [oi], N, 1))), s
+    assert inf_sent > 0
+    assert nan_thresholds == (2 if case == "nan_sampled" else 0)
+
+
 def test_bucket_deferred_masking_equals_immediate(L):
     """The deferred masking (first-k branches leave DGCSGDMemory.update's zeroing to the
     next K1) against the immediate one: identical payloads every step, identical
