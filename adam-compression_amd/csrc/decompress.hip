@@ -573,11 +573,21 @@ __global__ void __launch_bounds__(kBlock) k_clear_packed(RunSrc prev, float* __r
         for (int q = 0; q < 3; ++q)
             for (int j = threadIdx.x; j < z.n[q]; j += kBlock) z.p[q][j] = 0;
     }
+    // four lanes per entry zero the entry's whole 64-B granule (everything else in it
+    // is +0.0 already, or another previous entry): full-granule stores, not 4-B partial
+    // writes — 1.7x the line rate at 8M scattered lines (tools/scatterbench.hip)
     const Run run = prev.get_raw((int)blockIdx.y);
-    for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < run.count;
-         e += (long long)gridDim.x * kBlock) {
-        const long long i = load_idx<ID>(run.idx, e);
-        if (i >= 0 && i < n) grad[i] = 0.f;
+    const int part = (int)(threadIdx.x & 3);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(grad), hi = reinterpret_cast<uintptr_t>(grad + n);
+    for (long long t = (long long)blockIdx.x * kBlock + threadIdx.x; t < 4 * run.count;
+         t += (long long)gridDim.x * kBlock) {
+        const long long i = load_idx<ID>(run.idx, t >> 2);
+        if (i < 0 || i >= n) continue;
+        const uintptr_t g = reinterpret_cast<uintptr_t>(grad + i) & ~(uintptr_t)63;
+        if (g >= lo && g + 64 <= hi)
+            reinterpret_cast<float4*>(g)[part] = make_float4(0.f, 0.f, 0.f, 0.f);
+        else if (part == 0)
+            grad[i] = 0.f;   // a granule that crosses the buffer's ends: the word alone
     }
 }
 
@@ -604,7 +614,7 @@ static ZeroWords status_words(const DecWS& w) {
 
 template <int ID>
 static int launch_clear(const RunSrc& prev, const DecWS& w, float* grad, int64_t n, hipStream_t s) {
-    const dim3 grid((unsigned)grid_for(prev.capacity, kBlock, kMaxGrid / 2), (unsigned)prev.world);
+    const dim3 grid((unsigned)grid_for(4 * prev.capacity, kBlock, kMaxGrid / 2), (unsigned)prev.world);
     hipLaunchKernelGGL(k_clear_packed<ID>, grid, dim3(kBlock), 0, s, prev, grad, n, status_words(w));
     DGC_LAUNCHED();
     return DGC_OK;
