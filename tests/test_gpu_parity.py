@@ -578,6 +578,33 @@ def test_decompress_over_previous_output(L, N, W, cap, fp16, int32, shuffled):
                                         stream()) != 0
 
 
+@pytest.mark.parametrize("lead", [0, 1, 3])
+def test_multi_run_decompress_into_offset_view(L, lead):
+    """W = 4 runs decompressed into grad = buf[lead:]: with lead != 0 the 64-B granules
+    straddle the 4096-element chunks, so lone entries must fall back to word stores at
+    chunk edges (k_scatter_waves writes whole granules only inside its super-chunk)."""
+    N, W, cap = 600_000, 4, 1500   # ~40 entries per 4096-element chunk: the wave path, granule stores on
+    rng = np.random.default_rng(lead + 40)
+    runs = []
+    for r in range(W):
+        idx = np.sort(rng.choice(N, cap, replace=False))
+        idx[:8] = np.arange(4090, 4106)[r::2][:8] if r < 2 else idx[:8]   # entries around a chunk edge
+        idx = np.unique(idx)
+        runs.append((rng.standard_normal(idx.size).astype(np.float32), idx.astype(np.int64)))
+    payload, stride, vd, idt = _packed(L, runs, cap, False, False)
+    want = O.decompress([v for v, _ in runs], [i for _, i in runs], N, W)
+    tp = to_dev(payload)
+    wsz = L.dgc_decompress_packed_workspace(N, W, cap)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    buf = torch.full((N + lead,), float("nan"), device=DEV)
+    out = buf[lead:]
+    check(L, L.dgc_decompress_packed(P(tp), W, stride, cap, vd, idt, P(out), N, 1.0 / W, P(ws), wsz, stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(out.cpu().numpy()), bits(want))
+    if lead:
+        assert bool(torch.isnan(buf[:lead]).all())   # nothing written before the view
+
+
 def test_sparse_scatter_flags_out_of_range(L):
     N, cap = 10_000, 8
     for W in (1, 3):
