@@ -36,6 +36,9 @@ struct RSState {
     uint64_t k_rem;
     uint64_t nan_count;
     uint32_t tickets[4];
+    uint32_t spec_hit;                 // a speculative pass already fixed 22 prefix bits:
+    uint32_t spec_pad;                 // passes 0 and 1 are skipped (select.hip, k_rs_spec)
+    unsigned long long spec_above;     // keys above the speculative window
     unsigned long long hist[3][kRsBins];
 };
 
@@ -123,26 +126,34 @@ __device__ __forceinline__ uint64_t load_count(const unsigned long long* p) {
 }
 
 // Pick the bin of the k-th largest key from counts[0..bins). Thread t owns the
-// descending positions [per*t, per*t + per). Returns true in exactly one thread.
+// descending positions [per*t, per*t + per), per <= kPickMax. Returns true in exactly
+// one thread. The thread's counts are loaded once, all in flight together (unrolled,
+// predicated): a loop of dependent agent-scope loads costs a full L2 round trip per
+// bin, ~1 us each, and the last workgroup of every radix pass runs this.
+constexpr int kPickMax = 16;
 template <typename CountT>
 __device__ __forceinline__ bool pick_bin(const CountT* counts, int bins, uint64_t k, uint64_t* lds16, int* bin,
                                          uint64_t* above) {
     const int per = bins / (int)blockDim.x;
     const int t = threadIdx.x;
+    uint64_t c[kPickMax];
+#pragma unroll
+    for (int j = 0; j < kPickMax; ++j) c[j] = j < per ? load_count(&counts[bins - 1 - (per * t + j)]) : 0;
     uint64_t sum = 0;
-    for (int j = 0; j < per; ++j) sum += load_count(&counts[bins - 1 - (per * t + j)]);
+#pragma unroll
+    for (int j = 0; j < kPickMax; ++j) sum += c[j];
     uint64_t total;
     uint64_t run = block_exclusive_scan(sum, lds16, &total);
     bool hit = false;
     if (run < k && k <= run + sum) {
-        for (int j = 0; j < per; ++j) {
-            const uint64_t c = load_count(&counts[bins - 1 - (per * t + j)]);
-            if (!hit && run < k && k <= run + c) {
+#pragma unroll
+        for (int j = 0; j < kPickMax; ++j) {
+            if (!hit && j < per && run < k && k <= run + c[j]) {
                 hit = true;
                 *bin = bins - 1 - (per * t + j);
                 *above = run;
             }
-            run += c;
+            run += c[j];
         }
     }
     return hit;
@@ -177,6 +188,8 @@ __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
         st->k_rem = k;
         st->nan_count = 0;
         for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
+        st->spec_hit = 0;
+        st->spec_above = 0;
     }
 }
 
@@ -186,6 +199,7 @@ template <class Src>
 __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
     const int t = src.task(blockIdx.x);
     if (!src.active(t)) return;   // uniform per workgroup
+    if (pass < 2 && src.state(t)->spec_hit) return;   // a speculative pass fixed these digits
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t nan_cnt;
     __shared__ uint64_t lds16[16];

@@ -617,6 +617,83 @@ struct SampleKeys {
     }
 };
 
+// Speculative first pass of a sampled threshold (K3). The list threshold t_l = spec[0]
+// that K1 just listed at (m x the last threshold x its growth) bounds the new sampled
+// threshold from below in the steady state, within a factor 1.41 above. One pass
+// histograms the keys of [key(t_l) >> 10, + kSpecBins) by their 22-bit prefix (few
+// keys: no hot bins) and counts the keys above that window; when the ks-th largest key
+// falls in it, the 22-bit prefix and the rank left for the last 10 bits are known and
+// K3's passes 0 and 1 are skipped — one pass over the samples instead of two. Else
+// (first call, a threshold outside the window) the window's counts are cleared and the
+// three passes run as before; the result is the same either way.
+constexpr int kSpecBins = 2 * kRsBins;   // = hist[0] and hist[1] of the RSState, contiguous
+
+__global__ void __launch_bounds__(kBlock) k_rs_spec(SampleKeys src) {
+    const int t = src.task(blockIdx.x);
+    const float tl = src.w.spec ? src.w.spec[2 * t] : __builtin_huge_valf();
+    if (!(tl > 0.f && tl < 3.0e38f)) return;   // uniform: nothing to speculate from
+    RSState* st = src.state(t);
+    __shared__ uint32_t h[kSpecBins];
+    __shared__ uint32_t above_s, nan_s;
+    __shared__ uint64_t lds16[16];
+    __shared__ int sel_bin;
+    __shared__ uint64_t sel_above;
+    for (int b = threadIdx.x; b < kSpecBins; b += kBlock) h[b] = 0;
+    if (threadIdx.x == 0) {
+        above_s = 0;
+        nan_s = 0;
+        sel_bin = -1;
+    }
+    __syncthreads();
+    const uint32_t B0 = abs_key(tl) >> 10;
+    const int b0 = src.first_block(t), nb = src.blocks(t);
+    uint32_t my_above = 0, my_nan = 0;
+    src.visit(t, (int64_t)blockIdx.x - b0, nb, [&](uint32_t key) {
+        const uint32_t p = key >> 10;
+        if (p >= B0 + kSpecBins)
+            ++my_above;   // inf and NaN keys too
+        else if (p >= B0)
+            atomicAdd(&h[p - B0], 1u);
+        my_nan += key > 0x7F800000u;
+    });
+    my_above = wave_sum(my_above);
+    my_nan = wave_sum(my_nan);
+    if ((threadIdx.x & 63) == 0) {
+        if (my_above) atomicAdd(&above_s, my_above);
+        if (my_nan) atomicAdd(&nan_s, my_nan);
+    }
+    __syncthreads();
+    unsigned long long* gh = &st->hist[0][0];
+    for (int b = threadIdx.x; b < kSpecBins; b += kBlock)
+        if (h[b]) atomicAdd(&gh[b], (unsigned long long)h[b]);
+    if (threadIdx.x == 0) {
+        if (above_s) atomicAdd(&st->spec_above, (unsigned long long)above_s);
+        if (nan_s) atomicAdd((unsigned long long*)&st->nan_count, (unsigned long long)nan_s);
+    }
+    if (!last_block_arrival(&st->tickets[3], (uint32_t)nb)) return;
+    // the last workgroup: does the ks-th largest key fall in the window?
+    const uint64_t k = st->k_rem;
+    const uint64_t above = load_count(&st->spec_above);
+    if (above < k) {   // uniform
+        int bin;
+        uint64_t ab;
+        if (pick_bin(gh, kSpecBins, k - above, lds16, &bin, &ab)) {
+            sel_bin = bin;
+            sel_above = ab;
+        }
+    }
+    __syncthreads();
+    if (sel_bin >= 0) {
+        if (threadIdx.x == 0) {
+            st->prefix = (B0 + (uint32_t)sel_bin) << 10;
+            st->k_rem = k - above - sel_above;
+            st->spec_hit = 1;
+        }
+    } else {
+        for (int b = threadIdx.x; b < kSpecBins; b += kBlock) gh[b] = 0;   // passes 0 and 1 start clean
+    }
+}
+
 // Resets the radix state of every multi-block threshold task with its k (top_k_samples).
 __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
     const int t = blockIdx.x;
@@ -801,17 +878,35 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
 }
 
 // Chunked exclusive scan of a[0..m) into out[] by one workgroup; returns the total.
-// a[] holds totals accumulated by device atomics: read with agent-scope loads.
+// a[] holds totals accumulated by device atomics: read with agent-scope loads, in
+// chunks of kScanReg kept in registers so a chunk's loads are in flight together (a
+// loop of dependent loads pays an L2 round trip each); a thread's run of <= kScanReg
+// entries is loaded once.
+constexpr int kScanReg = 8;
 __device__ uint64_t block_scan_array(const unsigned long long* a, long long* out, int64_t m, uint64_t* lds16) {
     const int64_t per = ceil_div(m, (int64_t)blockDim.x);
     const int64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
+    uint64_t v[kScanReg];
     uint64_t local = 0;
-    for (int64_t i = b; i < e; ++i) local += load_count(&a[i]);
+    for (int64_t i0 = b; i0 < e; i0 += kScanReg) {
+#pragma unroll
+        for (int u = 0; u < kScanReg; ++u) v[u] = i0 + u < e ? load_count(&a[i0 + u]) : 0;
+#pragma unroll
+        for (int u = 0; u < kScanReg; ++u) local += v[u];
+    }
     uint64_t total;
     uint64_t run = block_exclusive_scan(local, lds16, &total);
-    for (int64_t i = b; i < e; ++i) {
-        out[i] = (long long)run;
-        run += load_count(&a[i]);
+    for (int64_t i0 = b; i0 < e; i0 += kScanReg) {
+        if (per > kScanReg) {
+#pragma unroll
+            for (int u = 0; u < kScanReg; ++u) v[u] = i0 + u < e ? load_count(&a[i0 + u]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScanReg; ++u)
+            if (i0 + u < e) {
+                out[i0 + u] = (long long)run;
+                run += v[u];
+            }
     }
     return total;
 }
@@ -830,6 +925,7 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
     __shared__ uint64_t lds16[16];
     __shared__ int finished, reset_rs;
     uint64_t local = 0;
+#pragma unroll 4
     for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) local += w.grp_cnt[d.grp0 + i];
     uint64_t n;
     block_exclusive_scan(local, lds16, &n);
@@ -2062,6 +2158,10 @@ static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStre
     if (L.grid[BT_SAMP] > 0) {
         hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w);
         DGC_LAUNCHED();
+        if (w.spec) {
+            hipLaunchKernelGGL(k_rs_spec, dim3((unsigned)L.grid[BT_SAMP]), dim3(kBlock), 0, s, SampleKeys{w, vec});
+            DGC_LAUNCHED();
+        }
         DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
     }
     return DGC_OK;
