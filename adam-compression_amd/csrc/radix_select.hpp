@@ -36,9 +36,8 @@ struct RSState {
     uint64_t k_rem;
     uint64_t nan_count;
     uint32_t tickets[4];
-    uint32_t spec_hit;                 // a speculative pass already fixed 22 prefix bits:
-    uint32_t spec_pad;                 // passes 0 and 1 are skipped (select.hip, k_rs_spec)
-    unsigned long long spec_above;     // keys above the speculative window
+    uint32_t win_n;                    // > 0: the passes read the K1 sample window list of
+    uint32_t win_pad;                  // win_n keys instead of the samples (select.hip)
     unsigned long long hist[3][kRsBins];
 };
 
@@ -188,8 +187,7 @@ __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
         st->k_rem = k;
         st->nan_count = 0;
         for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
-        st->spec_hit = 0;
-        st->spec_above = 0;
+        st->win_n = 0;
     }
 }
 
@@ -199,7 +197,6 @@ template <class Src>
 __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
     const int t = src.task(blockIdx.x);
     if (!src.active(t)) return;   // uniform per workgroup
-    if (pass < 2 && src.state(t)->spec_hit) return;   // a speculative pass fixed these digits
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t nan_cnt;
     __shared__ uint64_t lds16[16];

@@ -81,6 +81,7 @@ struct TDesc {
     int64_t k, S, ks, stride;          // num_selects, num_samples, top_k_samples, sample_stride
     int64_t upper_count, lower_count;  // floor(k * upper), ceil(lower * k)
     int64_t samp_off;       // offset of its samples in the flat sample buffer; -1: none / N == S
+    int64_t win_off, win_cap;          // its K1 sample window list in the sample buffer (cap 0: none)
     int64_t cand_off, cand_cap;        // K5 queue region: min(N, 64k - 1) candidates
     int64_t gpos_off;       // K5 pair slots: 2 x (cand_cap / 2 + 1)
     int64_t idx_base;       // added to the emitted indices (its flat offset in a batch, 0 alone)
@@ -107,13 +108,16 @@ struct SelState {
     // next K1, which streams vec and mmt anyway, zeroes them before compensating.
     int32_t def_mode, def_mask_mmt;
     float def_t;
-    int32_t pad;
+    int32_t win_keys;      // keys K3 read from the K1 sample window list (0: the samples)
     long long def_limit;
     uint32_t tickets[4];
     // Segments whose K1 list overflowed, counted by K1 into slot [epoch & 1] (64
     // shards against atomic contention); k_sel_init reads it and zeroes the other
     // slot for the next call, k_sel_finish advances the epoch.
     uint32_t spill[2][kSpillShards];
+    // Samples with key >= key(t_list) that K1 appended to the tensor's window list, in
+    // slot [epoch & 1] like spill (the count runs past win_cap when the list overflows).
+    uint32_t win_cnt[2];
     unsigned long long lower_cnt[kMaxLower + 1];   // counts at t_1..t_m (multi-threshold pass)
 };
 
@@ -228,6 +232,11 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         L.lowest_any |= sampled && (d.k > kHeapMax || d.n > 0xFFFFFFFFLL);   // see k_decide
         d.samp_off = (sampled && in[t].samples) ? samp : -1;
         if (d.samp_off >= 0) samp += (int64_t)align_up((size_t)(d.S + 1), 64);
+        // a window list for the multi-block thresholds; its size cannot depend on ks
+        // (dgc_compress_begin lays the workspace out without it)
+        d.win_cap = (d.samp_off >= 0 && d.S + 1 > kSmallN) ? std::min<int64_t>(d.S + 1, (d.S + 1) / 16 + 4096) : 0;
+        d.win_off = samp;
+        samp += (int64_t)align_up((size_t)d.win_cap, 64);
         d.cand_off = cand;
         d.cand_cap = nth_cand_cap(d.n, d.k);
         cand += d.cand_cap;
@@ -534,6 +543,11 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
         w.scnt[t] = sample ? scount : d.n;
     }
     float* sout = sample ? w.samples + d.samp_off : nullptr;
+    // the sample window list: every sample with key >= key(t_list) (inf and NaN too)
+    float* win = w.samples + d.win_off;
+    const uint32_t win_key = abs_key(tl);
+    const bool windowed = sample && d.win_cap > 0;
+    uint32_t* win_cnt = &st->win_cnt[st->epoch & 1];
     // waves past the tensor's last segment load nothing and list nothing, but stay for
     // the block barrier of the spill count
     int64_t q0 = 0, r0 = 0;
@@ -559,6 +573,8 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
         const bool ok = v < n4;
         float x[4] = {0.f, 0.f, 0.f, 0.f};
         uint32_t valid = 0;
+        bool hit = false;   // this lane's sample (at most one per float4: stride >= 4) joins the window
+        float hv = 0.f;
         if (ok) {
             x[0] = comp1<NEST, true>(gv[u].x, mv[u].x, vv[u].x, mom);
             x[1] = comp1<NEST, true>(gv[u].y, mv[u].y, vv[u].y, mom);
@@ -576,9 +592,22 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
                 const uint32_t j = r == 0 ? 0u : s32 - r;
                 if (j < 4 && ((valid >> j) & 1u)) {
                     const int64_t qi = q0 + q1 + (r == 0 ? 0 : 1);
-                    if (qi >= 0 && qi < scount) sout[qi] = fabsf(x[j]);
+                    if (qi >= 0 && qi < scount) {
+                        hv = fabsf(x[j]);
+                        sout[qi] = hv;
+                        hit = windowed && __float_as_uint(hv) >= win_key;
+                    }
                 }
             }
+        }
+        const uint64_t hb = __ballot(hit);
+        if (hb) {   // wave-uniform and rare (~3 ks of the S samples): one atomic per wave
+            const int leader = __ffsll((unsigned long long)hb) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(win_cnt, (uint32_t)__popcll(hb));
+            base = __shfl(base, leader);
+            const uint32_t pos = base + (uint32_t)__popcll(hb & ((1ull << lane) - 1));
+            if (hit && pos < (uint64_t)d.win_cap) win[pos] = hv;
         }
         list_append(ge_mask(x, valid, tl), x, u * 256, c, lo, lv);
     }
@@ -612,93 +641,34 @@ struct SampleKeys {
     template <class F>
     __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
         const TDesc d = w.td[t];   // by value: stores below cannot alias it
+        const uint32_t wn = w.rs[t].win_n;
+        if (wn) {
+            visit_dense(w.samples + d.win_off, wn, lb, nb, f);
+            return;
+        }
         const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
         visit_dense(x, w.scnt[t], lb, nb, f);
     }
 };
 
-// Speculative first pass of a sampled threshold (K3). The list threshold t_l = spec[0]
-// that K1 just listed at (m x the last threshold x its growth) bounds the new sampled
-// threshold from below in the steady state, within a factor 1.41 above. One pass
-// histograms the keys of [key(t_l) >> 10, + kSpecBins) by their 22-bit prefix (few
-// keys: no hot bins) and counts the keys above that window; when the ks-th largest key
-// falls in it, the 22-bit prefix and the rank left for the last 10 bits are known and
-// K3's passes 0 and 1 are skipped — one pass over the samples instead of two. Else
-// (first call, a threshold outside the window) the window's counts are cleared and the
-// three passes run as before; the result is the same either way.
-constexpr int kSpecBins = 2 * kRsBins;   // = hist[0] and hist[1] of the RSState, contiguous
-
-__global__ void __launch_bounds__(kBlock) k_rs_spec(SampleKeys src) {
-    const int t = src.task(blockIdx.x);
-    const float tl = src.w.spec ? src.w.spec[2 * t] : __builtin_huge_valf();
-    if (!(tl > 0.f && tl < 3.0e38f)) return;   // uniform: nothing to speculate from
-    RSState* st = src.state(t);
-    __shared__ uint32_t h[kSpecBins];
-    __shared__ uint32_t above_s, nan_s;
-    __shared__ uint64_t lds16[16];
-    __shared__ int sel_bin;
-    __shared__ uint64_t sel_above;
-    for (int b = threadIdx.x; b < kSpecBins; b += kBlock) h[b] = 0;
-    if (threadIdx.x == 0) {
-        above_s = 0;
-        nan_s = 0;
-        sel_bin = -1;
-    }
-    __syncthreads();
-    const uint32_t B0 = abs_key(tl) >> 10;
-    const int b0 = src.first_block(t), nb = src.blocks(t);
-    uint32_t my_above = 0, my_nan = 0;
-    src.visit(t, (int64_t)blockIdx.x - b0, nb, [&](uint32_t key) {
-        const uint32_t p = key >> 10;
-        if (p >= B0 + kSpecBins)
-            ++my_above;   // inf and NaN keys too
-        else if (p >= B0)
-            atomicAdd(&h[p - B0], 1u);
-        my_nan += key > 0x7F800000u;
-    });
-    my_above = wave_sum(my_above);
-    my_nan = wave_sum(my_nan);
-    if ((threadIdx.x & 63) == 0) {
-        if (my_above) atomicAdd(&above_s, my_above);
-        if (my_nan) atomicAdd(&nan_s, my_nan);
-    }
-    __syncthreads();
-    unsigned long long* gh = &st->hist[0][0];
-    for (int b = threadIdx.x; b < kSpecBins; b += kBlock)
-        if (h[b]) atomicAdd(&gh[b], (unsigned long long)h[b]);
-    if (threadIdx.x == 0) {
-        if (above_s) atomicAdd(&st->spec_above, (unsigned long long)above_s);
-        if (nan_s) atomicAdd((unsigned long long*)&st->nan_count, (unsigned long long)nan_s);
-    }
-    if (!last_block_arrival(&st->tickets[3], (uint32_t)nb)) return;
-    // the last workgroup: does the ks-th largest key fall in the window?
-    const uint64_t k = st->k_rem;
-    const uint64_t above = load_count(&st->spec_above);
-    if (above < k) {   // uniform
-        int bin;
-        uint64_t ab;
-        if (pick_bin(gh, kSpecBins, k - above, lds16, &bin, &ab)) {
-            sel_bin = bin;
-            sel_above = ab;
-        }
-    }
-    __syncthreads();
-    if (sel_bin >= 0) {
-        if (threadIdx.x == 0) {
-            st->prefix = (B0 + (uint32_t)sel_bin) << 10;
-            st->k_rem = k - above - sel_above;
-            st->spec_hit = 1;
-        }
-    } else {
-        for (int b = threadIdx.x; b < kSpecBins; b += kBlock) gh[b] = 0;   // passes 0 and 1 start clean
-    }
-}
-
-// Resets the radix state of every multi-block threshold task with its k (top_k_samples).
+// Resets the radix state of every multi-block threshold task with its k (top_k_samples)
+// and picks its keys. K1 appended every sample with key >= key(t_list) to the tensor's
+// window list; when that list is complete (count <= win_cap) and holds >= ks keys,
+// the ks-th largest sample is the ks-th largest of the list — every key above it is
+// in the list, NaN and inf keys included — so the three passes read the list (~3 ks
+// keys in the steady state) instead of the S samples. The result is the same either
+// way. An unpadded tail's samples are written outside K1: no list then.
 __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
     const int t = blockIdx.x;
     if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
-    rs_reset(w.rs + t, (uint64_t)w.td[t].ks);
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    RSState* rs = w.rs + t;
+    rs_reset(rs, (uint64_t)d.ks);
+    if (threadIdx.x == 0 && d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
+        const SelState* st = w.st + t;
+        const uint32_t cnt = st->win_cnt[st->epoch & 1];
+        if (cnt >= (uint64_t)d.ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
+    }
 }
 
 // One workgroup per small tensor: all three passes from LDS.
@@ -729,9 +699,11 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lis
         if (v) atomicAdd(&spills, v);
         st->spill[e ^ 1][threadIdx.x] = 0;   // slot of the next call's K1
     }
+    if (threadIdx.x == 0) st->win_cnt[e ^ 1] = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         const float t0 = w.thr[t];
+        st->win_keys = (d.win_cap > 0 && !d.tail) ? (int32_t)w.rs[t].win_n : 0;
         st->t0 = t0;
         st->t_cur = t0;
         st->list_spills = keep_lists ? (int32_t)spills : 0;
@@ -1890,7 +1862,7 @@ __global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info,
             r.overflow_segments = st->full_passes ? st->overflow : st->list_spills;
             r.full_passes = st->full_passes;
             r.tie_rule = st->tie_rule;
-            r.pad = 0;
+            r.window_keys = st->win_keys;
         }
         if (w.spec) {
             // spec[0]: next call's list threshold = m * t * growth, growth = t / spec[1] (the
@@ -2158,10 +2130,6 @@ static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStre
     if (L.grid[BT_SAMP] > 0) {
         hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w);
         DGC_LAUNCHED();
-        if (w.spec) {
-            hipLaunchKernelGGL(k_rs_spec, dim3((unsigned)L.grid[BT_SAMP]), dim3(kBlock), 0, s, SampleKeys{w, vec});
-            DGC_LAUNCHED();
-        }
         DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
     }
     return DGC_OK;

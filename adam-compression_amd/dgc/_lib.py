@@ -37,7 +37,7 @@ class SelectInfo(ctypes.Structure):
                 ("threshold0", ctypes.c_float), ("threshold", ctypes.c_float),
                 ("branch", ctypes.c_int32), ("recounts", ctypes.c_int32),
                 ("overflow_segments", ctypes.c_int32), ("full_passes", ctypes.c_int32),
-                ("tie_rule", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("tie_rule", ctypes.c_int32), ("window_keys", ctypes.c_int32)]
 
 
 INFO_BYTES = ctypes.sizeof(SelectInfo)
@@ -165,7 +165,8 @@ def require_cuda_f32(t, what):
 
 
 class Workspace:
-    """Grow-only device scratch buffers keyed by (device, tag): the library never allocates."""
+    """Grow-only device scratch buffers keyed by (device, tag): the library never allocates.
+    Zero-filled when (re)allocated: a compress workspace carries state between calls."""
 
     def __init__(self):
         self._bufs = {}
@@ -174,6 +175,6 @@ class Workspace:
         key = (str(device), tag)
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
             self._bufs[key] = buf
         return buf

@@ -215,7 +215,7 @@ class DGCBatch:
             out.append(dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
                             branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
                             overflow_segments=i.overflow_segments, full_passes=i.full_passes,
-                            tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule)))
+                            tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys))
         return out
 
     def transmitted(self, rank_payload=None):

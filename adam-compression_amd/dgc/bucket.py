@@ -90,7 +90,8 @@ class DGCBucket:
         self._pending = False
         L = _lib.lib()
         self.sampled = N != self.num_samples
-        self.ws = torch.empty(L.dgc_compress_workspace(N, self.k, self.num_samples), dtype=torch.uint8,
+        # zero-filled: per-tensor state (deferred masking, spill and window counts) lives in it
+        self.ws = torch.zeros(L.dgc_compress_workspace(N, self.k, self.num_samples), dtype=torch.uint8,
                               device=dev)
         self.spec = torch.full((2,), float("inf"), dtype=torch.float32, device=dev)
         self.info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
@@ -271,4 +272,4 @@ class DGCBucket:
         return dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
                     branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
                     overflow_segments=i.overflow_segments, full_passes=i.full_passes,
-                    tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule))
+                    tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys)

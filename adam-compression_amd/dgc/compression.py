@@ -297,7 +297,8 @@ class DGCCompressor:
         return dict(count=info.count, candidates=info.candidates, threshold0=info.threshold0,
                     threshold=info.threshold, branch=_lib.BRANCHES.get(info.branch, info.branch),
                     recounts=info.recounts, overflow_segments=info.overflow_segments,
-                    full_passes=info.full_passes, tie_rule=_lib.TIE_RULES.get(info.tie_rule, info.tie_rule))
+                    full_passes=info.full_passes, tie_rule=_lib.TIE_RULES.get(info.tie_rule, info.tie_rule),
+                    window_keys=info.window_keys)
 
     def decompress(self, tensor, ctx):
         """dgc/compression.py:179-198."""

@@ -118,7 +118,9 @@ typedef struct dgc_select_info {
     int32_t overflow_segments;/* segments whose candidate list spilled      */
     int32_t full_passes;      /* full re-reads of vec (0: served by the K1 lists) */
     int32_t tie_rule;         /* enum dgc_tie_rule                          */
-    int32_t pad;
+    int32_t window_keys;      /* > 0: threshold0 came from the K1 window list of this
+                                 many samples (those >= the list threshold), not a
+                                 pass over all samples; same value either way       */
 } dgc_select_info;
 
 const char* dgc_last_error(void);
@@ -174,7 +176,10 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
  * call whose t fell below its list threshold, else 1.05 x (list threshold / t) of
  * that call, within [spec_margin, 0.95]: the lists shrink while t moves predictably.
  * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
- * one workspace and must see the same sample_start/stride/params. */
+ * one workspace and must see the same sample_start/stride/params. The workspace
+ * carries per-tensor state from call to call (a deferred masking, the K1 list-spill
+ * and sample-window counts): zero-fill it before its first call, and give each
+ * tensor its own. */
 size_t dgc_compress_workspace(int64_t numel, int64_t num_selects, int64_t num_samples);
 int dgc_compress(const float* grad, float* mmt, float* vec, float momentum, int32_t nesterov,
                  int64_t sample_start, int64_t sample_stride, int64_t top_k_samples,

@@ -736,6 +736,8 @@ def test_large_bucket_properties(L, N):
     (1_048_576, 0.05, "layered", [1, 1, 1, 0.1], "sparse"),
     (1_000_000, 0.001, "normal", [1, 3, 9, 27, 1], "sparse+poke"),   # out written in place: dense fallback
     (1_000_000, 0.001, "normal", [1, 1, 1, 1], "sparse+alias"),      # out is the gradient buffer itself
+    (5_000_000, 0.001, "normal", [1, 1, 1, 1, 1], "sparse"),   # > 32K samples: K3 reads K1's window list
+    (5_000_000, 0.001, "normal", [1, 1, 0.1, 0.1, 3], "inline"),   # the window misses after the drop
 ])
 @pytest.mark.parametrize("shape", [None, "quarter"])
 def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monkeypatch):
@@ -753,7 +755,7 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monke
     m_o, v_o = np.zeros(N, np.float32), np.zeros(N, np.float32)
     rng = random.Random(7)
     out = torch.full((N,), float("nan"), device=DEV)   # the fill must clear it
-    served_by_lists = 0
+    served_by_lists = windowed = 0
     for s, sc in enumerate(scales):
         g = synth.gradient(300 + s, N, kind, float(sc))
         start = rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
@@ -778,10 +780,16 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monke
             assert np.array_equal(bits(b.mmt.cpu().numpy()), bits(m_o)), s
         assert np.array_equal(bits(out.cpu().numpy()), bits(O.decompress([ov], [oi], N, 1))), s
         served_by_lists += info["full_passes"] == 0
+        windowed += info["window_keys"] > 0
+        assert info["window_keys"] == 0 or attrs[2] + 1 > 32768, info   # only multi-block thresholds
+        assert bits(np.float32(info["threshold0"])) == bits(oinfo["thresholds"][0]), (s, info)
         if poke and s % 2 == 0:
             out[s:: 97].fill_(7.0)   # an in-place write the next step must not build on
     if scales == [1, 1, 1, 1, 1]:
-        assert served_by_lists >= 3        # the steady state skips the re-read of vec
+        # the steady state skips the re-read of vec, and K3's pass over all samples
+        assert served_by_lists >= (2 if N == 5_000_000 else 3), (served_by_lists, windowed)
+        if N == 5_000_000:
+            assert windowed >= 3, (served_by_lists, windowed)
 
 
 def _same_bits_or_nan(a, b):
@@ -792,16 +800,19 @@ def _same_bits_or_nan(a, b):
     return bool(np.all(both_nan | (bits(a) == bits(b))))
 
 
+@pytest.mark.parametrize("N", [1_000_003, 5_000_000])
 @pytest.mark.parametrize("case", ["nan_unsampled", "nan_sampled"])
-def test_bucket_nan_inf_gradients_match_oracle(L, case):
+def test_bucket_nan_inf_gradients_match_oracle(L, case, N):
     """NaN and +-inf gradients through DGCBucket against the oracle: an inf is selected
     like any large value; a NaN is never selected (|NaN| >= t is false) and stays in
     the velocity; a NaN among the strided samples makes the threshold NaN (topk ranks
     it first, min propagates it, dgc/compression.py:123) and nothing is selected,
-    through the whole adaptation loop. (NaN inputs: parity against the oracle's
-    restatement of torch's NaN ordering; the reference's goldens hold no NaN.)"""
+    through the whole adaptation loop — also when K3 reads K1's sample window list
+    (N = 5M: > 32K samples), which must then hold the NaN sample and the infs. (NaN
+    inputs: parity against the oracle's restatement of torch's NaN ordering; the
+    reference's goldens hold no NaN.)"""
     from dgc.bucket import DGCBucket
-    N, ratio = 1_000_003, 0.001
+    ratio = 0.001
     attrs = O.attributes(N, ratio)
     stride = attrs[4]
     rng = random.Random(11)
