@@ -111,6 +111,12 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
+    return v;
+}
+
 // Wire value store (fp32 / fp16 round-to-nearest-even, overflow -> inf like torch).
 __device__ __forceinline__ void store_value(void* out, int64_t pos, float x, int vdtype) {
     if (vdtype == DGC_F16)

@@ -57,6 +57,7 @@ constexpr int kCap = 64;                        // list slots per segment (6.25 
 constexpr int kSegTiles = kSeg / (kWave * 4);   // 4 float4 per lane per segment
 constexpr int kSuper = 4;                       // segments per wave in the full select pass
 constexpr int kGroupSegs = 1024;                // segments per group (1M elements)
+constexpr int kCountSegs = 4;                   // k_count_lists: segments per thread (a group per block)
 constexpr int kSegPerBlock4 = kBlock / kWave;   // 4 waves per workgroup
 constexpr int kSegPerBlock16 = kSegPerBlock4 * kSuper;
 constexpr int kMaxLower = 16;                   // thresholds per multi-threshold pass
@@ -129,7 +130,7 @@ struct SelCfg {
 };
 
 // Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
-enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_COUNT };
+enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_CNT, BT_COUNT };
 
 struct SelWS {
     int32_t T;
@@ -143,7 +144,7 @@ struct SelWS {
     float* samples;            // flat sample buffer
     int32_t* bt[BT_COUNT];     // block tables
     int32_t* small;            // tensors whose threshold runs in one workgroup
-    uint32_t* seg_lcnt;
+    uint32_t* seg_lcnt;        // list count at t_list (low 16 bits) | lmax_code (high 16 bits)
     uint32_t* seg_cnt;
     uint32_t* seg_gt;
     uint32_t* seg_eq;
@@ -194,6 +195,7 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg) {
         case BT_CAP16: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock16), cap);
         case BT_CAP4: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock4), cap);
         case BT_SEG: return ceil_div(d.nseg, (int64_t)kBlock);
+        case BT_CNT: return ceil_div(d.nseg, (int64_t)kBlock * kCountSegs);
         case BT_GRP: return ceil_div(d.nseg, (int64_t)(kGroupSegs / kEmitSplit));
         case BT_QUEUE: return ceil_div(d.k, (int64_t)kQueuePerBlock);
         case BT_SAMP: {
@@ -342,6 +344,22 @@ __global__ void k_put_starts(SelWS w, StartChunk c) {
 }
 
 // ------------------------------------------------------------------ tile helpers
+// Upper bound of a segment's largest |x| key, in 16-bit units: every key < code << 16.
+// k_count_lists skips the list of a segment whose code says every |x| < t_cur — at
+// 7B most lists hold an entry or two below t_cur, and reading them cost a 128-B line
+// per segment. NaN keys give codes above any finite threshold's key (never skipped).
+__device__ __forceinline__ uint32_t lmax_code(uint32_t max_key) { return (max_key >> 16) + 1; }
+// seg_lcnt packs the list count (<= kSeg) with the code: one 4-B store per segment
+__device__ __forceinline__ uint32_t lcnt_pack(uint32_t count, uint32_t code) { return count | (code << 16); }
+__device__ __forceinline__ uint32_t lcnt_count(uint32_t v) { return v & 0xFFFFu; }
+__device__ __forceinline__ uint32_t tile_max_key(const float (&x)[4], uint32_t valid) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if ((valid >> j) & 1u) m = max(m, abs_key(x[j]));
+    return m;
+}
+
 // Lane holds elements e0..e0+3 of a 256-element tile (e0 = tile base + 4*lane) of a
 // tensor whose elements start at v (local indices, n of them).
 template <bool ALIGNED>
@@ -562,7 +580,7 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
             vv[u] = ld_nt(vec + v);
         }
     }
-    uint32_t c = 0;
+    uint32_t c = 0, mk = 0;
     const int64_t seg = d.seg0 + ls;
     uint16_t* lo = w.lst_off + seg * kCap;
     float* lv = w.lst_val + seg * kCap;
@@ -610,9 +628,14 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
             if (hit && pos < (uint64_t)d.win_cap) win[pos] = hv;
         }
         list_append(ge_mask(x, valid, tl), x, u * 256, c, lo, lv);
+        mk = max(mk, tile_max_key(x, valid));
     }
     const bool spilled = c > (uint32_t)kCap;
-    if (lane == 0 && ls < d.nseg) w.seg_lcnt[seg] = (d.tail && ls == d.nseg - 1) ? (uint32_t)(kCap + 1) : c;
+    mk = wave_max(mk);
+    if (lane == 0 && ls < d.nseg) {
+        const bool tail = d.tail && ls == d.nseg - 1;   // its scalar tail is compensated outside K1
+        w.seg_lcnt[seg] = tail ? lcnt_pack(kCap + 1, 0xFFFFu) : lcnt_pack(c, lmax_code(mk));
+    }
     // one atomic per workgroup with a spilled segment (shard by block)
     const uint64_t any = __ballot(spilled);
     __shared__ uint32_t nsp;
@@ -727,17 +750,21 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lis
 }
 
 // ------------------------------------------------------------------ count passes
-// t_cur >= t_list: counts from the lists, one thread per segment; spilled segments
-// are re-read by the block's waves. One atomic per block into its group.
+// t_cur >= t_list: counts from the lists, kCountSegs segments per thread (one group
+// per workgroup): the list counts of a thread's segments, then their first 8 entries
+// (most lists are shorter), are all in flight before any is used — one thread per
+// segment paid two dependent round trips per segment in ~13 waves of workgroups at 7B.
+// Spilled segments are re-read by the block's waves. One atomic per block into its group.
+static_assert(kBlock * kCountSegs == kGroupSegs, "k_count_lists: one group per workgroup");
 __global__ void __launch_bounds__(kBlock)
 k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
-    const int t = task(w, BT_SEG, blockIdx.x);
+    const int t = task(w, BT_CNT, blockIdx.x);
     const SelState* st = w.st + t;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
-    __shared__ int spill[kBlock];
+    __shared__ int spill[kBlock * kCountSegs];
     __shared__ int nspill;
     __shared__ uint32_t bsum;
     if (threadIdx.x == 0) {
@@ -745,32 +772,61 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
         bsum = 0;
     }
     __syncthreads();
-    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_SEG][t]) * kBlock;
-    const int64_t ls = lseg0 + threadIdx.x;
-    uint32_t c = 0;
-    if (ls < d.nseg) {
-        const int64_t seg = d.seg0 + ls;
-        const uint32_t lc = w.seg_lcnt[seg];
-        if (lc <= (uint32_t)kCap) {
-            const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
-            float4 v[kCap / 4];
+    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_CNT][t]) * kBlock * kCountSegs;
+    uint32_t lc[kCountSegs];
+    const uint32_t tkey = abs_key(tc);
 #pragma unroll
-            for (int q = 0; q < kCap / 4; ++q)   // all loads issued before any use
-                if ((uint32_t)(4 * q) < lc) v[q] = l4[q];
-#pragma unroll
-            for (int q = 0; q < kCap / 4; ++q) {
-                const uint32_t e = 4 * q;
-                if (e < lc)
-                    c += (fabsf(v[q].x) >= tc) + (e + 1 < lc && fabsf(v[q].y) >= tc) +
-                         (e + 2 < lc && fabsf(v[q].z) >= tc) + (e + 3 < lc && fabsf(v[q].w) >= tc);
-            }
-            w.seg_cnt[seg] = c;
-        } else {
-            spill[atomicAdd(&nspill, 1)] = threadIdx.x;
-        }
+    for (int j = 0; j < kCountSegs; ++j) {
+        const int64_t ls = lseg0 + j * kBlock + threadIdx.x;
+        const uint32_t v = ls < d.nseg ? w.seg_lcnt[d.seg0 + ls] : 0u;
+        // a segment whose every |x| is below t_cur counts 0 without reading its list
+        // (or, spilled, its elements)
+        lc[j] = ((v >> 16) << 16) <= tkey ? 0u : lcnt_count(v);
     }
-    c = wave_sum(c);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&bsum, c);
+    float4 a[kCountSegs], b[kCountSegs];
+#pragma unroll
+    for (int j = 0; j < kCountSegs; ++j) {
+        const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + (d.seg0 + lseg0 + j * kBlock + threadIdx.x) * kCap);
+        if (lc[j] > 0 && lc[j] <= (uint32_t)kCap) a[j] = l4[0];
+        if (lc[j] > 4 && lc[j] <= (uint32_t)kCap) b[j] = l4[1];
+    }
+    uint32_t ctot = 0;
+#pragma unroll
+    for (int j = 0; j < kCountSegs; ++j) {
+        const int64_t ls = lseg0 + j * kBlock + threadIdx.x;
+        if (ls >= d.nseg) continue;
+        const int64_t seg = d.seg0 + ls;
+        const uint32_t n = lc[j];
+        if (n > (uint32_t)kCap) {
+            spill[atomicAdd(&nspill, 1)] = j * kBlock + threadIdx.x;
+            continue;
+        }
+        uint32_t c = 0;
+        if (n > 0)
+            c += (fabsf(a[j].x) >= tc) + (1 < n && fabsf(a[j].y) >= tc) + (2 < n && fabsf(a[j].z) >= tc) +
+                 (3 < n && fabsf(a[j].w) >= tc);
+        if (n > 4)
+            c += (fabsf(b[j].x) >= tc) + (5 < n && fabsf(b[j].y) >= tc) + (6 < n && fabsf(b[j].z) >= tc) +
+                 (7 < n && fabsf(b[j].w) >= tc);
+        if (n > 8) {   // the rest of a longer list, its loads issued together
+            const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
+            float4 v[kCap / 4 - 2];
+#pragma unroll
+            for (int q = 2; q < kCap / 4; ++q)
+                if ((uint32_t)(4 * q) < n) v[q - 2] = l4[q];
+#pragma unroll
+            for (int q = 2; q < kCap / 4; ++q) {
+                const uint32_t e = 4 * q;
+                if (e < n)
+                    c += (fabsf(v[q - 2].x) >= tc) + (e + 1 < n && fabsf(v[q - 2].y) >= tc) +
+                         (e + 2 < n && fabsf(v[q - 2].z) >= tc) + (e + 3 < n && fabsf(v[q - 2].w) >= tc);
+            }
+        }
+        w.seg_cnt[seg] = c;
+        ctot += c;
+    }
+    ctot = wave_sum(ctot);
+    if ((threadIdx.x & 63) == 0 && ctot) atomicAdd(&bsum, ctot);
     __syncthreads();
     const int wave = threadIdx.x >> 6;
     for (int q = wave; q < nspill; q += kSegPerBlock4) {
@@ -821,12 +877,16 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
                 uint16_t* lo = w.lst_off + seg * kCap;
                 float* lv = w.lst_val + seg * kCap;
                 if (ls < d.nseg) {   // uniform per wave
+                    uint32_t mk = 0;
 #pragma unroll
-                    for (int u = 0; u < kSegTiles; ++u)
+                    for (int u = 0; u < kSegTiles; ++u) {
                         list_append(ge_mask(x[sg * kSegTiles + u], valid[sg * kSegTiles + u], tc),
                                     x[sg * kSegTiles + u], u * 256, c, lo, lv);
+                        mk = max(mk, tile_max_key(x[sg * kSegTiles + u], valid[sg * kSegTiles + u]));
+                    }
+                    mk = wave_max(mk);
                     if (lane == 0) {
-                        w.seg_lcnt[seg] = c;
+                        w.seg_lcnt[seg] = lcnt_pack(c, lmax_code(mk));
                         w.seg_cnt[seg] = c;
                     }
                 }
@@ -1080,7 +1140,7 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     for (int j = 0; j <= kLowerLists; ++j) c[j] = 0;
     if (ls < d.nseg) {
         const int64_t seg = d.seg0 + ls;
-        const uint32_t lc = w.seg_lcnt[seg];
+        const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
         if (lc <= (uint32_t)kCap) {
             const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
             float4 v[kCap / 4];
@@ -1169,7 +1229,7 @@ struct CandKeys {
         const float tc = w.st[t].t_cur;
         for (int64_t ls = gw; ls < d.nseg; ls += nw) {
             const int64_t seg = d.seg0 + ls;
-            const uint32_t lc = w.seg_lcnt[seg];
+            const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
             if (lc <= (uint32_t)kCap) {
                 if (lane < lc) {
                     const float a = fabsf(w.lst_val[seg * kCap + lane]);
@@ -1215,7 +1275,7 @@ k_count_gt_eq(const float* __restrict__ vec_flat, SelWS w) {
     uint32_t gt = 0, eq = 0;
     if (ls < d.nseg) {
         const int64_t seg = d.seg0 + ls;
-        const uint32_t lc = w.seg_lcnt[seg];
+        const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
         if (lc <= (uint32_t)kCap) {
             for (uint32_t e = 0; e < lc; ++e) {
                 const float a = fabsf(w.lst_val[seg * kCap + e]);
@@ -1457,7 +1517,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
             const int64_t seg = d.seg0 + ls;
             ca = ca_src[seg];
             if (rs) cb = w.seg_eq[seg];
-            lc = w.seg_lcnt[seg];
+            lc = lcnt_count(w.seg_lcnt[seg]);
         }
         for (int q = 0; q < sub; ++q) {   // the same position in the group's earlier quarters
             const int64_t seg = d.seg0 + lg * kGroupSegs + (int64_t)q * kEmitSegs + threadIdx.x;
@@ -1628,7 +1688,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
             const int64_t seg = d.seg0 + ls;
             ca = rs ? w.seg_gt[seg] : w.seg_cnt[seg];
             cb = rs ? w.seg_eq[seg] : 0;
-            lc = w.seg_lcnt[seg];
+            lc = lcnt_count(w.seg_lcnt[seg]);
         }
         uint64_t tot;
         const uint32_t oa = (uint32_t)block_exclusive_scan((uint64_t)ca, lds16, &tot);
@@ -1940,7 +2000,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
         // (both gated per tensor on the device); need: 1 = lists, 2 = full, 3 = either
         if (need & 1) {
-            hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w);
+            hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w);
             DGC_LAUNCHED();
         }
         if (need & 2) {
