@@ -1519,10 +1519,13 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
             if (rs) cb = w.seg_eq[seg];
             lc = lcnt_count(w.seg_lcnt[seg]);
         }
-        for (int q = 0; q < sub; ++q) {   // the same position in the group's earlier quarters
-            const int64_t seg = d.seg0 + lg * kGroupSegs + (int64_t)q * kEmitSegs + threadIdx.x;
-            pa += ca_src[seg];
-            if (rs) pb += w.seg_eq[seg];
+#pragma unroll
+        for (int q = 0; q < kEmitSplit - 1; ++q) {   // the same position in the group's earlier
+            if (q < sub) {                             // quarters (loads in flight together)
+                const int64_t seg = d.seg0 + lg * kGroupSegs + (int64_t)q * kEmitSegs + threadIdx.x;
+                pa += ca_src[seg];
+                if (rs) pb += w.seg_eq[seg];
+            }
         }
         // (a list with nothing at the current threshold is not read: most of them at 1e-4)
         const bool short_list = ls < d.nseg && (ca > 0 || cb > 0) && lc <= (uint32_t)kEmitShort;
