@@ -1928,8 +1928,11 @@ __global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info,
             r.window_keys = st->win_keys;
         }
         if (w.spec) {
-            // spec[0]: next call's list threshold = m * t * growth, growth = t / spec[1] (the
-            // previous final threshold) clamped to [1, 1.5]; spec[1] := t. The margin m adapts:
+            // spec[0]: next call's list threshold = m * t * growth, growth = 2 - spec[1] / t
+            // (linear extrapolation from the previous final threshold spec[1]) clamped to
+            // [1, 1.5]; spec[1] := t. The ratio t / spec[1] overshoots while the growth
+            // decelerates — the accumulating velocity's threshold grows ~linearly, and on the
+            // bench the ratio extrapolation missed at step 5 (a full pass). The margin m adapts:
             // after a call whose threshold landed at or above its list threshold (a hit),
             // m = 1.05 x that call's list/final ratio, within [margin, kSpecMarginMax] — the
             // lists shrink towards the selection while the threshold moves predictably (at
@@ -1938,7 +1941,7 @@ __global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info,
             float* spec = w.spec + 2 * t;
             const float tc = st->t_cur;
             const float used = spec[0];
-            const float gr = fminf(fmaxf(tc / spec[1], 1.f), 1.5f);   // NaN (first call: inf/inf) -> 1
+            const float gr = fminf(fmaxf(2.f - spec[1] / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
             float m = margin;
             if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
                 m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));

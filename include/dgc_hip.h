@@ -172,7 +172,7 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
  * from the lists and the separate re-read of vec is skipped; otherwise one full pass
  * runs. Results are identical either way (spec only chooses the work).
  * On return spec[1] = the final threshold t and spec[0] = m x t x growth, growth =
- * t / (previous t) clamped to [1, 1.5]; m = spec_margin (0.8 is a good one) after a
+ * 2 - (previous t) / t (linear extrapolation) clamped to [1, 1.5]; m = spec_margin (0.8 is a good one) after a
  * call whose t fell below its list threshold, else 1.05 x (list threshold / t) of
  * that call, within [spec_margin, 0.95]: the lists shrink while t moves predictably.
  * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
