@@ -54,6 +54,16 @@ namespace dgc {
 
 constexpr int kSeg = 1024;                      // elements per segment
 constexpr int kCap = 64;                        // list slots per segment (6.25 %)
+// The lists of kLstTile consecutive segments interleave: entry e of segment s sits at
+// lcol(s) + e * kLstTile, so a 128-B line holds entries 0..7 of four lists. The
+// selection reads a list per segment (~7 entries at 1e-3): contiguous 256-B list slots
+// cost a line per segment there, the interleave a line per four. The four segments of
+// a tile are K1's (and the select pass's) four waves of one workgroup, so the tile's
+// lines fill in one L2.
+constexpr int kLstTile = 4;
+__host__ __device__ __forceinline__ int64_t lcol(int64_t seg) {
+    return (seg / kLstTile) * (kLstTile * kCap) + seg % kLstTile;
+}
 constexpr int kSegTiles = kSeg / (kWave * 4);   // 4 float4 per lane per segment
 constexpr int kSuper = 4;                       // segments per wave in the full select pass
 constexpr int kGroupSegs = 1024;                // segments per group (1M elements)
@@ -298,8 +308,8 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.seg_gt = c.take<uint32_t>(L.nseg);
     w.seg_eq = c.take<uint32_t>(L.nseg);
     w.seg_off = c.take<uint32_t>(L.nseg);
-    w.lst_off = c.take<uint16_t>(L.nseg * kCap);
-    w.lst_val = c.take<float>(L.nseg * kCap);
+    w.lst_off = c.take<uint16_t>(ceil_div(L.nseg, (int64_t)kLstTile) * kLstTile * kCap);
+    w.lst_val = c.take<float>(ceil_div(L.nseg, (int64_t)kLstTile) * kLstTile * kCap);
     w.queue = c.take<uint64_t>(L.ncand);
     w.cand_idx = c.take<int64_t>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
@@ -390,7 +400,8 @@ __device__ __forceinline__ uint32_t ge_mask(const float (&x)[4], uint32_t valid,
     return p & valid;
 }
 
-// Append the lanes' flagged elements (element order 4*lane + j) to a segment list.
+// Append the lanes' flagged elements (element order 4*lane + j) to a segment list
+// (lo / lv: its column, entries kLstTile apart).
 __device__ __forceinline__ void list_append(uint32_t p, const float (&x)[4], int tile_off, uint32_t& c,
                                             uint16_t* lo, float* lv) {
     if (__ballot(p != 0)) {
@@ -402,8 +413,8 @@ __device__ __forceinline__ void list_append(uint32_t p, const float (&x)[4], int
         for (int j = 0; j < 4; ++j) {
             if (p & (1u << j)) {
                 if (r < (uint32_t)kCap) {
-                    lo[r] = (uint16_t)(tile_off + 4 * lane + j);
-                    lv[r] = x[j];
+                    lo[r * kLstTile] = (uint16_t)(tile_off + 4 * lane + j);
+                    lv[r * kLstTile] = x[j];
                 }
                 ++r;
             }
@@ -582,8 +593,8 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     }
     uint32_t c = 0, mk = 0;
     const int64_t seg = d.seg0 + ls;
-    uint16_t* lo = w.lst_off + seg * kCap;
-    float* lv = w.lst_val + seg * kCap;
+    uint16_t* lo = w.lst_off + lcol(seg);
+    float* lv = w.lst_val + lcol(seg);
     if (st->def_mode && ls < d.nseg) apply_deferred_mask(*st, w, d, ls, lane, vv, mv);
 #pragma unroll
     for (int u = 0; u < kSegTiles; ++u) {
@@ -783,12 +794,14 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
         // (or, spilled, its elements)
         lc[j] = ((v >> 16) << 16) <= tkey ? 0u : lcnt_count(v);
     }
-    float4 a[kCountSegs], b[kCountSegs];
+    constexpr int kFirst = 8;   // entries loaded up front (one interleaved line)
+    float a[kCountSegs][kFirst];
 #pragma unroll
     for (int j = 0; j < kCountSegs; ++j) {
-        const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + (d.seg0 + lseg0 + j * kBlock + threadIdx.x) * kCap);
-        if (lc[j] > 0 && lc[j] <= (uint32_t)kCap) a[j] = l4[0];
-        if (lc[j] > 4 && lc[j] <= (uint32_t)kCap) b[j] = l4[1];
+        const float* lv = w.lst_val + lcol(d.seg0 + lseg0 + j * kBlock + threadIdx.x);
+#pragma unroll
+        for (int e = 0; e < kFirst; ++e)
+            if ((uint32_t)e < lc[j] && lc[j] <= (uint32_t)kCap) a[j][e] = lv[e * kLstTile];
     }
     uint32_t ctot = 0;
 #pragma unroll
@@ -802,25 +815,17 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
             continue;
         }
         uint32_t c = 0;
-        if (n > 0)
-            c += (fabsf(a[j].x) >= tc) + (1 < n && fabsf(a[j].y) >= tc) + (2 < n && fabsf(a[j].z) >= tc) +
-                 (3 < n && fabsf(a[j].w) >= tc);
-        if (n > 4)
-            c += (fabsf(b[j].x) >= tc) + (5 < n && fabsf(b[j].y) >= tc) + (6 < n && fabsf(b[j].z) >= tc) +
-                 (7 < n && fabsf(b[j].w) >= tc);
-        if (n > 8) {   // the rest of a longer list, its loads issued together
-            const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
-            float4 v[kCap / 4 - 2];
 #pragma unroll
-            for (int q = 2; q < kCap / 4; ++q)
-                if ((uint32_t)(4 * q) < n) v[q - 2] = l4[q];
+        for (int e = 0; e < kFirst; ++e) c += (uint32_t)e < n && fabsf(a[j][e]) >= tc;
+        // the rest of a longer list, 16 loads in flight at a time
+        const float* lv = w.lst_val + lcol(seg);
+        for (uint32_t e0 = kFirst; e0 < n; e0 += 16) {
+            float v[16];
 #pragma unroll
-            for (int q = 2; q < kCap / 4; ++q) {
-                const uint32_t e = 4 * q;
-                if (e < n)
-                    c += (fabsf(v[q - 2].x) >= tc) + (e + 1 < n && fabsf(v[q - 2].y) >= tc) +
-                         (e + 2 < n && fabsf(v[q - 2].z) >= tc) + (e + 3 < n && fabsf(v[q - 2].w) >= tc);
-            }
+            for (int q = 0; q < 16; ++q)
+                if (e0 + q < n) v[q] = lv[(e0 + q) * kLstTile];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) c += e0 + q < n && fabsf(v[q]) >= tc;
         }
         w.seg_cnt[seg] = c;
         ctot += c;
@@ -874,8 +879,8 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
                 const int64_t ls = sup * kSuper + sg;
                 const int64_t seg = d.seg0 + ls;
                 uint32_t c = 0;
-                uint16_t* lo = w.lst_off + seg * kCap;
-                float* lv = w.lst_val + seg * kCap;
+                uint16_t* lo = w.lst_off + lcol(seg);
+                float* lv = w.lst_val + lcol(seg);
                 if (ls < d.nseg) {   // uniform per wave
                     uint32_t mk = 0;
 #pragma unroll
@@ -1142,20 +1147,18 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         const int64_t seg = d.seg0 + ls;
         const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
         if (lc <= (uint32_t)kCap) {
-            const float4* l4 = reinterpret_cast<const float4*>(w.lst_val + seg * kCap);
-            float4 v[kCap / 4];
+            const float* lv = w.lst_val + lcol(seg);
+            for (uint32_t e0 = 0; e0 < lc; e0 += 16) {   // 16 loads in flight at a time
+                float v[16];
 #pragma unroll
-            for (int q = 0; q < kCap / 4; ++q)   // all loads issued before any use
-                if ((uint32_t)(4 * q) < lc) v[q] = l4[q];
+                for (int q = 0; q < 16; ++q)
+                    if (e0 + q < lc) v[q] = lv[(e0 + q) * kLstTile];
 #pragma unroll
-            for (int q = 0; q < kCap / 4; ++q) {
-                const uint32_t e = 4 * q;
-                const float a[4] = {fabsf(v[q].x), fabsf(v[q].y), fabsf(v[q].z), fabsf(v[q].w)};
+                for (int q = 0; q < 16; ++q)
+                    if (e0 + q < lc) {
+                        const float a = fabsf(v[q]);
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (e + r < lc) {
-#pragma unroll
-                        for (int j = 1; j <= kLowerLists; ++j) c[j] += (j <= ms) && a[r] >= th[j];
+                        for (int j = 1; j <= kLowerLists; ++j) c[j] += (j <= ms) && a >= th[j];
                     }
             }
         } else {
@@ -1232,7 +1235,7 @@ struct CandKeys {
             const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
             if (lc <= (uint32_t)kCap) {
                 if (lane < lc) {
-                    const float a = fabsf(w.lst_val[seg * kCap + lane]);
+                    const float a = fabsf(w.lst_val[lcol(seg) + lane * kLstTile]);
                     if (a >= tc) f(abs_key(a));
                 }
             } else {
@@ -1278,7 +1281,7 @@ k_count_gt_eq(const float* __restrict__ vec_flat, SelWS w) {
         const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
         if (lc <= (uint32_t)kCap) {
             for (uint32_t e = 0; e < lc; ++e) {
-                const float a = fabsf(w.lst_val[seg * kCap + e]);
+                const float a = fabsf(w.lst_val[lcol(seg) + e * kLstTile]);
                 gt += a > tk;
                 eq += a == tk;
             }
@@ -1529,18 +1532,16 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         }
         // (a list with nothing at the current threshold is not read: most of them at 1e-4)
         const bool short_list = ls < d.nseg && (ca > 0 || cb > 0) && lc <= (uint32_t)kEmitShort;
-        float4 sv[kEmitShort / 4];
-        uint4 so[kEmitShort / 8];
+        float v[kEmitShort];
+        uint16_t e[kEmitShort];
         if (short_list) {
-            const int64_t slot = (d.seg0 + ls) * kCap;
-            const float4* v4 = reinterpret_cast<const float4*>(w.lst_val + slot);
-            const uint4* o4 = reinterpret_cast<const uint4*>(w.lst_off + slot);
+            const int64_t col = lcol(d.seg0 + ls);
 #pragma unroll
-            for (int q = 0; q < kEmitShort / 4; ++q)
-                if ((uint32_t)(4 * q) < lc) sv[q] = v4[q];
-#pragma unroll
-            for (int q = 0; q < kEmitShort / 8; ++q)
-                if ((uint32_t)(8 * q) < lc) so[q] = o4[q];
+            for (int q = 0; q < kEmitShort; ++q)
+                if ((uint32_t)q < lc) {
+                    v[q] = w.lst_val[col + q * kLstTile];
+                    e[q] = w.lst_off[col + q * kLstTile];
+                }
         }
         // (earlier quarters' total << 32) | this quarter's counts: one scan gives both
         uint64_t tot;
@@ -1560,8 +1561,6 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         __syncthreads();   // obase_s
         if (work && short_list) {
             const long long ob0 = obase_s;
-            const float* v = reinterpret_cast<const float*>(sv);
-            const uint16_t* e = reinterpret_cast<const uint16_t*>(so);
             if (!rs) {   // the first `limit` entries >= tc, in index order
                 long long pos = ga + oa;
 #pragma unroll
@@ -1609,7 +1608,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
             x[q] = 0.f;
             e[q] = 0;
             if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
-                const int64_t slot = (d.seg0 + lseg0 + j0 + q) * kCap + lane;
+                const int64_t slot = lcol(d.seg0 + lseg0 + j0 + q) + lane * kLstTile;
                 x[q] = w.lst_val[slot];
                 e[q] = w.lst_off[slot];
             }
@@ -1721,7 +1720,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
             x[q] = 0.f;
             e[q] = 0;
             if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
-                const int64_t slot = (d.seg0 + lseg0 + j0 + q) * kCap + lane;
+                const int64_t slot = lcol(d.seg0 + lseg0 + j0 + q) + lane * kLstTile;
                 x[q] = w.lst_val[slot];
                 e[q] = w.lst_off[slot];
             }
