@@ -1481,12 +1481,16 @@ constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
 static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
 
 __global__ void __launch_bounds__(kEmitSegs)
-k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     const int t = task(w, BT_GRP, blockIdx.x);
     const SelState* st = w.st + t;
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
-    if (k5 != (o.queue != nullptr)) return;
+    // oa.queue set: the K5 tensors gather their candidates into the queue and the
+    // others emit their payload in the same launch; unset: the K5 tensors are skipped
+    if (k5 && !oa.queue) return;
+    EmitOut o = oa;
+    if (!k5) o.queue = nullptr;
     const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
@@ -1655,12 +1659,16 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
 // wave. More waves per quarter beat k_emit's short-list threads there (measured on
 // ResNet-50: 12 vs 15 us per launch).
 __global__ void __launch_bounds__(kGroupSegs)
-k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     const int t = task(w, BT_GRP, blockIdx.x);
     const SelState* st = w.st + t;
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
-    if (k5 != (o.queue != nullptr)) return;
+    // oa.queue set: the K5 tensors gather their candidates into the queue and the
+    // others emit their payload in the same launch; unset: the K5 tensors are skipped
+    if (k5 && !oa.queue) return;
+    EmitOut o = oa;
+    if (!k5) o.queue = nullptr;
     const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
@@ -2044,7 +2052,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         return DGC_OK;
     };
     auto resample_exact = [&]() -> int {
-        // nth_element path: gather candidates, replay the introselect, emit in its order
+        // nth_element path: gather candidates, replay the introselect, emit in its order.
+        // The gather launch also emits every other tensor's payload (the final emit).
         EmitOut g = o;
         g.queue = w.queue;
         g.cand = w.cand_idx;
@@ -2056,6 +2065,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         return DGC_OK;
     };
     DGC_TRY(keep_lists ? pass(3, true) : pass(2, false));
+    bool emitted = false;   // the payload of every non-K5 tensor is written
     if (sync_mode == DGC_SYNC_HOST) {
         // read the decisions back and launch only what they need
         std::vector<SelState> hs(L.T);
@@ -2092,7 +2102,10 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
                 any_low = true;
         }
         if (any_low) DGC_TRY(resample_lowest());
-        if (any_nth || any_heap) DGC_TRY(resample_exact());   // k_nth_select serves both
+        if (any_nth || any_heap) {   // k_nth_select serves both
+            DGC_TRY(resample_exact());
+            emitted = true;
+        }
     } else if (L.adapt_any) {
         // every kernel below early-exits on a device flag when it is not needed
         if (lower_fast) {
@@ -2104,9 +2117,10 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         if (p.resample) {
             if (L.lowest_any) DGC_TRY(resample_lowest());   // 4 gated launches no tensor here can need
             DGC_TRY(resample_exact());
+            emitted = true;
         }
     }
-    DGC_TRY(launch_emit(L, vec, w, o, s));
+    if (!emitted) DGC_TRY(launch_emit(L, vec, w, o, s));
     hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, count_out, info, margin,
                        (int)(p.update_memory == 2), (int)(p.masking != 0));
     DGC_LAUNCHED();
