@@ -12,7 +12,10 @@ each tensor at a 1024-element-aligned offset) and runs
     dgc_batch_compress   K1 over all tensors, K3 for all thresholds, the selection
                          chain with per-tensor state, one packed payload
     one allgather        the packed payload, RCCL over xGMI (gloo stages via the host)
-    decompress           dgc_decompress_packed (zero fill + scatter) over the flat gradient
+    decompress           dgc_decompress_packed (zero fill + scatter) over the flat gradient,
+                         or — into the batch's persistent output (``fill="sparse"``, the
+                         default) — dgc_decompress_packed_over: only the previous step's
+                         gathered indices are re-zeroed, as in ``DGCBucket``
 
 with O(1) launches per phase and no host synchronisation. The payload carries flat
 indices (tensor offset + index in the tensor), tensor after tensor.
@@ -46,7 +49,10 @@ class DGCBatch:
     def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
                  resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
-                 deferred_masking=True):
+                 deferred_masking=True, fill="sparse"):
+        if fill not in ("inline", "sparse"):
+            raise ValueError(f"fill must be 'inline' or 'sparse', not {fill!r}")
+        self.fill = fill
         self.device = torch.device(device or "cuda")
         self.names = [n for n, _ in named_shapes]
         self.shapes = {n: tuple(s) for n, s in named_shapes}
@@ -109,11 +115,27 @@ class DGCBatch:
         self.capacity = sum(a[0] for a in self.attrs)
         from .compression import _layout
         self.rank_stride, self.voff, self.ioff = _layout(self.capacity, self.vdtype, self.idtype)
-        self.payload = torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device)
-        self.gathered = (torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=self.device)
-                         if self.world > 1 else self.payload)
+        # fill="sparse": two payload / gather buffers, so the previous step's gathered
+        # indices stay readable for the re-zero; a new layout forgets them
+        nbuf = 2 if self.fill == "sparse" else 1
+        self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(nbuf)]
+        self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=self.device)
+                          for _ in range(nbuf)] if self.world > 1 else self._payloads)
+        self._par = 0
+        self._last_out = None
+        self._last_gathered = None
         self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(self.flat_numel, self.world, self.capacity),
                                   dtype=torch.uint8, device=self.device)
+
+    @property
+    def payload(self):
+        """This rank's packed payload of the current step."""
+        return self._payloads[self._par % len(self._payloads)]
+
+    @property
+    def gathered(self):
+        """The allgather buffer of the current step (the payload itself at W = 1)."""
+        return self._gathers[self._par % len(self._gathers)]
 
     def flush(self):
         """Applies a deferred masking now (no-op when none is pending)."""
@@ -164,6 +186,7 @@ class DGCBatch:
         masking the previous select left pending)."""
         starts = self.draw_starts() if starts is None else starts
         self.starts = starts
+        self._par += 1   # a step starts: the other payload / gather buffer
         arr = (ctypes.c_int64 * len(starts))(*starts)
         _lib.check(self._L.dgc_batch_compress_begin(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
                                                     self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
@@ -190,15 +213,35 @@ class DGCBatch:
             comm.allgather_packed_async(self.payload, out=self.gathered).wait()
 
     def decompress(self, out_flat=None):
-        """out = the rank-order sum of the gathered entries / W, +0.0 elsewhere (every tensor)."""
+        """out = the rank-order sum of the gathered entries / W, +0.0 elsewhere (every tensor).
+
+        fill="sparse": when ``out`` still holds exactly the previous decompress's result
+        (same storage, torch version counter unchanged — our writes are raw-pointer
+        writes) and is not the gradient buffer (the batched optimizer decompresses into
+        p.grad, rewritten by every backward), the zero_() re-zeroes only the previous
+        step's gathered indices (dgc_decompress_packed_over) instead of the whole
+        buffer: identical result, W * capacity slots instead of flat_numel."""
         out = self.out_flat if out_flat is None else out_flat
         L = self._L
         st = _lib.stream_of(self.device)
-        # the zero fill and the scatter in one call: the fill also resets the scatter's status words
-        _lib.check(L.dgc_decompress_packed(self.gathered.data_ptr(), self.world, self.rank_stride, self.capacity,
-                                           _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
-                                           self.flat_numel, 1.0 / self.world, self.dec_ws.data_ptr(),
-                                           self.dec_ws.numel(), st), "dgc_decompress_packed")
+        cur = self.gathered
+        args = (self.world, self.rank_stride, self.capacity, _lib.VD[self.vdtype], _lib.ID[self.idtype],
+                out.data_ptr(), self.flat_numel, 1.0 / self.world, self.dec_ws.data_ptr(), self.dec_ws.numel(), st)
+        aliased = out.untyped_storage().data_ptr() == self.grad_flat.untyped_storage().data_ptr()
+        reusable = (self.fill == "sparse" and not aliased and self._last_gathered is not None
+                    and self._last_gathered is not cur
+                    and self._last_out == (out.data_ptr(), out.numel(), out._version))
+        if reusable:
+            _lib.check(L.dgc_decompress_packed_over(cur.data_ptr(), self._last_gathered.data_ptr(), *args),
+                       "dgc_decompress_packed_over")
+        else:
+            # the zero fill and the scatter in one call: the fill also resets the scatter's status words
+            _lib.check(L.dgc_decompress_packed(cur.data_ptr(), *args), "dgc_decompress_packed")
+        if aliased:
+            self._last_out = self._last_gathered = None
+        else:
+            self._last_out = (out.data_ptr(), out.numel(), out._version)
+            self._last_gathered = cur
         return out
 
     def step(self, starts=None):

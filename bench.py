@@ -265,12 +265,13 @@ class ModelRun:
     step, the dense (dim <= 1) tensors as one flat allreduce + compensate(accumulate=False)
     (dgc/compression.py:173-177, 195-198)."""
 
-    def __init__(self, wl, rank, world, dev):
+    def __init__(self, wl, rank, world, dev, fill="auto"):
         from dgc import workloads
         from dgc.batch import DGCBatch
         comp, dense = workloads.split(getattr(workloads, wl["model"])())
         self.b = DGCBatch(comp, compress_ratio=wl["ratio"], momentum=0.9, nesterov=wl["nesterov"],
-                          fp16_values=wl["fp16"], int32_indices=wl["int32"], device=dev, world_size=world, seed=42)
+                          fp16_values=wl["fp16"], int32_indices=wl["int32"], device=dev, world_size=world, seed=42,
+                          fill="inline" if fill in ("inline", "allgather") else "sparse")
         self.n_comp = sum(self.b.numels)
         self.n_dense = sum(workloads.numel(s) for _, s in dense)
         self.world = world
@@ -335,7 +336,7 @@ class ModelRun:
 
     def config(self):
         return {"compressed_tensors": len(self.b.names), "compressed_elements": self.n_comp,
-                "dense_elements": self.n_dense, "num_selects_total": self.b.capacity}
+                "dense_elements": self.n_dense, "num_selects_total": self.b.capacity, "fill": self.b.fill}
 
 
 def hbm_probe(reads, writes, reps=5):
@@ -370,13 +371,13 @@ def step_bytes(run, world, full_passes):
     selection) + dense decompress write 4, the samples 4S, masking 8k, payload written
     k(vb+ib) + gathered W*k(vb+ib) read, scatter RMW 8Wk. `contract` keeps the 28 B
     of SURVEY.md §8d; `required` is what this step's path actually needs: no re-read
-    when the lists serve, and for the flat bucket's persistent output (fill "sparse")
+    when the lists serve, and for a persistent output (fill "sparse": bucket or batch)
     a re-zero of the previous step's W*k slots (4 B each) instead of the dense 4 B/elem."""
     n = run.n_comp if isinstance(run, ModelRun) else run.N
     k, S = run.k, run.S
     sparse = 4 * S + 8 * k + (1 + world) * k * (run.vbytes + run.ibytes) + 8 * world * k
     contract = 28 * n + sparse
-    rezero = isinstance(run, FlatRun) and run.b.fill == "sparse"
+    rezero = run.b.fill == "sparse"
     required = (20 + (0 if full_passes == 0 else 4) + (0 if rezero else 4)) * n + sparse + (4 * world * k if rezero else 0)
     if isinstance(run, ModelRun):   # dense tensors: read g, mmt; write mmt, out
         contract += 16 * run.n_dense
@@ -398,7 +399,7 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev)
+    run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev, args.fill)
 
     log(f"{args.workload}: rank {rank}/{world} set up")
     phases = ("compensate", "select", "allgather", "decompress")

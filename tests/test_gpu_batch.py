@@ -137,6 +137,9 @@ def test_batch_warmup_ratio_change():
             grads[name] = synth.gradient(77 * s + t, b.numels[t], "normal", 0.01)
             b.grad(name).copy_(torch.from_numpy(grads[name]).view(b.shapes[name]))
         b.compress()
+        if s == 4:
+            b.out_flat.add_(1.0)   # an in-place write (version bump): the next decompress fills densely
+        out = b.decompress()   # persistent output: sparse re-zero except after a ratio change
         torch.cuda.synchronize()
         sent = b.transmitted()
         for t, name in enumerate(b.names):
@@ -147,3 +150,34 @@ def test_batch_warmup_ratio_change():
             wv, wi = O.wire_cast(ov, oi, True, True)
             assert np.array_equal(sent[name][1].cpu().numpy(), oi), (s, name)
             assert np.array_equal(bits(sent[name][0].cpu().numpy()), bits(wv)), (s, name)
+            dense = O.decompress([wv], [oi], b.numels[t], 1)
+            assert np.array_equal(bits(b.out(name).reshape(-1).cpu().numpy()), bits(dense)), (s, name)
+        pad = torch.ones(b.flat_numel, dtype=torch.bool, device=DEV)
+        for off, n in zip(b.offsets, b.numels):
+            pad[off: off + n] = False
+        assert not bool(out[pad].any()), s
+
+
+def test_batch_sparse_rezero_matches_dense_fill():
+    """fill="sparse" (the persistent output's re-zero of the previous step's entries)
+    against fill="inline" (the dense zero_() every step): identical outputs, step by
+    step, on the ResNet-50 set with the bench's synthetic gradients."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc import workloads
+    from dgc.batch import DGCBatch
+    shapes, _ = workloads.split(workloads.resnet50())
+    bs = [DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, device=DEV, seed=3, fill=f)
+          for f in ("sparse", "inline")]
+    gen = torch.Generator(device=DEV)
+    for s in range(6):
+        gen.manual_seed(100 + s % 2)
+        g = torch.zeros(bs[0].flat_numel, device=DEV)
+        for off, n in zip(bs[0].offsets, bs[0].numels):
+            g[off: off + n] = torch.randn(n, generator=gen, device=DEV) * 1e-3
+        outs = []
+        for b in bs:
+            b.grad_flat.copy_(g)
+            b.compress()
+            outs.append(b.decompress())
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), s
