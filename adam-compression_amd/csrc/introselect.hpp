@@ -27,8 +27,10 @@
 // numpy, checked against torch.topk itself.
 //
 // Phases, by the size of the range still being partitioned:
+//   > kNthGMinCand      (select.hip) in global memory by G co-resident workgroups per
+//                       tensor, a barrier among them per pass (k_nth_global);
 //   > kNthLds entries   in global memory (L2 / Infinity-Cache resident), 8 waves, each
-//                       over a contiguous stretch, 4 tiles of loads in flight per lane;
+//                       over a contiguous stretch, 8 tiles of loads in flight per lane;
 //   > kNthWave entries  in LDS, same 8-wave step (four barriers per step);
 //   <= kNthWave         one wave, wave-synchronous (no workgroup barrier at all).
 // Entries are (key << 32 | j), key = |x| bits.
@@ -556,13 +558,233 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
     wave_sync();
 }
 
+// ---------------------------------------------------------------- multi-workgroup global phase
+// The global-memory steps (range > kNthLds) spread over G co-resident workgroups of
+// one tensor (k_nth_global, a cooperative launch): one workgroup's loads in flight
+// bound the one-workgroup phase (57k candidates: 50 us in 2 steps, tools/k5_prof.py).
+// The step is the same partition as nth_step_wg — the G x 8 waves take contiguous
+// stretches in order, so every stopper's rank is the same — with a barrier among the
+// G workgroups where nth_step_wg has __syncthreads: counts | pairing | swaps | advance.
+constexpr int kNthGMax = 32;      // workgroups per tensor
+constexpr int kNthGMk = 32768;    // stopper bytes per workgroup kept in LDS (512 tiles)
+
+struct NthG {
+    int64_t f, l, depth;
+    unsigned long long l_next, r_min;
+    uint32_t pivot, s;
+    int32_t heap_exit, go;
+    uint32_t bar_count, bar_gen;   // zeroed by k_sel_init
+    uint32_t bl[kNthGMax], br[kNthGMax];
+};
+
+// Barrier among the G workgroups of one tensor (all co-resident: cooperative launch).
+// Agent-scope release / acquire around the arrival make every workgroup's global
+// stores visible to the others across XCDs. The spin is bounded (~seconds): a broken
+// launch then yields a wrong result instead of a hung GPU.
+__device__ __forceinline__ void nthg_barrier(NthG* g, uint32_t G) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t gen = __hip_atomic_load(&g->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        const uint32_t a = atomicAdd(&g->bar_count, 1u);
+        if (a == G - 1) {
+            __hip_atomic_store(&g->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&g->bar_gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
+                if (__hip_atomic_load(&g->bar_gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __threadfence();
+    }
+    __syncthreads();
+}
+
+// Block 0, thread 0: the next step's median and the reset of its results, or the end
+// of the phase (go = 0: range <= kNthLds, or the depth-limit heap exit).
+__device__ void nthg_prepare(uint64_t* q, NthG* g, int64_t nth) {
+    int go = 0;
+    if (g->l - g->f > kNthLds && !g->heap_exit) {
+        if (g->depth == 0) {
+            nth_heap_select(q + g->f, nth + 1 - g->f, g->l - g->f, nth - g->f);
+            g->heap_exit = 1;
+        } else {
+            g->depth -= 1;
+            g->pivot = nth_median(q, g->f, g->l);
+            g->s = 0;
+            g->l_next = ~0ull;
+            g->r_min = ~0ull;
+            go = 1;
+        }
+    }
+    g->go = go;
+}
+
+// The global phase of std::nth_element(q, q + nth, q + n) by G workgroups (block b of
+// G); on return g->f / l / depth / heap_exit hold where the one-workgroup kernel goes on.
+// Ranges of <= min_run entries are left to the one-workgroup phase: below ~140k
+// candidates the four cross-XCD barriers per step cost more than the spread saves
+// (tools/k5ab.sh: 100k 0.28 vs 0.25 ms, 500k 0.43 vs 0.94, 1M 0.55 vs 1.44).
+__device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* lpos, uint32_t* rpos, NthG* g,
+                                 uint32_t b, uint32_t G, int64_t min_run) {
+    constexpr int kB = 8;   // tiles of loads in flight per lane
+    __shared__ uint8_t mk[kNthGMk];
+    __shared__ uint32_t wl[kNthWaves], wr[kNthWaves], pre_l, pre_r, tot_r, s_sh;
+    __shared__ int64_t sf, sl;
+    __shared__ uint32_t sP;
+    __shared__ int sgo;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (n <= min_run || nth >= n) {   // uniform over the G workgroups: no barrier needed
+        if (b == 0 && threadIdx.x == 0) {
+            g->f = 0;
+            g->l = n;
+            g->depth = n > 0 ? 2 * (int64_t)(63 - __clzll((unsigned long long)n)) : 0;
+            g->heap_exit = 0;
+        }
+        return;
+    }
+    if (b == 0 && threadIdx.x == 0) {
+        g->f = 0;
+        g->l = n;
+        g->depth = n > 0 ? 2 * (int64_t)(63 - __clzll((unsigned long long)n)) : 0;
+        g->heap_exit = 0;
+        if (n > 0 && nth < n)
+            nthg_prepare(q, g, nth);
+        else
+            g->go = 0;
+    }
+    nthg_barrier(g, G);
+    for (;;) {
+        if (threadIdx.x == 0) {
+            sgo = g->go;
+            sf = g->f;
+            sl = g->l;
+            sP = g->pivot;
+        }
+        __syncthreads();
+        if (!sgo) break;
+        const int64_t f = sf, l = sl;
+        const uint32_t P = sP;
+        const int64_t a0 = f + 1, base = nth_base(q, a0), R = l - base;
+        const int64_t GW = (int64_t)G * kNthWaves;
+        const int64_t per = ceil_div(ceil_div(R, GW), (int64_t)256) * 256;
+        const int64_t bb = base + (int64_t)b * kNthWaves * per;   // this workgroup's first tile
+        const int64_t wb = bb + wv * per, we = wb + per < l ? wb + per : l;
+        const bool keep = kNthWaves * per / 256 <= kNthGMk / 64;
+        // pass 1: stopper counts
+        uint32_t cl = 0, cr = 0;
+        for (int64_t t0 = wb; t0 < we; t0 += 256 * kB) {
+            uint64_t x[kB][4];
+            uint32_t valid[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) nth_load4(q, t0 + u * 256 + 4 * lane, a0, we, x[u], valid[u]);
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                uint32_t pl, pr;
+                stopper_masks(x[u], valid[u], P, pl, pr);
+                cl += __popc(pl);
+                cr += __popc(pr);
+                if (keep && t0 + u * 256 < we) mk[((t0 + u * 256 - bb) >> 8) * 64 + lane] = (uint8_t)(pl | (pr << 4));
+            }
+        }
+        cl = wave_sum(cl);
+        cr = wave_sum(cr);
+        if (lane == 0) {
+            wl[wv] = cl;
+            wr[wv] = cr;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t a = 0, c = 0;
+            for (int i = 0; i < kNthWaves; ++i) {
+                a += wl[i];
+                c += wr[i];
+            }
+            g->bl[b] = a;
+            g->br[b] = c;
+        }
+        nthg_barrier(g, G);
+        if (threadIdx.x == 0) {
+            uint32_t a = 0, c = 0, r = 0;
+            for (uint32_t i = 0; i < G; ++i) {
+                const uint32_t x = __hip_atomic_load(&g->bl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t y = __hip_atomic_load(&g->br[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                a += i < b ? x : 0u;
+                r += i < b ? y : 0u;
+                c += y;
+            }
+            pre_l = a;
+            pre_r = r;
+            tot_r = c;
+        }
+        __syncthreads();
+        // pass 2: ranks, pairing, paired positions; the stoppers before this wave's
+        // stretch: the workgroups before b, then the waves before wv
+        uint32_t runl = pre_l, runr = pre_r;
+        const uint32_t TR = tot_r;
+#pragma unroll
+        for (int i = 0; i < kNthWaves; ++i) {
+            runl += i < wv ? wl[i] : 0u;
+            runr += i < wv ? wr[i] : 0u;
+        }
+        uint32_t paired = 0, lnext = UINT32_MAX, rmin = UINT32_MAX;
+        if (keep) {
+            for (int64_t t0 = wb; t0 < we; t0 += 256) {
+                const uint32_t m = mk[((t0 - bb) >> 8) * 64 + lane];
+                pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+            }
+        } else {
+            for (int64_t t0 = wb; t0 < we; t0 += 256 * kB) {
+                uint64_t x[kB][4];
+                uint32_t valid[kB];
+#pragma unroll
+                for (int u = 0; u < kB; ++u) nth_load4(q, t0 + u * 256 + 4 * lane, a0, we, x[u], valid[u]);
+#pragma unroll
+                for (int u = 0; u < kB; ++u) {
+                    uint32_t pl, pr;
+                    stopper_masks(x[u], valid[u], P, pl, pr);
+                    pair_tile<false>(pl, pr, t0 + u * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+                }
+            }
+        }
+        paired = wave_sum(paired);
+        lnext = wave_min_u32(lnext);
+        rmin = wave_min_u32(rmin);
+        if (lane == 0) {
+            if (paired) atomicAdd(&g->s, paired);
+            if (lnext != UINT32_MAX) atomicMin(&g->l_next, (unsigned long long)(f + lnext));
+            if (rmin != UINT32_MAX) atomicMin(&g->r_min, (unsigned long long)(f + rmin));
+        }
+        nthg_barrier(g, G);
+        // pass 3: the swaps L_t <-> R_t, t < s, over all G workgroups
+        if (threadIdx.x == 0) s_sh = __hip_atomic_load(&g->s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        nth_swaps<8>(q, lpos, rpos, f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
+        nthg_barrier(g, G);
+        // the cut, the next range and the next median
+        if (b == 0 && threadIdx.x == 0) {
+            const int64_t rs = g->s ? (int64_t)g->r_min : g->l;
+            const int64_t ln = g->l_next == ~0ull ? INT64_MAX : (int64_t)g->l_next;
+            const int64_t cut = ln < rs ? ln : rs;
+            if (cut <= nth)
+                g->f = cut;
+            else
+                g->l = cut;
+            nthg_prepare(q, g, nth);
+        }
+        nthg_barrier(g, G);
+    }
+}
+
 // std::nth_element(q, q + nth, q + n, comp) in place, by the calling 512-thread
 // workgroup. gpos_l/gpos_r: global pair slots (>= n / 2 + 1 each) for the ranges
 // above kNthLds. Returns after a final barrier.
 // lq: the caller's LDS area of kNthLds entries (16-B aligned): the partition range
 // in the LDS phase, the stopper bytes in the global phase.
+// from: the state k_nth_global left (its global phase done), or null (start at [0, n)).
 __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r,
-                               uint64_t* lq) {
+                               uint64_t* lq, const NthG* from = nullptr) {
     __shared__ NthShared sh;
     __shared__ uint32_t llp[kNthLds / 2 + 1], lrp[kNthLds / 2 + 1];
     __shared__ uint8_t lmk[(kNthLds / 256 + 1) * 64];   // LDS phase stopper bytes
@@ -571,6 +793,12 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
         sh.l = n;
         sh.depth = n > 0 ? 2 * (int64_t)(63 - __clzll((unsigned long long)n)) : 0;
         sh.heap_exit = 0;
+        if (from && n > 0 && nth < n) {
+            sh.f = from->f;
+            sh.l = from->l;
+            sh.depth = from->depth;
+            sh.heap_exit = from->heap_exit;
+        }
     }
     __syncthreads();
     if (n <= 0 || nth >= n) return;

@@ -170,6 +170,7 @@ struct SelWS {
     uint64_t* queue;           // K5: (|x| key << 32 | j) for the candidates j, ascending index order
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
+    NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
     int64_t nseg, ngrp;
 };
 
@@ -191,6 +192,7 @@ struct TensorIn {
 struct Layout {
     int32_t T = 0;
     int64_t nseg = 0, ngrp = 0, nsamp = 0, ncand = 0, ngpos = 0;
+    int64_t max_cand = 0;       // the largest K5 candidate capacity of a tensor
     int32_t nsmall = 0;
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool lowest_any = false;    // some tensor can take the approximate partial_sort resample
@@ -252,6 +254,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.cand_off = cand;
         d.cand_cap = nth_cand_cap(d.n, d.k);
         cand += d.cand_cap;
+        L.max_cand = std::max(L.max_cand, d.cand_cap);
         d.gpos_off = gpos;
         gpos += 2 * (d.cand_cap / 2 + 1);
         d.idx_base = T > 1 ? d.off : 0;
@@ -313,6 +316,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.queue = c.take<uint64_t>(L.ncand);
     w.cand_idx = c.take<int64_t>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
+    w.nthg = c.take<NthG>(L.T);
     if (bytes) *bytes = c.bytes();
     return w;
 }
@@ -719,6 +723,10 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lis
     const int t = blockIdx.x;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     SelState* st = w.st + t;
+    if (threadIdx.x == 0) {   // K5's multi-workgroup barrier starts from zero
+        w.nthg[t].bar_count = 0;
+        w.nthg[t].bar_gen = 0;
+    }
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
         w.grp_gt[d.grp0 + i] = 0;
@@ -1888,8 +1896,20 @@ __device__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& 
 // gathered candidates (introselect.hpp: nth_element), or — partial_sort path, k <=
 // kHeapMax — heap select + sort_heap over vec, which also emits. They share one LDS area.
 static_assert(kHeapMax + (int64_t)kHeapThreads * kHeapPer <= kNthLds, "K5b: heap + chunk fit K5's LDS");
+// K5's global-memory phase by G workgroups per tensor (grid G x T, cooperative launch:
+// all co-resident); k_nth_select goes on from the state it leaves (introselect.hpp).
+__global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G, int64_t min_run) {
+    const int t = blockIdx.y;
+    const SelState* st = w.st + t;
+    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;
+    const TDesc d = w.td[t];
+    uint32_t* gl = w.gpos + d.gpos_off;
+    uint32_t* gr = gl + d.cand_cap / 2 + 1;
+    nth_global_multi(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, w.nthg + t, blockIdx.x, G, min_run);
+}
+
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
-                                                            EmitOut o) {
+                                                            EmitOut o, int from_global) {
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || !st->rs_nth) return;
@@ -1901,7 +1921,7 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     uint32_t* gl = w.gpos + d.gpos_off;
     uint32_t* gr = gl + d.cand_cap / 2 + 1;
-    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, lq);
+    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, lq, from_global ? w.nthg + t : nullptr);
 }
 
 // Result records; the payload's total count; and every tensor's next speculative
@@ -2001,6 +2021,38 @@ static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const 
     return DGC_OK;
 }
 
+// Workgroups per tensor for k_nth_global: half the CUs shared among the T tensors, at
+// most kNthGMax. Its workgroups wait for each other, so all of them must be resident at
+// once: <= CUs / 2 workgroups of 8 waves and 33 KB LDS (one fits a CU) guarantee that
+// with this stream's earlier kernels done. (hipLaunchCooperativeKernel checks the same
+// but cost ~29 us per launch on MI355X: more than the phase saves below ~200k candidates.)
+// <= 1 runs the one-workgroup global phase inside k_nth_select instead; so does a call
+// whose tensors all have candidate capacities <= kNthGMinCand, and so does a tensor
+// with <= kNthGMinCand candidates (decided on the device: below ~140k the four
+// cross-XCD barriers per step cost more than the spread saves, tools/k5ab.sh), and
+// DGC_K5_GLOBAL=wg (A/B, parity); DGC_K5_GLOBAL=multi skips both gates.
+constexpr int64_t kNthGMinCand = 196608;   // launch for capacities above, run for candidate counts above
+
+static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
+    static int per_dev = -1;
+    if (per_dev < 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_nth_global),
+                                                         kNthThreads, 0) != hipSuccess)
+            per_dev = 0;
+        else
+            per_dev = per_cu >= 1 ? cus / 2 : 0;
+
+    }
+    const char* force = std::getenv("DGC_K5_GLOBAL");   // wg | multi (parity tests run both)
+    if (force && std::strcmp(force, "wg") == 0) return 0;
+    if (max_cand <= kNthLds || (max_cand <= kNthGMinCand && !(force && std::strcmp(force, "multi") == 0))) return 0;
+    const int64_t g = T > 0 ? per_dev / T : 0;
+    return (uint32_t)std::min<int64_t>(g, kNthGMax);
+}
+
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
                        int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists, int sync_mode,
                        float margin, hipStream_t s) {
@@ -2058,7 +2110,14 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         g.queue = w.queue;
         g.cand = w.cand_idx;
         DGC_TRY(launch_emit(L, vec, w, g, s));
-        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o);
+        const uint32_t G = nth_global_groups(L.T, L.max_cand);
+        if (G > 1) {
+            const char* force = std::getenv("DGC_K5_GLOBAL");
+            const int64_t min_run = (force && std::strcmp(force, "multi") == 0) ? 0 : kNthGMinCand;
+            hipLaunchKernelGGL(k_nth_global, dim3(G, (unsigned)L.T), dim3(kNthThreads), 0, s, w, G, min_run);
+            DGC_LAUNCHED();
+        }
+        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0);
         DGC_LAUNCHED();
         hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
         DGC_LAUNCHED();

@@ -38,16 +38,20 @@ def _sets():
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("label,shape", [("mixed", None), ("resnet50", None), ("vgg16_bn", None),
-                                         ("mixed", "quarter"), ("resnet50", "quarter"), ("mixed+naninf", None)])
+                                         ("mixed", "quarter"), ("resnet50", "quarter"), ("mixed+naninf", None),
+                                         ("mixed", "k5multi"), ("resnet50", "k5multi")])
 def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
     """shape: the emit kernel (None: the library's choice — k_emit_wide for these few
-    groups; "quarter": k_emit, the flat buckets' kernel, forced). "+naninf": tensor "b"
+    groups; "quarter": k_emit, the flat buckets' kernel, forced), or "k5multi": the
+    resample replay's global phase over several workgroups per tensor (k_nth_global). "+naninf": tensor "b"
     gets a NaN at one of its samples on step 1 (its threshold turns NaN, nothing of it
     is selected), "odd" a NaN that is never sampled and "c" +-inf — the other tensors'
     selections must not notice."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    if shape:
+    if shape == "k5multi":   # K5's global phase over several workgroups per tensor, whatever the capacity
+        monkeypatch.setenv("DGC_K5_GLOBAL", "multi")
+    elif shape:
         monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
     from dgc.batch import DGCBatch
     naninf = label.endswith("+naninf")

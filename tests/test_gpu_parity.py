@@ -236,10 +236,15 @@ RESAMPLE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("k5", ["multi", "wg"])
 @pytest.mark.parametrize("case", RESAMPLE_CASES, ids=[c[0] for c in RESAMPLE_CASES])
-def test_resample_replays_torch_topk(L, case):
+def test_resample_replays_torch_topk(L, case, k5, monkeypatch):
     """K5: the resample's indices are torch.topk(importance[indices], k, sorted=False)'s,
-    IN ORDER (dgc/compression.py:134-137), so the payload bytes equal the reference's."""
+    IN ORDER (dgc/compression.py:134-137), so the payload bytes equal the reference's.
+    k5: the global-memory phase (> 12288 candidates) over several co-resident
+    workgroups (k_nth_global; by default only for candidate capacities > 262144) or
+    inside the one-workgroup kernel."""
+    monkeypatch.setenv("DGC_K5_GLOBAL", k5)
     name, n, ratio, kind, target = case
     attrs = O.attributes(n, ratio)
     k = attrs[1]
