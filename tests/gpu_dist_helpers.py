@@ -212,3 +212,54 @@ def bucket_worker(rank, world, port, fill, kind, queue):
         queue.put((rank, [("error", repr(e), traceback.format_exc())]))
     finally:
         dist.destroy_process_group()
+
+
+def batch_worker(rank, world, port, fill, kind, queue):
+    """DGCBatch at W ranks (one packed payload of every tensor, allgather, decompress
+    into the batch's persistent output — fill "sparse" re-zeroes only the previous
+    step's gathered indices) against the oracle over all ranks' payloads, per tensor
+    and step."""
+    import torch.distributed as dist
+    _init(rank, world, port)
+    problems = []
+    try:
+        from dgc.batch import DGCBatch
+        from oracle import dgc_oracle as O
+        from oracle import synth
+        dev = torch.device("cuda:0")
+        shapes = [("a", (1000, 300)), ("b", (257, 3, 3, 64)), ("c", (70001,)), ("d", (2000, 500))]
+        ratio = 0.001
+        b = DGCBatch(shapes, compress_ratio=ratio, momentum=0.9, nesterov=False, device=dev, world_size=world,
+                     seed=7, fill=fill)
+        state = {(q, n): (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
+                 for q in range(world) for i, n in enumerate(b.names)}
+        branches = []
+        for s in range(5):
+            gs = {(q, n): synth.gradient(1000 * s + 10 * i + q, b.numels[i], kind, 1e-3)
+                  for q in range(world) for i, n in enumerate(b.names)}
+            for n in b.names:
+                b.grad(n).copy_(torch.from_numpy(gs[(rank, n)]).view(b.shapes[n]))
+            b.compress()
+            b.exchange()
+            b.decompress()
+            torch.cuda.synchronize()
+            for i, n in enumerate(b.names):
+                attrs = O.attributes(b.numels[i], ratio)
+                vals, idxs = [], []
+                for q in range(world):
+                    m, v = state[(q, n)]
+                    ov, oi, info = O.compress_step(gs[(q, n)], m, v, attrs, b.starts[i])
+                    vals.append(ov)
+                    idxs.append(oi)
+                    if q == rank:
+                        branches.append(info["branch"])
+                want = O.decompress(vals, idxs, b.numels[i], world)
+                got = b.out(n).reshape(-1).cpu().numpy()
+                if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                    problems.append(("decompress", s, n, branches[-1]))
+        queue.put((rank, problems + [("branches", branches)]))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        queue.put((rank, [("error", repr(e), traceback.format_exc())]))
+    finally:
+        dist.destroy_process_group()

@@ -64,6 +64,18 @@ def test_bucket_w2_matches_oracle(fill, kind):
         assert "resample" in dict(out[0])["branches"]
 
 
+@pytest.mark.parametrize("world,fill,kind", [(2, "sparse", "normal"), (2, "sparse", "layered"),
+                                              (2, "inline", "normal"), (4, "sparse", "normal")])
+def test_batch_multirank_matches_oracle(world, fill, kind):
+    """DGCBatch with W ranks (processes) on one MI355X: one payload of every tensor,
+    one allgather, the decompress into the batch's persistent output (fill "sparse":
+    the previous step's W runs re-zeroed), against the oracle per tensor."""
+    out = run(G.batch_worker, world, fill, kind)
+    for rank, res in out.items():
+        problems = [r for r in res if r[0] != "branches"]
+        assert problems == [], (rank, res)
+
+
 @pytest.mark.timeout(240)
 @pytest.mark.parametrize("fill", ["allgather", "sparse"])
 def test_bucket_w4_matches_oracle(fill):
