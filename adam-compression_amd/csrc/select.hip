@@ -74,7 +74,8 @@ constexpr int kMaxLower = 16;                   // thresholds per multi-threshol
 constexpr int kSpillShards = 64;
 constexpr int kSpillDiv = 32;                   // lists dropped when > nseg/32 segments spill
 constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgroup
-constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole batch
+constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
+constexpr int kCapBlocksBatch = 8192;           // ... per whole batch of several tensors
 constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
 constexpr int kHeapMax = 4096;                  // K5b: exact partial_sort replay up to this k (heap in LDS)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
@@ -199,8 +200,14 @@ struct Layout {
     int64_t grid[BT_COUNT] = {};
 };
 
-static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg) {
-    const int64_t cap = std::max<int64_t>(1, ceil_div((int64_t)kCapBlocks * d.nseg, std::max<int64_t>(1, total_seg)));
+// Capped grids serve the launches that are most likely gated no-ops (the list count
+// usually serves), so a small grid keeps their cost down — for a flat bucket, whose
+// lists serve in the steady state. A model set's passes run most steps (its synthetic
+// thresholds jump), and there a 2048-block cap left the big tensors' passes
+// short of HBM rate: 8192 blocks took VGG-16-BN 0.896 -> 0.811 ms, ResNet-50 0.367 ->
+// 0.361 ms (same box, tools/ab_lib.sh).
+static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, int64_t cap_blocks) {
+    const int64_t cap = std::max<int64_t>(1, ceil_div(cap_blocks * d.nseg, std::max<int64_t>(1, total_seg)));
     switch (which) {
         case BT_K1: return ceil_div(d.nseg, (int64_t)kSegPerBlock4);
         case BT_FULL: return ceil_div(d.nseg, (int64_t)kSegPerBlock16);
@@ -277,7 +284,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         int64_t acc = 0;
         for (int32_t t = 0; t < T; ++t) {
             bt[which][t] = (int32_t)acc;
-            acc += bt_blocks(which, td[t], L.nseg);
+            acc += bt_blocks(which, td[t], L.nseg, T > 1 ? kCapBlocksBatch : kCapBlocks);
         }
         bt[which][T] = (int32_t)acc;
         L.grid[which] = acc;
