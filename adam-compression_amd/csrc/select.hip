@@ -75,7 +75,7 @@ constexpr int kSpillShards = 64;
 constexpr int kSpillDiv = 32;                   // lists dropped when > nseg/32 segments spill
 constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgroup
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
-constexpr int kCapBlocksBatch = 8192;           // ... per whole batch of several tensors
+constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
 constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
 constexpr int kHeapMax = 4096;                  // K5b: exact partial_sort replay up to this k (heap in LDS)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
@@ -205,7 +205,7 @@ struct Layout {
 // lists serve in the steady state. A model set's passes run most steps (its synthetic
 // thresholds jump), and there a 2048-block cap left the big tensors' passes
 // short of HBM rate: 8192 blocks took VGG-16-BN 0.896 -> 0.811 ms, ResNet-50 0.367 ->
-// 0.361 ms (same box, tools/ab_lib.sh).
+// 0.361 ms, 16384 VGG-16-BN 0.816 -> 0.805 ms, ResNet-50 unchanged (same box, tools/ab_lib.sh).
 static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, int64_t cap_blocks) {
     const int64_t cap = std::max<int64_t>(1, ceil_div(cap_blocks * d.nseg, std::max<int64_t>(1, total_seg)));
     switch (which) {
