@@ -559,28 +559,45 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
 }
 
 // ---------------------------------------------------------------- multi-workgroup global phase
-// The global-memory steps (range > kNthLds) spread over G co-resident workgroups of
-// one tensor (k_nth_global, a cooperative launch): one workgroup's loads in flight
-// bound the one-workgroup phase (57k candidates: 50 us in 2 steps, tools/k5_prof.py).
-// The step is the same partition as nth_step_wg — the G x 8 waves take contiguous
-// stretches in order, so every stopper's rank is the same — with a barrier among the
-// G workgroups where nth_step_wg has __syncthreads: counts | pairing | swaps | advance.
+// The global-memory steps (range > kNthLds) spread over G workgroups of one tensor
+// (k_nth_global, a plain launch sized so that all of them fit at once): one
+// workgroup's loads in flight bound the one-workgroup phase (57k candidates: 50 us in
+// 2 steps, tools/k5_prof.py). The step is the same partition as nth_step_wg — the G x
+// 8 waves take contiguous stretches in order, so every stopper's rank is the same —
+// with a barrier among the G workgroups where nth_step_wg has __syncthreads: counts |
+// pairing | swaps | advance.
+//
+// Residency. A plain launch does not guarantee that the G workgroups run at once (other
+// streams' or processes' kernels may hold CUs), and the per-step barriers would then
+// wait for a workgroup that cannot start until they exit. So the phase opens with a
+// CONSENSUS: every workgroup arrives; the last to arrive votes GO; a workgroup that
+// waited kNthGArriveTicks without seeing a vote votes ABORT. The first vote (one CAS on
+// `decide`) binds all G workgroups — a late arriver reads ABORT — so either all of them
+// are resident and run the phase (resident workgroups stay resident until they exit),
+// or none does and k_nth_select replays the whole nth_element on one workgroup from
+// [0, n): exact either way, reported as DGC_K5_FALLBACK. A per-step barrier that still
+// times out after GO (not expected to happen) marks the run DGC_K5_BROKEN, which the
+// engines raise on.
 constexpr int kNthGMax = 32;      // workgroups per tensor
 constexpr int kNthGMk = 32768;    // stopper bytes per workgroup kept in LDS (512 tiles)
+constexpr uint64_t kNthGArriveTicks = 2000000;   // 20 ms of the 100 MHz wall clock
+enum : uint32_t { kNthGUndecided = 0, kNthGGo = 1, kNthGAbort = 2 };
 
 struct NthG {
     int64_t f, l, depth;
     unsigned long long l_next, r_min;
     uint32_t pivot, s;
     int32_t heap_exit, go;
-    uint32_t bar_count, bar_gen;   // zeroed by k_sel_init
+    uint32_t bar_count, bar_gen;   // zeroed by k_sel_init, like arrive / decide / status
+    uint32_t arrive, decide;       // the residency consensus
+    uint32_t status;               // DGC_K5_FALLBACK | DGC_K5_BROKEN of this call
     uint32_t bl[kNthGMax], br[kNthGMax];
 };
 
-// Barrier among the G workgroups of one tensor (all co-resident: cooperative launch).
+// Barrier among the G workgroups of one tensor (all resident: see the consensus above).
 // Agent-scope release / acquire around the arrival make every workgroup's global
-// stores visible to the others across XCDs. The spin is bounded (~seconds): a broken
-// launch then yields a wrong result instead of a hung GPU.
+// stores visible to the others across XCDs. The spin is bounded (~seconds): should it
+// ever run out, the run is marked DGC_K5_BROKEN instead of hanging the GPU.
 __device__ __forceinline__ void nthg_barrier(NthG* g, uint32_t G) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -591,14 +608,45 @@ __device__ __forceinline__ void nthg_barrier(NthG* g, uint32_t G) {
             __hip_atomic_store(&g->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(&g->bar_gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         } else {
+            bool passed = false;
             for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
-                if (__hip_atomic_load(&g->bar_gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+                if (__hip_atomic_load(&g->bar_gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != gen) {
+                    passed = true;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (!passed) atomicOr(&g->status, (uint32_t)DGC_K5_BROKEN);
         }
         __threadfence();
     }
     __syncthreads();
+}
+
+// The residency consensus (see above): true = all G workgroups are here, run the phase.
+// G_expected is G itself except in the parity tests' forced-fallback mode.
+__device__ __forceinline__ bool nthg_consensus(NthG* g, uint32_t G_expected) {
+    __shared__ uint32_t verdict;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t a = atomicAdd(&g->arrive, 1u);
+        if (a + 1 == G_expected) {
+            atomicCAS(&g->decide, (uint32_t)kNthGUndecided, (uint32_t)kNthGGo);
+        } else {
+            const uint64_t t0 = wall_clock64();
+            while (__hip_atomic_load(&g->decide, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == kNthGUndecided) {
+                if (wall_clock64() - t0 > kNthGArriveTicks) {
+                    atomicCAS(&g->decide, (uint32_t)kNthGUndecided, (uint32_t)kNthGAbort);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        verdict = __hip_atomic_load(&g->decide, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+    }
+    __syncthreads();
+    return verdict == kNthGGo;
 }
 
 // Block 0, thread 0: the next step's median and the reset of its results, or the end
@@ -627,7 +675,7 @@ __device__ void nthg_prepare(uint64_t* q, NthG* g, int64_t nth) {
 // candidates the four cross-XCD barriers per step cost more than the spread saves
 // (tools/k5ab.sh: 100k 0.28 vs 0.25 ms, 500k 0.43 vs 0.94, 1M 0.55 vs 1.44).
 __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* lpos, uint32_t* rpos, NthG* g,
-                                 uint32_t b, uint32_t G, int64_t min_run) {
+                                 uint32_t b, uint32_t G, int64_t min_run, uint32_t G_expected) {
     constexpr int kB = 8;   // tiles of loads in flight per lane
     __shared__ uint8_t mk[kNthGMk];
     __shared__ uint32_t wl[kNthWaves], wr[kNthWaves], pre_l, pre_r, tot_r, s_sh;
@@ -641,6 +689,16 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
             g->l = n;
             g->depth = n > 0 ? 2 * (int64_t)(63 - __clzll((unsigned long long)n)) : 0;
             g->heap_exit = 0;
+        }
+        return;
+    }
+    if (!nthg_consensus(g, G_expected)) {   // not all resident: one workgroup does it all
+        if (b == 0 && threadIdx.x == 0) {
+            g->f = 0;
+            g->l = n;
+            g->depth = n > 0 ? 2 * (int64_t)(63 - __clzll((unsigned long long)n)) : 0;
+            g->heap_exit = 0;
+            atomicOr(&g->status, (uint32_t)DGC_K5_FALLBACK);
         }
         return;
     }

@@ -730,9 +730,12 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lis
     const int t = blockIdx.x;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     SelState* st = w.st + t;
-    if (threadIdx.x == 0) {   // K5's multi-workgroup barrier starts from zero
+    if (threadIdx.x == 0) {   // K5's multi-workgroup barrier and consensus start from zero
         w.nthg[t].bar_count = 0;
         w.nthg[t].bar_gen = 0;
+        w.nthg[t].arrive = 0;
+        w.nthg[t].decide = 0;
+        w.nthg[t].status = 0;
     }
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
@@ -1903,16 +1906,19 @@ __device__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& 
 // gathered candidates (introselect.hpp: nth_element), or — partial_sort path, k <=
 // kHeapMax — heap select + sort_heap over vec, which also emits. They share one LDS area.
 static_assert(kHeapMax + (int64_t)kHeapThreads * kHeapPer <= kNthLds, "K5b: heap + chunk fit K5's LDS");
-// K5's global-memory phase by G workgroups per tensor (grid G x T, cooperative launch:
-// all co-resident); k_nth_select goes on from the state it leaves (introselect.hpp).
-__global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G, int64_t min_run) {
+// K5's global-memory phase by G workgroups per tensor (grid G x T, a plain launch sized
+// so all of them fit at once; a residency consensus decides whether they run it, see
+// introselect.hpp); k_nth_select goes on from the state it leaves.
+__global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G, int64_t min_run,
+                                                            uint32_t G_expected) {
     const int t = blockIdx.y;
     const SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;
     const TDesc d = w.td[t];
     uint32_t* gl = w.gpos + d.gpos_off;
     uint32_t* gr = gl + d.cand_cap / 2 + 1;
-    nth_global_multi(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, w.nthg + t, blockIdx.x, G, min_run);
+    nth_global_multi(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, w.nthg + t, blockIdx.x, G, min_run,
+                     G_expected);
 }
 
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
@@ -1960,6 +1966,8 @@ __global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info,
             r.full_passes = st->full_passes;
             r.tie_rule = st->tie_rule;
             r.window_keys = st->win_keys;
+            r.k5_status = (int32_t)w.nthg[t].status;
+            r.reserved = 0;
         }
         if (w.spec) {
             // spec[0]: next call's list threshold = m * t * growth, growth = 2 - spec[1] / t
@@ -2055,7 +2063,8 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
     }
     const char* force = std::getenv("DGC_K5_GLOBAL");   // wg | multi (parity tests run both)
     if (force && std::strcmp(force, "wg") == 0) return 0;
-    if (max_cand <= kNthLds || (max_cand <= kNthGMinCand && !(force && std::strcmp(force, "multi") == 0))) return 0;
+    const bool multi = force && (std::strcmp(force, "multi") == 0 || std::strcmp(force, "abort") == 0);
+    if (max_cand <= kNthLds || (max_cand <= kNthGMinCand && !multi)) return 0;
     const int64_t g = T > 0 ? per_dev / T : 0;
     return (uint32_t)std::min<int64_t>(g, kNthGMax);
 }
@@ -2119,9 +2128,15 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_TRY(launch_emit(L, vec, w, g, s));
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
         if (G > 1) {
+            // DGC_K5_GLOBAL=multi: every range over several workgroups (parity); =abort: the
+            // kernel expects one workgroup more than launched, so the residency consensus
+            // times out and the one-workgroup replay takes over (the fallback's parity test)
             const char* force = std::getenv("DGC_K5_GLOBAL");
-            const int64_t min_run = (force && std::strcmp(force, "multi") == 0) ? 0 : kNthGMinCand;
-            hipLaunchKernelGGL(k_nth_global, dim3(G, (unsigned)L.T), dim3(kNthThreads), 0, s, w, G, min_run);
+            const bool multi = force && (std::strcmp(force, "multi") == 0 || std::strcmp(force, "abort") == 0);
+            const bool abort = force && std::strcmp(force, "abort") == 0;
+            const int64_t min_run = multi ? 0 : kNthGMinCand;
+            hipLaunchKernelGGL(k_nth_global, dim3(G, (unsigned)L.T), dim3(kNthThreads), 0, s, w, G, min_run,
+                               abort ? G + 1 : G);
             DGC_LAUNCHED();
         }
         hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0);

@@ -37,7 +37,24 @@ class SelectInfo(ctypes.Structure):
                 ("threshold0", ctypes.c_float), ("threshold", ctypes.c_float),
                 ("branch", ctypes.c_int32), ("recounts", ctypes.c_int32),
                 ("overflow_segments", ctypes.c_int32), ("full_passes", ctypes.c_int32),
-                ("tie_rule", ctypes.c_int32), ("window_keys", ctypes.c_int32)]
+                ("tie_rule", ctypes.c_int32), ("window_keys", ctypes.c_int32),
+                ("k5_status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+K5_FALLBACK, K5_BROKEN = 1, 2
+
+
+def info_dict(i, what):
+    """A dgc_select_info record as the engines report it; raises when the resample
+    replay's multi-workgroup phase broke (its selection would not be the reference's)."""
+    if i.k5_status & K5_BROKEN:
+        raise RuntimeError(f"{what}: the resample replay's multi-workgroup phase timed out at a barrier after it "
+                           "started (workgroups not co-resident?); this step's selection is not reliable")
+    return dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
+                branch=BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
+                overflow_segments=i.overflow_segments, full_passes=i.full_passes,
+                tie_rule=TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys,
+                k5_fallback=bool(i.k5_status & K5_FALLBACK))
 
 
 INFO_BYTES = ctypes.sizeof(SelectInfo)

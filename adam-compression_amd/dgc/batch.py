@@ -12,10 +12,13 @@ each tensor at a 1024-element-aligned offset) and runs
     dgc_batch_compress   K1 over all tensors, K3 for all thresholds, the selection
                          chain with per-tensor state, one packed payload
     one allgather        the packed payload, RCCL over xGMI (gloo stages via the host)
-    decompress           dgc_decompress_packed (zero fill + scatter) over the flat gradient,
-                         or — into the batch's persistent output (``fill="sparse"``, the
-                         default) — dgc_decompress_packed_over: only the previous step's
-                         gathered indices are re-zeroed, as in ``DGCBucket``
+    decompress           dgc_decompress_packed (zero fill + scatter) over the flat output
+                         (``fill="auto"``/``"inline"``, the default), or — opted in with
+                         ``fill="sparse"`` by a caller that owns the output and never writes
+                         it — dgc_decompress_packed_over: only the previous step's gathered
+                         indices are re-zeroed, as in ``DGCBucket`` (writes through ``.data``
+                         or raw pointers do not bump torch's version counter, so the
+                         re-zero cannot see them: see dgc/bucket.py)
 
 with O(1) launches per phase and no host synchronisation. The payload carries flat
 indices (tensor offset + index in the tensor), tensor after tensor.
@@ -49,9 +52,11 @@ class DGCBatch:
     def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
                  resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
-                 deferred_masking=True, fill="sparse"):
-        if fill not in ("inline", "sparse"):
-            raise ValueError(f"fill must be 'inline' or 'sparse', not {fill!r}")
+                 deferred_masking=True, fill="auto"):
+        if fill not in ("auto", "inline", "sparse"):
+            raise ValueError(f"fill must be 'auto', 'inline' or 'sparse', not {fill!r}")
+        if fill == "auto":   # the dense zero_() is always right; the re-zero is opt-in
+            fill = "inline"
         self.fill = fill
         self.device = torch.device(device or "cuda")
         self.names = [n for n, _ in named_shapes]
@@ -222,6 +227,10 @@ class DGCBatch:
         step's gathered indices (dgc_decompress_packed_over) instead of the whole
         buffer: identical result, W * capacity slots instead of flat_numel."""
         out = self.out_flat if out_flat is None else out_flat
+        _lib.require_cuda_f32(out, "DGCBatch.decompress")
+        if out.numel() != self.flat_numel or out.device != self.device:
+            raise ValueError(f"DGCBatch.decompress: out_flat must be a contiguous fp32 tensor of {self.flat_numel} "
+                             f"elements on {self.device} (got {out.numel()} on {out.device})")
         L = self._L
         st = _lib.stream_of(self.device)
         cur = self.gathered
@@ -255,10 +264,7 @@ class DGCBatch:
         out = []
         for t in range(len(self.names)):
             i = _lib.SelectInfo.from_buffer_copy(raw[t * _lib.INFO_BYTES:(t + 1) * _lib.INFO_BYTES])
-            out.append(dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
-                            branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
-                            overflow_segments=i.overflow_segments, full_passes=i.full_passes,
-                            tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys))
+            out.append(_lib.info_dict(i, f"DGCBatch tensor {self.names[t]}"))
         return out
 
     def transmitted(self, rank_payload=None):

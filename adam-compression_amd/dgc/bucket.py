@@ -17,7 +17,7 @@ every decision kept on the device:
   allgather is enqueued (ordered after the selection), so at W > 1 the 4 B/elem
   zero fill runs under the xGMI transfer instead of after it; the decompress then
   only scatters. ``"inline"`` runs fill + scatter after the allgather.
-  ``"sparse"`` (and ``"auto"``, the default) treats ``out`` as a persistent output
+  ``"sparse"`` (opt-in) treats ``out`` as a persistent output
   bucket: when it is the tensor the previous step decompressed into and nobody has
   written it since (same storage, same torch version counter), it is +0.0 except at
   the previous step's W*k gathered indices, so ``zero_()`` is a sparse re-zero of
@@ -28,6 +28,11 @@ every decision kept on the device:
   (first step, a new tensor, one modified in place) gets the dense fill. The
   payload (W = 1) / gather buffer (W > 1) alternates between two buffers so the
   previous step's indices survive the current step.
+  **What "sparse" cannot see**: writes through ``out.data`` (the reference's own idiom,
+  e.g. ``grad.data.mul_``) and raw-pointer writes do not bump torch's version counter,
+  so after one the re-zero would leave stale values. Only a caller that owns ``out``
+  and never writes it (the bench) should opt in; ``"auto"`` (the default) is the dense
+  fill ``"inline"``.
 
 The numerics are those of the drop-in ``DGCCompressor`` + ``DGCSGDMemory`` (same
 kernels); the sample start is drawn from a ``random.Random`` seeded identically on
@@ -98,8 +103,8 @@ class DGCBucket:
         self.rank_stride, self.voff, self.ioff = _layout(self.k, self.vdtype, self.idtype)
         if fill not in ("auto", "inline", "allgather", "sparse"):
             raise ValueError(f"fill must be 'auto', 'inline', 'allgather' or 'sparse', not {fill!r}")
-        if fill == "auto":
-            fill = "sparse"
+        if fill == "auto":   # the dense zero_() is always right; the re-zero is opt-in (see above)
+            fill = "inline"
         self.fill = fill
         nbuf = 2 if fill == "sparse" else 1   # the previous step's gathered indices stay readable
         self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
@@ -268,8 +273,4 @@ class DGCBucket:
 
     def last_info(self):
         raw = self.info.cpu().numpy().tobytes()
-        i = _lib.SelectInfo.from_buffer_copy(raw)
-        return dict(count=i.count, candidates=i.candidates, threshold0=i.threshold0, threshold=i.threshold,
-                    branch=_lib.BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
-                    overflow_segments=i.overflow_segments, full_passes=i.full_passes,
-                    tie_rule=_lib.TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys)
+        return _lib.info_dict(_lib.SelectInfo.from_buffer_copy(raw), "DGCBucket")

@@ -240,7 +240,7 @@ class DGCCompressor:
         _lib.check(L.dgc_select(_lib.ptr(vec), _lib.ptr(mmt), _lib.ptr(thr), params,
                                 base + voff, base + ioff, base, _lib.ptr(info), _lib.ptr(sbuf), sws,
                                 _lib.SYNC_HOST, stream), "dgc_select")
-        n = int(payload[:8].view(torch.int64).item())
+        n = self._count(info)
         values, indices = self._views(payload, lay, n)
         self._last_info = info
         return values.view(-1), indices.view(-1), numel, shape, k
@@ -273,7 +273,7 @@ class DGCCompressor:
                                           int(bool(mem.nesterov)), start, stride, ks, params, _lib.ptr(spec),
                                           _lib.SPEC_MARGIN, base + voff, base + ioff, base, _lib.ptr(info),
                                           _lib.ptr(ws), wsz, _lib.SYNC_HOST, _lib.stream_of(dev)), "dgc_compress")
-                n = int(payload[:8].view(torch.int64).item())
+                n = self._count(info)
                 values, indices = self._views(payload, lay, n)
                 self._last_info = info
             else:
@@ -290,15 +290,18 @@ class DGCCompressor:
             tensor = tensor.type(torch.float16)
         return tensor, ctx
 
+    @staticmethod
+    def _count(info):
+        """The emitted count, read with the whole selection record in ONE device-to-host
+        copy (the one host sync the exact-length [n, 1] outputs need); raises if the
+        resample replay reported a broken multi-workgroup phase."""
+        return _lib.info_dict(_lib.SelectInfo.from_buffer_copy(info.cpu().numpy().tobytes()),
+                              "DGCCompressor.compress")["count"]
+
     def last_info(self):
         """Selection record of the last compress (branch, counts, thresholds) — diagnostics."""
-        raw = self._last_info.cpu().numpy().tobytes()
-        info = _lib.SelectInfo.from_buffer_copy(raw)
-        return dict(count=info.count, candidates=info.candidates, threshold0=info.threshold0,
-                    threshold=info.threshold, branch=_lib.BRANCHES.get(info.branch, info.branch),
-                    recounts=info.recounts, overflow_segments=info.overflow_segments,
-                    full_passes=info.full_passes, tie_rule=_lib.TIE_RULES.get(info.tie_rule, info.tie_rule),
-                    window_keys=info.window_keys)
+        return _lib.info_dict(_lib.SelectInfo.from_buffer_copy(self._last_info.cpu().numpy().tobytes()),
+                              "DGCCompressor")
 
     def decompress(self, tensor, ctx):
         """dgc/compression.py:179-198."""

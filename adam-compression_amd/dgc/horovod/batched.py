@@ -24,8 +24,8 @@ with no host synchronisation. It does so by laying the parameters' state out fla
 Anything that rebinds those tensors (``zero_grad(set_to_none=True)`` followed by a
 backward, ``memory.load_state_dict``, ``compressor.initialize``) is detected at the
 next step and copied back into the flat layout, so the results never depend on it;
-keeping the views (``zero_grad(set_to_none=False)``, the batched optimizer's
-default) just avoids that copy.
+keeping the views (``zero_grad(set_to_none=False)``; torch's and so the wrapper's
+default is ``set_to_none=True``) just avoids that copy.
 
 Sample starts: one ``random.randint(0, stride - 1)`` per sampled compressed tensor,
 drawn from Python's global ``random`` in the order the hooks fired — the order in

@@ -173,8 +173,12 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             raise AssertionError("optimizer.zero_grad() was called after loss.backward() but before "
                                  "optimizer.step() or optimizer.synchronize(). This is prohibited as it "
                                  "can cause a race condition.")
-        if self._batched is not None and not args and not kwargs.get("set_to_none", False):
-            # keep the gradients as views of the flat buffers: zero them in place
+        # torch >= 2: zero_grad(set_to_none=True) by default, as the wrapped optimizer does
+        set_to_none = kwargs.get("set_to_none", args[0] if args else True)
+        if self._batched is not None and not set_to_none:
+            # zero_grad(set_to_none=False): the gradients stay views of the flat buffers
+            # and are zeroed in place; with None (the default) the next step copies the
+            # new gradients back into the flat layout (dgc/horovod/batched.py)
             if self._batched.zero_grads():
                 return None
         return super(self.__class__, self).zero_grad(*args, **kwargs)

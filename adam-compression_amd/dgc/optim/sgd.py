@@ -9,9 +9,11 @@ first step); ``d = d + momentum * buf`` (nesterov) or ``d = buf``; then
 On the MI355X every parameter group is ONE fused pass (``dgc_sgd_step``, K7 in
 ``csrc/sgd.hip``): read p, grad (+ the momentum buffer), write p (+ buffer), with
 the reference's torch-CPU rounding (``add(alpha)`` is one fused multiply-add), so the
-weights are bit-identical to the reference's. Parameters that live on the CPU (the
-gloo plumbing tests) take the reference's own op sequence. The optimizer state keeps
-the reference's layout (``state[p]["momentum_buffer"]``).
+weights are bit-identical to the reference's. Every other parameter — on the CPU (the
+gloo plumbing tests), or on the GPU but not a contiguous fp32 tensor with a contiguous
+fp32 gradient (fp16/bf16 weights, channels_last convolutions, a non-contiguous
+view) — takes the reference's own torch op sequence, as the reference accepts any of
+them. The optimizer state keeps the reference's layout (``state[p]["momentum_buffer"]``).
 """
 import ctypes
 
@@ -40,8 +42,17 @@ class DGCSGD(Optimizer):
             group.setdefault("nesterov", False)
 
     @staticmethod
+    def _fusable(p):
+        """A parameter K7 serves: contiguous fp32 CUDA weight and gradient (and, when it
+        exists, momentum buffer) on one device."""
+        g = p.grad
+        return (p.is_cuda and p.dtype == torch.float32 and p.data.is_contiguous() and g.is_cuda
+                and g.dtype == torch.float32 and g.is_contiguous() and g.device == p.device)
+
+    @staticmethod
     def _cpu_param(p, d_p, group, state):
-        """The reference's op sequence (dgc/optim/sgd.py:50-68) for a CPU parameter."""
+        """The reference's op sequence (dgc/optim/sgd.py:50-68), for a parameter K7 does
+        not serve (any device, dtype or layout)."""
         wd, mom = group["weight_decay"], group["momentum"]
         if wd == 0:
             p.add_(d_p, alpha=-group["lr"])
@@ -97,7 +108,8 @@ class DGCSGD(Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if p.is_cuda:
+                buf = self.state[p].get("momentum_buffer") if p in self.state else None
+                if self._fusable(p) and (buf is None or (buf.dtype == torch.float32 and buf.is_contiguous())):
                     by_dev.setdefault(p.device, []).append(p)
                 else:
                     self._cpu_param(p, p.grad, group, self.state[p])

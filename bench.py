@@ -61,8 +61,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
-    ap.add_argument("--fill", default="auto", choices=["auto", "inline", "allgather", "sparse"],
-                    help="flat bucket's zero_(): auto = sparse re-zero of the persistent output (dgc/bucket.py)")
+    ap.add_argument("--fill", default="sparse", choices=["inline", "allgather", "sparse"],
+                    help="decompress zero_(): sparse = re-zero only the previous step's entries of the bench's "
+                         "persistent output (the bench owns it and never writes it; dgc/bucket.py)")
     return ap.parse_args()
 
 
@@ -94,10 +95,13 @@ def cpu_model():
     return ""
 
 
-def cpu_baseline(wl, numel, steps, threads):
+def cpu_baseline(run, wl, numel, steps, threads):
     """The reference op sequence restated on torch CPU (oracle/torch_cpu.py, pinned to
     the reference's golden fixtures), timed on this host over a bounded sample of the
-    workload (rank 0, N=1 only): the same per-element work, fewer elements."""
+    workload (rank 0, N=1 only) with the GPU run's OWN inputs (BASELINE.md "Inputs"):
+    the two alternating gradient buffers copied back from HBM (model sets: every
+    compressed tensor; flat buckets: the first ``numel`` elements of each buffer) and
+    the sample starts drawn from ``random.Random(42)`` in the GPU engines' order."""
     from oracle import torch_cpu
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
@@ -105,32 +109,38 @@ def cpu_baseline(wl, numel, steps, threads):
     rng = random.Random(42)
     try:
         if wl["kind"] == "model":
-            from dgc import workloads
-            comp, dense = workloads.split(getattr(workloads, wl["model"])())
+            b = run.b
+            grads = [g.cpu() for g, _ in run.grads]
             tensors = []
-            for i, (name, shape) in enumerate(comp):
-                n = workloads.numel(shape)
+            for i, (off, n) in enumerate(zip(b.offsets, b.numels)):
                 attrs = torch_cpu.attributes(n, wl["ratio"])
-                g = torch.randn(n, generator=torch.Generator().manual_seed(i))
-                tensors.append((attrs, g, torch.zeros(n), torch.zeros(n), torch.empty(n)))
+                tensors.append((attrs, [g[off: off + n] for g in grads], torch.zeros(n), torch.zeros(n),
+                                torch.empty(n)))
             N = sum(t[0][0] for t in tensors)
+            state = {"i": 0}
 
             def step():
-                for attrs, g, m, v, out in tensors:
+                i = state["i"]
+                state["i"] += 1
+                for attrs, gs, m, v, out in tensors:   # DGCBatch.draw_starts' order
                     start = rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
-                    torch_cpu.cpu_step(g, m, v, out, attrs, start, nesterov=wl["nesterov"])
-            what = f"all {len(tensors)} compressed tensors ({N} elements) of {wl['model']}"
+                    torch_cpu.cpu_step(gs[i % 2], m, v, out, attrs, start, nesterov=wl["nesterov"])
+            what = (f"all {len(tensors)} compressed tensors ({N} elements) of {wl['model']}, the GPU run's "
+                    f"two gradient sets")
         else:
-            N = int(numel)
+            N = int(min(numel, run.N))
             attrs = torch_cpu.attributes(N, wl["ratio"])
-            g = torch.randn(N, generator=torch.Generator().manual_seed(1))
-            if wl["grad"] == "bf16":
-                g = g.to(torch.bfloat16).float()
+            gs = [g[:N].cpu() for g in run.grads]
             m, v, out = torch.zeros(N), torch.zeros(N), torch.empty(N)
+            state = {"i": 0}
 
             def step():
-                torch_cpu.cpu_step(g, m, v, out, attrs, rng.randint(0, attrs[4] - 1), nesterov=wl["nesterov"])
-            what = f"a {N}-element flat sample of the {wl['numel']}-element bucket at the same ratio"
+                i = state["i"]
+                state["i"] += 1
+                torch_cpu.cpu_step(gs[i % 2], m, v, out, attrs, rng.randint(0, attrs[4] - 1),
+                                   nesterov=wl["nesterov"])
+            what = (f"the first {N} elements of the GPU run's two {wl['numel']}-element gradient buffers "
+                    f"(same ratio, sample stride {attrs[4]})")
         step()   # warm-up
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -139,9 +149,9 @@ def cpu_baseline(wl, numel, steps, threads):
     finally:
         torch.set_num_threads(prev)
     return {"value": N / dt, "unit": "grad elements/s", "cores": threads, "kind": "port",
-            "sample": f"{what} x {steps} steps (compensate+sparsify+update+decompress, W=1, torch "
-                      f"{torch.__version__} CPU ops as the reference issues them): {dt * 1e3:.1f} ms/step on "
-                      f"{threads} thread(s); {cpu_model()}"}
+            "sample": f"{what} x {steps} steps after 1 warm-up step, sample starts from random.Random(42) "
+                      f"(compensate+sparsify+update+decompress, W=1, torch {torch.__version__} CPU ops as the "
+                      f"reference issues them): {dt * 1e3:.1f} ms/step on {threads} thread(s); {cpu_model()}"}
 
 
 # ---------------------------------------------------------------------------- profiles
@@ -206,6 +216,14 @@ def launch_plan(gpus, environ):
     return envs
 
 
+def check_devices(gpus, devices):
+    """Fails fast, before any rank is spawned or touches the GPU, when this node has
+    fewer devices than ranks (torch.cuda.device_count() does not initialise HIP)."""
+    if devices < gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} needs {gpus} visible GPUs, this node shows {devices} "
+                         f"(torch.cuda.device_count()); nothing was launched")
+
+
 def spawn(envs):
     """One child process per rank (started before this process touches the GPU);
     returns the first non-zero exit code, or 0."""
@@ -265,7 +283,7 @@ class ModelRun:
     step, the dense (dim <= 1) tensors as one flat allreduce + compensate(accumulate=False)
     (dgc/compression.py:173-177, 195-198)."""
 
-    def __init__(self, wl, rank, world, dev, fill="auto"):
+    def __init__(self, wl, rank, world, dev, fill="sparse"):
         from dgc import workloads
         from dgc.batch import DGCBatch
         comp, dense = workloads.split(getattr(workloads, wl["model"])())
@@ -388,6 +406,7 @@ def step_bytes(run, world, full_passes):
 # ---------------------------------------------------------------------------- main
 def main():
     args = parse()
+    check_devices(args.gpus, torch.cuda.device_count())
     envs = launch_plan(args.gpus, os.environ)
     if envs is not None:
         sys.exit(spawn(envs))
@@ -397,8 +416,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        backend = dist.get_backend()
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} but the process group has {dist.get_world_size()} ranks")
     run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev, args.fill)
 
     log(f"{args.workload}: rank {rank}/{world} set up")
@@ -450,12 +473,16 @@ def main():
         "value": world * run.elements / (ms_step * 1e-3),
         "unit": "grad elements/s",
         "n_gpus": world,
+        "world_size": dist.get_world_size() if world > 1 else 1,
+        "backend": (f"{backend} (RCCL over xGMI)" if backend == "nccl" else backend) if world > 1 else "none (1 rank)",
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
+        "vs_baseline_note": "null: BASELINE.md holds no published number for this metric (the reference publishes "
+                            "none); the CPU restatement of the reference timed on this host is cpu_baseline",
         "dtype": "f32",
         "data": "synthetic: torch.randn N(0,1) gradients (bf16-rounded for flat-7B-bf16; x1e-3 for the model "
                 "sets), 2 alternating buffers per rank (seed 0xD6C + 1000*rank + buffer); momentum/velocity "
@@ -470,7 +497,6 @@ def main():
         "step_hbm": {"required_bytes_per_rank": required, "contract_bytes_per_rank": contract,
                      "achieved_GBs": required / (ms_step * 1e-3) / 1e9,
                      "frac_of_8TBs": required / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "contract_frac_of_8TBs": contract / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "frac_of_measured_copy": required / (ms_step * 1e-3) / 1e9 / HBM_COPY_GBS},
         "hbm_probe": dict(probe, k1_frac_of_probe=k1_gbs / probe["GBs"],
                           step_frac_of_probe=required / (ms_step * 1e-3) / 1e9 / probe["GBs"]),
@@ -486,8 +512,8 @@ def main():
     if world == 1 and not args.no_cpu:
         cores = cpu_cores()
         log(f"CPU baseline on {cores} threads, then 1 thread")
-        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_numel, args.cpu_steps, cores)
-        res["cpu_baseline_1thread"] = cpu_baseline(wl, args.cpu_numel_1t, 2, 1)
+        res["cpu_baseline"] = cpu_baseline(run, wl, args.cpu_numel, args.cpu_steps, cores)
+        res["cpu_baseline_1thread"] = cpu_baseline(run, wl, args.cpu_numel_1t, 2, 1)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

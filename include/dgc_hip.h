@@ -121,7 +121,16 @@ typedef struct dgc_select_info {
     int32_t window_keys;      /* > 0: threshold0 came from the K1 window list of this
                                  many samples (those >= the list threshold), not a
                                  pass over all samples; same value either way       */
+    int32_t k5_status;        /* resample replay: bit 0 (DGC_K5_FALLBACK) the multi-
+                                 workgroup global phase found its workgroups not all
+                                 resident and left the whole replay to one workgroup
+                                 (exact, slower); bit 1 (DGC_K5_BROKEN) a barrier of that
+                                 phase timed out after it had started: the selection of
+                                 this tensor is NOT reliable (the engines raise)       */
+    int32_t reserved;
 } dgc_select_info;
+
+enum { DGC_K5_FALLBACK = 1, DGC_K5_BROKEN = 2 };
 
 const char* dgc_last_error(void);
 const char* dgc_version(void);

@@ -69,6 +69,106 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
+def _load_cfg(label):
+    if label == "tinynet":
+        cfg = json.load(open(os.path.join(GOLDEN, "optimizer.json")))
+        schedule = [(None, s) for s in range(cfg["steps"])]
+    else:
+        cfg = json.load(open(os.path.join(GOLDEN, "optimizer_resnet20.json")))
+        spe = cfg["steps_per_epoch"]
+        schedule = [(e if t == 0 else None, ei * spe + t) for ei, e in enumerate(cfg["epochs"]) for t in range(spe)]
+    return cfg, schedule
+
+
+def _setup(label, batch, dev, cfg, model_seed=None):
+    """The reference's training objects for a replay: model, DGCSGD, DGCSGDMemory,
+    DGCCompressor (initialised on the dim > 1 parameters, train.py:130-140) and the
+    DistributedOptimizer around them, plus a spy on compress (the per-tensor calls)."""
+    from dgc.comm import Average
+    from dgc.compression import DGCCompressor
+    from dgc.horovod import DistributedOptimizer
+    from dgc.memory import DGCSGDMemory
+    from dgc.optim import DGCSGD
+    from models import ResNet20, TinyNet
+    torch.manual_seed(cfg["model_seed"] if model_seed is None else model_seed)
+    if label == "tinynet":
+        model = TinyNet().to(dev)
+        comp_kw = dict(fp16_values=False, int32_indices=False, warmup_epochs=-1)
+    else:
+        model = ResNet20().to(dev)
+        comp_kw = dict(sample_ratio=cfg["sample_ratio"], fp16_values=cfg["fp16_values"],
+                       int32_indices=cfg["int32_indices"], warmup_epochs=cfg["warmup_epochs"])
+    opt = DGCSGD(model.parameters(), lr=cfg["lr"], momentum=cfg["momentum"],
+                 weight_decay=cfg["weight_decay"], nesterov=cfg["nesterov_sgd"])
+    mem = DGCSGDMemory(momentum=cfg["momentum"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        comp = DGCCompressor(cfg["ratio"], memory=mem, **comp_kw)
+        mem.initialize(model.named_parameters())
+        comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+    dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                backward_passes_per_step=1, op=Average, batch=batch)
+    calls = []
+    orig = comp.compress
+
+    def spy(tensor, name):
+        calls.append(name)
+        return orig(tensor, name)
+
+    comp.compress = spy
+    return dict(model=model, opt=opt, mem=mem, comp=comp, dopt=dopt, params=dict(model.named_parameters()),
+                calls=calls)
+
+
+def _replay_step(run, label, batch, rank, epoch, s, meta, trace, dev, problems, zero_grad=None):
+    """One training step of the reference's run: warmup ratio at an epoch start, the
+    recorded backward (hooks fire in the recorded order), step, zero_grad."""
+    if epoch is not None:
+        with contextlib.redirect_stdout(io.StringIO()):
+            run["comp"].warmup_compress_ratio(epoch)
+    key = f"{label}/s{s}/r{rank}"
+    order = meta[key]
+    grads = [trace[f"{key}/{j}"] for j in range(len(order))]
+    run["calls"].clear()
+    replay_backward(run["params"], order, grads, dev)
+    dopt = run["dopt"]
+    if (list(dopt._order) if batch else run["calls"]) != order:
+        problems.append(("hook order", s))
+    if batch and run["calls"]:
+        problems.append(("per-tensor compress in batch mode", s))
+    dopt.step()
+    if zero_grad is None:
+        dopt.zero_grad()    # torch >= 2 default: set_to_none=True
+    else:
+        dopt.zero_grad(set_to_none=zero_grad)
+    torch.cuda.synchronize()
+
+
+def _check_weights(run, label, cfg, want, s, rank, problems, tag="weights"):
+    model = run["model"]
+    if label == "tinynet":
+        for n, p in model.named_parameters():
+            w = want[f"s{s}/r{rank}/{n}"]
+            got = p.detach().cpu().numpy()
+            if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
+                problems.append((tag, s, n, float(np.abs(got - w).max())))
+    elif _digest(model) != cfg["step_digests"][s][rank]:
+        problems.append((tag + " digest", s))
+
+
+def _check_final(run, label, want, problems):
+    if label != "resnet20":
+        return
+    for n, p in run["model"].named_parameters():
+        got = p.detach().cpu().numpy()
+        w = want[f"final/{n}"]
+        if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
+            problems.append(("final", n, float(np.abs(got - w).max())))
+
+
+def _want(label):
+    return np.load(os.path.join(GOLDEN, "optimizer.npz" if label == "tinynet" else "optimizer_resnet20.npz"))
+
+
 def optimizer_replay_worker(rank, world, port, label, batch, queue):
     """label "tinynet": optimizer.npz (3 steps, nesterov DGCSGD, fp32/int64, ratio 0.01);
     label "resnet20": BASELINE configs[0] (ResNet-20, ratio 0.001 with the 5-epoch warmup
@@ -78,83 +178,85 @@ def optimizer_replay_worker(rank, world, port, label, batch, queue):
     _init(rank, world, port)
     problems = []
     try:
-        from dgc.comm import Average
-        from dgc.compression import DGCCompressor
-        from dgc.horovod import DistributedOptimizer
-        from dgc.memory import DGCSGDMemory
-        from dgc.optim import DGCSGD
-        from models import ResNet20, TinyNet
         dev = torch.device("cuda:0")
         meta = json.load(open(os.path.join(GOLDEN, "optimizer_trace.json")))
         trace = np.load(os.path.join(GOLDEN, "optimizer_trace.npz"))
-        if label == "tinynet":
-            cfg = json.load(open(os.path.join(GOLDEN, "optimizer.json")))
-            want = np.load(os.path.join(GOLDEN, "optimizer.npz"))
-            torch.manual_seed(cfg["model_seed"])
-            model = TinyNet().to(dev)
-            comp_kw = dict(fp16_values=False, int32_indices=False, warmup_epochs=-1)
-            schedule = [(None, s) for s in range(cfg["steps"])]
-        else:
-            cfg = json.load(open(os.path.join(GOLDEN, "optimizer_resnet20.json")))
-            final = np.load(os.path.join(GOLDEN, "optimizer_resnet20.npz"))
-            torch.manual_seed(cfg["model_seed"])
-            model = ResNet20().to(dev)
-            if _digest(model) != cfg["init_digest"]:
-                problems.append(("init", "digest"))
-            comp_kw = dict(sample_ratio=cfg["sample_ratio"], fp16_values=cfg["fp16_values"],
-                           int32_indices=cfg["int32_indices"], warmup_epochs=cfg["warmup_epochs"])
-            spe = cfg["steps_per_epoch"]
-            schedule = [(e if t == 0 else None, ei * spe + t) for ei, e in enumerate(cfg["epochs"])
-                        for t in range(spe)]
-        opt = DGCSGD(model.parameters(), lr=cfg["lr"], momentum=cfg["momentum"],
-                     weight_decay=cfg["weight_decay"], nesterov=cfg["nesterov_sgd"])
-        mem = DGCSGDMemory(momentum=cfg["momentum"])
-        with contextlib.redirect_stdout(io.StringIO()):
-            comp = DGCCompressor(cfg["ratio"], memory=mem, **comp_kw)
-            mem.initialize(model.named_parameters())
-            comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
-        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
-                                    backward_passes_per_step=1, op=Average, batch=batch)
-        params = dict(model.named_parameters())
+        cfg, schedule = _load_cfg(label)
+        want = _want(label)
+        run = _setup(label, batch, dev, cfg)
+        if label == "resnet20" and _digest(run["model"]) != cfg["init_digest"]:
+            problems.append(("init", "digest"))
         random.seed(cfg["random_seed"])
-        calls = []
-        orig = comp.compress
-
-        def spy(tensor, name):
-            calls.append(name)
-            return orig(tensor, name)
-
-        comp.compress = spy
         for epoch, s in schedule:
-            if epoch is not None:
-                with contextlib.redirect_stdout(io.StringIO()):
-                    comp.warmup_compress_ratio(epoch)
-            key = f"{label}/s{s}/r{rank}"
-            order = meta[key]
-            grads = [trace[f"{key}/{j}"] for j in range(len(order))]
-            calls.clear()
-            replay_backward(params, order, grads, dev)
-            if (list(dopt._order) if batch else calls) != order:
-                problems.append(("hook order", s))
-            if batch and calls:
-                problems.append(("per-tensor compress in batch mode", s))
-            dopt.step()
-            dopt.zero_grad()
-            torch.cuda.synchronize()
-            if label == "tinynet":
-                for n, p in model.named_parameters():
-                    w = want[f"s{s}/r{rank}/{n}"]
-                    got = p.detach().cpu().numpy()
-                    if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
-                        problems.append(("weights", s, n, float(np.abs(got - w).max())))
-            elif _digest(model) != cfg["step_digests"][s][rank]:
-                problems.append(("step digest", s))
-        if label == "resnet20":
-            for n, p in model.named_parameters():
-                got = p.detach().cpu().numpy()
-                w = final[f"final/{n}"]
-                if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
-                    problems.append(("final", n, float(np.abs(got - w).max())))
+            _replay_step(run, label, batch, rank, epoch, s, meta, trace, dev, problems)
+            _check_weights(run, label, cfg, want, s, rank, problems)
+        _check_final(run, label, want, problems)
+        queue.put((rank, problems))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        queue.put((rank, [("error", repr(e), traceback.format_exc())]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _checkpoint(run):
+    """train.py:244-253's checkpoint — model, optimizer and compression.memory state
+    dicts — through torch.save into memory (a copy of every tensor, as on disk)."""
+    buf = io.BytesIO()
+    torch.save({"model": run["model"].state_dict(), "optimizer": run["dopt"].state_dict(),
+                "compression": run["mem"].state_dict()}, buf)
+    buf.seek(0)
+    return buf
+
+
+def _restore(run, buf, dev):
+    """train.py:153-165's resume: load_state_dict of model, optimizer and memory."""
+    ck = torch.load(buf, map_location=dev, weights_only=True)
+    run["model"].load_state_dict(ck["model"])
+    run["dopt"].load_state_dict(ck["optimizer"])
+    run["mem"].load_state_dict(ck["compression"])
+
+
+def resume_worker(rank, world, port, label, batch, mode, resume_at, queue):
+    """Checkpoint / resume parity (SURVEY.md §8f row 4; train.py:153-165, 244-264;
+    dgc/memory.py:79-88): run the reference's replay to the epoch boundary
+    ``resume_at``, checkpoint model + optimizer + memory, then
+      mode "fresh":   build NEW objects (another model init), load the checkpoint, go on;
+      mode "inplace": run one more step (the state moves on), load the checkpoint into
+                      the SAME objects — the memory's tensors are replaced, so the
+                      batched step must copy them back into its flat layout — and go on.
+    Python's ``random`` state is carried with the checkpoint (the sample starts of an
+    uninterrupted run). The weights after every later step must equal the reference's
+    (the goldens), which the uninterrupted run also reproduces. In batch mode every other
+    step zeroes with set_to_none=False (the views stay bound), the rest with None."""
+    import torch.distributed as dist
+    _init(rank, world, port)
+    problems = []
+    try:
+        dev = torch.device("cuda:0")
+        meta = json.load(open(os.path.join(GOLDEN, "optimizer_trace.json")))
+        trace = np.load(os.path.join(GOLDEN, "optimizer_trace.npz"))
+        cfg, schedule = _load_cfg(label)
+        want = _want(label)
+        run = _setup(label, batch, dev, cfg)
+        random.seed(cfg["random_seed"])
+        zg = lambda s: (s % 2 == 1) if batch else None   # noqa: E731
+        for epoch, s in schedule[:resume_at]:
+            _replay_step(run, label, batch, rank, epoch, s, meta, trace, dev, problems, zero_grad=zg(s))
+            _check_weights(run, label, cfg, want, s, rank, problems)
+        buf = _checkpoint(run)
+        rstate = random.getstate()
+        if mode == "fresh":
+            run = _setup(label, batch, dev, cfg, model_seed=cfg["model_seed"] + 1000)
+        else:
+            epoch, s = schedule[resume_at]
+            _replay_step(run, label, batch, rank, epoch, s, meta, trace, dev, problems, zero_grad=zg(s))
+        _restore(run, buf, dev)
+        random.setstate(rstate)
+        for epoch, s in schedule[resume_at:]:
+            _replay_step(run, label, batch, rank, epoch, s, meta, trace, dev, problems, zero_grad=zg(s))
+            _check_weights(run, label, cfg, want, s, rank, problems, tag="resumed weights")
+        _check_final(run, label, want, problems)
         queue.put((rank, problems))
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback

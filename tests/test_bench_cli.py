@@ -30,3 +30,11 @@ def test_gpus_must_match_world_size():
     assert b.launch_plan(2, {"WORLD_SIZE": "2"}) is None
     with pytest.raises(SystemExit):
         b.launch_plan(8, {"WORLD_SIZE": "1"})
+
+
+def test_gpus_fail_fast_without_devices():
+    b = _bench()
+    b.check_devices(1, 1)
+    b.check_devices(2, 8)
+    with pytest.raises(SystemExit, match="needs 8 visible GPUs"):
+        b.check_devices(8, 1)

@@ -39,7 +39,8 @@ def _sets():
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("label,shape", [("mixed", None), ("resnet50", None), ("vgg16_bn", None),
                                          ("mixed", "quarter"), ("resnet50", "quarter"), ("mixed+naninf", None),
-                                         ("mixed", "k5multi"), ("resnet50", "k5multi")])
+                                         ("mixed", "k5multi"), ("resnet50", "k5multi"), ("mixed", "k5abort"),
+                                         ("resnet50", "k5abort")])
 def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
     """shape: the emit kernel (None: the library's choice — k_emit_wide for these few
     groups; "quarter": k_emit, the flat buckets' kernel, forced), or "k5multi": the
@@ -51,6 +52,8 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
         pytest.skip("no GPU")
     if shape == "k5multi":   # K5's global phase over several workgroups per tensor, whatever the capacity
         monkeypatch.setenv("DGC_K5_GLOBAL", "multi")
+    elif shape == "k5abort":   # ... whose residency consensus times out: the one-workgroup fallback
+        monkeypatch.setenv("DGC_K5_GLOBAL", "abort")
     elif shape:
         monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
     from dgc.batch import DGCBatch
@@ -64,6 +67,7 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
     state = {n: (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
              for i, n in enumerate(b.names)}
     branches = set()
+    fallbacks = replays = 0
     steps = 3 if label != "vgg16_bn" else 2
     for s in range(steps):
         # state read on odd and last steps only: reading flushes the deferred masking, so the
@@ -100,6 +104,10 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
             key = f"{label}/s{s}/{name}"
             branches.add(info["branch"])
             assert infos[t]["branch"] == info["branch"], key
+            replays += infos[t]["branch"] == "resample" and infos[t]["tie_rule"] == "exact"
+            fallbacks += infos[t]["k5_fallback"]
+            if shape != "k5abort":
+                assert not infos[t]["k5_fallback"], (key, infos[t])
             gv, gi = sent[name]
             assert np.array_equal(gi.cpu().numpy(), oi), key
             assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
@@ -119,6 +127,8 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
             assert not bool(b.vec_flat[pad].any())
     if label == "mixed":
         assert {"direct", "resample"} <= branches, branches
+    if shape == "k5abort":   # every replay that reached the consensus fell back, exactly
+        assert replays > 0 and fallbacks > 0, (replays, fallbacks)
 
 
 def test_batch_warmup_ratio_change():

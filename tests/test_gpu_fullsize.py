@@ -38,7 +38,7 @@ def test_flat_1b_bucket_steps_match_oracle():
         pytest.skip("needs ~40 GiB of free HBM")
     from dgc.bucket import DGCBucket
     N, steps = 10 ** 9, 10
-    b = DGCBucket(N, compress_ratio=1e-3, momentum=0.9, nesterov=True, device=DEV, seed=42)
+    b = DGCBucket(N, compress_ratio=1e-3, momentum=0.9, nesterov=True, device=DEV, seed=42, fill="sparse")
     attrs = O.attributes(N, 1e-3)
     rng = random.Random(42)
     gen = torch.Generator(device=DEV)
@@ -100,15 +100,38 @@ def _first_ge(vec, t, limit, chunk=1 << 28):
     return torch.cat(parts)
 
 
-@pytest.mark.timeout(900)
+def _bench_gradient(g, N, seed, bf16, chunk=1 << 30):
+    """bench.py's FlatRun buffer ``seed``: one generator seeded once, randn in 2^30
+    chunks, bf16-rounded for the bf16-origin workload — regenerated in place, so the
+    test holds one gradient buffer instead of the bench's two."""
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(seed)
+    for c0 in range(0, N, chunk):
+        c1 = min(N, c0 + chunk)
+        x = torch.randn(c1 - c0, generator=gen, device=DEV)
+        g[c0:c1] = x.to(torch.bfloat16).float() if bf16 else x
+        del x
+
+
+def _equal_chunks(a, b, chunk=1 << 28):
+    return all(torch.equal(a[c0:c0 + chunk].view(torch.int32), b[c0:c0 + chunk].view(torch.int32))
+               for c0 in range(0, a.numel(), chunk))
+
+
+@pytest.mark.timeout(1100)
 def test_flat_7b_bf16_steps_match_reference_ops():
-    """BASELINE configs[4] at full size: N = 7e9 (> 2^32, so indices past 32 bits),
-    bf16-origin gradients (dense ties), ratio 1e-4, nesterov, two steps through
-    DGCBucket as bench.py runs it. Checked against the reference's algorithm re-run
-    with torch ops on the GPU, chunked (the numpy oracle is too slow at 7e9): compensate
-    (bit-exact momentum/velocity), the sampled threshold (topk of the strided samples),
-    the adaptation loop on exact counts, the transmitted indices in order and values,
-    the masking, and the decompressed output."""
+    """BASELINE configs[4] at full size and at the bench's steady state: N = 7e9 (> 2^32,
+    so indices past 32 bits), bf16-origin gradients (dense ties), ratio 1e-4, nesterov,
+    EIGHT steps through DGCBucket exactly as bench.py runs it — its two alternating
+    gradient buffers (seeds 0xD6C, 0xD6C + 1), its persistent output with the sparse
+    re-zero, its sample starts. Checked after every step against the reference's
+    algorithm re-run with torch ops on the GPU, chunked (the numpy oracle is too slow at
+    7e9): compensate (bit-exact momentum/velocity, compared raw — NOT flushed — so the
+    deferred masking rides in the next K1 as in the bench), the sampled threshold (topk
+    of the strided samples), the adaptation loop on exact counts, the transmitted
+    indices in order and values, the masking, and the decompressed output. The run must
+    reach the bench's steady state: selections served by K1's candidate lists
+    (full_passes == 0) with K3 reading the sample window list (window_keys > 0)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.cuda.empty_cache()   # what earlier tests left cached
@@ -116,22 +139,19 @@ def test_flat_7b_bf16_steps_match_reference_ops():
     if free < 200 * 2 ** 30:
         pytest.skip("needs ~200 GiB of free HBM")
     from dgc.bucket import DGCBucket
-    N, ratio = 7 * 10 ** 9, 1e-4
-    b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=42)
+    N, ratio, steps = 7 * 10 ** 9, 1e-4, 8
+    b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=42, fill="sparse")
     numel, k, S, ks, stride = O.attributes(N, ratio)
     assert (b.k, b.stride, b.top_k_samples) == (k, stride, ks)
     g = torch.empty(N, device=DEV)
-    gen = torch.Generator(device=DEV)
-    gen.manual_seed(0xD6C)
-    for c0 in range(0, N, 1 << 30):
-        c1 = min(N, c0 + (1 << 30))
-        g[c0:c1] = torch.randn(c1 - c0, generator=gen, device=DEV).to(torch.bfloat16).float()
     mmt_e = torch.zeros(N, device=DEV)
     vec_e = torch.zeros(N, device=DEV)
     out = torch.empty(N, device=DEV)
     rng = random.Random(42)
     U, Lc = O.adapt_bounds(k)
-    for s in range(2):
+    seen = []
+    for s in range(steps):
+        _bench_gradient(g, N, 0xD6C + s % 2, bf16=True)
         start = rng.randint(0, stride - 1)
         b.step(g, out)
         torch.cuda.synchronize()
@@ -165,15 +185,21 @@ def test_flat_7b_bf16_steps_match_reference_ops():
         gv = b.payload[b.voff: b.voff + 4 * cnt].view(torch.float32).cpu()
         assert torch.equal(gi, want), s
         assert int(gi.max()) >= 2 ** 32 or int(want.max()) < 2 ** 32
-        wv = vec_e[want.to(DEV)].cpu()
+        wd = want.to(DEV)
+        wv = vec_e[wd].cpu()
         assert torch.equal(gv.view(torch.int32), wv.view(torch.int32)), s
-        vec_e[want.to(DEV)] = 0.0                             # DGCSGDMemory.update (dgc/memory.py:72-77)
-        mmt_e[want.to(DEV)] = 0.0
-        for c0 in range(0, N, 1 << 28):                       # state after masking, bit for bit
-            c1 = min(N, c0 + (1 << 28))
-            assert torch.equal(b.vec[c0:c1].view(torch.int32), vec_e[c0:c1].view(torch.int32)), (s, c0)
-            assert torch.equal(b.mmt[c0:c1].view(torch.int32), mmt_e[c0:c1].view(torch.int32)), (s, c0)
-        assert torch.equal(out[want.to(DEV)].cpu().view(torch.int32), wv.view(torch.int32))
+        deferred = branch != "resample"   # the first-k branches leave the zeroing to the next K1
+        if deferred:   # raw state (no flush) = the state before DGCSGDMemory.update
+            assert _equal_chunks(b._vec, vec_e) and _equal_chunks(b._mmt, mmt_e), s
+        vec_e[wd] = 0.0                                       # DGCSGDMemory.update (dgc/memory.py:72-77)
+        mmt_e[wd] = 0.0
+        if not deferred:
+            assert _equal_chunks(b._vec, vec_e) and _equal_chunks(b._mmt, mmt_e), s
+        assert torch.equal(out[wd].cpu().view(torch.int32), wv.view(torch.int32))
         assert sum(int(torch.count_nonzero(out[c0:c0 + (1 << 28)])) for c0 in range(0, N, 1 << 28)) == \
             int(torch.count_nonzero(wv))
+        seen.append((info["branch"], info["full_passes"], info["window_keys"]))
         print(f"7B step {s}: {info}, max index {int(gi.max())}", file=sys.stderr, flush=True)
+    assert _equal_chunks(b.vec, vec_e) and _equal_chunks(b.mmt, mmt_e)   # flushed at the end
+    # the bench's steady state: lists serve the selection and K3 reads the window list
+    assert any(fp == 0 and wk > 0 for _, fp, wk in seen[2:]), seen

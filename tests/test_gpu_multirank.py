@@ -53,6 +53,22 @@ def test_distributed_optimizer_w2_reproduces_reference_weights(label, batch):
 
 
 @pytest.mark.timeout(200)
+@pytest.mark.parametrize("batch", [False, True], ids=["per-tensor", "batched"])
+@pytest.mark.parametrize("label,mode,resume_at", [("resnet20", "fresh", 2), ("resnet20", "fresh", 4),
+                                                  ("resnet20", "inplace", 4), ("tinynet", "inplace", 1)])
+def test_checkpoint_resume_w2_reproduces_reference_weights(label, mode, resume_at, batch):
+    """train.py's checkpoint (model, optimizer, compression.memory state dicts) at an
+    epoch boundary and a resume — into fresh objects, or into the running ones after
+    the state moved on — continue exactly as the uninterrupted reference run: the weights
+    after every later step equal the goldens, per tensor and batched (whose flat layout
+    must take the loaded memory tensors back in, and whose deferred masking must be
+    flushed into the checkpoint)."""
+    out = run(G.resume_worker, 2, label, batch, mode, resume_at)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)
+
+
+@pytest.mark.timeout(200)
 @pytest.mark.parametrize("fill,kind", [("inline", "normal"), ("allgather", "normal"), ("allgather", "layered"),
                                        ("sparse", "normal"), ("sparse", "layered")])
 def test_bucket_w2_matches_oracle(fill, kind):

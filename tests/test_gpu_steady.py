@@ -1,0 +1,116 @@
+"""Parity at the steady state the bench times, for the two model-set workloads
+(BASELINE configs[1] ResNet-50, configs[2] VGG-16-BN): ``bench.py``'s own ``ModelRun``
+— the same ``DGCBatch`` settings, the same two alternating x1e-3 ``randn`` gradient
+sets (seeds 0xD6C + buffer), the same sample starts (``random.Random(42)``, one draw
+per sampled tensor per step), the same persistent output with the sparse re-zero —
+stepped 25 times and compared with the oracle after EVERY step, tensor by tensor:
+
+* branch, count, transmitted indices (in order) and wire values (fp16/int32 casts);
+* momentum and velocity as the bench leaves them, i.e. NOT flushed: the first-k
+  branches defer ``DGCSGDMemory.update``'s zeroing to the next K1 (so the raw state
+  must equal the pre-masking state there), the resample branch masks at once;
+* the decompressed output (W = 1) and the dense tensors' ``compensate(accumulate=False)``.
+
+Reference: dgc/compression.py:109-198, dgc/memory.py:50-77. The run must pass through
+what the bench's ``selection`` record shows — exact resample replays (K5) and full
+select passes — or the test fails."""
+import importlib.util
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from oracle import dgc_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_steady", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view({4: np.uint32, 2: np.uint16, 8: np.uint64}[a.dtype.itemsize])
+
+
+@pytest.mark.timeout(1100)
+@pytest.mark.parametrize("workload", ["resnet50", "vgg16_bn"])
+def test_model_set_bench_steady_state_matches_oracle(workload):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    bench = _bench()
+    wl = bench.WORKLOADS[workload]
+    run = bench.ModelRun(wl, 0, 1, DEV, "sparse")
+    b = run.b
+    assert b.fill == "sparse"
+    fp16, int32, nest, ratio = wl["fp16"], wl["int32"], wl["nesterov"], wl["ratio"]
+    host = [[g[off: off + n].cpu().numpy() for off, n in zip(b.offsets, b.numels)] for g, _ in run.grads]
+    dense_host = [gd.cpu().numpy() for _, gd in run.grads]
+    attrs = [O.attributes(n, ratio) for n in b.numels]
+    state = [(np.zeros(n, np.float32), np.zeros(n, np.float32)) for n in b.numels]
+    dense_m = np.zeros(run.n_dense, np.float32)
+    ref_rng = random.Random(42)
+    exact = full_pass_steps = resample_max = 0
+    branches = {}
+    steps = 25
+    for s in range(steps):
+        run.step(s)
+        torch.cuda.synchronize()
+        sent = b.transmitted()
+        infos = b.infos()
+        raw_m = b._mmt_flat.cpu().numpy()   # not b.mmt_flat: reading that would flush the deferred masking
+        raw_v = b._vec_flat.cpu().numpy()
+        out = b.out_flat.cpu().numpy()
+        full_pass_steps += any(i["full_passes"] for i in infos)
+        for t, name in enumerate(b.names):
+            N, off, a = b.numels[t], b.offsets[t], attrs[t]
+            start = ref_rng.randint(0, a[4] - 1) if a[0] != a[2] else 0
+            key = f"{workload}/step{s}/{name}"
+            assert start == b.starts[t], key
+            m_o, v_o = state[t]
+            O.compensate(host[s % 2][t], m_o, v_o, 0.9, nest)
+            ov, oi, oinfo = O.sparsify(v_o, a, start)
+            info = infos[t]
+            assert info["branch"] == oinfo["branch"], (key, info)
+            assert info["count"] == oi.size, (key, info)
+            wv, wi = O.wire_cast(ov, oi, fp16, int32)
+            gv, gi = sent[name]
+            assert np.array_equal(gi.cpu().numpy(), oi), (key, info)
+            assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
+            deferred = info["branch"] != "resample"   # k_sel_finish: first-k branches defer the masking
+            if deferred:   # raw state = the pre-masking state
+                assert np.array_equal(bits(raw_v[off: off + N]), bits(v_o)), key
+                assert np.array_equal(bits(raw_m[off: off + N]), bits(m_o)), key
+            O.update(m_o, v_o, oi)
+            if not deferred:
+                assert np.array_equal(bits(raw_v[off: off + N]), bits(v_o)), key
+                assert np.array_equal(bits(raw_m[off: off + N]), bits(m_o)), key
+            assert np.array_equal(bits(out[off: off + N]), bits(O.decompress([wv], [oi], N, 1))), key
+            branches[info["branch"]] = branches.get(info["branch"], 0) + 1
+            if info["branch"] == "resample":
+                exact += info["tie_rule"] == "exact"
+                resample_max = max(resample_max, info["candidates"])
+                assert info["tie_rule"] == "exact", (key, info)
+        # dense tensors: wire cast -> (W = 1 allreduce) -> compensate(accumulate=False)
+        src = dense_host[s % 2].astype(np.float16).astype(np.float32) if fp16 else dense_host[s % 2]
+        want = O.compensate(src, dense_m, None, 0.9, nest, accumulate=False)
+        assert np.array_equal(bits(run.dense_out.cpu().numpy()), bits(want)), (workload, s)
+        print(f"{workload} step {s}: branches so far {branches}, exact resamples {exact} "
+              f"(max {resample_max} candidates), steps with full passes {full_pass_steps}", file=sys.stderr,
+              flush=True)
+    # the flushed state at the end equals the oracle's
+    for t, name in enumerate(b.names):
+        m_o, v_o = state[t]
+        assert np.array_equal(bits(b.velocity_of(name).reshape(-1).cpu().numpy()), bits(v_o)), name
+        assert np.array_equal(bits(b.momentum_of(name).reshape(-1).cpu().numpy()), bits(m_o)), name
+    # the bench's dynamics were exercised: exact resample replays and full select passes
+    assert exact > 0 and full_pass_steps > 0, (branches, exact, full_pass_steps)

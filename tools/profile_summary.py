@@ -10,9 +10,14 @@ one pass on gfx950). Writes, for WORKLOAD:
   kstats_<W>.json              {kernel: calls, avg/min/max/total ms} (bench.py reads K1's avg)
   step_timeline_<W>.txt        the kernels of the last full step, with gaps
   pmc_<W>.json                 per kernel, the AVERAGE per launch of FETCH_SIZE and WRITE_SIZE
-                               (KB as rocprofv3 reports them) and HBM bytes per launch =
-                               2 x FETCH_SIZE x 1024 (gfx950 counts half the bytes of wide
-                               streaming reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE x 1024
+                               (KB as rocprofv3 reports them). HBM bytes per launch =
+                               2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 ONLY for the kernels
+                               whose reads are 16-B-per-lane coalesced streams (STREAMING:
+                               the guide calibrates the x2 for exactly that access shape,
+                               MI355X_MICROARCH.md §HBM "FETCH_SIZE reports exactly 1/2 ...";
+                               "other access widths are uncalibrated"); every other kernel
+                               gets hbm_bytes_per_launch = null and the uncalibrated range
+                               [FETCH + WRITE, 2 x FETCH + WRITE] instead.
 """
 import collections
 import csv
@@ -21,6 +26,13 @@ import json
 import os
 import shutil
 import sys
+
+
+# kernels whose global reads are 16-B-per-lane coalesced streams (float4 / dwordx4
+# tiles over contiguous vec / grad / mmt): K1, the full select pass, the lowering
+# counts, the probe and K7's multi-tensor apply
+STREAMING = ("k_compensate_list", "k_compensate4", "k_select_pass", "k_lower_counts", "k_probe", "k_sgd",
+             "k_fill_zero")
 
 
 def main():
@@ -79,10 +91,13 @@ def main():
                 continue
             avg = {c: sum(v) / len(v) for c, v in cs.items()}
             f_kb, w_kb = avg.get("FETCH_SIZE"), avg.get("WRITE_SIZE")
+            fb = f_kb * 1024 if f_kb is not None else 0
+            wb = w_kb * 1024 if w_kb is not None else 0
+            stream = any(s in k for s in STREAMING)
             res[k[:120]] = {"launches": max(len(v) for v in cs.values()), "FETCH_SIZE_KB_avg": f_kb,
-                            "WRITE_SIZE_KB_avg": w_kb,
-                            "hbm_bytes_per_launch": (2 * f_kb * 1024 if f_kb is not None else 0) +
-                            (w_kb * 1024 if w_kb is not None else 0)}
+                            "WRITE_SIZE_KB_avg": w_kb, "calibrated": stream,
+                            "hbm_bytes_per_launch": (2 * fb + wb) if stream else None,
+                            "hbm_bytes_per_launch_range": None if stream else [fb + wb, 2 * fb + wb]}
         with open(f"{out}/pmc_{wl}.json", "w") as f:
             json.dump({"command": command, "kernels": res}, f, indent=1)
     if bench:
@@ -97,7 +112,8 @@ def main():
             rf["rocprof_avg_launch_ms"] = v1.get("timed_avg_ms", v1["avg_ms"])
             rf["rocprof_source"] = f"{rel}/kstats_{wl}.json"
         if pmc and os.path.isdir(pmc):
-            t = [v["hbm_bytes_per_launch"] for name, v in res.items() if "k_compensate_list" in name]
+            t = [v["hbm_bytes_per_launch"] for name, v in res.items()
+                 if "k_compensate_list" in name and v["hbm_bytes_per_launch"] is not None]
             if t:
                 rf["traffic"] = max(t)
                 rf["traffic_source"] = f"{rel}/pmc_{wl}.json"
