@@ -44,6 +44,10 @@ constexpr int kNthThreads = 512;    // 8 waves: 256 VGPRs per lane for the batch
 constexpr int kNthWaves = kNthThreads / kWave;
 constexpr int kNthLds = 12288;   // entries partitioned in LDS (96 KB + 48 KB of pair slots)
 constexpr int kNthWave = 1024;   // entries finished by a single wave
+constexpr int kNthPairLds = kNthLds / 2 + 1;            // LDS pair slots per side
+constexpr int kNthMkLds = (kNthLds / 256 + 1) * 64;     // LDS-phase stopper bytes
+// LDS of the one-workgroup replay, carved by the caller (k_nth_select shares it with K5b)
+constexpr size_t kNthSmemBytes = (size_t)kNthLds * 8 + 2 * (size_t)kNthPairLds * 4 + kNthMkLds;
 
 __device__ __forceinline__ uint32_t qkey(uint64_t e) { return (uint32_t)(e >> 32); }
 
@@ -839,13 +843,13 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
 // workgroup. gpos_l/gpos_r: global pair slots (>= n / 2 + 1 each) for the ranges
 // above kNthLds. Returns after a final barrier.
 // lq: the caller's LDS area of kNthLds entries (16-B aligned): the partition range
-// in the LDS phase, the stopper bytes in the global phase.
+// in the LDS phase, the stopper bytes in the global phase; llp / lrp (kNthPairLds
+// each) and lmk (kNthMkLds bytes): the LDS phase's pair slots and stopper bytes.
 // from: the state k_nth_global left (its global phase done), or null (start at [0, n)).
 __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r,
-                               uint64_t* lq, const NthG* from = nullptr) {
+                               uint64_t* lq, uint32_t* llp, uint32_t* lrp, uint8_t* lmk,
+                               const NthG* from = nullptr) {
     __shared__ NthShared sh;
-    __shared__ uint32_t llp[kNthLds / 2 + 1], lrp[kNthLds / 2 + 1];
-    __shared__ uint8_t lmk[(kNthLds / 256 + 1) * 64];   // LDS phase stopper bytes
     if (threadIdx.x == 0) {
         sh.f = 0;
         sh.l = n;
@@ -875,7 +879,7 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     }
     __syncthreads();
     K5_STAMP(2);
-    nth_loop_wg<1, 2>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthLds / 256 + 1);   // LDS phase
+    nth_loop_wg<1, 2>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthMkLds / 64);   // LDS phase
     K5_STAMP(3);
     if (!sh.heap_exit && threadIdx.x < kWave) nth_tail_wave(lq, llp, lrp, sh, nth - f);   // one wave
     __syncthreads();

@@ -77,10 +77,7 @@ constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgrou
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
 constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
 constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
-constexpr int kHeapMax = 4096;                  // K5b: exact partial_sort replay up to this k (heap in LDS)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
-constexpr int kHeapThreads = 512;                // = kNthThreads: K5b runs inside k_nth_select
-constexpr int kHeapPer = 16;                    // K5b: consecutive elements per thread per chunk
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
 
@@ -196,7 +193,6 @@ struct Layout {
     int64_t max_cand = 0;       // the largest K5 candidate capacity of a tensor
     int32_t nsmall = 0;
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
-    bool lowest_any = false;    // some tensor can take the approximate partial_sort resample
     int64_t grid[BT_COUNT] = {};
 };
 
@@ -250,7 +246,6 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.lower_count = in[t].lower_count;
         const bool sampled = d.n != d.S;
         L.adapt_any |= sampled;
-        L.lowest_any |= sampled && (d.k > kHeapMax || d.n > 0xFFFFFFFFLL);   // see k_decide
         d.samp_off = (sampled && in[t].samples) ? samp : -1;
         if (d.samp_off >= 0) samp += (int64_t)align_up((size_t)(d.S + 1), 64);
         // a window list for the multi-block thresholds; its size cannot depend on ks
@@ -978,7 +973,7 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
     if (!st->active) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     __shared__ uint64_t lds16[16];
-    __shared__ int finished, reset_rs;
+    __shared__ int finished;
     uint64_t local = 0;
 #pragma unroll 4
     for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) local += w.grp_cnt[d.grp0 + i];
@@ -993,7 +988,6 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
         const bool adapt = d.n > d.S;
         st->n_cur = cnt;
         int done = 1;
-        reset_rs = 0;
         if (!adapt) {
             st->branch = DGC_BRANCH_DIRECT;
             st->limit = cnt < k ? cnt : k;
@@ -1004,17 +998,10 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
             if (cnt > d.upper_count) {
                 if (p.resample) {
                     st->branch = DGC_BRANCH_RESAMPLE;
-                    if (cnt < 64 * k && cnt <= d.cand_cap) {   // torch's nth_element path: replayed
-                        st->rs_nth = 1;
-                        st->tie_rule = DGC_TIES_EXACT;
-                    } else if (k <= kHeapMax && d.n <= 0xFFFFFFFFLL) {   // partial_sort path: replayed
-                        st->rs_nth = 2;
-                        st->tie_rule = DGC_TIES_EXACT;
-                    } else {                                    // partial_sort path, large k: lowest-index ties
-                        st->resample_pending = 1;
-                        st->tie_rule = DGC_TIES_LOWEST_INDEX;
-                        reset_rs = 1;
-                    }
+                    // torch's CPU topk: nth_element while k * 64 > candidates (K5), else
+                    // partial_sort (K5b) — both replayed exactly
+                    st->rs_nth = (cnt < 64 * k && cnt <= d.cand_cap) ? 1 : 2;
+                    st->tie_rule = DGC_TIES_EXACT;
                 } else {
                     st->t_cur = __fmul_rn(st->t_cur, p.upper);
                     done = 0;
@@ -1049,7 +1036,6 @@ __global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
     }
     __syncthreads();
     if (finished == 1) block_scan_array(w.grp_cnt + d.grp0, w.grp_off + d.grp0, d.ngrp, lds16);
-    if (reset_rs) rs_reset(w.rs + t, (uint64_t)d.k);
     __syncthreads();
     if (finished != 1)
         for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) w.grp_cnt[d.grp0 + i] = 0;
@@ -1803,109 +1789,332 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
 }
 
 // K5b: torch's CPU topk on its partial_sort path (k * 64 <= candidates, i.e. a sampled
-// threshold >= 64x too low), replayed exactly for k <= kHeapMax:
-// std::partial_sort(queue, queue + k, queue + n, greater) = heap select over the
-// candidates in index order — make_heap of the first k, then every later candidate
-// whose key beats the heap's top replaces it (pop_heap) — and sort_heap; queue[0..k)
-// is the output in that order (dgc/compression.py:134-137). The heap lives in LDS
-// and is worked by one thread (the order of ties depends on its exact layout); the
-// other threads stream vec in chunks, compact each chunk's candidates in index order
-// and pre-filter those that cannot beat the top (the top only rises). Then the emit
-// (values, wire casts, DGCSGDMemory.update's masking) in parallel.
+// threshold >= 64x too low), replayed EXACTLY for every k and N (dgc/compression.py:
+// 134-137): std::partial_sort(queue, queue + k, queue + n, greater) over the
+// candidates in index order = make_heap of the first k, then every later candidate
+// whose key beats the heap's top replaces it (pop_heap), then sort_heap; queue[0..k)
+// is the output in that order. Equal keys are indistinguishable to the heap's
+// comparisons, so which boundary ties survive and the order of equal keys come from
+// its exact layout — the replay runs the same operations on the same layout.
+//
+//   entries   (|x| key (31 bits) << 33) | element index (33 bits: N < 2^33)
+//   layout    node i in LDS for i < kHeapTop (levels 0..13), else in the tensor's K5
+//             queue region (>= k entries: cand_cap = min(64k - 1, N) >= k)
+//   fill      the workgroup streams vec in index order, block-scans the candidates
+//             (|x| >= t_cur) and writes the first k to nodes 0..k-1
+//   make_heap level by level, one thread per parent (parents of one level own
+//             disjoint subtrees, so this is std::__make_heap's descending order)
+//   select    per 2048-element chunk, the candidates that beat the root are compacted
+//             in order; wave 0 re-checks each against the live root and replaces it:
+//             the min-child path to a leaf is found 5 levels per load (62 lanes load
+//             the hole's subtree, the path is resolved with readlanes), then
+//             std::__push_heap's stop on the (monotone) path is one ballot, and the
+//             shifted nodes are written in parallel
+//   sort_heap k - 1 pops by wave 0, the same replacement on a shrinking heap
+//   emit      payload slot p <- node p: values, wire casts, DGCSGDMemory.update's masking
+//
+// Sequential by nature (~k ln(n/k) replacements + k pops); reached only when the
+// sampled threshold came out >= 64x too low, never by the benchmarked workloads.
+constexpr int kHeapTop = 16383;                  // nodes in LDS (levels 0..13)
+constexpr int kHeapChunk = kNthThreads * 4;      // vec elements per step: one float4 per thread
+constexpr int kHeapSub = 5;                      // levels of the path resolved per load
+constexpr int kHeapKeyShift = 33;
+constexpr uint64_t kHeapIdxMask = (1ull << kHeapKeyShift) - 1;
+constexpr size_t kHeapSmemBytes = (size_t)(kHeapTop + 1 + kHeapChunk) * 8;   // nodes + hot list
+constexpr size_t kK5SmemBytes = kHeapSmemBytes > kNthSmemBytes ? kHeapSmemBytes : kNthSmemBytes;
+
+__device__ __forceinline__ uint32_t hkey(uint64_t e) { return (uint32_t)(e >> kHeapKeyShift); }
+
+struct HeapNodes {
+    uint64_t* lds;   // nodes [0, kHeapTop)
+    uint64_t* g;     // nodes >= kHeapTop (indexed by node)
+    __device__ __forceinline__ uint64_t ld(int64_t i) const { return i < kHeapTop ? lds[i] : g[i]; }
+    __device__ __forceinline__ void st(int64_t i, uint64_t v) const {
+        if (i < kHeapTop)
+            lds[i] = v;
+        else
+            g[i] = v;
+    }
+};
+
+// std::__adjust_heap + std::__push_heap on nodes [0, len) from `hole` with value v,
+// comp = key greater (the root holds the smallest key). One thread (make_heap).
+__device__ void heap_adjust1(const HeapNodes& h, int64_t hole, int64_t len, uint64_t v) {
+    const int64_t top = hole;
+    int64_t child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        const uint64_t r = h.ld(child), l = h.ld(child - 1);
+        uint64_t c = r;
+        if (hkey(r) > hkey(l)) {
+            child--;
+            c = l;
+        }
+        h.st(hole, c);
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        h.st(hole, h.ld(child - 1));
+        hole = child - 1;
+    }
+    int64_t parent = (hole - 1) / 2;
+    while (hole > top) {
+        const uint64_t pv = h.ld(parent);
+        if (!(hkey(pv) > hkey(v))) break;
+        h.st(hole, pv);
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    h.st(hole, v);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// std::__adjust_heap(first, 0, len, v) — the root replaced by v — by ONE wave (all 64
+// lanes, uniform arguments). Returns the new root. The min-child path from the root:
+// lanes 2^d - 2 .. 2^(d+1) - 3 hold the hole's descendants at depth d = 1..5, loaded
+// at once; the choice at each level (right child unless the left key is smaller;
+// a lone left child at the end) is resolved from them with readlanes. Along the path
+// the keys never decrease (heap order), so push_heap's climb stops at J = the first
+// path node whose key exceeds v's: nodes p_0..p_(J-2) take the values of p_1..p_(J-1),
+// p_(J-1) takes v, the rest keep theirs — written by lanes 0..J-1 at once.
+__device__ uint64_t heap_replace_root(const HeapNodes& h, int64_t len, uint64_t v) {
+    const int lane = threadIdx.x & 63;
+    uint64_t pidx = 0, pval = 0;   // lane j-1: path node p_j and its value a_j
+    int m = 0;                     // path length
+    int64_t hole = 0;
+    bool more = len > 1;
+    while (more) {
+        // this lane's descendant of `hole`: depth dl (1..5), offset ol
+        const int dl = 31 - __clz(lane + 2);               // lane + 2 in [2^dl, 2^(dl+1))
+        const int64_t ol = (int64_t)(lane + 2) - (1ll << dl);
+        const int64_t node = ((hole + 1) << dl) - 1 + ol;
+        uint64_t val = 0;
+        if (lane < 62 && node < len) val = h.ld(node);
+        int64_t off = 0;   // the hole's offset among the subtree nodes of its depth
+        for (int d = 1; d <= kHeapSub; ++d) {
+            const int base = (1 << d) - 2;
+            int64_t child;
+            uint64_t cval;
+            if (hole < (len - 1) / 2) {   // two children
+                const uint64_t l = readlane64(val, base + (int)(2 * off));
+                const uint64_t r = readlane64(val, base + (int)(2 * off) + 1);
+                if (hkey(r) > hkey(l)) {
+                    child = 2 * hole + 1;
+                    cval = l;
+                    off = 2 * off;
+                } else {
+                    child = 2 * hole + 2;
+                    cval = r;
+                    off = 2 * off + 1;
+                }
+            } else if ((len & 1) == 0 && hole == (len - 2) / 2) {   // a lone left child, then stop
+                child = 2 * hole + 1;
+                cval = readlane64(val, base + (int)(2 * off));
+                off = 2 * off;
+                more = false;
+            } else {
+                more = false;
+                break;
+            }
+            if (lane == m) {
+                pidx = (uint64_t)child;
+                pval = cval;
+            }
+            ++m;
+            hole = child;
+            if (!more) break;
+        }
+    }
+    // J - 1 = the first lane (path index) whose value's key exceeds v's; m if none
+    const uint64_t above = __ballot(lane < m && hkey(pval) > hkey(v));
+    const int jm1 = above ? __builtin_ctzll(above) : m;
+    const uint64_t up = (uint64_t)__shfl_up((long long)pidx, 1);
+    const int64_t parent = lane == 0 ? 0 : (int64_t)up;   // p_(lane) for lane >= 1, p_0 = root
+    if (lane < jm1)
+        h.st(parent, pval);   // p_(lane) <- a_(lane+1)
+    else if (lane == jm1)
+        h.st(parent, v);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the next replacement reads these
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return jm1 == 0 ? v : readlane64(pval, 0);
+}
+
+// Chunk loads: 4 consecutive elements of vec per thread, kHeapAhead chunks (16 KB) in
+// flight per batch, the next batch issued before the current one is processed — the
+// workgroup streams vec at a CU's load rate instead of one round trip per chunk.
+constexpr int kHeapAhead = 8;
+
+__device__ __forceinline__ void heap_load(const float* vec, int64_t n, int64_t c0, bool al, float (&x)[4]) {
+    const int64_t e0 = c0 + 4 * (int64_t)threadIdx.x;
+    if (al && e0 + 3 < n) {
+        const float4 v = *reinterpret_cast<const float4*>(vec + e0);
+        x[0] = v.x;
+        x[1] = v.y;
+        x[2] = v.z;
+        x[3] = v.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = e0 + j < n ? vec[e0 + j] : 0.f;
+    }
+}
+
+// Candidate bits of a thread's 4 elements at chunk c0 (|x| >= tc; NaN never is).
+__device__ __forceinline__ uint32_t heap_cands(int64_t n, int64_t c0, float tc, const float (&x)[4]) {
+    const int64_t e0 = c0 + 4 * (int64_t)threadIdx.x;
+    uint32_t cm = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cm |= (uint32_t)(e0 + j < n && fabsf(x[j]) >= tc) << j;
+    return cm;
+}
+
+// Streams the chunks from c_begin in index order, kHeapAhead at a time with the next
+// batch in flight; f(c0, x) returns false to stop (uniformly). Returns the chunk it
+// stopped at (n rounded up to a chunk when it ran to the end).
+template <class F>
+__device__ int64_t heap_stream(const float* vec, int64_t n, int64_t c_begin, bool al, F&& f) {
+    constexpr int64_t kBatch = (int64_t)kHeapAhead * kHeapChunk;
+    float xa[kHeapAhead][4], xb[kHeapAhead][4];
+#pragma unroll
+    for (int u = 0; u < kHeapAhead; ++u) heap_load(vec, n, c_begin + u * kHeapChunk, al, xa[u]);
+    for (int64_t b0 = c_begin; b0 < n; b0 += kBatch) {
+#pragma unroll
+        for (int u = 0; u < kHeapAhead; ++u) heap_load(vec, n, b0 + kBatch + u * kHeapChunk, al, xb[u]);
+#pragma unroll
+        for (int u = 0; u < kHeapAhead; ++u) {
+            const int64_t c0 = b0 + u * kHeapChunk;
+            if (c0 >= n) return c0;
+            if (!f(c0, xa[u])) return c0;
+        }
+#pragma unroll
+        for (int u = 0; u < kHeapAhead; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xa[u][j] = xb[u][j];
+    }
+    return n;
+}
+
 __device__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o, int t,
-                               uint64_t* heap, uint64_t* hot) {
+                               uint64_t* smem) {
     const SelState* st = w.st + t;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
-    const int64_t k = d.k;
-    constexpr int64_t kChunkElems = (int64_t)kHeapThreads * kHeapPer;
+    const int64_t k = d.k, n = d.n;
+    const bool al = aligned16(vec);
+    const HeapNodes h{smem, w.queue + d.cand_off};
+    uint64_t* hot = smem + kHeapTop + 1;
     __shared__ uint64_t lds16[16];
+    __shared__ uint64_t root_sh;
     __shared__ long long obase_s;
     const int tid = threadIdx.x;
-    int64_t filled = 0;   // candidates seen so far (uniform)
-    for (int64_t c0 = 0; c0 < d.n; c0 += kChunkElems) {
-        const int64_t e0 = c0 + (int64_t)tid * kHeapPer;
-        float x[kHeapPer];
-        uint32_t cm = 0;
-#pragma unroll
-        for (int j = 0; j < kHeapPer; ++j) {
-            const bool ok = e0 + j < d.n;
-            x[j] = ok ? vec[e0 + j] : 0.f;
-            cm |= (uint32_t)(ok && fabsf(x[j]) >= tc) << j;
-        }
+    // ---- fill: the first k candidates, in index order, become nodes 0..k-1
+    int64_t filled = 0, skip = 0;   // skip: candidates of the last fill chunk that went into the heap
+    const int64_t c_fill = heap_stream(vec, n, 0, al, [&](int64_t c0, const float (&x)[4]) -> bool {
+        const uint32_t cm = heap_cands(n, c0, tc, x);
         uint64_t total;
-        const uint64_t base = block_exclusive_scan((uint64_t)__popc(cm), lds16, &total);
-        const int64_t fnew = filled + (int64_t)total;
-        if (filled < k) {   // the first k candidates fill the heap in index order
-            uint64_t r = base;
+        uint64_t r = block_exclusive_scan((uint64_t)__popc(cm), lds16, &total);
+        const int64_t e0 = c0 + 4 * (int64_t)tid;
 #pragma unroll
-            for (int j = 0; j < kHeapPer; ++j) {
-                if ((cm >> j) & 1u) {
-                    const int64_t g = filled + (int64_t)r++;
-                    if (g < k) heap[g] = ((uint64_t)abs_key(x[j]) << 32) | (uint64_t)(uint32_t)(e0 + j);
-                }
+        for (int j = 0; j < 4; ++j) {
+            if ((cm >> j) & 1u) {
+                const int64_t g = filled + (int64_t)r++;
+                if (g < k) h.st(g, ((uint64_t)abs_key(x[j]) << kHeapKeyShift) | (uint64_t)(e0 + j));
             }
-            __syncthreads();
-            if (fnew >= k && tid == 0 && k >= 2) {   // std::__make_heap
-                for (int64_t parent = (k - 2) / 2;; --parent) {
-                    nth_adjust_heap(heap, parent, k, heap[parent]);
-                    if (parent == 0) break;
-                }
-            }
-            __syncthreads();
         }
-        if (fnew > k) {   // candidates past the first k: the heap-select loop
-            const uint32_t top = qkey(heap[0]);
-            uint32_t hm = 0;
-            uint64_t r = base;
-#pragma unroll
-            for (int j = 0; j < kHeapPer; ++j) {
-                if ((cm >> j) & 1u) {
-                    const int64_t g = filled + (int64_t)r++;
-                    if (g >= k && abs_key(x[j]) > top) hm |= 1u << j;
-                }
-            }
-            uint64_t htot;
-            const uint64_t hb = block_exclusive_scan((uint64_t)__popc(hm), lds16, &htot);
-            uint64_t q = hb;
-#pragma unroll
-            for (int j = 0; j < kHeapPer; ++j)
-                if ((hm >> j) & 1u) hot[q++] = ((uint64_t)abs_key(x[j]) << 32) | (uint64_t)(uint32_t)(e0 + j);
-            __syncthreads();
-            if (tid == 0) {
-                for (uint64_t h = 0; h < htot; ++h) {   // comp(candidate, top): strictly greater
-                    const uint64_t v = hot[h];
-                    if (qkey(v) > qkey(heap[0])) nth_adjust_heap(heap, 0, k, v);
-                }
-            }
-            __syncthreads();
+        if (filled + (int64_t)total >= k) {
+            skip = k - filled;
+            filled = k;
+            return false;
         }
-        filled = fnew;
-    }
-    if (tid == 0) {   // std::__sort_heap
-        for (int64_t last = k; last > 1;) {
-            --last;
-            const uint64_t v = heap[last];
-            heap[last] = heap[0];
-            nth_adjust_heap(heap, 0, last, v);
+        filled += (int64_t)total;
+        return true;
+    });
+    __syncthreads();
+    // ---- make_heap, level by level (deepest parents first)
+    if (k >= 2) {
+        const int64_t last_parent = (k - 2) / 2;
+        const int top_level = 63 - __clzll((unsigned long long)(last_parent + 1));
+        for (int lv = top_level; lv >= 0; --lv) {
+            const int64_t p0 = (1ll << lv) - 1;
+            const int64_t p1 = std::min<int64_t>((2ll << lv) - 2, last_parent);
+            for (int64_t p = p0 + tid; p <= p1; p += kNthThreads) heap_adjust1(h, p, k, h.ld(p));
+            __syncthreads();
         }
     }
+    // ---- heap select over the candidates after the first k, from the chunk the fill ended in
+    if (tid == 0) root_sh = h.ld(0);
+    __syncthreads();
+    heap_stream(vec, n, c_fill, al, [&](int64_t c0, const float (&x)[4]) -> bool {
+        const uint32_t cm = heap_cands(n, c0, tc, x);
+        const uint32_t rk = hkey(root_sh);
+        uint32_t hm = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hm |= (uint32_t)(((cm >> j) & 1u) && abs_key(x[j]) > rk) << j;
+        if (skip > 0) {   // the chunk where the fill ended: its first `skip` candidates are in the heap
+            uint64_t tot;
+            uint64_t r = block_exclusive_scan((uint64_t)__popc(cm), lds16, &tot);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((cm >> j) & 1u) {
+                    if ((int64_t)r < skip) hm &= ~(1u << j);
+                    ++r;
+                }
+            skip = 0;
+        }
+        if (!__syncthreads_or(hm != 0)) return true;
+        uint64_t htot;
+        const uint64_t hb = block_exclusive_scan((uint64_t)__popc(hm), lds16, &htot);
+        const int64_t e0 = c0 + 4 * (int64_t)tid;
+        uint64_t q = hb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((hm >> j) & 1u) hot[q++] = ((uint64_t)abs_key(x[j]) << kHeapKeyShift) | (uint64_t)(e0 + j);
+        __syncthreads();
+        if (tid < kWave) {   // wave 0: comp(candidate, top) is "strictly greater"
+            uint64_t root = root_sh;
+            for (uint64_t i = 0; i < htot; ++i) {
+                const uint64_t v = hot[i];
+                if (hkey(v) > hkey(root)) root = heap_replace_root(h, k, v);
+            }
+            if (tid == 0) root_sh = root;
+        }
+        __syncthreads();
+        return true;
+    });
+    // ---- sort_heap: k - 1 pops by wave 0
+    if (tid < kWave) {
+        for (int64_t last = k - 1; last >= 1; --last) {
+            const uint64_t v = h.ld(last);
+            const uint64_t root = h.ld(0);
+            if (tid == 0) h.st(last, root);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            (void)heap_replace_root(h, last, v);
+        }
+    }
+    __syncthreads();
+    // ---- emit: payload slot p <- node p
     if (tid < kWave) {
         const long long b = out_base(w, t);
         if (tid == 0) obase_s = b;
     }
     __syncthreads();
-    for (int64_t p = tid; p < k; p += kHeapThreads) {
-        const int64_t li = (int64_t)(uint32_t)heap[p];
+    for (int64_t p = tid; p < k; p += kNthThreads) {
+        const int64_t li = (int64_t)(h.ld(p) & kHeapIdxMask);
         emit_one(o, d, obase_s + p, li, vec[li]);
     }
 }
 
 // K5 / K5b, one workgroup per tensor: the reference's resample topk replayed on the
-// gathered candidates (introselect.hpp: nth_element), or — partial_sort path, k <=
-// kHeapMax — heap select + sort_heap over vec, which also emits. They share one LDS area.
-static_assert(kHeapMax + (int64_t)kHeapThreads * kHeapPer <= kNthLds, "K5b: heap + chunk fit K5's LDS");
+// gathered candidates (introselect.hpp: nth_element), or — partial_sort path — heap
+// select + sort_heap over vec, which also emits. They share one LDS area.
+static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // K5's global-memory phase by G workgroups per tensor (grid G x T, a plain launch sized
 // so all of them fit at once; a residency consensus decides whether they run it, see
 // introselect.hpp); k_nth_select goes on from the state it leaves.
@@ -1926,15 +2135,19 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || !st->rs_nth) return;
-    __shared__ __align__(16) uint64_t lq[kNthLds];
+    __shared__ __align__(16) uint64_t smem[kK5SmemBytes / 8];
     if (st->rs_nth == 2) {
-        heap_select_wg(vec_flat, w, o, t, lq, lq + kHeapMax);
+        heap_select_wg(vec_flat, w, o, t, smem);
         return;
     }
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     uint32_t* gl = w.gpos + d.gpos_off;
     uint32_t* gr = gl + d.cand_cap / 2 + 1;
-    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, lq, from_global ? w.nthg + t : nullptr);
+    uint32_t* llp = reinterpret_cast<uint32_t*>(smem + kNthLds);
+    uint32_t* lrp = llp + kNthPairLds;
+    uint8_t* lmk = reinterpret_cast<uint8_t*>(lrp + kNthPairLds);
+    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, smem, llp, lrp, lmk,
+                   from_global ? w.nthg + t : nullptr);
 }
 
 // Result records; the payload's total count; and every tensor's next speculative
@@ -2111,14 +2324,6 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     };
     EmitOut o{p.update_memory ? vec : nullptr, (p.update_memory && p.masking) ? mmt : nullptr, values, indices,
               p.vdtype, p.idtype, nullptr, nullptr, (int32_t)(p.update_memory == 2)};
-    auto resample_lowest = [&]() -> int {
-        // partial_sort path (>= 64k candidates): radix k-th value, ties lowest index first.
-        // rs state reset by k_decide when it chose this path
-        DGC_TRY(radix_select_passes(CandKeys{w, vec}, (int)L.grid[BT_CAP4], s));
-        hipLaunchKernelGGL(k_count_gt_eq, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w);
-        DGC_LAUNCHED();
-        return DGC_OK;
-    };
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
@@ -2172,18 +2377,9 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
                 DGC_TRY(pass((any_list ? 1 : 0) | (any_full ? 2 : 0), false));
             }
         }
-        bool any_nth = false, any_low = false, any_heap = false;
-        for (const SelState& h : hs) {
-            if (h.branch != DGC_BRANCH_RESAMPLE) continue;
-            if (h.rs_nth == 1)
-                any_nth = true;
-            else if (h.rs_nth == 2)
-                any_heap = true;
-            else
-                any_low = true;
-        }
-        if (any_low) DGC_TRY(resample_lowest());
-        if (any_nth || any_heap) {   // k_nth_select serves both
+        bool any_resample = false;
+        for (const SelState& h : hs) any_resample |= h.branch == DGC_BRANCH_RESAMPLE;
+        if (any_resample) {   // k_nth_select serves both paths (K5, K5b)
             DGC_TRY(resample_exact());
             emitted = true;
         }
@@ -2196,7 +2392,6 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
             for (int i = 0; i < p.max_iters; ++i) DGC_TRY(pass(3, true));
         }
         if (p.resample) {
-            if (L.lowest_any) DGC_TRY(resample_lowest());   // 4 gated launches no tensor here can need
             DGC_TRY(resample_exact());
             emitted = true;
         }
