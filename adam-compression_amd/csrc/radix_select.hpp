@@ -109,6 +109,7 @@ struct DenseKeys {
     __device__ __forceinline__ bool active(int) const { return true; }
     __device__ __forceinline__ RSState* state(int) const { return st; }
     __device__ __forceinline__ float* out(int) const { return result; }
+    __device__ __forceinline__ void done(int) const {}
     template <class F>
     __device__ __forceinline__ void visit(int, int64_t lb, int64_t nb, F&& f) const {
         visit_dense(x, n, lb, nb, f);
@@ -248,6 +249,10 @@ __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
                 if (out) *out = nans ? __uint_as_float(0x7FC00000u) : __uint_as_float(st->prefix);
             }
         }
+    }
+    if (pass == 2) {   // the task's k-th largest key is known: the source's follow-up
+        __syncthreads();
+        src.done(t);
     }
 }
 

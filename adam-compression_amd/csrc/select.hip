@@ -169,6 +169,7 @@ struct SelWS {
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
+    uint32_t* fin_ticket;      // k_emit_queue's last-workgroup ticket (zeroed by k_sel_init)
     int64_t nseg, ngrp;
 };
 
@@ -319,6 +320,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.cand_idx = c.take<int64_t>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
     w.nthg = c.take<NthG>(L.T);
+    w.fin_ticket = c.take<uint32_t>(16);
     if (bytes) *bytes = c.bytes();
     return w;
 }
@@ -667,62 +669,12 @@ __global__ void k_no_lists(SelWS w) {
     for (int t = threadIdx.x; t < w.T; t += blockDim.x) w.st[t].t_list = __builtin_huge_valf();
 }
 
-// ------------------------------------------------------------------ K3 thresholds
-// Sample keys of the tensors (or |vec| itself for a direct tensor, N == S).
-struct SampleKeys {
-    SelWS w;
-    const float* vec_flat;
-    __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_SAMP], w.T, b); }
-    __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_SAMP][t]; }
-    __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_SAMP][t + 1] - w.bt[BT_SAMP][t]; }
-    __device__ __forceinline__ bool active(int) const { return true; }
-    __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
-    __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
-    template <class F>
-    __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
-        const TDesc d = w.td[t];   // by value: stores below cannot alias it
-        const uint32_t wn = w.rs[t].win_n;
-        if (wn) {
-            visit_dense(w.samples + d.win_off, wn, lb, nb, f);
-            return;
-        }
-        const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
-        visit_dense(x, w.scnt[t], lb, nb, f);
-    }
-};
-
-// Resets the radix state of every multi-block threshold task with its k (top_k_samples)
-// and picks its keys. K1 appended every sample with key >= key(t_list) to the tensor's
-// window list; when that list is complete (count <= win_cap) and holds >= ks keys,
-// the ks-th largest sample is the ks-th largest of the list — every key above it is
-// in the list, NaN and inf keys included — so the three passes read the list (~3 ks
-// keys in the steady state) instead of the S samples. The result is the same either
-// way. An unpadded tail's samples are written outside K1: no list then.
-__global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
-    const int t = blockIdx.x;
-    if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    RSState* rs = w.rs + t;
-    rs_reset(rs, (uint64_t)d.ks);
-    if (threadIdx.x == 0 && d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
-        const SelState* st = w.st + t;
-        const uint32_t cnt = st->win_cnt[st->epoch & 1];
-        if (cnt >= (uint64_t)d.ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
-    }
-}
-
-// One workgroup per small tensor: all three passes from LDS.
-__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat) {
-    const int t = w.small[blockIdx.x];
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
-    rs_small_wg(x, w.scnt[t], (uint64_t)d.ks, w.thr + t);
-}
-
 // ------------------------------------------------------------------ state
-// One workgroup per tensor: reset the tensor's state for this call.
-__global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lists) {
-    const int t = blockIdx.x;
+// Reset tensor t's selection state for this call, by the whole calling workgroup (any
+// size): the workgroup that just produced its sampled threshold (k_rs_small_multi, or
+// the last workgroup of the final k_rs_hist pass — no launch of its own), or
+// k_sel_init for a pure selection (dgc_select, the threshold given).
+__device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     SelState* st = w.st + t;
     if (threadIdx.x == 0) {   // K5's multi-workgroup barrier and consensus start from zero
@@ -731,7 +683,9 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lis
         w.nthg[t].arrive = 0;
         w.nthg[t].decide = 0;
         w.nthg[t].status = 0;
+        if (t == 0) *w.fin_ticket = 0;
     }
+    __syncthreads();   // the caller's threshold (thr[t]) is written
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
         w.grp_gt[d.grp0 + i] = 0;
@@ -773,15 +727,190 @@ __global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lis
     }
 }
 
+// Chunked exclusive scan of a[0..m) into out[] by one workgroup; returns the total.
+// a[] holds totals accumulated by device atomics: read with agent-scope loads, in
+// chunks of kScanReg kept in registers so a chunk's loads are in flight together (a
+// loop of dependent loads pays an L2 round trip each); a thread's run of <= kScanReg
+// entries is loaded once.
+constexpr int kScanReg = 8;
+__device__ uint64_t block_scan_array(const unsigned long long* a, long long* out, int64_t m, uint64_t* lds16) {
+    const int64_t per = ceil_div(m, (int64_t)blockDim.x);
+    const int64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
+    uint64_t v[kScanReg];
+    uint64_t local = 0;
+    for (int64_t i0 = b; i0 < e; i0 += kScanReg) {
+#pragma unroll
+        for (int u = 0; u < kScanReg; ++u) v[u] = i0 + u < e ? load_count(&a[i0 + u]) : 0;
+#pragma unroll
+        for (int u = 0; u < kScanReg; ++u) local += v[u];
+    }
+    uint64_t total;
+    uint64_t run = block_exclusive_scan(local, lds16, &total);
+    for (int64_t i0 = b; i0 < e; i0 += kScanReg) {
+        if (per > kScanReg) {
+#pragma unroll
+            for (int u = 0; u < kScanReg; ++u) v[u] = i0 + u < e ? load_count(&a[i0 + u]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScanReg; ++u)
+            if (i0 + u < e) {
+                out[i0 + u] = (long long)run;
+                run += v[u];
+            }
+    }
+    return total;
+}
+
+// One step of the reference's adaptation loop (dgc/compression.py:128-149) on the
+// count of the pass that just ran, for tensor t, by the whole calling workgroup (any
+// size): the workgroup of the count pass that arrived last for the tensor (no launch
+// of its own). With resample (the default) the loop can only lower the threshold until
+// the count reaches lower*k, so the first "lower" step hands over to ONE
+// multi-threshold pass (k_lower_counts) instead of recounting one threshold per pass;
+// without resample the threshold may also rise, and each step is a recount (count
+// pass + decide), like the reference. The group totals are other workgroups' device
+// atomics of this launch: read with agent-scope loads (last_block_arrival).
+__device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t) {
+    SelState* st = w.st + t;
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    __shared__ uint64_t lds16[16];
+    __shared__ int finished;
+    uint64_t local = 0;
+    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) local += load_count(&w.grp_cnt[d.grp0 + i]);
+    uint64_t n;
+    block_exclusive_scan(local, lds16, &n);
+    if (threadIdx.x == 0) {
+        if (st->t_cur < st->t_list) {   // a full select pass just re-listed at t_cur
+            st->t_list = st->t_cur;
+            st->full_passes += 1;
+        }
+        const long long cnt = (long long)n, k = d.k;
+        const bool adapt = d.n > d.S;
+        st->n_cur = cnt;
+        int done = 1;
+        if (!adapt) {
+            st->branch = DGC_BRANCH_DIRECT;
+            st->limit = cnt < k ? cnt : k;
+        } else if (st->iter >= p.max_iters) {
+            st->branch = DGC_BRANCH_EXHAUSTED;
+            st->limit = cnt < k ? cnt : k;
+        } else if (cnt > k) {
+            if (cnt > d.upper_count) {
+                if (p.resample) {
+                    st->branch = DGC_BRANCH_RESAMPLE;
+                    // torch's CPU topk: nth_element while k * 64 > candidates (K5), else
+                    // partial_sort (K5b) — both replayed exactly
+                    st->rs_nth = (cnt < 64 * k && cnt <= d.cand_cap) ? 1 : 2;
+                    st->tie_rule = DGC_TIES_EXACT;
+                } else {
+                    st->t_cur = __fmul_rn(st->t_cur, p.upper);
+                    done = 0;
+                }
+            } else {
+                st->branch = DGC_BRANCH_TRUNC;
+                st->limit = k;
+            }
+        } else if (cnt < d.lower_count) {
+            if (p.resample && st->iter == 0 && p.max_iters <= kMaxLower) {
+                st->lower_pending = 1;   // k_lower_counts finds the final threshold in one pass
+                done = 2;
+            } else {
+                st->t_cur = __fmul_rn(st->t_cur, p.lower);
+                done = 0;
+            }
+        } else {
+            st->branch = DGC_BRANCH_OK;
+            st->limit = cnt;
+        }
+        if (done == 0) {
+            st->iter += 1;
+            st->recounts += 1;
+            st->overflow = 0;
+        } else if (done == 1) {
+            st->active = 0;
+            st->done = 1;
+        } else {
+            st->active = 0;
+        }
+        finished = done;
+    }
+    __syncthreads();
+    if (finished == 1) block_scan_array(w.grp_cnt + d.grp0, w.grp_off + d.grp0, d.ngrp, lds16);
+    __syncthreads();
+    if (finished != 1)
+        for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) w.grp_cnt[d.grp0 + i] = 0;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_sel_init(SelWS w, int keep_lists) {
+    sel_init_tensor(w, blockIdx.x, keep_lists);
+}
+
+// ------------------------------------------------------------------ K3 thresholds
+// Sample keys of the tensors (or |vec| itself for a direct tensor, N == S).
+struct SampleKeys {
+    SelWS w;
+    const float* vec_flat;
+    __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_SAMP], w.T, b); }
+    __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_SAMP][t]; }
+    __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_SAMP][t + 1] - w.bt[BT_SAMP][t]; }
+    __device__ __forceinline__ bool active(int) const { return true; }
+    __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
+    __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
+    // the final pass's last workgroup: the threshold is known, reset the selection state
+    __device__ __forceinline__ void done(int t) const { sel_init_tensor(w, t, 1); }
+    template <class F>
+    __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
+        const TDesc d = w.td[t];   // by value: stores below cannot alias it
+        const uint32_t wn = w.rs[t].win_n;
+        if (wn) {
+            visit_dense(w.samples + d.win_off, wn, lb, nb, f);
+            return;
+        }
+        const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
+        visit_dense(x, w.scnt[t], lb, nb, f);
+    }
+};
+
+// Resets the radix state of every multi-block threshold task with its k (top_k_samples)
+// and picks its keys. K1 appended every sample with key >= key(t_list) to the tensor's
+// window list; when that list is complete (count <= win_cap) and holds >= ks keys,
+// the ks-th largest sample is the ks-th largest of the list — every key above it is
+// in the list, NaN and inf keys included — so the three passes read the list (~3 ks
+// keys in the steady state) instead of the S samples. The result is the same either
+// way. An unpadded tail's samples are written outside K1: no list then.
+__global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
+    const int t = blockIdx.x;
+    if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    RSState* rs = w.rs + t;
+    rs_reset(rs, (uint64_t)d.ks);
+    if (threadIdx.x == 0 && d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
+        const SelState* st = w.st + t;
+        const uint32_t cnt = st->win_cnt[st->epoch & 1];
+        if (cnt >= (uint64_t)d.ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
+    }
+}
+
+// One workgroup per small tensor: all three passes from LDS, then the tensor's
+// selection state reset (sel_init_tensor).
+__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat) {
+    const int t = w.small[blockIdx.x];
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
+    rs_small_wg(x, w.scnt[t], (uint64_t)d.ks, w.thr + t);
+    sel_init_tensor(w, t, 1);
+}
+
 // ------------------------------------------------------------------ count passes
 // t_cur >= t_list: counts from the lists, kCountSegs segments per thread (one group
 // per workgroup): the list counts of a thread's segments, then their first 8 entries
 // (most lists are shorter), are all in flight before any is used — one thread per
 // segment paid two dependent round trips per segment in ~13 waves of workgroups at 7B.
-// Spilled segments are re-read by the block's waves. One atomic per block into its group.
+// Spilled segments are re-read by the block's waves. One atomic per block into its group;
+// the tensor's last workgroup then takes the adaptation step (decide_tensor).
 static_assert(kBlock * kCountSegs == kGroupSegs, "k_count_lists: one group per workgroup");
 __global__ void __launch_bounds__(kBlock)
-k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
+k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     const int t = task(w, BT_CNT, blockIdx.x);
     const SelState* st = w.st + t;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
@@ -857,15 +986,19 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w) {
     }
     __syncthreads();
     if (threadIdx.x == 0 && bsum) atomicAdd(&w.grp_cnt[d.grp0 + lseg0 / kGroupSegs], (unsigned long long)bsum);
+    // the tensor's last workgroup takes the adaptation step (no k_decide launch)
+    if (last_block_arrival(&w.st[t].tickets[3], (uint32_t)(w.bt[BT_CNT][t + 1] - w.bt[BT_CNT][t])))
+        decide_tensor(w, p, t);
 }
 
 // t_cur < t_list: full select pass at t_cur — one wave per kSuper segments (16
 // float4 loads in flight per lane), re-lists every segment; seg_lcnt = seg_cnt.
 // `which` = BT_FULL (one-shot) or BT_CAP16 (grid-stride within the tensor, for a
-// launch that is most likely a gated no-op).
+// launch that is most likely a gated no-op). The tensor's last workgroup then takes the
+// adaptation step (decide_tensor).
 template <bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
-k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
+k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) {
     const int t = task(w, which, blockIdx.x);
     const SelState* st = w.st + t;
     if (!st->active || st->t_cur >= st->t_list) return;
@@ -925,120 +1058,8 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which) {
         }
         __syncthreads();
     }
-}
-
-// Chunked exclusive scan of a[0..m) into out[] by one workgroup; returns the total.
-// a[] holds totals accumulated by device atomics: read with agent-scope loads, in
-// chunks of kScanReg kept in registers so a chunk's loads are in flight together (a
-// loop of dependent loads pays an L2 round trip each); a thread's run of <= kScanReg
-// entries is loaded once.
-constexpr int kScanReg = 8;
-__device__ uint64_t block_scan_array(const unsigned long long* a, long long* out, int64_t m, uint64_t* lds16) {
-    const int64_t per = ceil_div(m, (int64_t)blockDim.x);
-    const int64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
-    uint64_t v[kScanReg];
-    uint64_t local = 0;
-    for (int64_t i0 = b; i0 < e; i0 += kScanReg) {
-#pragma unroll
-        for (int u = 0; u < kScanReg; ++u) v[u] = i0 + u < e ? load_count(&a[i0 + u]) : 0;
-#pragma unroll
-        for (int u = 0; u < kScanReg; ++u) local += v[u];
-    }
-    uint64_t total;
-    uint64_t run = block_exclusive_scan(local, lds16, &total);
-    for (int64_t i0 = b; i0 < e; i0 += kScanReg) {
-        if (per > kScanReg) {
-#pragma unroll
-            for (int u = 0; u < kScanReg; ++u) v[u] = i0 + u < e ? load_count(&a[i0 + u]) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kScanReg; ++u)
-            if (i0 + u < e) {
-                out[i0 + u] = (long long)run;
-                run += v[u];
-            }
-    }
-    return total;
-}
-
-// One step of the reference's adaptation loop (dgc/compression.py:128-149) on the
-// count of the pass that just ran, one workgroup per tensor. With resample (the
-// default) the loop can only lower the threshold until the count reaches lower*k,
-// so the first "lower" step hands over to ONE multi-threshold pass (k_lower_counts)
-// instead of recounting one threshold per pass; without resample the threshold may
-// also rise, and each step is a recount (count pass + decide), like the reference.
-__global__ void __launch_bounds__(kScanThreads) k_decide(SelWS w, SelCfg p) {
-    const int t = blockIdx.x;
-    SelState* st = w.st + t;
-    if (!st->active) return;
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    __shared__ uint64_t lds16[16];
-    __shared__ int finished;
-    uint64_t local = 0;
-#pragma unroll 4
-    for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) local += w.grp_cnt[d.grp0 + i];
-    uint64_t n;
-    block_exclusive_scan(local, lds16, &n);
-    if (threadIdx.x == 0) {
-        if (st->t_cur < st->t_list) {   // a full select pass just re-listed at t_cur
-            st->t_list = st->t_cur;
-            st->full_passes += 1;
-        }
-        const long long cnt = (long long)n, k = d.k;
-        const bool adapt = d.n > d.S;
-        st->n_cur = cnt;
-        int done = 1;
-        if (!adapt) {
-            st->branch = DGC_BRANCH_DIRECT;
-            st->limit = cnt < k ? cnt : k;
-        } else if (st->iter >= p.max_iters) {
-            st->branch = DGC_BRANCH_EXHAUSTED;
-            st->limit = cnt < k ? cnt : k;
-        } else if (cnt > k) {
-            if (cnt > d.upper_count) {
-                if (p.resample) {
-                    st->branch = DGC_BRANCH_RESAMPLE;
-                    // torch's CPU topk: nth_element while k * 64 > candidates (K5), else
-                    // partial_sort (K5b) — both replayed exactly
-                    st->rs_nth = (cnt < 64 * k && cnt <= d.cand_cap) ? 1 : 2;
-                    st->tie_rule = DGC_TIES_EXACT;
-                } else {
-                    st->t_cur = __fmul_rn(st->t_cur, p.upper);
-                    done = 0;
-                }
-            } else {
-                st->branch = DGC_BRANCH_TRUNC;
-                st->limit = k;
-            }
-        } else if (cnt < d.lower_count) {
-            if (p.resample && st->iter == 0 && p.max_iters <= kMaxLower) {
-                st->lower_pending = 1;   // k_lower_counts finds the final threshold in one pass
-                done = 2;
-            } else {
-                st->t_cur = __fmul_rn(st->t_cur, p.lower);
-                done = 0;
-            }
-        } else {
-            st->branch = DGC_BRANCH_OK;
-            st->limit = cnt;
-        }
-        if (done == 0) {
-            st->iter += 1;
-            st->recounts += 1;
-            st->overflow = 0;
-        } else if (done == 1) {
-            st->active = 0;
-            st->done = 1;
-        } else {
-            st->active = 0;
-        }
-        finished = done;
-    }
-    __syncthreads();
-    if (finished == 1) block_scan_array(w.grp_cnt + d.grp0, w.grp_off + d.grp0, d.ngrp, lds16);
-    __syncthreads();
-    if (finished != 1)
-        for (int64_t i = threadIdx.x; i < d.ngrp; i += kScanThreads) w.grp_cnt[d.grp0 + i] = 0;
+    // the tensor's last workgroup takes the adaptation step (no k_decide launch)
+    if (last_block_arrival(&w.st[t].tickets[3], (uint32_t)nb)) decide_tensor(w, p, t);
 }
 
 // Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
@@ -1211,139 +1232,6 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         } else {
             for (int j = 1; j <= ms; ++j) st->lower_cnt[j] = 0;   // k_lower_counts recounts every t_j
         }
-    }
-}
-
-// ------------------------------------------------------------------ resample (partial_sort path)
-// Candidate keys (|x| >= t_cur) for the resample radix select: the segment list
-// when complete, a re-read of vec when it spilled. One wave per segment.
-struct CandKeys {
-    SelWS w;
-    const float* vec_flat;
-    __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_CAP4], w.T, b); }
-    __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_CAP4][t]; }
-    __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_CAP4][t + 1] - w.bt[BT_CAP4][t]; }
-    __device__ __forceinline__ bool active(int t) const { return w.st[t].resample_pending != 0; }
-    __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
-    __device__ __forceinline__ float* out(int t) const { return &w.st[t].tk; }
-    template <class F>
-    __device__ __forceinline__ void visit(int t, int64_t lb, int64_t nb, F&& f) const {
-        const TDesc d = w.td[t];   // by value: stores below cannot alias it
-        const float* vec = vec_flat + d.off;
-        const int lane = threadIdx.x & 63;
-        const int64_t gw = (lb * blockDim.x + threadIdx.x) >> 6;
-        const int64_t nw = (nb * blockDim.x) >> 6;
-        const float tc = w.st[t].t_cur;
-        for (int64_t ls = gw; ls < d.nseg; ls += nw) {
-            const int64_t seg = d.seg0 + ls;
-            const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
-            if (lc <= (uint32_t)kCap) {
-                if (lane < lc) {
-                    const float a = fabsf(w.lst_val[lcol(seg) + lane * kLstTile]);
-                    if (a >= tc) f(abs_key(a));
-                }
-            } else {
-                float x[kSegTiles][4];
-                uint32_t valid[kSegTiles];
-                load_segment(vec, d.n, ls, x, valid);
-#pragma unroll
-                for (int u = 0; u < kSegTiles; ++u) {
-                    const uint32_t pm = ge_mask(x[u], valid[u], tc);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (pm & (1u << j)) f(abs_key(x[u][j]));
-                }
-            }
-        }
-    }
-};
-
-// Per-segment counts of |x| > tk and |x| == tk (both imply |x| >= t_cur), one
-// thread per segment, spilled segments re-read by waves; the tensor's last
-// workgroup scans its group totals and sets the tie quota k - #greater.
-__global__ void __launch_bounds__(kBlock)
-k_count_gt_eq(const float* __restrict__ vec_flat, SelWS w) {
-    const int t = task(w, BT_SEG, blockIdx.x);
-    SelState* st = w.st + t;
-    if (!st->resample_pending) return;
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    const float* vec = vec_flat + d.off;
-    const float tk = st->tk;
-    __shared__ int spill[kBlock];
-    __shared__ int nspill;
-    __shared__ uint32_t bgt, beq;
-    if (threadIdx.x == 0) {
-        nspill = 0;
-        bgt = beq = 0;
-    }
-    __syncthreads();
-    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_SEG][t]) * kBlock;
-    const int64_t ls = lseg0 + threadIdx.x;
-    uint32_t gt = 0, eq = 0;
-    if (ls < d.nseg) {
-        const int64_t seg = d.seg0 + ls;
-        const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
-        if (lc <= (uint32_t)kCap) {
-            for (uint32_t e = 0; e < lc; ++e) {
-                const float a = fabsf(w.lst_val[lcol(seg) + e * kLstTile]);
-                gt += a > tk;
-                eq += a == tk;
-            }
-            w.seg_gt[seg] = gt;
-            w.seg_eq[seg] = eq;
-        } else {
-            spill[atomicAdd(&nspill, 1)] = threadIdx.x;
-        }
-    }
-    gt = wave_sum(gt);
-    eq = wave_sum(eq);
-    if ((threadIdx.x & 63) == 0) {
-        if (gt) atomicAdd(&bgt, gt);
-        if (eq) atomicAdd(&beq, eq);
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int q = wave; q < nspill; q += kSegPerBlock4) {
-        const int64_t ls2 = lseg0 + spill[q];
-        uint32_t g2 = 0, e2 = 0;
-        float x[kSegTiles][4];
-        uint32_t valid[kSegTiles];
-        load_segment(vec, d.n, ls2, x, valid);
-#pragma unroll
-        for (int u = 0; u < kSegTiles; ++u) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float a = fabsf(x[u][j]);
-                const bool ok = (valid[u] >> j) & 1u;
-                g2 += ok && a > tk;
-                e2 += ok && a == tk;
-            }
-        }
-        g2 = wave_sum(g2);
-        e2 = wave_sum(e2);
-        if (lane == 0) {
-            w.seg_gt[d.seg0 + ls2] = g2;
-            w.seg_eq[d.seg0 + ls2] = e2;
-            if (g2) atomicAdd(&bgt, g2);
-            if (e2) atomicAdd(&beq, e2);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int64_t g = d.grp0 + lseg0 / kGroupSegs;
-        if (bgt) atomicAdd(&w.grp_gt[g], (unsigned long long)bgt);
-        if (beq) atomicAdd(&w.grp_eq[g], (unsigned long long)beq);
-    }
-    const uint32_t nb = (uint32_t)(w.bt[BT_SEG][t + 1] - w.bt[BT_SEG][t]);
-    if (!last_block_arrival(&st->tickets[1], nb)) return;
-    __shared__ uint64_t lds16[16];
-    const uint64_t G = block_scan_array(w.grp_gt + d.grp0, w.grp_gt_off + d.grp0, d.ngrp, lds16);
-    __syncthreads();
-    block_scan_array(w.grp_eq + d.grp0, w.grp_eq_off + d.grp0, d.ngrp, lds16);
-    if (threadIdx.x == 0) {
-        st->n_greater = (long long)G;
-        st->tie_quota = d.k - (long long)G;
-        st->limit = d.k;
     }
 }
 
@@ -1768,24 +1656,101 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     }
 }
 
-// K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
-// wire casts and the masking of DGCSGDMemory.update.
-__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
-    const int t = task(w, BT_QUEUE, blockIdx.x);
-    const SelState* st = w.st + t;
-    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1)) return;
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    __shared__ long long obase_s;
-    if (threadIdx.x < kWave) {
-        const long long b = out_base(w, t);
-        if (threadIdx.x == 0) obase_s = b;
+// Result records; the payload's total count; and every tensor's next speculative
+// list threshold, margin x t_cur x growth. One workgroup (any size): k_sel_finish, or
+// the last workgroup of k_emit_queue.
+struct FinishArgs {
+    int64_t* count_out;
+    dgc_select_info* info;
+    float margin;
+    int32_t defer, mask_mmt;
+    int32_t on;   // k_emit_queue: its last workgroup runs the finish (no k_sel_finish launch)
+};
+
+__device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
+    int64_t* count_out = f.count_out;
+    dgc_select_info* info = f.info;
+    const float margin = f.margin;
+    const int defer = f.defer, mask_mmt = f.mask_mmt;
+    __shared__ unsigned long long total;
+    if (threadIdx.x == 0) total = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < w.T; t += blockDim.x) {
+        SelState* st = w.st + t;
+        st->epoch += 1;
+        const long long cnt = final_count(*st, w.td[t].k);
+        // what the next K1 must zero (first-k branches of a deferring engine only)
+        st->def_mode = (defer && st->branch != DGC_BRANCH_RESAMPLE && !w.td[t].tail && cnt > 0) ? 1 : 0;
+        st->def_t = st->t_cur;
+        st->def_limit = st->limit;
+        st->def_mask_mmt = mask_mmt;
+        atomicAdd(&total, (unsigned long long)cnt);
+        if (info) {
+            dgc_select_info& r = info[t];
+            r.count = cnt;
+            r.candidates = st->n_cur;
+            r.threshold0 = st->t0;
+            r.threshold = st->t_cur;
+            r.branch = st->branch;
+            r.recounts = st->recounts;
+            r.overflow_segments = st->full_passes ? st->overflow : st->list_spills;
+            r.full_passes = st->full_passes;
+            r.tie_rule = st->tie_rule;
+            r.window_keys = st->win_keys;
+            r.k5_status = (int32_t)w.nthg[t].status;
+            r.reserved = 0;
+        }
+        if (w.spec) {
+            // spec[0]: next call's list threshold = m * t * growth, growth = 2 - spec[1] / t
+            // (linear extrapolation from the previous final threshold spec[1]) clamped to
+            // [1, 1.5]; spec[1] := t. The ratio t / spec[1] overshoots while the growth
+            // decelerates — the accumulating velocity's threshold grows ~linearly, and on the
+            // bench the ratio extrapolation missed at step 5 (a full pass). The margin m adapts:
+            // after a call whose threshold landed at or above its list threshold (a hit),
+            // m = 1.05 x that call's list/final ratio, within [margin, kSpecMarginMax] — the
+            // lists shrink towards the selection while the threshold moves predictably (at
+            // 1B on the bench's dynamics 4 % of the elements at 0.8 vs 0.7 % at 0.95); a
+            // miss (the threshold fell below it: a full select pass ran) resets m to margin.
+            float* spec = w.spec + 2 * t;
+            const float tc = st->t_cur;
+            const float used = spec[0];
+            const float gr = fminf(fmaxf(2.f - spec[1] / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
+            float m = margin;
+            if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
+                m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
+            spec[0] = (tc == tc && tc > 0.f && tc < __builtin_huge_valf()) ? tc * m * gr : __builtin_huge_valf();
+            spec[1] = tc;
+        }
     }
     __syncthreads();
-    const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
-    if (q >= d.k) return;
-    const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
-    const int64_t li = w.cand_idx[d.cand_off + j];
-    emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
+    if (threadIdx.x == 0 && count_out) *count_out = (int64_t)total;
+}
+
+__global__ void k_sel_finish(SelWS w, FinishArgs f) { sel_finish_body(w, f); }
+
+// K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
+// wire casts and the masking of DGCSGDMemory.update.
+// The launch's last workgroup (f.on) then runs the finish of the whole call.
+__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_flat, SelWS w, EmitOut o,
+                                                       FinishArgs f) {
+    const int t = task(w, BT_QUEUE, blockIdx.x);
+    const SelState* st = w.st + t;
+    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1) {   // uniform per workgroup
+        const TDesc d = w.td[t];   // by value: stores below cannot alias it
+        __shared__ long long obase_s;
+        if (threadIdx.x < kWave) {
+            const long long b = out_base(w, t);
+            if (threadIdx.x == 0) obase_s = b;
+        }
+        __syncthreads();
+        const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
+        if (q < d.k) {
+            const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
+            const int64_t li = w.cand_idx[d.cand_off + j];
+            emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
+        }
+    }
+    if (f.on && last_block_arrival(w.fin_ticket, gridDim.x)) sel_finish_body(w, f);
 }
 
 // K5b: torch's CPU topk on its partial_sort path (k * 64 <= candidates, i.e. a sampled
@@ -2150,64 +2115,6 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
                    from_global ? w.nthg + t : nullptr);
 }
 
-// Result records; the payload's total count; and every tensor's next speculative
-// list threshold, margin x t_cur x growth. One workgroup.
-__global__ void k_sel_finish(SelWS w, int64_t* count_out, dgc_select_info* info, float margin, int defer,
-                             int mask_mmt) {
-    __shared__ unsigned long long total;
-    if (threadIdx.x == 0) total = 0;
-    __syncthreads();
-    for (int t = threadIdx.x; t < w.T; t += blockDim.x) {
-        SelState* st = w.st + t;
-        st->epoch += 1;
-        const long long cnt = final_count(*st, w.td[t].k);
-        // what the next K1 must zero (first-k branches of a deferring engine only)
-        st->def_mode = (defer && st->branch != DGC_BRANCH_RESAMPLE && !w.td[t].tail && cnt > 0) ? 1 : 0;
-        st->def_t = st->t_cur;
-        st->def_limit = st->limit;
-        st->def_mask_mmt = mask_mmt;
-        atomicAdd(&total, (unsigned long long)cnt);
-        if (info) {
-            dgc_select_info& r = info[t];
-            r.count = cnt;
-            r.candidates = st->n_cur;
-            r.threshold0 = st->t0;
-            r.threshold = st->t_cur;
-            r.branch = st->branch;
-            r.recounts = st->recounts;
-            r.overflow_segments = st->full_passes ? st->overflow : st->list_spills;
-            r.full_passes = st->full_passes;
-            r.tie_rule = st->tie_rule;
-            r.window_keys = st->win_keys;
-            r.k5_status = (int32_t)w.nthg[t].status;
-            r.reserved = 0;
-        }
-        if (w.spec) {
-            // spec[0]: next call's list threshold = m * t * growth, growth = 2 - spec[1] / t
-            // (linear extrapolation from the previous final threshold spec[1]) clamped to
-            // [1, 1.5]; spec[1] := t. The ratio t / spec[1] overshoots while the growth
-            // decelerates — the accumulating velocity's threshold grows ~linearly, and on the
-            // bench the ratio extrapolation missed at step 5 (a full pass). The margin m adapts:
-            // after a call whose threshold landed at or above its list threshold (a hit),
-            // m = 1.05 x that call's list/final ratio, within [margin, kSpecMarginMax] — the
-            // lists shrink towards the selection while the threshold moves predictably (at
-            // 1B on the bench's dynamics 4 % of the elements at 0.8 vs 0.7 % at 0.95); a
-            // miss (the threshold fell below it: a full select pass ran) resets m to margin.
-            float* spec = w.spec + 2 * t;
-            const float tc = st->t_cur;
-            const float used = spec[0];
-            const float gr = fminf(fmaxf(2.f - spec[1] / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
-            float m = margin;
-            if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
-                m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
-            spec[0] = (tc == tc && tc > 0.f && tc < __builtin_huge_valf()) ? tc * m * gr : __builtin_huge_valf();
-            spec[1] = tc;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && count_out) *count_out = (int64_t)total;
-}
-
 __global__ void k_spec_reset(float* spec, int32_t T) {
     for (int i = threadIdx.x; i < 2 * T; i += blockDim.x) spec[i] = __builtin_huge_valf();
 }
@@ -2285,29 +2192,32 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
                        int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists, int sync_mode,
                        float margin, hipStream_t s) {
-    hipLaunchKernelGGL(k_sel_init, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, w, keep_lists);
-    DGC_LAUNCHED();
+    // keep_lists: a compress call, whose K3 kernels already reset every tensor's state
+    // (sel_init_tensor) when they produced its threshold; a pure selection resets here
+    if (!keep_lists) {
+        hipLaunchKernelGGL(k_sel_init, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, w, 0);
+        DGC_LAUNCHED();
+    }
     const bool al = aligned16(vec);
     // resample=True with max_iters <= kMaxLower: one multi-threshold pass replaces the lowers
     const bool lower_fast = p.resample && p.max_iters <= kMaxLower;
     auto pass = [&](int need, bool likely_lists) -> int {
         // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
         // (both gated per tensor on the device); need: 1 = lists, 2 = full, 3 = either
+        // each count kernel's last workgroup per tensor takes the adaptation step
         if (need & 1) {
-            hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w);
+            hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w, p);
             DGC_LAUNCHED();
         }
         if (need & 2) {
             const int which = likely_lists ? BT_CAP16 : BT_FULL;
             const unsigned grid = (unsigned)L.grid[which];
             if (al)
-                hipLaunchKernelGGL(k_select_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, which);
+                hipLaunchKernelGGL(k_select_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, which, p);
             else
-                hipLaunchKernelGGL(k_select_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, which);
+                hipLaunchKernelGGL(k_select_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, which, p);
             DGC_LAUNCHED();
         }
-        hipLaunchKernelGGL(k_decide, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, w, p);
-        DGC_LAUNCHED();
         return DGC_OK;
     };
     auto lower = [&]() -> int {
@@ -2324,6 +2234,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     };
     EmitOut o{p.update_memory ? vec : nullptr, (p.update_memory && p.masking) ? mmt : nullptr, values, indices,
               p.vdtype, p.idtype, nullptr, nullptr, (int32_t)(p.update_memory == 2)};
+    const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0};
+    bool finished = false;   // the payload count and records are written
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
@@ -2346,8 +2258,11 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
         hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0);
         DGC_LAUNCHED();
-        hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
+        FinishArgs f = fin;
+        f.on = 1;   // k_emit_queue's last workgroup finishes the call
+        hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o, f);
         DGC_LAUNCHED();
+        finished = true;
         return DGC_OK;
     };
     DGC_TRY(keep_lists ? pass(3, true) : pass(2, false));
@@ -2397,9 +2312,10 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
     }
     if (!emitted) DGC_TRY(launch_emit(L, vec, w, o, s));
-    hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, count_out, info, margin,
-                       (int)(p.update_memory == 2), (int)(p.masking != 0));
-    DGC_LAUNCHED();
+    if (!finished) {
+        hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(256), 0, s, w, fin);
+        DGC_LAUNCHED();
+    }
     return DGC_OK;
 }
 

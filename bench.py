@@ -326,11 +326,17 @@ class ModelRun:
             if pair:
                 pair[1].record()
         # dense tensors: (fp16 wire cast) -> allreduce Average -> compensate(accumulate=False)
-        self.dense_wire.copy_(gd)
-        if self.world > 1:
-            from dgc import comm
-            comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Average))
-        src = self.dense_wire if self.dense_wire.dtype == torch.float32 else self.dense_wire.float()
+        # (dgc/compression.py:173-177, 195-198). An fp32 wire at W = 1 is the gradient
+        # itself (the reference allreduces p.grad in place; one rank leaves it as is);
+        # otherwise the wire buffer keeps the bench's fixed gradient buffers intact.
+        if self.dense_wire.dtype == torch.float32 and self.world == 1:
+            src = gd
+        else:
+            self.dense_wire.copy_(gd)
+            if self.world > 1:
+                from dgc import comm
+                comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Average))
+            src = self.dense_wire if self.dense_wire.dtype == torch.float32 else self.dense_wire.float()
         self._lib.check(L.dgc_compensate(src.data_ptr(), self.dense_mmt.data_ptr(), None, self.dense_out.data_ptr(),
                                          self.n_dense, 0.9, int(self.nesterov), 0, None, 0, 1, 0,
                                          self._lib.stream_of(g.device)), "dgc_compensate")
