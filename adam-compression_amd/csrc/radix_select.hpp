@@ -37,9 +37,7 @@ struct RSState {
     uint64_t nan_count;
     uint32_t tickets[4];
     uint32_t win_n;                    // > 0: the passes read the K1 sample window list of
-                                       // win_n keys instead of the samples (select.hip)
-    uint32_t skip;                     // 1: one workgroup already selected from the window
-                                       // (k_rs_window); the multi-block passes skip the task
+    uint32_t win_pad;                  // win_n keys instead of the samples (select.hip)
     unsigned long long hist[3][kRsBins];
 };
 
@@ -191,7 +189,6 @@ __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
         st->nan_count = 0;
         for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
         st->win_n = 0;
-        st->skip = 0;
     }
 }
 
@@ -291,70 +288,6 @@ __device__ void rs_small_wg(const float* __restrict__ x, int64_t n, uint64_t k, 
         for (int i = threadIdx.x; i < n; i += kScanThreads) {
             const uint32_t key = keys[i];
             if ((key & pmask) == pre) atomicAdd(&h[(key >> shift) & dmask], 1u);
-        }
-        __syncthreads();
-        int bin;
-        uint64_t above;
-        if (pick_bin(h, rs_bins(pass), k_rem, lds16, &bin, &above)) {
-            sel_bin = bin;
-            sel_above = above;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0 && sel_bin >= 0) {
-            prefix |= (uint32_t)sel_bin << shift;
-            k_rem -= sel_above;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0)
-        *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
-    __syncthreads();
-}
-
-// All three passes of one key set in global memory by ONE 1024-thread workgroup, for
-// key sets of up to a few hundred thousand keys (the K1 sample window list, ~3 ks
-// keys): pass 0 reads every key; pass 1 reads them again and stages the keys under
-// pass 0's prefix in LDS (<= kWinStage of them: the only keys passes 1 and 2 count);
-// pass 2 then runs from LDS, else from global memory again. Three launches of the
-// multi-block passes (and their arrival tickets) cost ~12 us each at 1B; this is one.
-constexpr int kWinStage = 16384;
-__device__ void rs_window_wg(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
-    __shared__ uint32_t h[kRsBins];
-    __shared__ uint32_t stage[kWinStage];
-    __shared__ uint64_t lds16[16];
-    __shared__ uint32_t nan_cnt, prefix, nstage;
-    __shared__ uint64_t k_rem;
-    __shared__ int sel_bin;
-    __shared__ uint64_t sel_above;
-    if (threadIdx.x == 0) {
-        nan_cnt = 0;
-        prefix = 0;
-        nstage = 0;
-        k_rem = k;
-    }
-    for (int pass = 0; pass < 3; ++pass) {
-        for (int b = threadIdx.x; b < kRsBins; b += blockDim.x) h[b] = 0;
-        if (threadIdx.x == 0) sel_bin = -1;
-        __syncthreads();
-        const uint32_t pmask = rs_pmask(pass), dmask = rs_dmask(pass), pre = prefix;
-        const int shift = rs_shift(pass);
-        const uint32_t smask = rs_pmask(1), spre = pre & smask;   // pass 0's prefix (pass 1 stages under it)
-        if (pass == 2 && nstage <= (uint32_t)kWinStage) {
-            for (uint32_t i = threadIdx.x; i < nstage; i += blockDim.x) {
-                const uint32_t key = stage[i];
-                if ((key & pmask) == pre) atomicAdd(&h[(key >> shift) & dmask], 1u);
-            }
-        } else {
-            uint32_t my_nan = 0;
-            visit_dense(x, n, 0, 1, [&](uint32_t key) {
-                if (pass == 0) my_nan += key > 0x7F800000u;
-                if (pass == 1 && (key & smask) == spre) {
-                    const uint32_t i = atomicAdd(&nstage, 1u);
-                    if (i < (uint32_t)kWinStage) stage[i] = key;
-                }
-                if ((key & pmask) == pre) atomicAdd(&h[(key >> shift) & dmask], 1u);
-            });
-            if (my_nan) atomicAdd(&nan_cnt, my_nan);
         }
         __syncthreads();
         int bin;

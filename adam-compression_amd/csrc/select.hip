@@ -853,7 +853,7 @@ struct SampleKeys {
     __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_SAMP], w.T, b); }
     __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_SAMP][t]; }
     __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_SAMP][t + 1] - w.bt[BT_SAMP][t]; }
-    __device__ __forceinline__ bool active(int t) const { return !w.rs[t].skip; }   // k_rs_window did it
+    __device__ __forceinline__ bool active(int) const { return true; }
     __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
     __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
     // the final pass's last workgroup: the threshold is known, reset the selection state
@@ -875,32 +875,20 @@ struct SampleKeys {
 // and picks its keys. K1 appended every sample with key >= key(t_list) to the tensor's
 // window list; when that list is complete (count <= win_cap) and holds >= ks keys,
 // the ks-th largest sample is the ks-th largest of the list — every key above it is
-// in the list, NaN and inf keys included — so the selection reads the list (~3 ks
-// keys in the steady state) instead of the S samples: in THIS workgroup, all three
-// passes (rs_window_wg), then the tensor's selection state reset, and the multi-block
-// passes skip it. Otherwise they run over the samples. The result is the same either
+// in the list, NaN and inf keys included — so the three passes read the list (~3 ks
+// keys in the steady state) instead of the S samples. The result is the same either
 // way. An unpadded tail's samples are written outside K1: no list then.
-__global__ void __launch_bounds__(kScanThreads) k_rs_window(SelWS w) {
+__global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
     const int t = blockIdx.x;
-    if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;   // a small tensor: k_rs_small_multi
+    if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     RSState* rs = w.rs + t;
     rs_reset(rs, (uint64_t)d.ks);
-    __shared__ uint32_t wn;
-    if (threadIdx.x == 0) {
-        wn = 0;
-        if (d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
-            const SelState* st = w.st + t;
-            const uint32_t cnt = st->win_cnt[st->epoch & 1];
-            if (cnt >= (uint64_t)d.ks && cnt <= (uint64_t)d.win_cap) wn = cnt;
-        }
-        rs->win_n = wn;
+    if (threadIdx.x == 0 && d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
+        const SelState* st = w.st + t;
+        const uint32_t cnt = st->win_cnt[st->epoch & 1];
+        if (cnt >= (uint64_t)d.ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
     }
-    __syncthreads();
-    if (!wn) return;
-    rs_window_wg(w.samples + d.win_off, wn, (uint64_t)d.ks, w.thr + t);
-    if (threadIdx.x == 0) rs->skip = 1;
-    sel_init_tensor(w, t, 1);
 }
 
 // One workgroup per small tensor: all three passes from LDS, then the tensor's
@@ -2411,7 +2399,7 @@ static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStre
         DGC_LAUNCHED();
     }
     if (L.grid[BT_SAMP] > 0) {
-        hipLaunchKernelGGL(k_rs_window, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, w);
+        hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w);
         DGC_LAUNCHED();
         DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
     }
