@@ -68,7 +68,16 @@ __device__ K5Prof g_k5prof;
 #define K5_SUB(i, global) \
     do { if ((global) && blockIdx.x == 0 && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
          g_k5prof.sub[i] += t_ - k5_t0; k5_t0 = t_; } } while (0)
+// single-wave tail: sub[4] median, sub[5] loads + pairing, sub[6] swaps + cut
+#define K5_WSUB_BEGIN() unsigned long long k5w_t0 = wall_clock64()
+#define K5_WSUB_RESET() do { k5w_t0 = wall_clock64(); } while (0)
+#define K5_WSUB(i) \
+    do { if (blockIdx.x == 0 && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
+         g_k5prof.sub[i] += t_ - k5w_t0; k5w_t0 = t_; } } while (0)
 #else
+#define K5_WSUB_BEGIN() do { } while (0)
+#define K5_WSUB_RESET() do { } while (0)
+#define K5_WSUB(i) do { } while (0)
 #define K5_SUB_BEGIN() do { } while (0)
 #define K5_SUB(i, global) do { } while (0)
 #define K5_STAMP(i) do { } while (0)
@@ -507,6 +516,7 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
 // The same step by one wave on an LDS range of <= kNthWave entries: no workgroup barrier.
 __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, int64_t f, int64_t l) {
     constexpr int kTiles = kNthWave / 256 + 1;   // the range <= kNthWave, from a base <= a0
+    K5_WSUB_BEGIN();
     const int lane = threadIdx.x & 63;
     const uint32_t P = qkey(q[f]);
     const int64_t a0 = f + 1, base = nth_base(q, a0);
@@ -531,8 +541,10 @@ __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, in
         if (t0 < l) pair_tile<true>(m[u] & 15u, m[u] >> 4, t0, f, TR, runl, runr, lpos, rpos, s, lnext, rmin);
     }
     wave_sync();   // the pair slots are written
+    K5_WSUB(5);
     nth_swaps<2>(q, lpos, rpos, f, s, lane, kWave);
     wave_sync();   // the swaps are done
+    K5_WSUB(6);
     const int64_t rs = s ? f + (int64_t)rmin : l;
     const int64_t ln = lnext == UINT32_MAX ? INT64_MAX : f + (int64_t)lnext;
     return ln < rs ? ln : rs;
@@ -542,6 +554,7 @@ __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, in
 __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth) {
     int64_t f = sh.f, l = sh.l, depth = sh.depth;
     const int lane = threadIdx.x & 63;
+    K5_WSUB_BEGIN();
     while (l - f > 3) {
         if (depth == 0) {
             if (lane == 0) nth_heap_select(q + f, nth + 1 - f, l - f, nth - f);
@@ -550,8 +563,10 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
         }
         depth -= 1;
         K5_STEP(2);
+        K5_WSUB_RESET();
         if (lane == 0) (void)nth_median(q, f, l);
         wave_sync();
+        K5_WSUB(4);
         const int64_t cut = nth_step_wave(q, lpos, rpos, f, l);
         if (cut <= nth)
             f = cut;

@@ -169,7 +169,7 @@ struct SelWS {
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
-    uint32_t* fin_ticket;      // k_emit_queue's last-workgroup ticket (zeroed by k_sel_init)
+    uint32_t* fin_ticket;      // k_nth_select's last-workgroup ticket (zeroed by sel_init_tensor)
     int64_t nseg, ngrp;
 };
 
@@ -1658,13 +1658,13 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
 
 // Result records; the payload's total count; and every tensor's next speculative
 // list threshold, margin x t_cur x growth. One workgroup (any size): k_sel_finish, or
-// the last workgroup of k_emit_queue.
+// the last workgroup of k_nth_select.
 struct FinishArgs {
     int64_t* count_out;
     dgc_select_info* info;
     float margin;
     int32_t defer, mask_mmt;
-    int32_t on;   // k_emit_queue: its last workgroup runs the finish (no k_sel_finish launch)
+    int32_t on;   // k_nth_select: its last workgroup runs the finish (no k_sel_finish launch)
 };
 
 __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
@@ -1730,27 +1730,22 @@ __global__ void k_sel_finish(SelWS w, FinishArgs f) { sel_finish_body(w, f); }
 
 // K5 emit: output slot q <- candidate queue[q] (the topk's order), with values,
 // wire casts and the masking of DGCSGDMemory.update.
-// The launch's last workgroup (f.on) then runs the finish of the whole call.
-__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_flat, SelWS w, EmitOut o,
-                                                       FinishArgs f) {
+__global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const int t = task(w, BT_QUEUE, blockIdx.x);
     const SelState* st = w.st + t;
-    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1) {   // uniform per workgroup
-        const TDesc d = w.td[t];   // by value: stores below cannot alias it
-        __shared__ long long obase_s;
-        if (threadIdx.x < kWave) {
-            const long long b = out_base(w, t);
-            if (threadIdx.x == 0) obase_s = b;
-        }
-        __syncthreads();
-        const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
-        if (q < d.k) {
-            const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
-            const int64_t li = w.cand_idx[d.cand_off + j];
-            emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
-        }
+    if (!(st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1)) return;
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    __shared__ long long obase_s;
+    if (threadIdx.x < kWave) {
+        const long long b = out_base(w, t);
+        if (threadIdx.x == 0) obase_s = b;
     }
-    if (f.on && last_block_arrival(w.fin_ticket, gridDim.x)) sel_finish_body(w, f);
+    __syncthreads();
+    const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
+    if (q >= d.k) return;
+    const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
+    const int64_t li = w.cand_idx[d.cand_off + j];
+    emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
 }
 
 // K5b: torch's CPU topk on its partial_sort path (k * 64 <= candidates, i.e. a sampled
@@ -2095,24 +2090,26 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G,
                      G_expected);
 }
 
+// The last of the T workgroups to finish (f.on) then runs the finish of the whole call
+// (T arrivals on one ticket; nothing it writes is read by k_emit_queue).
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
-                                                            EmitOut o, int from_global) {
+                                                            EmitOut o, int from_global, FinishArgs f) {
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
-    if (st->branch != DGC_BRANCH_RESAMPLE || !st->rs_nth) return;
     __shared__ __align__(16) uint64_t smem[kK5SmemBytes / 8];
-    if (st->rs_nth == 2) {
+    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) {   // uniform per workgroup
         heap_select_wg(vec_flat, w, o, t, smem);
-        return;
+    } else if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1) {
+        const TDesc d = w.td[t];   // by value: stores below cannot alias it
+        uint32_t* gl = w.gpos + d.gpos_off;
+        uint32_t* gr = gl + d.cand_cap / 2 + 1;
+        uint32_t* llp = reinterpret_cast<uint32_t*>(smem + kNthLds);
+        uint32_t* lrp = llp + kNthPairLds;
+        uint8_t* lmk = reinterpret_cast<uint8_t*>(lrp + kNthPairLds);
+        nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, smem, llp, lrp, lmk,
+                       from_global ? w.nthg + t : nullptr);
     }
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    uint32_t* gl = w.gpos + d.gpos_off;
-    uint32_t* gr = gl + d.cand_cap / 2 + 1;
-    uint32_t* llp = reinterpret_cast<uint32_t*>(smem + kNthLds);
-    uint32_t* lrp = llp + kNthPairLds;
-    uint8_t* lmk = reinterpret_cast<uint8_t*>(lrp + kNthPairLds);
-    nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, smem, llp, lrp, lmk,
-                   from_global ? w.nthg + t : nullptr);
+    if (f.on && last_block_arrival(w.fin_ticket, gridDim.x)) sel_finish_body(w, f);
 }
 
 __global__ void k_spec_reset(float* spec, int32_t T) {
@@ -2256,13 +2253,13 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
                                abort ? G + 1 : G);
             DGC_LAUNCHED();
         }
-        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0);
-        DGC_LAUNCHED();
         FinishArgs f = fin;
-        f.on = 1;   // k_emit_queue's last workgroup finishes the call
-        hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o, f);
+        f.on = 1;   // k_nth_select's last workgroup finishes the call
+        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0, f);
         DGC_LAUNCHED();
         finished = true;
+        hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
+        DGC_LAUNCHED();
         return DGC_OK;
     };
     DGC_TRY(keep_lists ? pass(3, true) : pass(2, false));

@@ -46,7 +46,8 @@ def main():
             t = [x * 0.01 for x in p.t]   # us
             ph = dict(global_us=t[1] - t[0], load_us=t[2] - t[1], lds_us=t[3] - t[2], wave_us=t[4] - t[3],
                       store_us=t[5] - t[4], total_us=t[5] - t[0], g_pass1_us=p.sub[0] * 0.01,
-                      g_pass2_us=p.sub[1] * 0.01, g_swap_us=p.sub[2] * 0.01, g_prepare_us=p.sub[3] * 0.01)
+                      g_pass2_us=p.sub[1] * 0.01, g_swap_us=p.sub[2] * 0.01, g_prepare_us=p.sub[3] * 0.01,
+                      w_median_us=p.sub[4] * 0.01, w_pair_us=p.sub[5] * 0.01, w_swap_us=p.sub[6] * 0.01)
             best = ph if best is None else {key: min(v, ph[key]) for key, v in best.items()}
         r.update({key: round(v, 1) for key, v in best.items()})
         r.update(steps_global=p.steps[0], steps_lds=p.steps[1], steps_wave=p.steps[2])
