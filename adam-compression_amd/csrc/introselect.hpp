@@ -205,19 +205,55 @@ __device__ __forceinline__ int64_t nth_base(const uint64_t* q, int64_t a0) {
     return a0 - (int64_t)((reinterpret_cast<uintptr_t>(q + a0) >> 3) & 1u);
 }
 
+// Pair slots: the positions (relative to f) of the t-th swapped left stopper L_t and of
+// its partner R_t. Plain arrays (LDS phase, single-wave tail, multi-workgroup phase),
+// or split (the one-workgroup global phase): slots t < cap in LDS, the rest in global
+// memory — a 57k-candidate step swaps ~14k pairs, whose 4-B slot stores and loads
+// were most of its time in global memory.
+struct PlainSlots {
+    uint32_t* l;
+    uint32_t* r;
+    __device__ __forceinline__ void put_l(uint32_t t, uint32_t v) const { l[t] = v; }
+    __device__ __forceinline__ void put_r(uint32_t t, uint32_t v) const { r[t] = v; }
+    __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
+    __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[t]; }
+};
+
+struct SplitSlots {
+    uint32_t* ll;   // LDS, cap each
+    uint32_t* lr;
+    uint32_t cap;
+    uint32_t* gl;   // global, indexed by t
+    uint32_t* gr;
+    __device__ __forceinline__ void put_l(uint32_t t, uint32_t v) const {
+        if (t < cap)
+            ll[t] = v;
+        else
+            gl[t] = v;
+    }
+    __device__ __forceinline__ void put_r(uint32_t t, uint32_t v) const {
+        if (t < cap)
+            lr[t] = v;
+        else
+            gr[t] = v;
+    }
+    __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return t < cap ? ll[t] : gl[t]; }
+    __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return t < cap ? lr[t] : gr[t]; }
+};
+
 // The step's swaps L_t <-> R_t, t < s (disjoint positions), by threads tid of nt:
 // kNthSwapBatch pairs per thread with all their loads in flight before any store
 // (8 for the global-memory phase, 2 in LDS where latency is short and registers count).
-template <int kNthSwapBatch>
-__device__ __forceinline__ void nth_swaps(uint64_t* q, const uint32_t* lpos, const uint32_t* rpos, int64_t f,
-                                          uint32_t s, uint32_t tid, uint32_t nt) {
+template <int kNthSwapBatch, class Slots>
+__device__ __forceinline__ void nth_swaps(uint64_t* q, const Slots& sl, int64_t f, uint32_t s, uint32_t tid,
+                                          uint32_t nt) {
     for (uint32_t t0 = tid; t0 < s; t0 += nt * kNthSwapBatch) {
         uint32_t li[kNthSwapBatch], ri[kNthSwapBatch];
 #pragma unroll
         for (int j = 0; j < kNthSwapBatch; ++j) {
             const uint32_t t = t0 + j * nt;
-            li[j] = t < s ? lpos[t] : 0u;
-            ri[j] = t < s ? rpos[t] : 0u;
+            li[j] = t < s ? sl.get_l(t) : 0u;
+            ri[j] = t < s ? sl.get_r(t) : 0u;
         }
         uint64_t a[kNthSwapBatch], b[kNthSwapBatch];
 #pragma unroll
@@ -275,9 +311,9 @@ __device__ __forceinline__ uint32_t first_in_tile(const uint64_t (&m)[4]) {
 // unswapped left stopper), rmin (smallest swapped right stopper); INT64_MAX = none.
 // BALLOT: accumulated wave-uniformly from ballots (a few tiles: no reduction after);
 // else per lane, for the caller to reduce once after many tiles.
-template <bool BALLOT>
+template <bool BALLOT, class Slots>
 __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile, int64_t f, uint32_t TR,
-                                          uint32_t& runl, uint32_t& runr, uint32_t* lpos, uint32_t* rpos,
+                                          uint32_t& runl, uint32_t& runr, const Slots& sl,
                                           uint32_t& paired, uint32_t& lnext, uint32_t& rmin) {
     // positions relative to f (32-bit: a range is < 2^32 entries); lnext / rmin too,
     // UINT32_MAX = none
@@ -299,7 +335,7 @@ __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile
         if (after >= (int64_t)runl + tl) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                if ((pl >> j) & 1u) lpos[rl++] = rel0 + (uint32_t)j;
+                if ((pl >> j) & 1u) sl.put_l(rl++, rel0 + (uint32_t)j);
             }
             paired += (uint32_t)__popc(pl);
             runl += tl;
@@ -312,7 +348,7 @@ __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile
                 const uint32_t i = rel0 + (uint32_t)j;
                 if ((pr >> j) & 1u) {
                     rr += 1;
-                    rpos[TR - rr] = i;
+                    sl.put_r(TR - rr, i);
                     rmin = i < rmin ? i : rmin;
                 }
                 if (((pl >> j) & 1u) && i < lnext) lnext = i;
@@ -333,8 +369,8 @@ __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile
         // R_{u+1} = i with u = #(key >= P in (i, l)); swapped iff #(key <= P in [f+1, i)) >= u + 1
         const uint32_t u = TR - rr_incl;
         const bool swr = isr && rl >= u + 1;
-        if (swl) lpos[rl] = i;
-        if (swr) rpos[u] = i;
+        if (swl) sl.put_l(rl, i);
+        if (swr) sl.put_r(u, i);
         if (BALLOT) {
             msl[j] = __ballot(swl);
             mln[j] = __ballot(isl && !swl);
@@ -382,9 +418,8 @@ struct NthShared {
 // step's swaps are done and sh.s / l_next / r_min hold its result. Pass 1 keeps each
 // lane's stopper bits of each tile in mk (one byte, LDS) when the step's tiles fit
 // mk_tiles, so pass 2 reads bytes instead of the entries; otherwise it reloads them.
-template <int kNthBatch, int kSwapBatch>
-__device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, uint8_t* mk,
-                            int64_t mk_tiles) {
+template <int kNthBatch, int kSwapBatch, class Slots>
+__device__ void nth_step_wg(uint64_t* q, const Slots& sl, NthShared& sh, uint8_t* mk, int64_t mk_tiles) {
     const int64_t f = sh.f, l = sh.l;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t P = sh.pivot;
@@ -431,7 +466,7 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     if (keep) {
         for (int64_t t0 = wb; t0 < we; t0 += 256) {
             const uint32_t m = mk[((t0 - base) >> 8) * 64 + lane];
-            pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+            pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, sl, paired, lnext, rmin);
         }
     } else {
         for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
@@ -443,7 +478,7 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
             for (int b = 0; b < kNthBatch; ++b) {
                 uint32_t pl, pr;
                 stopper_masks(x[b], valid[b], P, pl, pr);
-                pair_tile<false>(pl, pr, t0 + b * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+                pair_tile<false>(pl, pr, t0 + b * 256, f, TR, runl, runr, sl, paired, lnext, rmin);
             }
         }
     }
@@ -458,7 +493,7 @@ __device__ void nth_step_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     __syncthreads();
     K5_SUB(1, kNthBatch == 8);
     // pass 3: the swaps L_t <-> R_t, t < s (disjoint positions)
-    nth_swaps<kSwapBatch>(q, lpos, rpos, f, sh.s, threadIdx.x, kNthThreads);
+    nth_swaps<kSwapBatch>(q, sl, f, sh.s, threadIdx.x, kNthThreads);
     __syncthreads();
     K5_SUB(2, kNthBatch == 8);
 }
@@ -478,9 +513,12 @@ __device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop
 
 // The introselect loop on q[f, l) by the whole workgroup while the range exceeds
 // `stop` entries; ends with a barrier, sh.f/l/depth updated or sh.heap_exit set.
-template <int kNthBatch, int kSwapBatch>
+// GLOBAL (the one-workgroup global-memory phase): mk_arena (arena_bytes of LDS) holds
+// the step's stopper bytes and, after them, as many LDS pair slots as fit (the rest
+// in gpos_l / gpos_r); otherwise mk / mk_tiles and the plain LDS slots lpos / rpos.
+template <int kNthBatch, int kSwapBatch, bool GLOBAL>
 __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth,
-                            int64_t stop, uint8_t* mk, int64_t mk_tiles) {
+                            int64_t stop, uint8_t* mk, int64_t mk_tiles, size_t arena_bytes = 0) {
     // thread 0 prepares a step: depth check, median, reset of the step's results
     auto prepare = [&]() -> bool {
         if (sh.l - sh.f <= stop) return false;
@@ -501,7 +539,18 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     __syncthreads();
     while (go) {
         K5_STEP(stop == kNthLds ? 0 : 1);
-        nth_step_wg<kNthBatch, kSwapBatch>(q, lpos, rpos, sh, mk, mk_tiles);
+        if (GLOBAL) {
+            // the step's stopper bytes first (one per lane per 256-entry tile), then slots
+            const int64_t tiles = (sh.l - sh.f) / 256 + 2;
+            const size_t mk_bytes = (size_t)tiles * 64 <= arena_bytes / 2 ? (size_t)tiles * 64 : 0;
+            const size_t off = (mk_bytes + 15) & ~(size_t)15;
+            const uint32_t cap = (uint32_t)((arena_bytes - off) / 8);
+            uint32_t* ll = reinterpret_cast<uint32_t*>(mk + off);
+            const SplitSlots sl{ll, ll + cap, cap, lpos, rpos};
+            nth_step_wg<kNthBatch, kSwapBatch>(q, sl, sh, mk, mk_bytes ? tiles : 0);
+        } else {
+            nth_step_wg<kNthBatch, kSwapBatch>(q, PlainSlots{lpos, rpos}, sh, mk, mk_tiles);
+        }
         K5_SUB_BEGIN();
         if (threadIdx.x == 0) {
             nth_advance(q, sh, nth, stop);
@@ -538,11 +587,12 @@ __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, in
 #pragma unroll
     for (int u = 0; u < kTiles; ++u) {
         const int64_t t0 = base + 256 * u;
-        if (t0 < l) pair_tile<true>(m[u] & 15u, m[u] >> 4, t0, f, TR, runl, runr, lpos, rpos, s, lnext, rmin);
+        if (t0 < l) pair_tile<true>(m[u] & 15u, m[u] >> 4, t0, f, TR, runl, runr, PlainSlots{lpos, rpos}, s, lnext,
+                                    rmin);
     }
     wave_sync();   // the pair slots are written
     K5_WSUB(5);
-    nth_swaps<2>(q, lpos, rpos, f, s, lane, kWave);
+    nth_swaps<2>(q, PlainSlots{lpos, rpos}, f, s, lane, kWave);
     wave_sync();   // the swaps are done
     K5_WSUB(6);
     const int64_t rs = s ? f + (int64_t)rmin : l;
@@ -809,7 +859,8 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
         if (keep) {
             for (int64_t t0 = wb; t0 < we; t0 += 256) {
                 const uint32_t m = mk[((t0 - bb) >> 8) * 64 + lane];
-                pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+                pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, PlainSlots{lpos, rpos}, paired, lnext,
+                                 rmin);
             }
         } else {
             for (int64_t t0 = wb; t0 < we; t0 += 256 * kB) {
@@ -821,7 +872,8 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
                 for (int u = 0; u < kB; ++u) {
                     uint32_t pl, pr;
                     stopper_masks(x[u], valid[u], P, pl, pr);
-                    pair_tile<false>(pl, pr, t0 + u * 256, f, TR, runl, runr, lpos, rpos, paired, lnext, rmin);
+                    pair_tile<false>(pl, pr, t0 + u * 256, f, TR, runl, runr, PlainSlots{lpos, rpos}, paired, lnext,
+                                     rmin);
                 }
             }
         }
@@ -837,7 +889,7 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
         // pass 3: the swaps L_t <-> R_t, t < s, over all G workgroups
         if (threadIdx.x == 0) s_sh = __hip_atomic_load(&g->s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        nth_swaps<8>(q, lpos, rpos, f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
+        nth_swaps<8>(q, PlainSlots{lpos, rpos}, f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
         nthg_barrier(g, G);
         // the cut, the next range and the next median
         if (b == 0 && threadIdx.x == 0) {
@@ -881,8 +933,10 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     if (n <= 0 || nth >= n) return;
     K5_STAMP(0);
     // global phase: lq (unused until the LDS phase) holds the stopper bytes
-    nth_loop_wg<8, 8>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<uint8_t*>(lq),
-                      (int64_t)(kNthLds * sizeof(uint64_t) / 64));
+    // the whole LDS area (lq, llp, lrp, lmk: contiguous, carved by the caller) is the
+    // global phase's arena: stopper bytes + LDS pair slots
+    nth_loop_wg<8, 8, true>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<uint8_t*>(lq), 0,
+                            kNthSmemBytes);
     K5_STAMP(1);
     if (sh.heap_exit) return;
     const int64_t f = sh.f, m = sh.l - sh.f;                          // <= kNthLds entries left
@@ -894,7 +948,7 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     }
     __syncthreads();
     K5_STAMP(2);
-    nth_loop_wg<1, 2>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthMkLds / 64);   // LDS phase
+    nth_loop_wg<1, 2, false>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthMkLds / 64);   // LDS phase
     K5_STAMP(3);
     if (!sh.heap_exit && threadIdx.x < kWave) nth_tail_wave(lq, llp, lrp, sh, nth - f);   // one wave
     __syncthreads();
