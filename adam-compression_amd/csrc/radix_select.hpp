@@ -179,6 +179,36 @@ __device__ __forceinline__ bool last_block_arrival(uint32_t* ticket, uint32_t nb
     return is_last;
 }
 
+// last_block_arrival for many workgroups: arrivals spread over 8 shard counters (lb %
+// 8: one shard per XCD under round-robin placement), and the shard's last arrival
+// arrives at the top counter tk[8] — a ~1000-way arrival on one word costs ~12 us
+// (MI355X_MICROARCH.md "fanin"), eight ~125-way ones run side by side. tk: 9 words,
+// zero at rest (each last arrival resets its word). lb: the block's index among the
+// nblocks of the task.
+__device__ __forceinline__ bool last_block_arrival8(uint32_t* tk, uint32_t lb, uint32_t nblocks) {
+    if (nblocks <= 64) return last_block_arrival(tk + 8, nblocks);
+    __shared__ int is_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t sh = lb & 7u;
+        const uint32_t members = nblocks / 8 + (sh < (nblocks & 7u) ? 1u : 0u);
+        const uint32_t a = __hip_atomic_fetch_add(tk + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = 0;
+        if (a == members - 1) {
+            __hip_atomic_store(tk + sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t b = __hip_atomic_fetch_add(tk + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b == 7u) {
+                __hip_atomic_store(tk + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        is_last = last;
+    }
+    __syncthreads();
+    return is_last;
+}
+
 // ---------------------------------------------------------------- kernels
 __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
     for (int b = threadIdx.x; b < 3 * kRsBins; b += blockDim.x) (&st->hist[0][0])[b] = 0;
@@ -198,6 +228,7 @@ template <class Src>
 __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
     const int t = src.task(blockIdx.x);
     if (!src.active(t)) return;   // uniform per workgroup
+    if ((int)blockIdx.x - src.first_block(t) >= src.blocks(t)) return;   // not a participant of the task
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t nan_cnt;
     __shared__ uint64_t lds16[16];

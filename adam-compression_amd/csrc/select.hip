@@ -120,6 +120,7 @@ struct SelState {
     int32_t win_keys;      // keys K3 read from the K1 sample window list (0: the samples)
     long long def_limit;
     uint32_t tickets[4];
+    uint32_t tk8[9];       // sharded arrival of the count passes (last_block_arrival8)
     // Segments whose K1 list overflowed, counted by K1 into slot [epoch & 1] (64
     // shards against atomic contention); k_sel_init reads it and zeroes the other
     // slot for the next call, k_sel_finish advances the epoch.
@@ -723,6 +724,7 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         st->rs_nth = 0;
         st->tie_rule = DGC_TIES_NONE;
         for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
+        for (int i = 0; i < 9; ++i) st->tk8[i] = 0;
         for (int i = 0; i <= kMaxLower; ++i) st->lower_cnt[i] = 0;
     }
 }
@@ -852,7 +854,14 @@ struct SampleKeys {
     const float* vec_flat;
     __device__ __forceinline__ int task(int b) const { return task_of_block(w.bt[BT_SAMP], w.T, b); }
     __device__ __forceinline__ int first_block(int t) const { return w.bt[BT_SAMP][t]; }
-    __device__ __forceinline__ int blocks(int t) const { return w.bt[BT_SAMP][t + 1] - w.bt[BT_SAMP][t]; }
+    // participating workgroups: all of the task's for the samples; for the window list
+    // (~3 ks keys) one per 4096 keys — 512 workgroups over 83k clustered keys paid
+    // their histogram flushes on the same few bins and a 512-way arrival per pass
+    __device__ __forceinline__ int blocks(int t) const {
+        const int all = w.bt[BT_SAMP][t + 1] - w.bt[BT_SAMP][t];
+        const uint32_t wn = w.rs[t].win_n;
+        return wn ? min(all, (int)((wn + 4095u) / 4096u)) : all;
+    }
     __device__ __forceinline__ bool active(int) const { return true; }
     __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
     __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
@@ -987,7 +996,8 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     __syncthreads();
     if (threadIdx.x == 0 && bsum) atomicAdd(&w.grp_cnt[d.grp0 + lseg0 / kGroupSegs], (unsigned long long)bsum);
     // the tensor's last workgroup takes the adaptation step (no k_decide launch)
-    if (last_block_arrival(&w.st[t].tickets[3], (uint32_t)(w.bt[BT_CNT][t + 1] - w.bt[BT_CNT][t])))
+    if (last_block_arrival8(w.st[t].tk8, (uint32_t)((int64_t)blockIdx.x - w.bt[BT_CNT][t]),
+                            (uint32_t)(w.bt[BT_CNT][t + 1] - w.bt[BT_CNT][t])))
         decide_tensor(w, p, t);
 }
 
@@ -1059,7 +1069,8 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
         __syncthreads();
     }
     // the tensor's last workgroup takes the adaptation step (no k_decide launch)
-    if (last_block_arrival(&w.st[t].tickets[3], (uint32_t)nb)) decide_tensor(w, p, t);
+    if (last_block_arrival8(w.st[t].tk8, (uint32_t)((int64_t)blockIdx.x - w.bt[which][t]), (uint32_t)nb))
+        decide_tensor(w, p, t);
 }
 
 // Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
