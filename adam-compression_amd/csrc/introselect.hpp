@@ -562,37 +562,71 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
 }
 
 // ---------------------------------------------------------------- single-wave tail
-// The same step by one wave on an LDS range of <= kNthWave entries: no workgroup barrier.
+// The same step by one wave on an LDS range of <= kNthWave entries: no workgroup
+// barrier. Leaner than pair_tile's per-element swap test (a single wave's dependent
+// instruction chain is the tail's cost: ~1.6 us per step measured, tools/k5_prof.py):
+// EVERY left stopper stores its position at its rank from the left (lpos), every right
+// stopper at its rank from the left too (rposL); then L_t = lpos[t - 1] and R_t =
+// rposL[TR - t], and the swap count s = #{t : L_t < R_t} — a monotone predicate, L
+// rising and R falling — is found by a two-round search over the slots.
+struct RevSlots {   // pairs t: lpos[t] <-> rposL[TR - 1 - t]
+    const uint32_t* l;
+    const uint32_t* r;
+    uint32_t TR;
+    __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
+    __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[TR - 1 - t]; }
+};
+
 __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, int64_t f, int64_t l) {
     constexpr int kTiles = kNthWave / 256 + 1;   // the range <= kNthWave, from a base <= a0
     K5_WSUB_BEGIN();
     const int lane = threadIdx.x & 63;
     const uint32_t P = qkey(q[f]);
     const int64_t a0 = f + 1, base = nth_base(q, a0);
-    uint32_t TR = 0, m[kTiles];
+    const uint32_t below[4] = {0u, 1u, 3u, 7u};
+    uint32_t runl = 0, runr = 0;
 #pragma unroll
     for (int u = 0; u < kTiles; ++u) {
         const int64_t t0 = base + 256 * u;
-        m[u] = 0;
-        if (t0 < l) {
-            uint64_t x[4];
-            uint32_t valid, pl, pr;
-            nth_load4(q, t0 + 4 * lane, a0, l, x, valid);
-            stopper_masks(x, valid, P, pl, pr);
-            TR += wave_count4(pr);
-            m[u] = pl | (pr << 4);
+        if (t0 >= l) break;   // uniform
+        uint64_t x[4];
+        uint32_t valid, pl, pr;
+        nth_load4(q, t0 + 4 * lane, a0, l, x, valid);
+        stopper_masks(x, valid, P, pl, pr);
+        uint32_t bl, tl, br, tr;
+        wave_prefix4(pl, bl, tl);
+        wave_prefix4(pr, br, tr);
+        const uint32_t rel0 = (uint32_t)(t0 - f) + 4u * (uint32_t)lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if ((pl >> j) & 1u) lpos[runl + bl + (uint32_t)__popc(pl & below[j])] = rel0 + (uint32_t)j;
+            if ((pr >> j) & 1u) rpos[runr + br + (uint32_t)__popc(pr & below[j])] = rel0 + (uint32_t)j;
         }
+        runl += tl;
+        runr += tr;
     }
-    uint32_t runl = 0, runr = 0, s = 0, lnext = UINT32_MAX, rmin = UINT32_MAX;
-#pragma unroll
-    for (int u = 0; u < kTiles; ++u) {
-        const int64_t t0 = base + 256 * u;
-        if (t0 < l) pair_tile<true>(m[u] & 15u, m[u] >> 4, t0, f, TR, runl, runr, PlainSlots{lpos, rpos}, s, lnext,
-                                    rmin);
+    wave_sync();   // the slots are written
+    const uint32_t TL = runl, TR = runr, M = TL < TR ? TL : TR;
+    // s = the first t in [0, M) with lpos[t] >= rposL[TR - 1 - t] (M if none)
+    uint32_t s = M;
+    if (M > 0) {
+        const uint32_t stride = (M + 63) / 64;
+        const uint32_t ti = (uint32_t)lane * stride + stride - 1;   // the last t of lane's block
+        const bool fail1 = ti < M ? lpos[ti] >= rpos[TR - 1 - ti] : true;
+        const uint64_t b1 = __ballot(fail1);
+        const uint32_t blk = (uint32_t)__builtin_ctzll(b1);   // the first block holding a failure (or past M)
+        const uint32_t t2 = blk * stride + (uint32_t)lane;
+        const bool in2 = (uint32_t)lane < stride && t2 < M;
+        const bool fail2 = in2 ? lpos[t2] >= rpos[TR - 1 - t2] : ((uint32_t)lane >= stride ? true : t2 >= M);
+        const uint64_t b2 = __ballot(fail2);
+        const uint32_t first = blk * stride + (uint32_t)__builtin_ctzll(b2);
+        s = first < M ? first : M;
     }
-    wave_sync();   // the pair slots are written
     K5_WSUB(5);
-    nth_swaps<2>(q, PlainSlots{lpos, rpos}, f, s, lane, kWave);
+    nth_swaps<2>(q, RevSlots{lpos, rpos, TR}, f, s, lane, kWave);
+    // L_(s+1) (the first unswapped left stopper) and R_s (the smallest swapped right one)
+    const uint32_t lnext = s < TL ? lpos[s] : UINT32_MAX;
+    const uint32_t rmin = s > 0 ? rpos[TR - s] : UINT32_MAX;
     wave_sync();   // the swaps are done
     K5_WSUB(6);
     const int64_t rs = s ? f + (int64_t)rmin : l;
