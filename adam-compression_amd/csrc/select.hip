@@ -772,20 +772,6 @@ __device__ uint64_t block_scan_array(const unsigned long long* a, long long* out
 // without resample the threshold may also rise, and each step is a recount (count
 // pass + decide), like the reference. The group totals are other workgroups' device
 // atomics of this launch: read with agent-scope loads (last_block_arrival).
-// The threshold a full select pass lists at. The first count of a call (iter 0) that
-// may still take the "lower" step (resample, <= kMaxLower iterations, N > S) lists at
-// the LOWEST threshold that step can reach, t_cur x lower^max_iters (the reference's
-// fl32 sequence): the lists then serve the multi-threshold count (k_lower_lists) and
-// the recount at the chosen t_j (k_count_lists), so a lowering tensor reads vec once
-// instead of three times (pass, k_lower_counts, second pass). Otherwise t_cur. Every
-// list holds every element >= its threshold; consumers filter at t_cur.
-__device__ __forceinline__ float relist_threshold(const SelState& st, const TDesc& d, const SelCfg& p) {
-    float t = st.t_cur;
-    if (p.resample && p.max_iters <= kMaxLower && st.iter == 0 && d.n > d.S)
-        for (int j = 1; j <= p.max_iters; ++j) t = __fmul_rn(t, p.lower);
-    return t;
-}
-
 __device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t) {
     SelState* st = w.st + t;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -796,8 +782,8 @@ __device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t) {
     uint64_t n;
     block_exclusive_scan(local, lds16, &n);
     if (threadIdx.x == 0) {
-        if (st->t_cur < st->t_list) {   // a full select pass just re-listed (relist_threshold)
-            st->t_list = relist_threshold(*st, d, p);
+        if (st->t_cur < st->t_list) {   // a full select pass just re-listed at t_cur
+            st->t_list = st->t_cur;
             st->full_passes += 1;
         }
         const long long cnt = (long long)n, k = d.k;
@@ -1029,7 +1015,6 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
-    const float tlo = relist_threshold(*st, d, p);   // the lists' threshold (<= tc)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int kTiles = kSuper * kSegTiles;   // 16
     __shared__ uint32_t wcnt[kSegPerBlock4];
@@ -1049,27 +1034,24 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
             for (int sg = 0; sg < kSuper; ++sg) {
                 const int64_t ls = sup * kSuper + sg;
                 const int64_t seg = d.seg0 + ls;
-                uint32_t c = 0, cc = 0;   // list count (at tlo), count at tc
+                uint32_t c = 0;
                 uint16_t* lo = w.lst_off + lcol(seg);
                 float* lv = w.lst_val + lcol(seg);
                 if (ls < d.nseg) {   // uniform per wave
                     uint32_t mk = 0;
 #pragma unroll
                     for (int u = 0; u < kSegTiles; ++u) {
-                        const float (&xt)[4] = x[sg * kSegTiles + u];
-                        const uint32_t vt = valid[sg * kSegTiles + u];
-                        list_append(ge_mask(xt, vt, tlo), xt, u * 256, c, lo, lv);
-                        cc += __popc(ge_mask(xt, vt, tc));
-                        mk = max(mk, tile_max_key(xt, vt));
+                        list_append(ge_mask(x[sg * kSegTiles + u], valid[sg * kSegTiles + u], tc),
+                                    x[sg * kSegTiles + u], u * 256, c, lo, lv);
+                        mk = max(mk, tile_max_key(x[sg * kSegTiles + u], valid[sg * kSegTiles + u]));
                     }
                     mk = wave_max(mk);
-                    cc = wave_sum(cc);
                     if (lane == 0) {
                         w.seg_lcnt[seg] = lcnt_pack(c, lmax_code(mk));
-                        w.seg_cnt[seg] = cc;
+                        w.seg_cnt[seg] = c;
                     }
                 }
-                ctot += cc;
+                ctot += c;
                 novf += c > (uint32_t)kCap;
             }
         }
@@ -1167,7 +1149,7 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
 // is the reference's j* and k_lower_counts' pass over vec is skipped; otherwise the
 // counts are cleared and k_lower_counts recounts every t_j over vec. One thread per
 // segment, like k_count_lists.
-constexpr int kLowerLists = kMaxLower;
+constexpr int kLowerLists = 4;
 
 __global__ void __launch_bounds__(kBlock)
 k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {

@@ -866,6 +866,40 @@ def test_bucket_steps_match_oracle(L, N, ratio, kind, scales, fill, shape, monke
             assert windowed >= 3, (served_by_lists, windowed)
 
 
+@pytest.mark.parametrize("engine", ["bucket", "batch"])
+def test_default_fill_survives_data_writes(L, engine):
+    """The default fill ("auto" = the dense zero_()) stays right when the caller writes
+    the output through ``.data`` between steps — the reference's own idiom, which
+    leaves torch's version counter alone, so only the dense fill can be trusted then
+    (the opt-in "sparse" re-zero cannot see such a write)."""
+    from dgc.batch import DGCBatch
+    from dgc.bucket import DGCBucket
+    N, ratio = 1_000_000, 0.001
+    attrs = O.attributes(N, ratio)
+    m_o, v_o = np.zeros(N, np.float32), np.zeros(N, np.float32)
+    rng = random.Random(9)
+    if engine == "bucket":
+        b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=9)
+        assert b.fill == "inline"
+        out = torch.empty(N, device=DEV)
+    else:
+        b = DGCBatch([("w", (N,))], compress_ratio=ratio, momentum=0.9, nesterov=True, device=DEV, seed=9)
+        assert b.fill == "inline"
+    for s in range(4):
+        g = synth.gradient(40 + s, N, "normal")
+        start = rng.randint(0, attrs[4] - 1)
+        if engine == "bucket":
+            b.step(to_dev(g), out)
+            got = out
+        else:
+            b.grad("w").copy_(to_dev(g))
+            got = b.step()[:N]
+        torch.cuda.synchronize()
+        ov, oi, _ = O.compress_step(g, m_o, v_o, attrs, start, nesterov=True)
+        assert np.array_equal(bits(got.cpu().numpy()), bits(O.decompress([ov], [oi], N, 1))), (engine, s)
+        got.data.add_(3.0)   # no version bump: the next step must not build on this buffer's zeros
+
+
 def _same_bits_or_nan(a, b):
     """Bitwise equal, except that any NaN matches any NaN (numpy and the GPU may carry
     different NaN payloads through the momentum arithmetic)."""
