@@ -20,7 +20,10 @@ thousands of tie-heavy inputs, and tests/test_oracle_golden.py against the refer
 golden resample steps, in order.
 
 The nth_element partition is written in the same data-parallel form the GPU kernel
-(csrc/resample.hip) uses, so this file is also that kernel's specification. One
+(K5: ``adam-compression_amd/csrc/introselect.hpp``, launched from ``csrc/select.hip``'s
+``k_nth_select`` / ``k_nth_global``) uses, so this file is also that kernel's
+specification; ``partial_sort`` below is what K5b (``heap_select_wg`` in
+``csrc/select.hip``) replays. One
 ``__unguarded_partition(first + 1, last, pivot = first)`` is, with P the pivot key:
 
     L_1 < L_2 < ...  positions in [first+1, last) with key <= P  (left scan stops)
