@@ -668,7 +668,7 @@ __device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthSh
 // 2 steps, tools/k5_prof.py). The step is the same partition as nth_step_wg — the G x
 // 8 waves take contiguous stretches in order, so every stopper's rank is the same —
 // with a barrier among the G workgroups where nth_step_wg has __syncthreads: counts |
-// pairing | swaps | advance.
+// pairing | swaps (+ the advance, run by the last workgroup to arrive).
 //
 // Residency. A plain launch does not guarantee that the G workgroups run at once (other
 // streams' or processes' kernels may hold CUs), and the per-step barriers would then
@@ -697,33 +697,50 @@ struct NthG {
     uint32_t bl[kNthGMax], br[kNthGMax];
 };
 
-// Barrier among the G workgroups of one tensor (all resident: see the consensus above).
-// Agent-scope release / acquire around the arrival make every workgroup's global
-// stores visible to the others across XCDs. The spin is bounded (~seconds): should it
-// ever run out, the run is marked DGC_K5_BROKEN instead of hanging the GPU.
-__device__ __forceinline__ void nthg_barrier(NthG* g, uint32_t G) {
+// Barrier among the G workgroups of one tensor (all resident: see the consensus above),
+// in the form of MI355X_MICROARCH.md's barrier-counter: every wave's stores drained,
+// one lane's agent-scope RELEASE fence (the L2 write-back that makes this workgroup's
+// stores visible across XCDs), one arrival, a relaxed poll of the generation word with
+// s_sleep, one ACQUIRE fence (the L1 invalidate) — two single fences, not the two full
+// __threadfence()s per barrier of round 2. The LAST arriver first runs `last` (thread
+// 0, after its own acquire: it sees every workgroup's data) and only then releases the
+// others, so the step's advance needs no barrier of its own. The spin is bounded
+// (~seconds): should it run out, the run is marked DGC_K5_BROKEN instead of hanging.
+template <class F>
+__device__ __forceinline__ void nthg_barrier(NthG* g, uint32_t G, F&& last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t gen = __hip_atomic_load(&g->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence();
-        const uint32_t a = atomicAdd(&g->bar_count, 1u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t a = __hip_atomic_fetch_add(&g->bar_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a == G - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            last();
             __hip_atomic_store(&g->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&g->bar_gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&g->bar_gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             bool passed = false;
             for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
-                if (__hip_atomic_load(&g->bar_gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != gen) {
+                if (__hip_atomic_load(&g->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) {
                     passed = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
             if (!passed) atomicOr(&g->status, (uint32_t)DGC_K5_BROKEN);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        __threadfence();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+}
+
+__device__ __forceinline__ void nthg_barrier(NthG* g, uint32_t G) {
+    nthg_barrier(g, G, [] {});
 }
 
 // The residency consensus (see above): true = all G workgroups are here, run the phase.
@@ -924,9 +941,8 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
         if (threadIdx.x == 0) s_sh = __hip_atomic_load(&g->s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         nth_swaps<8>(q, PlainSlots{lpos, rpos}, f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
-        nthg_barrier(g, G);
-        // the cut, the next range and the next median
-        if (b == 0 && threadIdx.x == 0) {
+        // the last arriver: the cut, the next range and the next median (all swaps visible)
+        nthg_barrier(g, G, [&] {
             const int64_t rs = g->s ? (int64_t)g->r_min : g->l;
             const int64_t ln = g->l_next == ~0ull ? INT64_MAX : (int64_t)g->l_next;
             const int64_t cut = ln < rs ? ln : rs;
@@ -935,8 +951,7 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
             else
                 g->l = cut;
             nthg_prepare(q, g, nth);
-        }
-        nthg_barrier(g, G);
+        });
     }
 }
 

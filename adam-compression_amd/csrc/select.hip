@@ -2176,7 +2176,8 @@ static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const 
 // with <= kNthGMinCand candidates (decided on the device: below ~140k the four
 // cross-XCD barriers per step cost more than the spread saves, tools/k5ab.sh), and
 // DGC_K5_GLOBAL=wg (A/B, parity); DGC_K5_GLOBAL=multi skips both gates.
-constexpr int64_t kNthGMinCand = 196608;   // launch for capacities above, run for candidate counts above
+constexpr int64_t kNthGMinCand = 40000;    // launch for capacities above, run for candidate counts above
+constexpr int64_t kNthGPerTensor = 16;      // workgroups per tensor of the multi-workgroup phase
 
 static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
     static int per_dev = -1;
@@ -2195,8 +2196,11 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
     if (force && std::strcmp(force, "wg") == 0) return 0;
     const bool multi = force && (std::strcmp(force, "multi") == 0 || std::strcmp(force, "abort") == 0);
     if (max_cand <= kNthLds || (max_cand <= kNthGMinCand && !multi)) return 0;
-    const int64_t g = T > 0 ? per_dev / T : 0;
-    return (uint32_t)std::min<int64_t>(g, kNthGMax);
+    // per tensor, not per call: only the few tensors whose candidates exceed the gate run
+    // the phase (the others' workgroups exit at once), so a batch of many tensors still
+    // spreads its big resamples widely (54 tensors used to get 2 workgroups each)
+    (void)T;
+    return (uint32_t)std::min<int64_t>(per_dev, kNthGPerTensor);
 }
 
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
