@@ -70,12 +70,14 @@ def model_candidates(model):
 def main():
     L = _lib.lib()
     cases = [(400_000, 400, 2_000), (1_000_000, 1000, 6_000), (2_000_000, 2000, 12_000),
-             (4_000_000, 2360, 30_000), (10_000_000, 10_000, 100_000), (50_000_000, 20_000, 500_000),
+             (4_000_000, 2360, 30_000), (4_000_000, 2360, 45_000), (4_000_000, 2360, 57_000),
+             (10_000_000, 10_000, 100_000), (50_000_000, 20_000, 500_000),
              (100_000_000, 102_761, 1_000_000)]
     for n, k, target in cases:
         print(json.dumps(select_case(L, n, k, target)), flush=True)
-    for model in ("resnet50", "vgg16_bn"):
-        print(json.dumps({model: model_candidates(model)}), flush=True)
+    if os.environ.get("K5_MODELS", "1") == "1":
+        for model in ("resnet50", "vgg16_bn"):
+            print(json.dumps({model: model_candidates(model)}), flush=True)
 
 
 if __name__ == "__main__":
