@@ -2176,8 +2176,7 @@ static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const 
 // with <= kNthGMinCand candidates (decided on the device: below ~140k the four
 // cross-XCD barriers per step cost more than the spread saves, tools/k5ab.sh), and
 // DGC_K5_GLOBAL=wg (A/B, parity); DGC_K5_GLOBAL=multi skips both gates.
-constexpr int64_t kNthGMinCand = 40000;    // launch for capacities above, run for candidate counts above
-constexpr int64_t kNthGPerTensor = 16;      // workgroups per tensor of the multi-workgroup phase
+constexpr int64_t kNthGMinCand = 98304;    // launch for capacities above, run for candidate counts above
 
 static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
     static int per_dev = -1;
@@ -2196,11 +2195,12 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
     if (force && std::strcmp(force, "wg") == 0) return 0;
     const bool multi = force && (std::strcmp(force, "multi") == 0 || std::strcmp(force, "abort") == 0);
     if (max_cand <= kNthLds || (max_cand <= kNthGMinCand && !multi)) return 0;
-    // per tensor, not per call: only the few tensors whose candidates exceed the gate run
-    // the phase (the others' workgroups exit at once), so a batch of many tensors still
-    // spreads its big resamples widely (54 tensors used to get 2 workgroups each)
-    (void)T;
-    return (uint32_t)std::min<int64_t>(per_dev, kNthGPerTensor);
+    // measured (tools/run_k5.sh): 16 workgroups per tensor for every tensor of a batch
+    // from 40k candidates made ResNet-50 0.358 -> 0.373 ms (864 workgroups launched per
+    // step, and at 45-57k candidates the spread phase is no faster than one workgroup:
+    // 0.141-0.144 ms either way); it pays from ~100k (500k: 0.945 -> 0.371 ms)
+    const int64_t g = T > 0 ? per_dev / T : 0;
+    return (uint32_t)std::min<int64_t>(g, kNthGMax);
 }
 
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
