@@ -76,14 +76,14 @@ static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, int64_t sort_cap
 
 template <int VD>
 __device__ __forceinline__ float load_val(const void* p, long long e) {
-    if (VD == DGC_F16) return __half2float(reinterpret_cast<const __half*>(p)[e]);
-    return reinterpret_cast<const float*>(p)[e];
+    if (VD == DGC_F16) return (float)((const DGC_GLB _Float16*)p)[e];   // typed: global_ loads; exact widening
+    return ((const DGC_GLB float*)p)[e];
 }
 
 template <int ID>
 __device__ __forceinline__ long long load_idx(const void* p, long long e) {
-    if (ID == DGC_I32) return reinterpret_cast<const int32_t*>(p)[e];
-    return reinterpret_cast<const int64_t*>(p)[e];
+    if (ID == DGC_I32) return ((const DGC_GLB int32_t*)p)[e];
+    return ((const DGC_GLB int64_t*)p)[e];
 }
 
 // Where the runs come from: a table in the workspace (concatenated input), or the
@@ -565,16 +565,11 @@ k_scatter_waves(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float s
         const float val = scale != 1.0f ? __fmul_rn(a, scale) : a;
         if (alone) {
             const int pos = (int)((reinterpret_cast<uintptr_t>(dst) - g) >> 2);
-            float4* g4 = reinterpret_cast<float4*>(g);
+            DGC_GLB f4v* g4 = (DGC_GLB f4v*)g;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (pos >> 2 == q) {
-                    if ((pos & 3) == 0) v.x = val;
-                    if ((pos & 3) == 1) v.y = val;
-                    if ((pos & 3) == 2) v.z = val;
-                    if ((pos & 3) == 3) v.w = val;
-                }
+                f4v v = {0.f, 0.f, 0.f, 0.f};
+                if (pos >> 2 == q) v[pos & 3] = val;
                 g4[q] = v;
             }
         } else if (head) {
@@ -634,7 +629,7 @@ __global__ void __launch_bounds__(kBlock) k_clear_packed(RunSrc prev, float* __r
         if (i < 0 || i >= n) continue;
         const uintptr_t g = reinterpret_cast<uintptr_t>(grad + i) & ~(uintptr_t)63;
         if (g >= lo && g + 64 <= hi)
-            reinterpret_cast<float4*>(g)[part] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ((DGC_GLB f4v*)g)[part] = f4v{0.f, 0.f, 0.f, 0.f};
         else if (part == 0)
             grad[i] = 0.f;   // a granule that crosses the buffer's ends: the word alone
     }

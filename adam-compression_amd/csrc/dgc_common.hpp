@@ -79,6 +79,46 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
     return x * q + (x < r ? x : r) + i;
 }
 
+// Address-space-typed pointers. A generic pointer into LDS or global memory becomes a
+// flat_ access unless the compiler can prove where it points, and it cannot once two
+// stores are merged through a select of their addresses, or a pointer comes out of a
+// kernel-argument struct: K5's global-phase loads and pair-slot stores were all flat.
+// Typed pointers give ds_ / global_ instructions; as_of<P>::ptr<U> rebinds a pointer
+// type to another pointee in the same address space (templates over both kinds).
+#define DGC_GLB __attribute__((address_space(1)))
+#define DGC_LDS __attribute__((address_space(3)))
+template <class P>
+struct as_of {
+    template <class U>
+    using ptr = U*;
+};
+template <class T>
+struct as_of<DGC_GLB T*> {
+    template <class U>
+    using ptr = DGC_GLB U*;
+};
+template <class T>
+struct as_of<DGC_LDS T*> {
+    template <class U>
+    using ptr = DGC_LDS U*;
+};
+template <class P, class U>
+using rebind_t = typename as_of<P>::template ptr<U>;
+template <class T>
+__device__ __forceinline__ DGC_GLB T* glb(T* p) { return (DGC_GLB T*)p; }
+template <class T>
+__device__ __forceinline__ DGC_LDS T* lds(T* p) { return (DGC_LDS T*)p; }
+
+// Wave-uniform values the compiler cannot prove uniform (threadIdx.x >> 6, LDS reads):
+// in SGPRs, loops and branches on them are scalar instead of exec-masked.
+__device__ __forceinline__ uint32_t uniform32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int wave_id() { return (int)uniform32(threadIdx.x >> 6); }
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -88,19 +128,23 @@ __device__ __forceinline__ uint32_t abs_key(float x) {
     return __float_as_uint(x) & 0x7FFFFFFFu;   // |x| bit pattern: uint order == float order
 }
 
+// acc + popcount(m & lanes below this one): two v_mbcnt, no 64-bit mask arithmetic.
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m, uint32_t acc) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
+}
+
 // Exclusive prefix over (lane, j) order of 4 predicate bits per lane (bit j of p),
 // i.e. element order 4*lane + j. Returns the lane's base and the wave total.
 __device__ __forceinline__ void wave_prefix4(uint32_t p, uint32_t& lane_base, uint32_t& total) {
     const uint64_t m0 = __ballot(p & 1u), m1 = __ballot(p & 2u);
     const uint64_t m2 = __ballot(p & 4u), m3 = __ballot(p & 8u);
-    const uint64_t lt = lanemask_lt();
-    lane_base = __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+    lane_base = mbcnt64(m3, mbcnt64(m2, mbcnt64(m1, mbcnt64(m0, 0u))));
     total = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
 }
 
 __device__ __forceinline__ void wave_prefix1(bool p, uint32_t& lane_base, uint32_t& total) {
     const uint64_t m = __ballot(p);
-    lane_base = __popcll(m & lanemask_lt());
+    lane_base = mbcnt64(m, 0u);
     total = __popcll(m);
 }
 

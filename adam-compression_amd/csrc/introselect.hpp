@@ -58,10 +58,14 @@ struct K5Prof {
     unsigned long long t[8];
     unsigned int steps[4];
     unsigned long long sub[8];   // global-phase step parts, summed over steps
+    unsigned long long bt[64][8];   // per workgroup (tensor) < 64: the same stamps, [6] kernel end
+    long long bn[64];               // its candidate count
 };
 __device__ K5Prof g_k5prof;
 #define K5_STAMP(i) \
-    do { if (blockIdx.x == 0 && threadIdx.x == 0) g_k5prof.t[i] = wall_clock64(); } while (0)
+    do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
+         if (blockIdx.x == 0) g_k5prof.t[i] = t_; \
+         if (blockIdx.x < 64) g_k5prof.bt[blockIdx.x][i] = t_; } } while (0)
 #define K5_STEP(i) \
     do { if (blockIdx.x == 0 && threadIdx.x == 0) g_k5prof.steps[i] += 1; } while (0)
 #define K5_SUB_BEGIN() unsigned long long k5_t0 = wall_clock64()
@@ -93,7 +97,8 @@ __device__ __forceinline__ void wave_sync() {
 // ---------------------------------------------------------------- heaps (depth limit)
 // std::__adjust_heap + std::__push_heap on q[0..n) with comp = key greater (the
 // heap's "largest" is the smallest key). Single thread.
-__device__ void nth_adjust_heap(uint64_t* q, int64_t hole, int64_t n, uint64_t v) {
+template <class QP>
+__device__ void nth_adjust_heap(QP q, int64_t hole, int64_t n, uint64_t v) {
     const int64_t top = hole;
     int64_t child = hole;
     while (child < (n - 1) / 2) {
@@ -118,7 +123,8 @@ __device__ void nth_adjust_heap(uint64_t* q, int64_t hole, int64_t n, uint64_t v
 
 // std::__heap_select(q, q + mid, q + n), then iter_swap(q, q + nth): the depth-limit
 // exit of std::__introselect. Single thread; reached only by adversarial inputs.
-__device__ void nth_heap_select(uint64_t* q, int64_t mid, int64_t n, int64_t nth) {
+template <class QP>
+__device__ void nth_heap_select(QP q, int64_t mid, int64_t n, int64_t nth) {
     if (mid >= 2) {
         for (int64_t parent = (mid - 2) / 2;; --parent) {
             nth_adjust_heap(q, parent, mid, q[parent]);
@@ -140,7 +146,8 @@ __device__ void nth_heap_select(uint64_t* q, int64_t mid, int64_t n, int64_t nth
 // std::__move_median_to_first(f, f+1, mid, l-1) with comp = key greater. One thread;
 // the four entries are loaded together (one round trip when q is in global memory).
 // Returns the pivot key.
-__device__ __forceinline__ uint32_t nth_median(uint64_t* q, int64_t f, int64_t l) {
+template <class QP>
+__device__ __forceinline__ uint32_t nth_median(QP q, int64_t f, int64_t l) {
     const int64_t a = f + 1, b = f + (l - f) / 2, c = l - 1;
     const uint64_t ea = q[a], eb = q[b], ec = q[c], ef = q[f];
     const uint32_t ka = qkey(ea), kb = qkey(eb), kc = qkey(ec);
@@ -159,7 +166,8 @@ __device__ __forceinline__ uint32_t nth_median(uint64_t* q, int64_t f, int64_t l
 }
 
 // std::__insertion_sort of q[f, l) (<= 3 entries after the loop). One thread.
-__device__ void nth_insertion_sort(uint64_t* q, int64_t f, int64_t l) {
+template <class QP>
+__device__ void nth_insertion_sort(QP q, int64_t f, int64_t l) {
     for (int64_t i = f + 1; i < l; ++i) {
         const uint64_t v = q[i];
         if (qkey(v) > qkey(q[f])) {
@@ -179,15 +187,17 @@ __device__ void nth_insertion_sort(uint64_t* q, int64_t f, int64_t l) {
 // Lane's 4 consecutive entries of a 256-entry tile, positions in [begin, end). Tiles
 // are laid from a 16-B-aligned base (nth_base), so a lane whose 4 entries are all in
 // range reads them with two 16-B loads.
-__device__ __forceinline__ void nth_load4(const uint64_t* q, int64_t e0, int64_t begin, int64_t end,
-                                          uint64_t (&x)[4], uint32_t& valid) {
+template <class QP>
+__device__ __forceinline__ void nth_load4(QP q, int64_t e0, int64_t begin, int64_t end, uint64_t (&x)[4],
+                                          uint32_t& valid) {
     if (e0 >= begin && e0 + 3 < end) {
-        const uint4 a = *reinterpret_cast<const uint4*>(q + e0);
-        const uint4 b = *reinterpret_cast<const uint4*>(q + e0 + 2);
-        x[0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
-        x[1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
-        x[2] = (uint64_t)b.x | ((uint64_t)b.y << 32);
-        x[3] = (uint64_t)b.z | ((uint64_t)b.w << 32);
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));   // no constructor: any address space
+        const u64x2 a = *reinterpret_cast<rebind_t<QP, const u64x2>>(q + e0);
+        const u64x2 b = *reinterpret_cast<rebind_t<QP, const u64x2>>(q + e0 + 2);
+        x[0] = a[0];
+        x[1] = a[1];
+        x[2] = b[0];
+        x[3] = b[1];
         valid = 0xFu;
         return;
     }
@@ -201,7 +211,8 @@ __device__ __forceinline__ void nth_load4(const uint64_t* q, int64_t e0, int64_t
 }
 
 // The first tile position at or below a0 whose address is 16-B aligned.
-__device__ __forceinline__ int64_t nth_base(const uint64_t* q, int64_t a0) {
+template <class QP>
+__device__ __forceinline__ int64_t nth_base(QP q, int64_t a0) {
     return a0 - (int64_t)((reinterpret_cast<uintptr_t>(q + a0) >> 3) & 1u);
 }
 
@@ -210,21 +221,29 @@ __device__ __forceinline__ int64_t nth_base(const uint64_t* q, int64_t a0) {
 // or split (the one-workgroup global phase): slots t < cap in LDS, the rest in global
 // memory — a 57k-candidate step swaps ~14k pairs, whose 4-B slot stores and loads
 // were most of its time in global memory.
-struct PlainSlots {
-    uint32_t* l;
-    uint32_t* r;
+template <class SP>
+struct PlainSlotsT {
+    SP l;
+    SP r;
     __device__ __forceinline__ void put_l(uint32_t t, uint32_t v) const { l[t] = v; }
     __device__ __forceinline__ void put_r(uint32_t t, uint32_t v) const { r[t] = v; }
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[t]; }
+    // all slots below `end` in the fast store (uniform test), and that store
+    __device__ __forceinline__ bool fast(uint32_t) const { return true; }
+    __device__ __forceinline__ void fl(uint32_t t, uint32_t v) const { l[t] = v; }
+    __device__ __forceinline__ void fr(uint32_t t, uint32_t v) const { r[t] = v; }
 };
 
+template <class SP>
+__device__ __forceinline__ PlainSlotsT<SP> plain_slots(SP l, SP r) { return PlainSlotsT<SP>{l, r}; }
+
 struct SplitSlots {
-    uint32_t* ll;   // LDS, cap each
-    uint32_t* lr;
+    DGC_LDS uint32_t* ll;   // cap each
+    DGC_LDS uint32_t* lr;
     uint32_t cap;
-    uint32_t* gl;   // global, indexed by t
-    uint32_t* gr;
+    DGC_GLB uint32_t* gl;   // indexed by t
+    DGC_GLB uint32_t* gr;
     __device__ __forceinline__ void put_l(uint32_t t, uint32_t v) const {
         if (t < cap)
             ll[t] = v;
@@ -239,13 +258,16 @@ struct SplitSlots {
     }
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return t < cap ? ll[t] : gl[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return t < cap ? lr[t] : gr[t]; }
+    __device__ __forceinline__ bool fast(uint32_t end) const { return end <= cap; }
+    __device__ __forceinline__ void fl(uint32_t t, uint32_t v) const { ll[t] = v; }
+    __device__ __forceinline__ void fr(uint32_t t, uint32_t v) const { lr[t] = v; }
 };
 
 // The step's swaps L_t <-> R_t, t < s (disjoint positions), by threads tid of nt:
 // kNthSwapBatch pairs per thread with all their loads in flight before any store
 // (8 for the global-memory phase, 2 in LDS where latency is short and registers count).
-template <int kNthSwapBatch, class Slots>
-__device__ __forceinline__ void nth_swaps(uint64_t* q, const Slots& sl, int64_t f, uint32_t s, uint32_t tid,
+template <int kNthSwapBatch, class Slots, class QP>
+__device__ __forceinline__ void nth_swaps(QP q, const Slots& sl, int64_t f, uint32_t s, uint32_t tid,
                                           uint32_t nt) {
     for (uint32_t t0 = tid; t0 < s; t0 += nt * kNthSwapBatch) {
         uint32_t li[kNthSwapBatch], ri[kNthSwapBatch];
@@ -418,11 +440,11 @@ struct NthShared {
 // step's swaps are done and sh.s / l_next / r_min hold its result. Pass 1 keeps each
 // lane's stopper bits of each tile in mk (one byte, LDS) when the step's tiles fit
 // mk_tiles, so pass 2 reads bytes instead of the entries; otherwise it reloads them.
-template <int kNthBatch, int kSwapBatch, class Slots>
-__device__ void nth_step_wg(uint64_t* q, const Slots& sl, NthShared& sh, uint8_t* mk, int64_t mk_tiles) {
-    const int64_t f = sh.f, l = sh.l;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t P = sh.pivot;
+template <int kNthBatch, int kSwapBatch, class Slots, class QP, class MP>
+__device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t mk_tiles) {
+    const int64_t f = uniform64(sh.f), l = uniform64(sh.l);
+    const int lane = threadIdx.x & 63, wv = wave_id();
+    const uint32_t P = uniform32(sh.pivot);
     const int64_t a0 = f + 1, base = nth_base(q, a0), R = l - base;
     const int64_t per = ceil_div(ceil_div(R, (int64_t)kNthWaves), (int64_t)256) * 256;
     const int64_t wb = base + wv * per, we = wb + per < l ? wb + per : l;
@@ -461,12 +483,91 @@ __device__ void nth_step_wg(uint64_t* q, const Slots& sl, NthShared& sh, uint8_t
         runr += i < wv ? b : 0u;
         TR += b;
     }
+    runl = uniform32(runl);
+    runr = uniform32(runr);
+    TR = uniform32(TR);
     // pass 2: ranks, pairing, paired positions
     uint32_t paired = 0, lnext = UINT32_MAX, rmin = UINT32_MAX;
     if (keep) {
+        // Whole-tile cases from the tile's ballots (wave-uniform; pair_tile's reasoning):
+        // a left-swap tile (all its left stoppers swapped, none of its right) ranks only
+        // its left stoppers, a right-swap tile only its right ones, a tile between them
+        // (neither side swapped) only feeds l_next; only the crossing tile(s) take the
+        // per-element test. lnext_u / rmin_u: the wave's first such position (tiles go up).
+        uint32_t paired_u = 0, lnext_u = UINT32_MAX, rmin_u = UINT32_MAX;
+        const uint32_t below[4] = {0u, 1u, 3u, 7u};
+#ifdef DGC_K5_PROF
+        const unsigned long long k5_loop0 = wall_clock64();
+        uint32_t k5_mixed = 0;
+#endif
         for (int64_t t0 = wb; t0 < we; t0 += 256) {
             const uint32_t m = mk[((t0 - base) >> 8) * 64 + lane];
-            pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, sl, paired, lnext, rmin);
+            const uint32_t pl = m & 15u, pr = m >> 4;
+            uint64_t bl[4], br[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bl[j] = __ballot((pl >> j) & 1u);
+                br[j] = __ballot((pr >> j) & 1u);
+            }
+            const uint32_t tl = (uint32_t)(__popcll(bl[0]) + __popcll(bl[1]) + __popcll(bl[2]) + __popcll(bl[3]));
+            const uint32_t tr = (uint32_t)(__popcll(br[0]) + __popcll(br[1]) + __popcll(br[2]) + __popcll(br[3]));
+            const uint32_t t32 = (uint32_t)(t0 - f), rel0 = t32 + 4u * (uint32_t)lane;
+            const int64_t after = (int64_t)TR - runr - tr, from = (int64_t)TR - runr;
+            if (after >= (int64_t)runl + tl) {
+                if (tl) {
+                    const uint32_t r0 = runl + ((mbcnt64(bl[0], 0u) + mbcnt64(bl[1], 0u)) +
+                                                (mbcnt64(bl[2], 0u) + mbcnt64(bl[3], 0u)));
+                    if (sl.fast(runl + tl)) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if ((pl >> j) & 1u) sl.fl(r0 + __popc(pl & below[j]), rel0 + (uint32_t)j);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if ((pl >> j) & 1u) sl.put_l(r0 + __popc(pl & below[j]), rel0 + (uint32_t)j);
+                    }
+                    paired_u += tl;
+                }
+            } else if ((int64_t)runl >= from) {
+                if (tr) {
+                    // R at rank rr (1-based, from f) takes slot TR - rr
+                    const uint32_t r0 = runr + ((mbcnt64(br[0], 0u) + mbcnt64(br[1], 0u)) +
+                                                (mbcnt64(br[2], 0u) + mbcnt64(br[3], 0u)));
+                    if (sl.fast((uint32_t)from)) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if ((pr >> j) & 1u) sl.fr(TR - 1u - r0 - __popc(pr & below[j]), rel0 + (uint32_t)j);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if ((pr >> j) & 1u) sl.put_r(TR - 1u - r0 - __popc(pr & below[j]), rel0 + (uint32_t)j);
+                    }
+                    if (rmin_u == UINT32_MAX) rmin_u = t32 + first_in_tile(br);
+                }
+                if (tl && lnext_u == UINT32_MAX) lnext_u = t32 + first_in_tile(bl);
+            } else if (after + tr < (int64_t)runl + 1 && (int64_t)runl + tl < after + 1) {
+                if (tl && lnext_u == UINT32_MAX) lnext_u = t32 + first_in_tile(bl);
+            } else {
+                pair_tile<false>(pl, pr, t0, f, TR, runl, runr, sl, paired, lnext, rmin);
+#ifdef DGC_K5_PROF
+                k5_mixed += 1;
+#endif
+                continue;
+            }
+            runl += tl;
+            runr += tr;
+        }
+#ifdef DGC_K5_PROF
+        if (kNthBatch == 8 && blockIdx.x == 0 && lane == 0) {   // sub[7]: wave 0's tile loop; steps[3]: mixed tiles
+            if (wv == 0) g_k5prof.sub[7] += wall_clock64() - k5_loop0;
+            atomicAdd(&g_k5prof.steps[3], k5_mixed);
+        }
+#endif
+        // fold the uniform results into lane 0's (reduced below)
+        if (lane == 0) {
+            paired += paired_u;
+            lnext = lnext_u < lnext ? lnext_u : lnext;
+            rmin = rmin_u < rmin ? rmin_u : rmin;
         }
     } else {
         for (int64_t t0 = wb; t0 < we; t0 += 256 * kNthBatch) {
@@ -498,9 +599,8 @@ __device__ void nth_step_wg(uint64_t* q, const Slots& sl, NthShared& sh, uint8_t
     K5_SUB(2, kNthBatch == 8);
 }
 
-// Thread 0, after a step: the cut, the next range, and either the next step's
-// median (returns 1), a depth-limit heap exit, or the end of this phase (returns 0).
-__device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop) {
+// Thread 0, after a step: the cut and the next range.
+__device__ __forceinline__ void nth_advance(NthShared& sh, int64_t nth) {
     const int64_t rs = sh.s ? (int64_t)sh.r_min : sh.l;
     const int64_t ln = sh.l_next == ~0ull ? INT64_MAX : (int64_t)sh.l_next;
     const int64_t cut = ln < rs ? ln : rs;
@@ -508,7 +608,6 @@ __device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop
         sh.f = cut;
     else
         sh.l = cut;
-    return 0;
 }
 
 // The introselect loop on q[f, l) by the whole workgroup while the range exceeds
@@ -516,9 +615,10 @@ __device__ int nth_advance(uint64_t* q, NthShared& sh, int64_t nth, int64_t stop
 // GLOBAL (the one-workgroup global-memory phase): mk_arena (arena_bytes of LDS) holds
 // the step's stopper bytes and, after them, as many LDS pair slots as fit (the rest
 // in gpos_l / gpos_r); otherwise mk / mk_tiles and the plain LDS slots lpos / rpos.
-template <int kNthBatch, int kSwapBatch, bool GLOBAL>
-__device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth,
-                            int64_t stop, uint8_t* mk, int64_t mk_tiles, size_t arena_bytes = 0) {
+// Pointers typed by address space (dgc_common.hpp: DGC_GLB / DGC_LDS).
+template <int kNthBatch, int kSwapBatch, bool GLOBAL, class QP, class SP>
+__device__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& sh, int64_t nth, int64_t stop,
+                            DGC_LDS uint8_t* mk, int64_t mk_tiles, size_t arena_bytes = 0) {
     // thread 0 prepares a step: depth check, median, reset of the step's results
     auto prepare = [&]() -> bool {
         if (sh.l - sh.f <= stop) return false;
@@ -539,21 +639,21 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
     __syncthreads();
     while (go) {
         K5_STEP(stop == kNthLds ? 0 : 1);
-        if (GLOBAL) {
+        if constexpr (GLOBAL) {
             // the step's stopper bytes first (one per lane per 256-entry tile), then slots
             const int64_t tiles = (sh.l - sh.f) / 256 + 2;
             const size_t mk_bytes = (size_t)tiles * 64 <= arena_bytes / 2 ? (size_t)tiles * 64 : 0;
             const size_t off = (mk_bytes + 15) & ~(size_t)15;
             const uint32_t cap = (uint32_t)((arena_bytes - off) / 8);
-            uint32_t* ll = reinterpret_cast<uint32_t*>(mk + off);
+            DGC_LDS uint32_t* ll = reinterpret_cast<DGC_LDS uint32_t*>(mk + off);
             const SplitSlots sl{ll, ll + cap, cap, lpos, rpos};
             nth_step_wg<kNthBatch, kSwapBatch>(q, sl, sh, mk, mk_bytes ? tiles : 0);
         } else {
-            nth_step_wg<kNthBatch, kSwapBatch>(q, PlainSlots{lpos, rpos}, sh, mk, mk_tiles);
+            nth_step_wg<kNthBatch, kSwapBatch>(q, plain_slots(lpos, rpos), sh, mk, mk_tiles);
         }
         K5_SUB_BEGIN();
         if (threadIdx.x == 0) {
-            nth_advance(q, sh, nth, stop);
+            nth_advance(sh, nth);
             go = prepare();
         }
         __syncthreads();
@@ -570,14 +670,15 @@ __device__ void nth_loop_wg(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShar
 // rposL[TR - t], and the swap count s = #{t : L_t < R_t} — a monotone predicate, L
 // rising and R falling — is found by a two-round search over the slots.
 struct RevSlots {   // pairs t: lpos[t] <-> rposL[TR - 1 - t]
-    const uint32_t* l;
-    const uint32_t* r;
+    const DGC_LDS uint32_t* l;
+    const DGC_LDS uint32_t* r;
     uint32_t TR;
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[TR - 1 - t]; }
 };
 
-__device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, int64_t f, int64_t l) {
+__device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DGC_LDS uint32_t* rpos, int64_t f,
+                                 int64_t l) {
     constexpr int kTiles = kNthWave / 256 + 1;   // the range <= kNthWave, from a base <= a0
     K5_WSUB_BEGIN();
     const int lane = threadIdx.x & 63;
@@ -635,7 +736,8 @@ __device__ int64_t nth_step_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, in
 }
 
 // Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
-__device__ void nth_tail_wave(uint64_t* q, uint32_t* lpos, uint32_t* rpos, NthShared& sh, int64_t nth) {
+__device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DGC_LDS uint32_t* rpos, NthShared& sh,
+                              int64_t nth) {
     int64_t f = sh.f, l = sh.l, depth = sh.depth;
     const int lane = threadIdx.x & 63;
     K5_WSUB_BEGIN();
@@ -910,7 +1012,7 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
         if (keep) {
             for (int64_t t0 = wb; t0 < we; t0 += 256) {
                 const uint32_t m = mk[((t0 - bb) >> 8) * 64 + lane];
-                pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, PlainSlots{lpos, rpos}, paired, lnext,
+                pair_tile<false>(m & 15u, m >> 4, t0, f, TR, runl, runr, plain_slots(lpos, rpos), paired, lnext,
                                  rmin);
             }
         } else {
@@ -923,7 +1025,7 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
                 for (int u = 0; u < kB; ++u) {
                     uint32_t pl, pr;
                     stopper_masks(x[u], valid[u], P, pl, pr);
-                    pair_tile<false>(pl, pr, t0 + u * 256, f, TR, runl, runr, PlainSlots{lpos, rpos}, paired, lnext,
+                    pair_tile<false>(pl, pr, t0 + u * 256, f, TR, runl, runr, plain_slots(lpos, rpos), paired, lnext,
                                      rmin);
                 }
             }
@@ -940,7 +1042,7 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
         // pass 3: the swaps L_t <-> R_t, t < s, over all G workgroups
         if (threadIdx.x == 0) s_sh = __hip_atomic_load(&g->s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        nth_swaps<8>(q, PlainSlots{lpos, rpos}, f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
+        nth_swaps<8>(q, plain_slots(lpos, rpos), f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
         // the last arriver: the cut, the next range and the next median (all swaps visible)
         nthg_barrier(g, G, [&] {
             const int64_t rs = g->s ? (int64_t)g->r_min : g->l;
@@ -962,9 +1064,10 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
 // in the LDS phase, the stopper bytes in the global phase; llp / lrp (kNthPairLds
 // each) and lmk (kNthMkLds bytes): the LDS phase's pair slots and stopper bytes.
 // from: the state k_nth_global left (its global phase done), or null (start at [0, n)).
-__device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gpos_l, uint32_t* gpos_r,
-                               uint64_t* lq, uint32_t* llp, uint32_t* lrp, uint8_t* lmk,
-                               const NthG* from = nullptr) {
+__device__ __forceinline__ void nth_element_wg(DGC_GLB uint64_t* q, int64_t n, int64_t nth, DGC_GLB uint32_t* gpos_l,
+                                               DGC_GLB uint32_t* gpos_r, DGC_LDS uint64_t* lq, DGC_LDS uint32_t* llp,
+                                               DGC_LDS uint32_t* lrp, DGC_LDS uint8_t* lmk,
+                                               const NthG* from = nullptr) {
     __shared__ NthShared sh;
     if (threadIdx.x == 0) {
         sh.f = 0;
@@ -980,11 +1083,14 @@ __device__ void nth_element_wg(uint64_t* q, int64_t n, int64_t nth, uint32_t* gp
     }
     __syncthreads();
     if (n <= 0 || nth >= n) return;
+#ifdef DGC_K5_PROF
+    if (threadIdx.x == 0 && blockIdx.x < 64) g_k5prof.bn[blockIdx.x] = n;
+#endif
     K5_STAMP(0);
     // global phase: lq (unused until the LDS phase) holds the stopper bytes
     // the whole LDS area (lq, llp, lrp, lmk: contiguous, carved by the caller) is the
     // global phase's arena: stopper bytes + LDS pair slots
-    nth_loop_wg<8, 8, true>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<uint8_t*>(lq), 0,
+    nth_loop_wg<8, 8, true>(q, gpos_l, gpos_r, sh, nth, kNthLds, reinterpret_cast<DGC_LDS uint8_t*>(lq), 0,
                             kNthSmemBytes);
     K5_STAMP(1);
     if (sh.heap_exit) return;

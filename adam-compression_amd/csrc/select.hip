@@ -33,9 +33,10 @@
 //                resample / lower / raise / exhausted) + scan of the group totals.
 //                resample=True: the first "lower" hands over to ONE multi-threshold
 //                pass; resample=False: a recount per step.
-//   resample     nth_element path (< 64k candidates): the candidates are gathered in
-//                index order and torch's CPU topk is replayed exactly (K5,
-//                introselect.hpp); partial_sort path: radix k-th value, lowest-index ties.
+//   resample     torch's CPU topk replayed exactly: nth_element path (candidates <
+//                64 k): the candidates are gathered in index order and the introselect
+//                replayed (K5, introselect.hpp); partial_sort path: heap select +
+//                sort_heap over vec (K5b, heap_select_wg).
 //   emit         (1 workgroup per group): positions (after the tensors before it in
 //                the batch), fp32/fp16 values, int64/int32 indices, masking writes.
 //
@@ -101,16 +102,13 @@ struct TDesc {
 };
 
 struct SelState {
-    float t0, t_cur, tk, t_list;
+    float t0, t_cur, t_list;
     int32_t branch, iter, recounts, active;
     long long n_cur;       // count at t_cur
     long long limit;       // FIRSTK: emit the first `limit` candidates
-    long long n_greater;   // RESAMPLE: candidates > tk
-    long long tie_quota;   // RESAMPLE: k - n_greater ties, lowest index first
-    int32_t resample_pending, overflow, done, lower_pending;
+    int32_t overflow, done, lower_pending;
     int32_t full_passes, list_spills, epoch;
-    int32_t rs_nth;        // RESAMPLE: 1 = exact nth_element replay (K5), 2 = exact
-                           // partial_sort replay (K5b), 0 = radix + lowest-index ties
+    int32_t rs_nth;        // RESAMPLE: 1 = nth_element replay (K5), 2 = partial_sort replay (K5b)
     int32_t tie_rule;      // DGC_TIES_*: how the resample chose among boundary ties
     // Deferred momentum masking (DGCSGDMemory.update, dgc/memory.py:72-77): the last
     // call emitted "the first def_limit elements >= def_t" without zeroing them; the
@@ -155,17 +153,11 @@ struct SelWS {
     int32_t* small;            // tensors whose threshold runs in one workgroup
     uint32_t* seg_lcnt;        // list count at t_list (low 16 bits) | lmax_code (high 16 bits)
     uint32_t* seg_cnt;
-    uint32_t* seg_gt;
-    uint32_t* seg_eq;
     uint32_t* seg_off;         // in-group output offset of each segment's first emitted entry
     uint16_t* lst_off;
     float* lst_val;
-    unsigned long long* grp_cnt;   // grp_cnt, grp_gt, grp_eq: contiguous
-    unsigned long long* grp_gt;
-    unsigned long long* grp_eq;
+    unsigned long long* grp_cnt;
     long long* grp_off;
-    long long* grp_gt_off;
-    long long* grp_eq_off;
     uint64_t* queue;           // K5: (|x| key << 32 | j) for the candidates j, ascending index order
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
@@ -174,8 +166,8 @@ struct SelWS {
     int64_t nseg, ngrp;
 };
 
-// Candidates the exact resample replays: torch's CPU topk runs nth_element while
-// k * 64 > n (else partial_sort, which is not replayed), so at most 64k - 1 of them.
+// Candidates the nth_element replay (K5) gathers: torch's CPU topk runs nth_element
+// while k * 64 > n (else partial_sort, replayed over vec by K5b), so at most 64k - 1.
 __host__ __device__ inline int64_t nth_cand_cap(int64_t numel, int64_t k) {
     const int64_t c = 64 * k - 1;
     return c < numel ? c : numel;
@@ -304,16 +296,10 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     for (int which = 0; which < BT_COUNT; ++which) w.bt[which] = c.take<int32_t>(L.T + 1);
     w.small = c.take<int32_t>(L.T);
     w.samples = c.take<float>(L.nsamp);
-    w.grp_cnt = c.take<unsigned long long>(3 * L.ngrp);
-    w.grp_gt = w.grp_cnt ? w.grp_cnt + L.ngrp : nullptr;
-    w.grp_eq = w.grp_gt ? w.grp_gt + L.ngrp : nullptr;
+    w.grp_cnt = c.take<unsigned long long>(L.ngrp);
     w.grp_off = c.take<long long>(L.ngrp);
-    w.grp_gt_off = c.take<long long>(L.ngrp);
-    w.grp_eq_off = c.take<long long>(L.ngrp);
     w.seg_lcnt = c.take<uint32_t>(L.nseg);
     w.seg_cnt = c.take<uint32_t>(L.nseg);
-    w.seg_gt = c.take<uint32_t>(L.nseg);
-    w.seg_eq = c.take<uint32_t>(L.nseg);
     w.seg_off = c.take<uint32_t>(L.nseg);
     w.lst_off = c.take<uint16_t>(ceil_div(L.nseg, (int64_t)kLstTile) * kLstTile * kCap);
     w.lst_val = c.take<float>(ceil_div(L.nseg, (int64_t)kLstTile) * kLstTile * kCap);
@@ -687,11 +673,7 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         if (t == 0) *w.fin_ticket = 0;
     }
     __syncthreads();   // the caller's threshold (thr[t]) is written
-    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
-        w.grp_cnt[d.grp0 + i] = 0;
-        w.grp_gt[d.grp0 + i] = 0;
-        w.grp_eq[d.grp0 + i] = 0;
-    }
+    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) w.grp_cnt[d.grp0 + i] = 0;
     __shared__ uint32_t spills;
     if (threadIdx.x == 0) spills = 0;
     __syncthreads();
@@ -711,12 +693,10 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         st->list_spills = keep_lists ? (int32_t)spills : 0;
         // no K1 lists, or too many overflowed lists to be worth serving: one full pass
         if (!keep_lists || (int64_t)spills * kSpillDiv > d.nseg) st->t_list = __builtin_huge_valf();
-        st->tk = 0.f;
         st->branch = -1;
-        st->n_cur = st->limit = st->n_greater = st->tie_quota = 0;
+        st->n_cur = st->limit = 0;
         st->iter = st->recounts = 0;
         st->active = 1;
-        st->resample_pending = 0;
         st->overflow = 0;
         st->done = 0;
         st->lower_pending = 0;
@@ -1324,47 +1304,6 @@ __device__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d
     }
 }
 
-// RESAMPLE (partial_sort path): |x| > tk always, |x| == tk while the running tie rank is below T.
-__device__ void emit_reread_resample(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long bg,
-                                     long long bt, float tk, long long T, long long obase, const EmitOut& o) {
-    const int lane = threadIdx.x & 63;
-    uint32_t run_g = 0, run_t = 0;
-    float xs[kSegTiles][4];
-    uint32_t vs[kSegTiles];
-    load_segment(vec, d.n, ls, xs, vs);
-#pragma unroll
-    for (int tile = 0; tile < kSegTiles; ++tile) {
-        const float(&x)[4] = xs[tile];
-        const uint32_t valid = vs[tile];
-        const int64_t e0 = ls * kSeg + tile * 256 + 4 * lane;
-        uint32_t pg = 0, pe = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float a = fabsf(x[j]);
-            pg |= (uint32_t)(a > tk) << j;
-            pe |= (uint32_t)(a == tk) << j;
-        }
-        pg &= valid;
-        pe &= valid;
-        if (__ballot((pg | pe) != 0)) {
-            uint32_t lg, tg, lt, tt;
-            wave_prefix4(pg, lg, tg);
-            wave_prefix4(pe, lt, tt);
-            uint32_t rg = run_g + lg, rt = run_t + lt;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool gt = (pg >> j) & 1u, eq = (pe >> j) & 1u;
-                const long long tb = bt + rt;
-                if (gt || (eq && tb < T)) emit_one(o, d, obase + bg + rg + (tb < T ? tb : T), e0 + j, x[j]);
-                rg += gt;
-                rt += eq;
-            }
-            run_g += tg;
-            run_t += tt;
-        }
-    }
-}
-
 // kEmitSplit workgroups of kEmitSegs threads per group of kGroupSegs segments, one
 // thread per segment of its quarter. In-group offsets: the quarter's exclusive scan
 // plus the counts of the group's earlier quarters (read by the same threads, packed
@@ -1396,17 +1335,16 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     if (k5 && !oa.queue) return;
     EmitOut o = oa;
     if (!k5) o.queue = nullptr;
-    const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
-    const bool defer_here = o.defer && !rs && !k5 && !d.tail;
+    const bool defer_here = o.defer && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
     const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
     const int64_t lg = lb / kEmitSplit;                      // group within the tensor
     const int sub = (int)(lb % kEmitSplit);                  // its quarter
     const int64_t g = d.grp0 + lg;
     const int64_t lseg0 = lg * kGroupSegs + (int64_t)sub * kEmitSegs;   // first segment of the quarter
-    __shared__ uint32_t off_a[kEmitSegs], off_b[kEmitSegs], lcn[kEmitSegs];
+    __shared__ uint32_t off_a[kEmitSegs], lcn[kEmitSegs];
     __shared__ uint64_t lds16[16];
     __shared__ long long obase_s;
     if (threadIdx.x < kWave) {
@@ -1414,33 +1352,28 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
         if (threadIdx.x == 0) obase_s = b;
     }
     const long long limit = k5 ? st->n_cur : st->limit;
-    const long long T = st->tie_quota;
-    const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
-    const long long gb = rs ? w.grp_eq_off[g] : 0;
-    const float tc = st->t_cur, tk = st->tk;
+    const long long ga = w.grp_off[g];
+    const float tc = st->t_cur;
     {
         // thread jq <-> segment jq of the quarter, plus the earlier quarters' counts at
         // the same position
         const int jq = (int)threadIdx.x;
         const int64_t ls = lseg0 + jq;
-        const uint32_t* ca_src = rs ? w.seg_gt : w.seg_cnt;
-        uint32_t ca = 0, cb = 0, lc = 0, pa = 0, pb = 0;
+        uint32_t ca = 0, lc = 0, pa = 0;
         if (ls < d.nseg) {
             const int64_t seg = d.seg0 + ls;
-            ca = ca_src[seg];
-            if (rs) cb = w.seg_eq[seg];
+            ca = w.seg_cnt[seg];
             lc = lcnt_count(w.seg_lcnt[seg]);
         }
 #pragma unroll
         for (int q = 0; q < kEmitSplit - 1; ++q) {   // the same position in the group's earlier
             if (q < sub) {                             // quarters (loads in flight together)
                 const int64_t seg = d.seg0 + lg * kGroupSegs + (int64_t)q * kEmitSegs + threadIdx.x;
-                pa += ca_src[seg];
-                if (rs) pb += w.seg_eq[seg];
+                pa += w.seg_cnt[seg];
             }
         }
         // (a list with nothing at the current threshold is not read: most of them at 1e-4)
-        const bool short_list = ls < d.nseg && (ca > 0 || cb > 0) && lc <= (uint32_t)kEmitShort;
+        const bool short_list = ls < d.nseg && ca > 0 && lc <= (uint32_t)kEmitShort;
         float v[kEmitShort];
         uint16_t e[kEmitShort];
         if (short_list) {
@@ -1456,43 +1389,20 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
         uint64_t tot;
         const uint64_t ra = block_exclusive_scan(((uint64_t)pa << 32) | ca, lds16, &tot);
         const uint32_t oa = (uint32_t)(tot >> 32) + (uint32_t)ra;
-        uint32_t ob = 0;
-        if (rs) {
-            __syncthreads();
-            const uint64_t rb = block_exclusive_scan(((uint64_t)pb << 32) | cb, lds16, &tot);
-            ob = (uint32_t)(tot >> 32) + (uint32_t)rb;
-        }
-        const bool work = rs ? (ca > 0 || (cb > 0 && gb + ob < T)) : (ca > 0 && ga + oa < limit);
+        const bool work = ca > 0 && ga + oa < limit;
         if (defer_here && ls < d.nseg) w.seg_off[d.seg0 + ls] = oa;
         off_a[jq] = oa;
-        off_b[jq] = ob;
         lcn[jq] = (work && !short_list) ? lc : kEmitSkip;
         __syncthreads();   // obase_s
-        if (work && short_list) {
+        if (work && short_list) {   // the first `limit` entries >= tc, in index order
             const long long ob0 = obase_s;
-            if (!rs) {   // the first `limit` entries >= tc, in index order
-                long long pos = ga + oa;
+            long long pos = ga + oa;
 #pragma unroll
-                for (int j = 0; j < kEmitShort; ++j)
-                    if ((uint32_t)j < lc && fabsf(v[j]) >= tc) {
-                        if (pos < limit) emit_one(o, d, ob0 + pos, ls * kSeg + e[j], v[j], !defer_here);
-                        ++pos;
-                    }
-            } else {     // every entry > tk, and entries == tk while the tie rank is below T
-                long long rg = ga + oa, rt = gb + ob;
-#pragma unroll
-                for (int j = 0; j < kEmitShort; ++j) {
-                    if ((uint32_t)j >= lc) continue;
-                    const float a = fabsf(v[j]);
-                    if (a > tk) {
-                        emit_one(o, d, ob0 + rg + (rt < T ? rt : T), ls * kSeg + e[j], v[j]);
-                        ++rg;
-                    } else if (a == tk) {
-                        if (rt < T) emit_one(o, d, ob0 + rg + rt, ls * kSeg + e[j], v[j]);
-                        ++rt;
-                    }
+            for (int j = 0; j < kEmitShort; ++j)
+                if ((uint32_t)j < lc && fabsf(v[j]) >= tc) {
+                    if (pos < limit) emit_one(o, d, ob0 + pos, ls * kSeg + e[j], v[j], !defer_here);
+                    ++pos;
                 }
-            }
         }
     }
     __syncthreads();
@@ -1527,32 +1437,17 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
             const uint32_t L = lcn[j0 + q];
             if (L == kEmitSkip || L > (uint32_t)kCap) continue;
             const int64_t ls = lseg0 + j0 + q;
-            const long long ba = ga + off_a[j0 + q], bb = gb + off_b[j0 + q];
-            const bool in = (uint32_t)lane < L;
-            const float a = fabsf(x[q]);
-            const int64_t li = ls * kSeg + e[q];
-            if (!rs) {
-                const bool sel = in && a >= tc;
-                const uint64_t m = __ballot(sel);
-                const long long pos = ba + __popcll(m & lt);
-                if (sel && pos < limit) emit_one(o, d, obase + pos, li, x[q], !defer_here);
-            } else {
-                const bool gt = in && a > tk, eq = in && a == tk;
-                const uint64_t mg = __ballot(gt), me = __ballot(eq);
-                const long long tb = bb + __popcll(me & lt);
-                if (gt || (eq && tb < T)) emit_one(o, d, obase + ba + __popcll(mg & lt) + (tb < T ? tb : T), li, x[q]);
-            }
+            const long long ba = ga + off_a[j0 + q];
+            const bool sel = (uint32_t)lane < L && fabsf(x[q]) >= tc;
+            const uint64_t m = __ballot(sel);
+            const long long pos = ba + __popcll(m & lt);
+            if (sel && pos < limit) emit_one(o, d, obase + pos, ls * kSeg + e[q], x[q], !defer_here);
         }
     }
     while (spilled) {   // rare: one wave re-reads the segment's 1024 elements
         const int j = jw + __builtin_ctzll(spilled);
         spilled &= spilled - 1;
-        const int64_t ls = lseg0 + j;
-        const long long ba = ga + off_a[j], bb = gb + off_b[j];
-        if (rs)
-            emit_reread_resample(vec, d, ls, ba, bb, tk, T, obase, o);
-        else
-            emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o, !defer_here);
+        emit_reread_firstk(vec, d, lseg0 + j, ga + off_a[j], limit, obase, tc, o, !defer_here);
     }
 }
 
@@ -1574,10 +1469,9 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     if (k5 && !oa.queue) return;
     EmitOut o = oa;
     if (!k5) o.queue = nullptr;
-    const bool rs = st->branch == DGC_BRANCH_RESAMPLE && !k5;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
-    const bool defer_here = o.defer && !rs && !k5 && !d.tail;
+    const bool defer_here = o.defer && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
     const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
     constexpr int split = kEmitSplit;
@@ -1585,7 +1479,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     const int sub = (int)(lb % split);                       // its share this workgroup emits
     const int64_t g = d.grp0 + lg;
     const int64_t lseg0 = lg * kGroupSegs;
-    __shared__ uint32_t off_a[kGroupSegs], off_b[kGroupSegs], lcn[kGroupSegs];
+    __shared__ uint32_t off_a[kGroupSegs], lcn[kGroupSegs];
     __shared__ uint64_t lds16[16];
     __shared__ long long obase_s;
     if (threadIdx.x < kWave) {
@@ -1593,32 +1487,26 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
         if (threadIdx.x == 0) obase_s = b;
     }
     const long long limit = k5 ? st->n_cur : st->limit;
-    const long long T = st->tie_quota;
-    const long long ga = rs ? w.grp_gt_off[g] : w.grp_off[g];
-    const long long gb = rs ? w.grp_eq_off[g] : 0;
+    const long long ga = w.grp_off[g];
     {
         const int64_t ls = lseg0 + threadIdx.x;
-        uint32_t ca = 0, cb = 0, lc = 0;
+        uint32_t ca = 0, lc = 0;
         if (ls < d.nseg) {
             const int64_t seg = d.seg0 + ls;
-            ca = rs ? w.seg_gt[seg] : w.seg_cnt[seg];
-            cb = rs ? w.seg_eq[seg] : 0;
+            ca = w.seg_cnt[seg];
             lc = lcnt_count(w.seg_lcnt[seg]);
         }
         uint64_t tot;
         const uint32_t oa = (uint32_t)block_exclusive_scan((uint64_t)ca, lds16, &tot);
-        __syncthreads();
-        const uint32_t ob = rs ? (uint32_t)block_exclusive_scan((uint64_t)cb, lds16, &tot) : 0u;
-        const bool work = rs ? (ca > 0 || (cb > 0 && gb + ob < T)) : (ca > 0 && ga + oa < limit);
+        const bool work = ca > 0 && ga + oa < limit;
         if (defer_here && ls < d.nseg && (int)threadIdx.x / (kGroupSegs / split) == sub)
             w.seg_off[d.seg0 + ls] = oa;
         off_a[threadIdx.x] = oa;
-        off_b[threadIdx.x] = ob;
         lcn[threadIdx.x] = work ? lc : kEmitSkip;
     }
     __syncthreads();
     const long long obase = obase_s;
-    const float tc = st->t_cur, tk = st->tk;
+    const float tc = st->t_cur;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt();
     constexpr int wave_segs = kGroupSegs / split / (kGroupSegs / kWave);
@@ -1643,28 +1531,15 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
             const uint32_t L = lcn[j0 + q];
             if (L == kEmitSkip) continue;
             const int64_t ls = lseg0 + j0 + q;
-            const long long ba = ga + off_a[j0 + q], bb = gb + off_b[j0 + q];
+            const long long ba = ga + off_a[j0 + q];
             if (L > (uint32_t)kCap) {
-                if (rs)
-                    emit_reread_resample(vec, d, ls, ba, bb, tk, T, obase, o);
-                else
-                    emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o, !defer_here);
+                emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o, !defer_here);
                 continue;
             }
-            const bool in = (uint32_t)lane < L;
-            const float a = fabsf(x[q]);
-            const int64_t li = ls * kSeg + e[q];
-            if (!rs) {
-                const bool sel = in && a >= tc;
-                const uint64_t m = __ballot(sel);
-                const long long pos = ba + __popcll(m & lt);
-                if (sel && pos < limit) emit_one(o, d, obase + pos, li, x[q], !defer_here);
-            } else {
-                const bool gt = in && a > tk, eq = in && a == tk;
-                const uint64_t mg = __ballot(gt), me = __ballot(eq);
-                const long long tb = bb + __popcll(me & lt);
-                if (gt || (eq && tb < T)) emit_one(o, d, obase + ba + __popcll(mg & lt) + (tb < T ? tb : T), li, x[q]);
-            }
+            const bool sel = (uint32_t)lane < L && fabsf(x[q]) >= tc;
+            const uint64_t m = __ballot(sel);
+            const long long pos = ba + __popcll(m & lt);
+            if (sel && pos < limit) emit_one(o, d, obase + pos, ls * kSeg + e[q], x[q], !defer_here);
         }
     }
 }
@@ -1799,12 +1674,12 @@ constexpr size_t kK5SmemBytes = kHeapSmemBytes > kNthSmemBytes ? kHeapSmemBytes 
 __device__ __forceinline__ uint32_t hkey(uint64_t e) { return (uint32_t)(e >> kHeapKeyShift); }
 
 struct HeapNodes {
-    uint64_t* lds;   // nodes [0, kHeapTop)
-    uint64_t* g;     // nodes >= kHeapTop (indexed by node)
-    __device__ __forceinline__ uint64_t ld(int64_t i) const { return i < kHeapTop ? lds[i] : g[i]; }
+    DGC_LDS uint64_t* l;   // nodes [0, kHeapTop)
+    DGC_GLB uint64_t* g;   // nodes >= kHeapTop (indexed by node)
+    __device__ __forceinline__ uint64_t ld(int64_t i) const { return i < kHeapTop ? l[i] : g[i]; }
     __device__ __forceinline__ void st(int64_t i, uint64_t v) const {
         if (i < kHeapTop)
-            lds[i] = v;
+            l[i] = v;
         else
             g[i] = v;
     }
@@ -1950,7 +1825,7 @@ __device__ __forceinline__ uint32_t heap_cands(int64_t n, int64_t c0, float tc, 
 // batch in flight; f(c0, x) returns false to stop (uniformly). Returns the chunk it
 // stopped at (n rounded up to a chunk when it ran to the end).
 template <class F>
-__device__ int64_t heap_stream(const float* vec, int64_t n, int64_t c_begin, bool al, F&& f) {
+__device__ __forceinline__ int64_t heap_stream(const float* vec, int64_t n, int64_t c_begin, bool al, F&& f) {
     constexpr int64_t kBatch = (int64_t)kHeapAhead * kHeapChunk;
     float xa[kHeapAhead][4], xb[kHeapAhead][4];
 #pragma unroll
@@ -1972,7 +1847,7 @@ __device__ int64_t heap_stream(const float* vec, int64_t n, int64_t c_begin, boo
     return n;
 }
 
-__device__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o, int t,
+__device__ __forceinline__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o, int t,
                                uint64_t* smem) {
     const SelState* st = w.st + t;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -1980,7 +1855,7 @@ __device__ void heap_select_wg(const float* __restrict__ vec_flat, const SelWS& 
     const float tc = st->t_cur;
     const int64_t k = d.k, n = d.n;
     const bool al = aligned16(vec);
-    const HeapNodes h{smem, w.queue + d.cand_off};
+    const HeapNodes h{lds(smem), glb(w.queue + d.cand_off)};
     uint64_t* hot = smem + kHeapTop + 1;
     __shared__ uint64_t lds16[16];
     __shared__ uint64_t root_sh;
@@ -2110,19 +1985,22 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
     __shared__ __align__(16) uint64_t smem[kK5SmemBytes / 8];
+    K5_STAMP(7);
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) {   // uniform per workgroup
         heap_select_wg(vec_flat, w, o, t, smem);
     } else if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1) {
         const TDesc d = w.td[t];   // by value: stores below cannot alias it
-        uint32_t* gl = w.gpos + d.gpos_off;
-        uint32_t* gr = gl + d.cand_cap / 2 + 1;
-        uint32_t* llp = reinterpret_cast<uint32_t*>(smem + kNthLds);
-        uint32_t* lrp = llp + kNthPairLds;
-        uint8_t* lmk = reinterpret_cast<uint8_t*>(lrp + kNthPairLds);
-        nth_element_wg(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, smem, llp, lrp, lmk,
+        DGC_GLB uint32_t* gl = glb(w.gpos + d.gpos_off);
+        DGC_GLB uint32_t* gr = gl + d.cand_cap / 2 + 1;
+        DGC_LDS uint64_t* lq = lds(smem);
+        DGC_LDS uint32_t* llp = reinterpret_cast<DGC_LDS uint32_t*>(lq + kNthLds);
+        DGC_LDS uint32_t* lrp = llp + kNthPairLds;
+        DGC_LDS uint8_t* lmk = reinterpret_cast<DGC_LDS uint8_t*>(lrp + kNthPairLds);
+        nth_element_wg(glb(w.queue + d.cand_off), st->n_cur, d.k - 1, gl, gr, lq, llp, lrp, lmk,
                        from_global ? w.nthg + t : nullptr);
     }
     if (f.on && last_block_arrival(w.fin_ticket, gridDim.x)) sel_finish_body(w, f);
+    K5_STAMP(6);
 }
 
 __global__ void k_spec_reset(float* spec, int32_t T) {
@@ -2173,8 +2051,8 @@ static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const 
 // but cost ~29 us per launch on MI355X: more than the phase saves below ~200k candidates.)
 // <= 1 runs the one-workgroup global phase inside k_nth_select instead; so does a call
 // whose tensors all have candidate capacities <= kNthGMinCand, and so does a tensor
-// with <= kNthGMinCand candidates (decided on the device: below ~140k the four
-// cross-XCD barriers per step cost more than the spread saves, tools/k5ab.sh), and
+// with <= kNthGMinCand candidates (decided on the device: below ~100k the three
+// cross-XCD barriers per step cost as much as the spread saves, tools/run_k5.sh), and
 // DGC_K5_GLOBAL=wg (A/B, parity); DGC_K5_GLOBAL=multi skips both gates.
 constexpr int64_t kNthGMinCand = 98304;    // launch for capacities above, run for candidate counts above
 
@@ -2199,7 +2077,10 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
     // from 40k candidates made ResNet-50 0.358 -> 0.373 ms (864 workgroups launched per
     // step, and at 45-57k candidates the spread phase is no faster than one workgroup:
     // 0.141-0.144 ms either way); it pays from ~100k (500k: 0.945 -> 0.371 ms)
+    // fewer than 4 per tensor (a batch of many tensors: ResNet-50's 54) spread too little
+    // to pay the barriers, and the launch alone is ~5.7 us per step (rocprofv3)
     const int64_t g = T > 0 ? per_dev / T : 0;
+    if (g < 4 && !multi) return 0;
     return (uint32_t)std::min<int64_t>(g, kNthGMax);
 }
 

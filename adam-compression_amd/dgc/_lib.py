@@ -21,7 +21,7 @@ SYNC_DEVICE, SYNC_HOST = 0, 1
 VD = {torch.float32: 0, torch.float16: 1}
 ID = {torch.int64: 0, torch.int32: 1}
 BRANCHES = {0: "direct", 1: "ok", 2: "trunc", 3: "resample", 4: "exhausted"}
-TIE_RULES = {0: "none", 1: "exact", 2: "lowest_index"}
+TIE_RULES = {0: "none", 1: "exact"}
 
 
 class SelectParams(ctypes.Structure):

@@ -74,13 +74,12 @@ enum dgc_branch {
     DGC_BRANCH_EXHAUSTED = 4  /* max_adaptation_iters recounts used up    */
 };
 
-/* How a resample chose among the candidates tied at its k-th value. */
+/* How a resample chose among the candidates tied at its k-th value: always torch's
+ * CPU topk replayed exactly, on both of its paths (nth_element for k*64 > n candidates,
+ * partial_sort otherwise) — the reference's indices in the reference's order. */
 enum dgc_tie_rule {
-    DGC_TIES_NONE = 0,          /* no resample this call                                   */
-    DGC_TIES_EXACT = 1,         /* torch's CPU topk replayed (nth_element path, k*64 > n):  */
-                                /* the reference's indices in the reference's order         */
-    DGC_TIES_LOWEST_INDEX = 2   /* partial_sort path (k*64 <= n candidates, not replayed):  */
-                                /* strictly greater, then the lowest-index ties, ascending  */
+    DGC_TIES_NONE = 0,   /* no resample this call */
+    DGC_TIES_EXACT = 1   /* torch's topk replayed */
 };
 
 /* Per-tensor selection parameters: DGCCompressor.attributes[name]

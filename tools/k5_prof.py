@@ -23,7 +23,8 @@ from k5_bench import select_case  # noqa: E402
 
 
 class K5Prof(ctypes.Structure):
-    _fields_ = [("t", ctypes.c_uint64 * 8), ("steps", ctypes.c_uint32 * 4), ("sub", ctypes.c_uint64 * 8)]
+    _fields_ = [("t", ctypes.c_uint64 * 8), ("steps", ctypes.c_uint32 * 4), ("sub", ctypes.c_uint64 * 8),
+                ("bt", (ctypes.c_uint64 * 8) * 64), ("bn", ctypes.c_int64 * 64)]
 
 
 def main():
@@ -47,10 +48,10 @@ def main():
             ph = dict(global_us=t[1] - t[0], load_us=t[2] - t[1], lds_us=t[3] - t[2], wave_us=t[4] - t[3],
                       store_us=t[5] - t[4], total_us=t[5] - t[0], g_pass1_us=p.sub[0] * 0.01,
                       g_pass2_us=p.sub[1] * 0.01, g_swap_us=p.sub[2] * 0.01, g_prepare_us=p.sub[3] * 0.01,
-                      w_median_us=p.sub[4] * 0.01, w_pair_us=p.sub[5] * 0.01, w_swap_us=p.sub[6] * 0.01)
+                      w_median_us=p.sub[4] * 0.01, w_pair_us=p.sub[5] * 0.01, w_swap_us=p.sub[6] * 0.01, g_pass2_loop_w0_us=p.sub[7] * 0.01)
             best = ph if best is None else {key: min(v, ph[key]) for key, v in best.items()}
         r.update({key: round(v, 1) for key, v in best.items()})
-        r.update(steps_global=p.steps[0], steps_lds=p.steps[1], steps_wave=p.steps[2])
+        r.update(steps_global=p.steps[0], steps_lds=p.steps[1], steps_wave=p.steps[2], g_mixed_tiles=p.steps[3])
         print(json.dumps(r), flush=True)
 
 

@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out/k5
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -q -x --timeout 600 --timeout-method thread -m gpu tests \
-    -k "replays_torch_topk or partial_sort or batch_matches or steady or k5" > gpurun_out/k5/tests.log 2>&1 \
+    -k "replays_torch_topk or partial_sort or batch_matches or steady or k5 or decompress" > gpurun_out/k5/tests.log 2>&1 \
     || { tail -30 gpurun_out/k5/tests.log; exit 1; }
 tail -2 gpurun_out/k5/tests.log
 for wl in resnet50 vgg16_bn; do
@@ -17,4 +17,4 @@ for mode in wg default multi; do
   K5_MODELS=0 timeout -k 10 300 python tools/k5_bench.py > gpurun_out/k5/k5bench_$mode.txt 2>&1 || exit $?
 done
 unset DGC_K5_GLOBAL
-tail -12 gpurun_out/k5/k5bench_*.txt
+tail -n 12 gpurun_out/k5/k5bench_*.txt
