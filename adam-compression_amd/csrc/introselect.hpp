@@ -221,22 +221,30 @@ __device__ __forceinline__ int64_t nth_base(QP q, int64_t a0) {
 // or split (the one-workgroup global phase): slots t < cap in LDS, the rest in global
 // memory — a 57k-candidate step swaps ~14k pairs, whose 4-B slot stores and loads
 // were most of its time in global memory.
+// fast / fl / fr: all slots below `end` in LDS (a uniform test), and the store there
+// for element `on` of a lane — unconditional: an element that is no stopper writes the
+// lane's word of a 64-word dummy instead. (A store under `if` became an exec-mask
+// branch around it, four per tile in the pairing pass.)
 template <class SP>
 struct PlainSlotsT {
     SP l;
     SP r;
+    SP d;   // the dummy words (LDS slots only)
     __device__ __forceinline__ void put_l(uint32_t t, uint32_t v) const { l[t] = v; }
     __device__ __forceinline__ void put_r(uint32_t t, uint32_t v) const { r[t] = v; }
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[t]; }
-    // all slots below `end` in the fast store (uniform test), and that store
     __device__ __forceinline__ bool fast(uint32_t) const { return true; }
-    __device__ __forceinline__ void fl(uint32_t t, uint32_t v) const { l[t] = v; }
-    __device__ __forceinline__ void fr(uint32_t t, uint32_t v) const { r[t] = v; }
+    __device__ __forceinline__ void fl(bool on, uint32_t t, uint32_t v) const {
+        *(on ? l + t : d + (threadIdx.x & 63)) = v;
+    }
+    __device__ __forceinline__ void fr(bool on, uint32_t t, uint32_t v) const {
+        *(on ? r + t : d + (threadIdx.x & 63)) = v;
+    }
 };
 
 template <class SP>
-__device__ __forceinline__ PlainSlotsT<SP> plain_slots(SP l, SP r) { return PlainSlotsT<SP>{l, r}; }
+__device__ __forceinline__ PlainSlotsT<SP> plain_slots(SP l, SP r, SP d = nullptr) { return PlainSlotsT<SP>{l, r, d}; }
 
 struct SplitSlots {
     DGC_LDS uint32_t* ll;   // cap each
@@ -244,6 +252,7 @@ struct SplitSlots {
     uint32_t cap;
     DGC_GLB uint32_t* gl;   // indexed by t
     DGC_GLB uint32_t* gr;
+    DGC_LDS uint32_t* d;    // the dummy words
     __device__ __forceinline__ void put_l(uint32_t t, uint32_t v) const {
         if (t < cap)
             ll[t] = v;
@@ -259,8 +268,12 @@ struct SplitSlots {
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return t < cap ? ll[t] : gl[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return t < cap ? lr[t] : gr[t]; }
     __device__ __forceinline__ bool fast(uint32_t end) const { return end <= cap; }
-    __device__ __forceinline__ void fl(uint32_t t, uint32_t v) const { ll[t] = v; }
-    __device__ __forceinline__ void fr(uint32_t t, uint32_t v) const { lr[t] = v; }
+    __device__ __forceinline__ void fl(bool on, uint32_t t, uint32_t v) const {
+        *(on ? ll + t : d + (threadIdx.x & 63)) = v;
+    }
+    __device__ __forceinline__ void fr(bool on, uint32_t t, uint32_t v) const {
+        *(on ? lr + t : d + (threadIdx.x & 63)) = v;
+    }
 };
 
 // The step's swaps L_t <-> R_t, t < s (disjoint positions), by threads tid of nt:
@@ -519,8 +532,7 @@ __device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t
                                                 (mbcnt64(bl[2], 0u) + mbcnt64(bl[3], 0u)));
                     if (sl.fast(runl + tl)) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if ((pl >> j) & 1u) sl.fl(r0 + __popc(pl & below[j]), rel0 + (uint32_t)j);
+                        for (int j = 0; j < 4; ++j) sl.fl((pl >> j) & 1u, r0 + __popc(pl & below[j]), rel0 + (uint32_t)j);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
@@ -536,7 +548,7 @@ __device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t
                     if (sl.fast((uint32_t)from)) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            if ((pr >> j) & 1u) sl.fr(TR - 1u - r0 - __popc(pr & below[j]), rel0 + (uint32_t)j);
+                            sl.fr((pr >> j) & 1u, TR - 1u - r0 - __popc(pr & below[j]), rel0 + (uint32_t)j);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
@@ -635,6 +647,7 @@ __device__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& sh, int64_t nth, 
         return true;
     };
     __shared__ int go;
+    __shared__ uint32_t dummy[kWave];   // the unconditional slot stores' sink (PlainSlotsT::fl)
     if (threadIdx.x == 0) go = !sh.heap_exit && prepare();
     __syncthreads();
     while (go) {
@@ -646,10 +659,10 @@ __device__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& sh, int64_t nth, 
             const size_t off = (mk_bytes + 15) & ~(size_t)15;
             const uint32_t cap = (uint32_t)((arena_bytes - off) / 8);
             DGC_LDS uint32_t* ll = reinterpret_cast<DGC_LDS uint32_t*>(mk + off);
-            const SplitSlots sl{ll, ll + cap, cap, lpos, rpos};
+            const SplitSlots sl{ll, ll + cap, cap, lpos, rpos, lds(dummy)};
             nth_step_wg<kNthBatch, kSwapBatch>(q, sl, sh, mk, mk_bytes ? tiles : 0);
         } else {
-            nth_step_wg<kNthBatch, kSwapBatch>(q, plain_slots(lpos, rpos), sh, mk, mk_tiles);
+            nth_step_wg<kNthBatch, kSwapBatch>(q, plain_slots(lpos, rpos, lds(dummy)), sh, mk, mk_tiles);
         }
         K5_SUB_BEGIN();
         if (threadIdx.x == 0) {
@@ -685,6 +698,8 @@ __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DG
     const uint32_t P = qkey(q[f]);
     const int64_t a0 = f + 1, base = nth_base(q, a0);
     const uint32_t below[4] = {0u, 1u, 3u, 7u};
+    __shared__ uint32_t dummy_s[kWave];
+    DGC_LDS uint32_t* dummy = lds(dummy_s);
     uint32_t runl = 0, runr = 0;
 #pragma unroll
     for (int u = 0; u < kTiles; ++u) {
@@ -699,9 +714,9 @@ __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DG
         wave_prefix4(pr, br, tr);
         const uint32_t rel0 = (uint32_t)(t0 - f) + 4u * (uint32_t)lane;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if ((pl >> j) & 1u) lpos[runl + bl + (uint32_t)__popc(pl & below[j])] = rel0 + (uint32_t)j;
-            if ((pr >> j) & 1u) rpos[runr + br + (uint32_t)__popc(pr & below[j])] = rel0 + (uint32_t)j;
+        for (int j = 0; j < 4; ++j) {   // unconditional stores (see PlainSlotsT::fl)
+            *(((pl >> j) & 1u) ? lpos + runl + bl + (uint32_t)__popc(pl & below[j]) : dummy + lane) = rel0 + (uint32_t)j;
+            *(((pr >> j) & 1u) ? rpos + runr + br + (uint32_t)__popc(pr & below[j]) : dummy + lane) = rel0 + (uint32_t)j;
         }
         runl += tl;
         runr += tr;
