@@ -867,26 +867,31 @@ struct SampleKeys {
 // in the list, NaN and inf keys included — so the three passes read the list (~3 ks
 // keys in the steady state) instead of the S samples. The result is the same either
 // way. An unpadded tail's samples are written outside K1: no list then.
-__global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w) {
+// ks1 > 0: tensor 0's top_k_samples (the one-tensor compress: dgc_compress_begin's
+// table was laid out without it, and this saves re-uploading the table).
+__device__ __forceinline__ int64_t ks_of(const TDesc& d, int t, int64_t ks1) { return ks1 > 0 && t == 0 ? ks1 : d.ks; }
+
+__global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w, int64_t ks1) {
     const int t = blockIdx.x;
     if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const int64_t ks = ks_of(d, t, ks1);
     RSState* rs = w.rs + t;
-    rs_reset(rs, (uint64_t)d.ks);
+    rs_reset(rs, (uint64_t)ks);
     if (threadIdx.x == 0 && d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
         const SelState* st = w.st + t;
         const uint32_t cnt = st->win_cnt[st->epoch & 1];
-        if (cnt >= (uint64_t)d.ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
+        if (cnt >= (uint64_t)ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
     }
 }
 
 // One workgroup per small tensor: all three passes from LDS, then the tensor's
 // selection state reset (sel_init_tensor).
-__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat) {
+__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat, int64_t ks1) {
     const int t = w.small[blockIdx.x];
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
-    rs_small_wg(x, w.scnt[t], (uint64_t)d.ks, w.thr + t);
+    rs_small_wg(x, w.scnt[t], (uint64_t)ks_of(d, t, ks1), w.thr + t);
     sel_init_tensor(w, t, 1);
 }
 
@@ -2288,13 +2293,13 @@ int kth_largest(const float* x, int64_t n, int64_t k, float* out, void* ws, size
 
 // K3 of every tensor of the call: the small ones in one workgroup each, the rest in
 // three multi-block passes.
-static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStream_t s) {
+static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStream_t s, int64_t ks1 = 0) {
     if (L.nsmall) {
-        hipLaunchKernelGGL(k_rs_small_multi, dim3((unsigned)L.nsmall), dim3(kScanThreads), 0, s, w, vec);
+        hipLaunchKernelGGL(k_rs_small_multi, dim3((unsigned)L.nsmall), dim3(kScanThreads), 0, s, w, vec, ks1);
         DGC_LAUNCHED();
     }
     if (L.grid[BT_SAMP] > 0) {
-        hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w);
+        hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w, ks1);
         DGC_LAUNCHED();
         DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
     }
@@ -2397,9 +2402,9 @@ int compress_finish(float* vec, float* mmt, int64_t s_start, int64_t s_stride, i
     SelWS w;
     OneTable ot{};
     DGC_TRY(one_ws(p, s_start, s_stride, top_k_samples, spec, ws, ws_bytes, L, w, ot));
-    hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);   // begin's table had no top_k_samples
-    DGC_LAUNCHED();
-    DGC_TRY(thresholds(w, L, vec, s));
+    // the table dgc_compress_begin wrote serves as is (the layout does not depend on
+    // top_k_samples); K3 gets top_k_samples in its arguments
+    DGC_TRY(thresholds(w, L, vec, s, top_k_samples));
     dgc_select_params q = *p;
     // DGCSGDMemory.update fused into the emit (1), or deferred into the next K1 (2)
     q.update_memory = p->update_memory == 2 ? 2 : 1;
