@@ -119,6 +119,9 @@ struct SelState {
     long long def_limit;
     uint32_t tickets[4];
     uint32_t tk8[9];       // sharded arrival of the count passes (last_block_arrival8)
+    uint32_t ce_ticket;    // k_count_emit: groups in ticket order (look-back)
+    int32_t ce_fail;       // k_count_emit: a look-back timed out (its emit is not trusted)
+    int32_t spec_emitted;  // k_count_emit's first-k payload stands: k_emit skips the tensor
     // Segments whose K1 list overflowed, counted by K1 into slot [epoch & 1] (64
     // shards against atomic contention); k_sel_init reads it and zeroes the other
     // slot for the next call, k_sel_finish advances the epoch.
@@ -158,6 +161,7 @@ struct SelWS {
     float* lst_val;
     unsigned long long* grp_cnt;
     long long* grp_off;
+    unsigned long long* grp_lb;    // k_count_emit's decoupled look-back words, one per group
     uint64_t* queue;           // K5: (|x| key << 32 | j) for the candidates j, ascending index order
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
@@ -187,6 +191,7 @@ struct Layout {
     int64_t max_cand = 0;       // the largest K5 candidate capacity of a tensor
     int32_t nsmall = 0;
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
+    bool tail_any = false;      // some tensor is compensated partly outside K1 (unpadded tail)
     int64_t grid[BT_COUNT] = {};
 };
 
@@ -256,6 +261,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.idx_base = T > 1 ? d.off : 0;
         d.nv4 = padded ? ceil_div(d.n, (int64_t)4) : d.n / 4;
         d.tail = (!padded && (d.n & 3)) ? 1 : 0;
+        L.tail_any |= d.tail != 0;
         d.inv_stride = 1.0 / (double)(d.stride > 0 ? d.stride : 1);
         d.inv_stride_f = 1.0f / (float)(d.stride > 0 ? d.stride : 1);
         seg_end = std::max(seg_end, d.seg0 + d.nseg);
@@ -298,6 +304,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.samples = c.take<float>(L.nsamp);
     w.grp_cnt = c.take<unsigned long long>(L.ngrp);
     w.grp_off = c.take<long long>(L.ngrp);
+    w.grp_lb = c.take<unsigned long long>(L.ngrp);
     w.seg_lcnt = c.take<uint32_t>(L.nseg);
     w.seg_cnt = c.take<uint32_t>(L.nseg);
     w.seg_off = c.take<uint32_t>(L.nseg);
@@ -673,7 +680,10 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         if (t == 0) *w.fin_ticket = 0;
     }
     __syncthreads();   // the caller's threshold (thr[t]) is written
-    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) w.grp_cnt[d.grp0 + i] = 0;
+    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
+        w.grp_cnt[d.grp0 + i] = 0;
+        w.grp_lb[d.grp0 + i] = 0;
+    }
     __shared__ uint32_t spills;
     if (threadIdx.x == 0) spills = 0;
     __syncthreads();
@@ -706,6 +716,9 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         for (int i = 0; i < 4; ++i) st->tickets[i] = 0;
         for (int i = 0; i < 9; ++i) st->tk8[i] = 0;
         for (int i = 0; i <= kMaxLower; ++i) st->lower_cnt[i] = 0;
+        st->ce_ticket = 0;
+        st->ce_fail = 0;
+        st->spec_emitted = 0;
     }
 }
 
@@ -752,7 +765,7 @@ __device__ uint64_t block_scan_array(const unsigned long long* a, long long* out
 // without resample the threshold may also rise, and each step is a recount (count
 // pass + decide), like the reference. The group totals are other workgroups' device
 // atomics of this launch: read with agent-scope loads (last_block_arrival).
-__device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t) {
+__device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t, int spec = 0) {
     SelState* st = w.st + t;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     __shared__ uint64_t lds16[16];
@@ -811,6 +824,8 @@ __device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t) {
         } else if (done == 1) {
             st->active = 0;
             st->done = 1;
+            // a first-k branch after k_count_emit: its speculative payload is the emit
+            if (spec && st->branch != DGC_BRANCH_RESAMPLE && !st->ce_fail) st->spec_emitted = 1;
         } else {
             st->active = 0;
         }
@@ -1334,6 +1349,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     const int t = task(w, BT_GRP, blockIdx.x);
     const SelState* st = w.st + t;
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
+    if (st->spec_emitted) return;                                        // k_count_emit did
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
     // oa.queue set: the K5 tensors gather their candidates into the queue and the
     // others emit their payload in the same launch; unset: the K5 tensors are skipped
@@ -1468,6 +1484,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     const int t = task(w, BT_GRP, blockIdx.x);
     const SelState* st = w.st + t;
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
+    if (st->spec_emitted) return;                                        // k_count_emit did
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
     // oa.queue set: the K5 tensors gather their candidates into the queue and the
     // others emit their payload in the same launch; unset: the K5 tensors are skipped
@@ -1547,6 +1564,223 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
             if (sel && pos < limit) emit_one(o, d, obase + pos, ls * kSeg + e[q], x[q], !defer_here);
         }
     }
+}
+
+// The first count pass of a ONE-tensor call whose lists serve t_cur (the flat
+// bucket's steady state), fused with a speculative first-k emit: k_count_lists and
+// k_emit read the same list lines one after the other (flat-1B: 32 + 57 us, 7B:
+// 112 + 132 us). One workgroup per group, in ticket order; a thread counts four
+// consecutive segments, whose list entries e share one 16-B word of a 128-B line.
+// The group's offset comes from a decoupled look-back over the earlier groups' words
+// (aggregate, then inclusive prefix; a group only waits for groups that took their
+// ticket before it, so all of them are running). Every entry >= t_cur at a position
+// < k is written: exactly the payload of every first-k branch (ok, trunc, direct,
+// exhausted: the first min(count, k)). When decide picks one, spec_emitted makes
+// k_emit skip the tensor; otherwise (resample, lower) the later passes emit again
+// over it. Host-gated to calls whose emit would not mask (deferred or pure selection)
+// and whose payload starts at slot 0 (one tensor).
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbPre = 1ull << 63, kLbVal = kLbAgg - 1;
+constexpr int kLbSpin = 1 << 22;   // polls (with s_sleep) before a look-back gives up: ~seconds
+constexpr int kCeStage = 2048;     // entries a group stages in LDS for coalesced payload writes
+#ifdef DGC_K5_PROF
+__device__ unsigned long long g_ce_prof[2048][6];   // tools/ce_prof.py: per-group phase stamps
+#define CE_STAMP(i) do { if (threadIdx.x == 0 && lg < 2048) g_ce_prof[lg][i] = wall_clock64(); } while (0)
+#else
+#define CE_STAMP(i) do { } while (0)
+#endif
+
+__global__ void __launch_bounds__(kBlock)
+k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
+    static_assert(kBlock * kCountSegs == kGroupSegs && kCountSegs == kLstTile, "k_count_emit layout");
+    SelState* st = w.st;
+    if (!st->active || !(st->t_cur >= st->t_list)) return;
+    const TDesc d = w.td[0];   // by value: stores below cannot alias it
+    const float* vec = vec_flat + d.off;
+    const float tc = st->t_cur;
+    const uint32_t tkey = abs_key(tc);
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    __shared__ uint32_t lg_s;
+    __shared__ int nspill;
+    __shared__ int spill[kGroupSegs];
+    __shared__ uint32_t spill_cnt[kGroupSegs];   // a spilled segment's count, then its offset
+    __shared__ uint64_t lds16[16];
+    __shared__ unsigned long long prefix_s;
+    __shared__ float stage_v[kCeStage];
+    __shared__ uint32_t stage_i[kCeStage];
+    if (tid == 0) {
+        lg_s = atomicAdd(&st->ce_ticket, 1u);
+        nspill = 0;
+    }
+    __syncthreads();
+    const int64_t lg = lg_s;
+    CE_STAMP(0);
+    const int64_t ls0 = lg * kGroupSegs + kCountSegs * tid;   // this thread's 4 segments
+    const int64_t seg0 = d.seg0 + ls0;                        // a multiple of 4 (one tensor: seg0 = 0)
+    uint32_t n[kCountSegs], c[kCountSegs], lc[kCountSegs];
+    if (ls0 + 3 < d.nseg) {   // one 16-B load
+        const uint4 u = *reinterpret_cast<const uint4*>(w.seg_lcnt + seg0);
+        lc[0] = u.x; lc[1] = u.y; lc[2] = u.z; lc[3] = u.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < kCountSegs; ++q) lc[q] = ls0 + q < d.nseg ? w.seg_lcnt[seg0 + q] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kCountSegs; ++q) {
+        n[q] = ((lc[q] >> 16) << 16) <= tkey ? 0u : lcnt_count(lc[q]);   // every |x| < t_cur: nothing
+        c[q] = 0;
+    }
+    uint32_t nmax = 0;   // the longest complete list of the four
+#pragma unroll
+    for (int q = 0; q < kCountSegs; ++q)
+        if (n[q] <= (uint32_t)kCap) nmax = max(nmax, n[q]);
+    constexpr int kFirst = 8;   // entries 0..7: the four lists' share of one 128-B line
+    const float* lv = w.lst_val + lcol(seg0);
+    float4 a[kFirst];
+#pragma unroll
+    for (int e = 0; e < kFirst; ++e)
+        if ((uint32_t)e < nmax) a[e] = *reinterpret_cast<const float4*>(lv + e * kLstTile);
+#pragma unroll
+    for (int e = 0; e < kFirst; ++e) {
+        const float x[4] = {a[e].x, a[e].y, a[e].z, a[e].w};
+#pragma unroll
+        for (int q = 0; q < kCountSegs; ++q) c[q] += (uint32_t)e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
+    }
+    for (uint32_t e = kFirst; e < nmax; ++e) {   // longer lists (rare)
+        const float4 b = *reinterpret_cast<const float4*>(lv + e * kLstTile);
+        const float x[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < kCountSegs; ++q) c[q] += e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
+    }
+#pragma unroll
+    for (int q = 0; q < kCountSegs; ++q)
+        if (ls0 + q < d.nseg && n[q] > (uint32_t)kCap) spill[atomicAdd(&nspill, 1)] = kCountSegs * tid + q;
+    __syncthreads();
+    for (int i = wave; i < nspill; i += kBlock / kWave) {   // spilled segments: a wave re-reads each
+        const int j = spill[i];
+        const uint32_t cs = wave_count_segment(vec, d.n, lg * kGroupSegs + j, tc);
+        if (lane == 0) spill_cnt[j] = cs;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kCountSegs; ++q)
+        if (ls0 + q < d.nseg && n[q] > (uint32_t)kCap) c[q] = spill_cnt[kCountSegs * tid + q];
+    CE_STAMP(1);
+    const uint32_t mine = c[0] + c[1] + c[2] + c[3];
+    uint64_t total;
+    const uint32_t tbase = (uint32_t)block_exclusive_scan((uint64_t)mine, lds16, &total);
+    uint32_t off[kCountSegs];
+    off[0] = tbase;
+#pragma unroll
+    for (int q = 1; q < kCountSegs; ++q) off[q] = off[q - 1] + c[q - 1];
+#pragma unroll
+    for (int q = 0; q < kCountSegs; ++q)
+        if (ls0 + q < d.nseg) {
+            w.seg_cnt[seg0 + q] = c[q];
+            w.seg_off[seg0 + q] = off[q];
+            if (n[q] > (uint32_t)kCap) spill_cnt[kCountSegs * tid + q] = off[q];   // now its offset
+        }
+    // the group's offset: decoupled look-back by wave 0, 64 predecessors per poll (one
+    // load each, in flight together: a walk of one load at a time paid ~1 us per group)
+    if (wave == 0) {
+        unsigned long long* lb = w.grp_lb + d.grp0;
+        if (lane == 0) {
+            if (total) atomicAdd(&w.grp_cnt[d.grp0 + lg], (unsigned long long)total);
+            __hip_atomic_store(&lb[lg], (lg == 0 ? kLbPre : kLbAgg) | total, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        unsigned long long prefix = 0;
+        bool ok = true;
+        int64_t j = lg - 1;   // the window's closest predecessor
+        int spin = 0;
+        while (j >= 0) {
+            const int64_t jj = j - lane;
+            // before group 0: an inclusive prefix of 0
+            const unsigned long long v =
+                jj >= 0 ? __hip_atomic_load(&lb[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
+            const uint64_t pre = __ballot((v & kLbPre) != 0), unready = __ballot(v == 0);
+            const int first = pre ? __builtin_ctzll(pre) : kWave;   // the closest inclusive prefix
+            const uint64_t need = first >= kWave - 1 ? ~0ull : ((2ull << first) - 1);
+            if (unready & need) {   // a group in the window has not published yet: poll again
+                if (++spin > kLbSpin) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            prefix += wave_sum(lane <= first ? (v & kLbVal) : 0ull);
+            if (first < kWave) break;
+            j -= kWave;
+        }
+        if (lane == 0) {
+            if (lg > 0 && ok)
+                __hip_atomic_store(&lb[lg], kLbPre | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!ok) atomicExch(&st->ce_fail, 1);   // no emit from this group: k_emit will run
+            prefix_s = ok ? prefix : ~0ull;
+        }
+    }
+    __syncthreads();
+    CE_STAMP(2);
+    const unsigned long long P = prefix_s;
+    const long long limit = d.k;
+    // Payload writes one entry per lane in slot order: a group whose entries fit stages
+    // them in LDS and copies them out coalesced (written where they fall, a lane per four
+    // lists, they were 4- and 8-B stores to 64 lines per instruction: 81 -> 71 us at 1B).
+    const bool emit = P != ~0ull && (long long)P < limit;
+    const bool staged = emit && nspill == 0 && total <= (uint64_t)kCeStage;
+    if (emit) {
+        // the entries >= t_cur at positions P + off + rank < k
+        const uint16_t* lo = w.lst_off + lcol(seg0);
+        for (uint32_t e0 = 0; e0 < nmax; e0 += kFirst) {
+            if ((long long)(P + off[0]) >= limit) break;
+            uint2 ob[kFirst];
+            float4 vb[kFirst];
+#pragma unroll
+            for (int e = 0; e < kFirst; ++e)
+                if (e0 + e < nmax) {
+                    ob[e] = *reinterpret_cast<const uint2*>(lo + (e0 + e) * kLstTile);
+                    vb[e] = e0 == 0 ? a[e] : *reinterpret_cast<const float4*>(lv + (e0 + e) * kLstTile);
+                }
+#pragma unroll
+            for (int e = 0; e < kFirst; ++e) {
+                if (e0 + e >= nmax) break;
+                const float x[4] = {vb[e].x, vb[e].y, vb[e].z, vb[e].w};
+                const uint32_t oo[4] = {ob[e].x & 0xFFFFu, ob[e].x >> 16, ob[e].y & 0xFFFFu, ob[e].y >> 16};
+#pragma unroll
+                for (int q = 0; q < kCountSegs; ++q)
+                    if (e0 + e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc) {
+                        const uint32_t r = off[q];   // in-group slot
+                        if (staged) {
+                            stage_v[r] = x[q];
+                            stage_i[r] = (uint32_t)(kCountSegs * tid + q) * kSeg + oo[q];
+                        } else if ((long long)(P + r) < limit) {
+                            emit_one(o, d, (long long)(P + r), (ls0 + q) * kSeg + oo[q], x[q], false);
+                        }
+                        off[q] = r + 1;
+                    }
+            }
+        }
+    }
+    if (emit && !staged)
+        for (int i = wave; i < nspill; i += kBlock / kWave) {   // spilled segments: a wave re-reads each
+            const int j = spill[i];
+            emit_reread_firstk(vec, d, lg * kGroupSegs + j, (long long)(P + spill_cnt[j]), limit, 0, tc, o, false);
+        }
+    CE_STAMP(3);
+    if (staged) {
+        __syncthreads();
+        const long long m = std::min<long long>((long long)total, limit - (long long)P);
+        const int64_t gbase = lg * kGroupSegs * (int64_t)kSeg;   // the group's first element
+        for (long long i = tid; i < m; i += kBlock) {
+            store_value(o.values, (long long)P + i, stage_v[i], o.vdtype);
+            store_index(o.indices, (long long)P + i, d.idx_base + gbase + stage_i[i], o.idtype);
+        }
+    }
+    CE_STAMP(4);
+    // the tensor's last workgroup takes the adaptation step
+    if (last_block_arrival8(st->tk8, (uint32_t)lg, (uint32_t)(w.bt[BT_CNT][1] - w.bt[BT_CNT][0])))
+        decide_tensor(w, p, 0, 1);
+    CE_STAMP(5);
 }
 
 // Result records; the payload's total count; and every tensor's next speculative
@@ -2101,12 +2335,21 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     const bool al = aligned16(vec);
     // resample=True with max_iters <= kMaxLower: one multi-threshold pass replaces the lowers
     const bool lower_fast = p.resample && p.max_iters <= kMaxLower;
-    auto pass = [&](int need, bool likely_lists) -> int {
+    EmitOut o{p.update_memory ? vec : nullptr, (p.update_memory && p.masking) ? mmt : nullptr, values, indices,
+              p.vdtype, p.idtype, nullptr, nullptr, (int32_t)(p.update_memory == 2)};
+    // the first list count of a one-tensor call also writes the first-k payload
+    // (k_count_emit) when that emit would not mask and the payload starts at slot 0
+    const bool fuse = keep_lists && L.T == 1 && !L.tail_any && sync_mode == DGC_SYNC_DEVICE &&
+                      (p.update_memory == 2 || p.update_memory == 0) && !std::getenv("DGC_NO_COUNT_EMIT");
+    auto pass = [&](int need, bool likely_lists, bool fused = false) -> int {
         // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
         // (both gated per tensor on the device); need: 1 = lists, 2 = full, 3 = either
         // each count kernel's last workgroup per tensor takes the adaptation step
         if (need & 1) {
-            hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w, p);
+            if (fused)
+                hipLaunchKernelGGL(k_count_emit, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w, p, o);
+            else
+                hipLaunchKernelGGL(k_count_lists, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w, p);
             DGC_LAUNCHED();
         }
         if (need & 2) {
@@ -2132,8 +2375,6 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    EmitOut o{p.update_memory ? vec : nullptr, (p.update_memory && p.masking) ? mmt : nullptr, values, indices,
-              p.vdtype, p.idtype, nullptr, nullptr, (int32_t)(p.update_memory == 2)};
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0};
     bool finished = false;   // the payload count and records are written
     auto resample_exact = [&]() -> int {
@@ -2165,7 +2406,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    DGC_TRY(keep_lists ? pass(3, true) : pass(2, false));
+    DGC_TRY(keep_lists ? pass(3, true, fuse) : pass(2, false));
     bool emitted = false;   // the payload of every non-K5 tensor is written
     if (sync_mode == DGC_SYNC_HOST) {
         // read the decisions back and launch only what they need
@@ -2675,6 +2916,11 @@ extern "C" int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt
 }
 
 #ifdef DGC_K5_PROF
+extern "C" int dgc_ce_prof(void* out) {
+    DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_ce_prof), sizeof(dgc::g_ce_prof)));
+    return DGC_OK;
+}
+
 extern "C" int dgc_k5_prof(void* out, int reset) {
     if (reset) {
         dgc::K5Prof z{};
