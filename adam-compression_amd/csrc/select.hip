@@ -1635,10 +1635,15 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
         if (n[q] <= (uint32_t)kCap) nmax = max(nmax, n[q]);
     constexpr int kFirst = 8;   // entries 0..7: the four lists' share of one 128-B line
     const float* lv = w.lst_val + lcol(seg0);
+    const uint16_t* lo = w.lst_off + lcol(seg0);
     float4 a[kFirst];
+    uint2 ao[kFirst];   // their offsets too: the emit below then needs no second round trip
 #pragma unroll
     for (int e = 0; e < kFirst; ++e)
-        if ((uint32_t)e < nmax) a[e] = *reinterpret_cast<const float4*>(lv + e * kLstTile);
+        if ((uint32_t)e < nmax) {
+            a[e] = *reinterpret_cast<const float4*>(lv + e * kLstTile);
+            ao[e] = *reinterpret_cast<const uint2*>(lo + e * kLstTile);
+        }
 #pragma unroll
     for (int e = 0; e < kFirst; ++e) {
         const float x[4] = {a[e].x, a[e].y, a[e].z, a[e].w};
@@ -1730,7 +1735,6 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
     const bool staged = emit && nspill == 0 && total <= (uint64_t)kCeStage;
     if (emit) {
         // the entries >= t_cur at positions P + off + rank < k
-        const uint16_t* lo = w.lst_off + lcol(seg0);
         for (uint32_t e0 = 0; e0 < nmax; e0 += kFirst) {
             if ((long long)(P + off[0]) >= limit) break;
             uint2 ob[kFirst];
@@ -1738,7 +1742,7 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
 #pragma unroll
             for (int e = 0; e < kFirst; ++e)
                 if (e0 + e < nmax) {
-                    ob[e] = *reinterpret_cast<const uint2*>(lo + (e0 + e) * kLstTile);
+                    ob[e] = e0 == 0 ? ao[e] : *reinterpret_cast<const uint2*>(lo + (e0 + e) * kLstTile);
                     vb[e] = e0 == 0 ? a[e] : *reinterpret_cast<const float4*>(lv + (e0 + e) * kLstTile);
                 }
 #pragma unroll
