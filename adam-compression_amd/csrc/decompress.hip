@@ -595,7 +595,7 @@ k_scatter_overflow(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, floa
 }
 
 // ---------------------------------------------------------------- host side
-static int vbytes(int vd) { return vd == DGC_F16 ? 2 : 4; }
+static int vbytes(int vd) { return vd == DGC_F32 ? 4 : 2; }   // F16, BF16: 2
 static int ibytes(int id) { return id == DGC_I32 ? 4 : 8; }
 
 // words zeroed by the dense fill's first block (a null pointer with a zero count skips)

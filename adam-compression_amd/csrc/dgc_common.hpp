@@ -148,22 +148,103 @@ __device__ __forceinline__ void wave_prefix1(bool p, uint32_t& lane_base, uint32
     total = __popcll(m);
 }
 
+// ---------------------------------------------------------------- wave64 reductions
+// 32-bit reductions and scans over the wave with DPP (gfx9: row_shr within 16-lane
+// rows, then row_bcast:15 / row_bcast:31 across rows): VALU ops with a lane-shifted
+// operand, a few cycles each, where __shfl_xor / __shfl_up lower to ds_bpermute_b32 —
+// an LDS-crossbar round trip each, six dependent ones per reduction, which set the
+// pace of every one-wave chain (K5's tail, the last-workgroup steps). Call with all 64
+// lanes active. Invalid source lanes (out of the row, or disabled) read `id`.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t v, uint32_t id) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, ROWS, 0xf, false);
+}
+struct DppAdd {
+    static constexpr uint32_t id = 0u;
+    __device__ __forceinline__ static uint32_t op(uint32_t a, uint32_t b) { return a + b; }
+};
+struct DppMax {
+    static constexpr uint32_t id = 0u;
+    __device__ __forceinline__ static uint32_t op(uint32_t a, uint32_t b) { return a > b ? a : b; }
+};
+struct DppMin {
+    static constexpr uint32_t id = 0xFFFFFFFFu;
+    __device__ __forceinline__ static uint32_t op(uint32_t a, uint32_t b) { return a < b ? a : b; }
+};
+// Inclusive scan in lane order.
+template <class Op>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v = Op::op(v, dpp_src<0x111, 0xf>(v, Op::id));   // row_shr:1
+    v = Op::op(v, dpp_src<0x112, 0xf>(v, Op::id));   // row_shr:2
+    v = Op::op(v, dpp_src<0x114, 0xf>(v, Op::id));   // row_shr:4
+    v = Op::op(v, dpp_src<0x118, 0xf>(v, Op::id));   // row_shr:8
+    v = Op::op(v, dpp_src<0x142, 0xa>(v, Op::id));   // row_bcast:15 into rows 1, 3
+    v = Op::op(v, dpp_src<0x143, 0xc>(v, Op::id));   // row_bcast:31 into rows 2, 3
+    return v;
+}
+// Whole-wave reduction, wave-uniform (an SGPR).
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan<Op>(v), 63);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
+    if constexpr (sizeof(T) == 4) {
+        return (T)wave_reduce<DppAdd>((uint32_t)v);
+    } else {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        return v;
+    }
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
-    return v;
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) { return wave_reduce<DppMax>(v); }
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return wave_reduce<DppMin>(v); }
+
+// ---------------------------------------------------------------- 16-bit floats
+// bf16 <-> fp32 as c10::BFloat16 does it: widening is exact (the 16 bits are the top
+// half of the fp32 pattern); narrowing rounds to nearest even, NaN -> 0x7FC0
+// (c10/util/BFloat16.h round_to_nearest_even). fp16: v_cvt_f16_f32 (RNE, overflow
+// -> inf), as c10::Half.
+__host__ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
+    union { uint32_t u; float f; } c{(uint32_t)b << 16};
+    return c.f;
+}
+__host__ __device__ __forceinline__ uint16_t f32_to_bf16(float x) {
+    union { float f; uint32_t u; } c{x};
+    if ((c.u & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)0x7FC0u;
+    return (uint16_t)((c.u + 0x7FFFu + ((c.u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+// The empty asm pins x as an fp32 register value: otherwise fptrunc(fmul(fpext(h), m))
+// becomes v_fma_mix*_f16 — ONE rounding of the exact product to fp16 where ATen rounds
+// the fp32 product first (double rounding; they differ on fp16 ties, e.g. 0.96435546875
+// * 0.9f).
+__device__ __forceinline__ uint16_t f32_to_f16(float x) {
+    asm volatile("" : "+v"(x));
+    return __builtin_bit_cast(uint16_t, (_Float16)x);
+}
+// 16-bit storage of dtype DT (DGC_BF16 / DGC_F16)
+template <int DT>
+__device__ __forceinline__ float h16_to_f32(uint16_t v) { return DT == DGC_BF16 ? bf16_to_f32(v) : f16_to_f32(v); }
+template <int DT>
+__device__ __forceinline__ uint16_t f32_to_h16(float x) { return DT == DGC_BF16 ? f32_to_bf16(x) : f32_to_f16(x); }
+// fp32 -> DT -> fp32: what one ATen op on a DT tensor leaves (it computes in fp32)
+template <int DT>
+__device__ __forceinline__ float round16(float x) { return h16_to_f32<DT>(f32_to_h16<DT>(x)); }
+// threshold * bound for a tensor of dtype td (0-dim tensor times a Python float: fp32
+// product, then rounded to the tensor's dtype)
+__device__ __forceinline__ float thr_mul(float t, float f, int td) {
+    const float p = __fmul_rn(t, f);
+    return td == DGC_BF16 ? round16<DGC_BF16>(p) : td == DGC_F16 ? round16<DGC_F16>(p) : p;
 }
 
-// Wire value store (fp32 / fp16 round-to-nearest-even, overflow -> inf like torch).
+// Wire value store (fp32 / fp16 / bf16 round-to-nearest-even, overflow -> inf like torch).
 __device__ __forceinline__ void store_value(void* out, int64_t pos, float x, int vdtype) {
-    if (vdtype == DGC_F16)
+    if (vdtype == DGC_BF16)
+        reinterpret_cast<uint16_t*>(out)[pos] = f32_to_bf16(x);
+    else if (vdtype == DGC_F16)
         reinterpret_cast<__half*>(out)[pos] = __float2half_rn(x);
     else
         reinterpret_cast<float*>(out)[pos] = x;

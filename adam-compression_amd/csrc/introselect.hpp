@@ -53,7 +53,9 @@ __device__ __forceinline__ uint32_t qkey(uint64_t e) { return (uint32_t)(e >> 32
 
 #ifdef DGC_K5_PROF
 // tools/k5_prof: phase timestamps (wall clock, 100 MHz) and step counts of the last
-// K5 run by workgroup 0 — a profiling build only (make k5prof).
+// K5 run by workgroup 0 — a profiling build only (make k5prof). Sub-phase sums and
+// step counts accumulate in LDS (a global read-modify-write per sub-phase would put a
+// memory round trip into every step it times) and reach g_k5prof once, at the end.
 struct K5Prof {
     unsigned long long t[8];
     unsigned int steps[4];
@@ -62,23 +64,34 @@ struct K5Prof {
     long long bn[64];               // its candidate count
 };
 __device__ K5Prof g_k5prof;
+__shared__ unsigned long long k5_lsub[8];
+__shared__ unsigned int k5_lsteps[4];
+#define K5_PROF_BEGIN() \
+    do { if (threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) k5_lsub[i_] = 0; \
+         for (int i_ = 0; i_ < 4; ++i_) k5_lsteps[i_] = 0; } __syncthreads(); } while (0)
+#define K5_PROF_END() \
+    do { __syncthreads(); if (threadIdx.x == 0 && blockIdx.x == 0) { \
+         for (int i_ = 0; i_ < 8; ++i_) g_k5prof.sub[i_] += k5_lsub[i_]; \
+         for (int i_ = 0; i_ < 3; ++i_) g_k5prof.steps[i_] += k5_lsteps[i_]; } } while (0)
 #define K5_STAMP(i) \
     do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
          if (blockIdx.x == 0) g_k5prof.t[i] = t_; \
          if (blockIdx.x < 64) g_k5prof.bt[blockIdx.x][i] = t_; } } while (0)
 #define K5_STEP(i) \
-    do { if (blockIdx.x == 0 && threadIdx.x == 0) g_k5prof.steps[i] += 1; } while (0)
+    do { if (threadIdx.x == 0) k5_lsteps[i] += 1; } while (0)
 #define K5_SUB_BEGIN() unsigned long long k5_t0 = wall_clock64()
 #define K5_SUB(i, global) \
-    do { if ((global) && blockIdx.x == 0 && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
-         g_k5prof.sub[i] += t_ - k5_t0; k5_t0 = t_; } } while (0)
+    do { if ((global) && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
+         k5_lsub[i] += t_ - k5_t0; k5_t0 = t_; } } while (0)
 // single-wave tail: sub[4] median, sub[5] loads + pairing, sub[6] swaps + cut
 #define K5_WSUB_BEGIN() unsigned long long k5w_t0 = wall_clock64()
 #define K5_WSUB_RESET() do { k5w_t0 = wall_clock64(); } while (0)
 #define K5_WSUB(i) \
-    do { if (blockIdx.x == 0 && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
-         g_k5prof.sub[i] += t_ - k5w_t0; k5w_t0 = t_; } } while (0)
+    do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
+         k5_lsub[i] += t_ - k5w_t0; k5w_t0 = t_; } } while (0)
 #else
+#define K5_PROF_BEGIN() do { } while (0)
+#define K5_PROF_END() do { } while (0)
 #define K5_WSUB_BEGIN() do { } while (0)
 #define K5_WSUB_RESET() do { } while (0)
 #define K5_WSUB(i) do { } while (0)
@@ -429,14 +442,6 @@ __device__ __forceinline__ void pair_tile(uint32_t pl, uint32_t pr, int64_t tile
     runr += tr;
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t a = __shfl_xor(v, o);
-        v = a < v ? a : v;
-    }
-    return v;
-}
 
 // ---------------------------------------------------------------- workgroup step
 struct NthShared {
@@ -675,74 +680,99 @@ __device__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& sh, int64_t nth, 
 }
 
 // ---------------------------------------------------------------- single-wave tail
-// The same step by one wave on an LDS range of <= kNthWave entries: no workgroup
-// barrier. Leaner than pair_tile's per-element swap test (a single wave's dependent
-// instruction chain is the tail's cost: ~1.6 us per step measured, tools/k5_prof.py):
-// EVERY left stopper stores its position at its rank from the left (lpos), every right
-// stopper at its rank from the left too (rposL); then L_t = lpos[t - 1] and R_t =
-// rposL[TR - t], and the swap count s = #{t : L_t < R_t} — a monotone predicate, L
-// rising and R falling — is found by a two-round search over the slots.
-struct RevSlots {   // pairs t: lpos[t] <-> rposL[TR - 1 - t]
-    const DGC_LDS uint32_t* l;
-    const DGC_LDS uint32_t* r;
-    uint32_t TR;
-    __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
-    __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[TR - 1 - t]; }
-};
-
-__device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DGC_LDS uint32_t* rpos, int64_t f,
-                                 int64_t l) {
+// The same step by one wave on an LDS range of <= kNthWave entries, wave-synchronous
+// (no workgroup barrier), with as few dependent LDS round trips as the step allows —
+// a single wave's latency chain is the tail's whole cost:
+//   1. every tile of the range loaded at once (<= 5 x 4 entries per lane, registers);
+//   2. from the tiles' ballots alone, every element's swap test (pair_tile's: L_{rl+1}
+//      swapped iff #(key >= P right of it) >= rl + 1; R with u stoppers right of it
+//      iff rl >= u + 1), so s, L_{s+1} and R_s come from ballots, not from a search;
+//   3. each swapped element stores its ENTRY (from registers) at its pair slot (xl[t]
+//      for L_t, xr[u] for R_u: one store, the two tests exclude each other);
+//   4. each swapped element loads its partner's entry from the other slot array and
+//      stores it at its own position.
+// Stores the unswapped elements would make go to a per-lane dummy word (an exec-mask
+// branch per store otherwise). The pivot key P comes from the median in a register.
+// xl / xr / dummy: >= kNthWave / 2, kNthWave / 2 and kWave u64 of LDS.
+__device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* xl, DGC_LDS uint64_t* xr,
+                                 DGC_LDS uint64_t* dummy, int64_t f, int64_t l, uint32_t P) {
     constexpr int kTiles = kNthWave / 256 + 1;   // the range <= kNthWave, from a base <= a0
     K5_WSUB_BEGIN();
     const int lane = threadIdx.x & 63;
-    const uint32_t P = qkey(q[f]);
     const int64_t a0 = f + 1, base = nth_base(q, a0);
-    const uint32_t below[4] = {0u, 1u, 3u, 7u};
-    __shared__ uint32_t dummy_s[kWave];
-    DGC_LDS uint32_t* dummy = lds(dummy_s);
-    uint32_t runl = 0, runr = 0;
+    const int nt = (int)uniform32((uint32_t)((l - base + 255) / 256));
+    const uint32_t rb0 = (uint32_t)(base - f);   // 0 or 1: tile positions relative to f
+    uint64_t x[kTiles][4];
+    uint32_t pl[kTiles], pr[kTiles];
 #pragma unroll
     for (int u = 0; u < kTiles; ++u) {
-        const int64_t t0 = base + 256 * u;
-        if (t0 >= l) break;   // uniform
-        uint64_t x[4];
-        uint32_t valid, pl, pr;
-        nth_load4(q, t0 + 4 * lane, a0, l, x, valid);
-        stopper_masks(x, valid, P, pl, pr);
-        uint32_t bl, tl, br, tr;
-        wave_prefix4(pl, bl, tl);
-        wave_prefix4(pr, br, tr);
-        const uint32_t rel0 = (uint32_t)(t0 - f) + 4u * (uint32_t)lane;
+        if (u >= nt) break;   // uniform: most tail steps span one or two tiles
+        uint32_t valid = 0;
+        nth_load4(q, base + 256 * u + 4 * lane, a0, l, x[u], valid);
+        stopper_masks(x[u], valid, P, pl[u], pr[u]);
+    }
+    // per tile: the lane's L / R bases and the tile totals (wave-uniform)
+    uint32_t lb[kTiles], rb[kTiles], tl[kTiles], tr[kTiles], TR = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {   // unconditional stores (see PlainSlotsT::fl)
-            *(((pl >> j) & 1u) ? lpos + runl + bl + (uint32_t)__popc(pl & below[j]) : dummy + lane) = rel0 + (uint32_t)j;
-            *(((pr >> j) & 1u) ? rpos + runr + br + (uint32_t)__popc(pr & below[j]) : dummy + lane) = rel0 + (uint32_t)j;
+    for (int u = 0; u < kTiles; ++u) {
+        if (u >= nt) break;
+        wave_prefix4(pl[u], lb[u], tl[u]);
+        wave_prefix4(pr[u], rb[u], tr[u]);
+        TR += tr[u];
+    }
+    uint32_t runl = 0, runr = 0, nsw = 0, lnext = UINT32_MAX, rmin = UINT32_MAX;
+    uint32_t slot[kTiles][4], sw[kTiles];
+#pragma unroll
+    for (int u = 0; u < kTiles; ++u) {
+        if (u >= nt) break;
+        uint32_t rl = runl + lb[u], rr = runr + rb[u], bits = 0;
+        const uint32_t rel0 = rb0 + 256u * (uint32_t)u + 4u * (uint32_t)lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool isl = (pl[u] >> j) & 1u, isr = (pr[u] >> j) & 1u;
+            const uint32_t rr_incl = rr + (isr ? 1u : 0u);
+            const uint32_t ur = TR - rr_incl;   // right stoppers after this element
+            const bool swl = isl && ur >= rl + 1;
+            const bool swr = isr && rl >= ur + 1;
+            slot[u][j] = swl ? rl : ur;
+            *(swl ? xl + rl : swr ? xr + ur : dummy + lane) = x[u][j];
+            bits |= (swl ? 1u : 0u) << j | (swr ? 16u : 0u) << j;
+            nsw += swl ? 1u : 0u;
+            const uint32_t i = rel0 + (uint32_t)j;
+            if (isl && !swl && i < lnext) lnext = i;
+            if (swr && i < rmin) rmin = i;
+            rl += isl ? 1u : 0u;
+            rr = rr_incl;
         }
-        runl += tl;
-        runr += tr;
+        sw[u] = bits;
+        runl += tl[u];
+        runr += tr[u];
     }
-    wave_sync();   // the slots are written
-    const uint32_t TL = runl, TR = runr, M = TL < TR ? TL : TR;
-    // s = the first t in [0, M) with lpos[t] >= rposL[TR - 1 - t] (M if none)
-    uint32_t s = M;
-    if (M > 0) {
-        const uint32_t stride = (M + 63) / 64;
-        const uint32_t ti = (uint32_t)lane * stride + stride - 1;   // the last t of lane's block
-        const bool fail1 = ti < M ? lpos[ti] >= rpos[TR - 1 - ti] : true;
-        const uint64_t b1 = __ballot(fail1);
-        const uint32_t blk = (uint32_t)__builtin_ctzll(b1);   // the first block holding a failure (or past M)
-        const uint32_t t2 = blk * stride + (uint32_t)lane;
-        const bool in2 = (uint32_t)lane < stride && t2 < M;
-        const bool fail2 = in2 ? lpos[t2] >= rpos[TR - 1 - t2] : ((uint32_t)lane >= stride ? true : t2 >= M);
-        const uint64_t b2 = __ballot(fail2);
-        const uint32_t first = blk * stride + (uint32_t)__builtin_ctzll(b2);
-        s = first < M ? first : M;
-    }
+    const uint32_t s = uniform32(wave_sum(nsw));
+    lnext = uniform32(wave_min_u32(lnext));
+    rmin = uniform32(wave_min_u32(rmin));
+    wave_sync();   // the pair slots are written
     K5_WSUB(5);
-    nth_swaps<2>(q, RevSlots{lpos, rpos, TR}, f, s, lane, kWave);
-    // L_(s+1) (the first unswapped left stopper) and R_s (the smallest swapped right one)
-    const uint32_t lnext = s < TL ? lpos[s] : UINT32_MAX;
-    const uint32_t rmin = s > 0 ? rpos[TR - s] : UINT32_MAX;
+    uint64_t y[kTiles][4];
+#pragma unroll
+    for (int u = 0; u < kTiles; ++u) {
+        if (u >= nt) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool swl = (sw[u] >> j) & 1u, swr = (sw[u] >> (4 + j)) & 1u;
+            y[u][j] = *(swl ? xr + slot[u][j] : swr ? xl + slot[u][j] : dummy + lane);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kTiles; ++u) {
+        if (u >= nt) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool on = (sw[u] >> j) & 0x11u;
+            const uint32_t i = rb0 + 256u * (uint32_t)u + 4u * (uint32_t)lane + (uint32_t)j;
+            *(on ? q + f + i : dummy + lane) = y[u][j];
+        }
+    }
     wave_sync();   // the swaps are done
     K5_WSUB(6);
     const int64_t rs = s ? f + (int64_t)rmin : l;
@@ -751,10 +781,13 @@ __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DG
 }
 
 // Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
-__device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DGC_LDS uint32_t* rpos, NthShared& sh,
-                              int64_t nth) {
+// slots: >= kNthWave + kWave u64 of LDS (the pair slots and the dummy words).
+__device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* slots, NthShared& sh, int64_t nth) {
     int64_t f = sh.f, l = sh.l, depth = sh.depth;
     const int lane = threadIdx.x & 63;
+    DGC_LDS uint64_t* xl = slots;
+    DGC_LDS uint64_t* xr = slots + kNthWave / 2;
+    DGC_LDS uint64_t* dummy = slots + kNthWave;
     K5_WSUB_BEGIN();
     while (l - f > 3) {
         if (depth == 0) {
@@ -765,10 +798,12 @@ __device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint32_t* lpos, DGC_L
         depth -= 1;
         K5_STEP(2);
         K5_WSUB_RESET();
-        if (lane == 0) (void)nth_median(q, f, l);
+        uint32_t p = 0;
+        if (lane == 0) p = nth_median(q, f, l);
+        const uint32_t P = uniform32(p);   // lane 0's (every lane is active here)
         wave_sync();
         K5_WSUB(4);
-        const int64_t cut = nth_step_wave(q, lpos, rpos, f, l);
+        const int64_t cut = nth_step_wave(q, xl, xr, dummy, f, l, P);
         if (cut <= nth)
             f = cut;
         else
@@ -1101,6 +1136,7 @@ __device__ __forceinline__ void nth_element_wg(DGC_GLB uint64_t* q, int64_t n, i
 #ifdef DGC_K5_PROF
     if (threadIdx.x == 0 && blockIdx.x < 64) g_k5prof.bn[blockIdx.x] = n;
 #endif
+    K5_PROF_BEGIN();
     K5_STAMP(0);
     // global phase: lq (unused until the LDS phase) holds the stopper bytes
     // the whole LDS area (lq, llp, lrp, lmk: contiguous, carved by the caller) is the
@@ -1120,12 +1156,16 @@ __device__ __forceinline__ void nth_element_wg(DGC_GLB uint64_t* q, int64_t n, i
     K5_STAMP(2);
     nth_loop_wg<1, 2, false>(lq, llp, lrp, sh, nth - f, kNthWave, lmk, kNthMkLds / 64);   // LDS phase
     K5_STAMP(3);
-    if (!sh.heap_exit && threadIdx.x < kWave) nth_tail_wave(lq, llp, lrp, sh, nth - f);   // one wave
+    // one wave; its pair slots and dummy words (u64, 8-B aligned) in llp
+    static_assert((kNthWave + kWave) * 8 <= kNthPairLds * 4, "tail slots in llp");
+    if (!sh.heap_exit && threadIdx.x < kWave)
+        nth_tail_wave(lq, reinterpret_cast<DGC_LDS uint64_t*>(llp), sh, nth - f);
     __syncthreads();
     K5_STAMP(4);
     for (int64_t i = threadIdx.x; i < m; i += kNthThreads) q[f + i] = lq[i];
     __syncthreads();
     K5_STAMP(5);
+    K5_PROF_END();
 }
 
 }  // namespace dgc

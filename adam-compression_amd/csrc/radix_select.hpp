@@ -27,6 +27,10 @@
 namespace dgc {
 
 constexpr int kRsBins = 2048;
+
+#ifndef RS_STAMP
+#define RS_STAMP(i) do { } while (0)   // tools/rsbench.hip: phase timestamps
+#endif
 constexpr int kSmallN = 32768;
 constexpr int kScanThreads = 1024;
 
@@ -287,55 +291,140 @@ __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
     }
 }
 
-// All three passes of one key set of <= kSmallN keys in ONE 1024-thread workgroup,
-// keys staged in LDS: x[0..n) -> *out = k-th largest |x| (NaN if any |x| is NaN).
-__device__ void rs_small_wg(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
-    __shared__ uint32_t keys[kSmallN];
+// Exclusive scan of one u32 per thread over a kScanThreads workgroup (lds32: 16
+// words); returns the prefix, *total the workgroup total. Two barriers.
+__device__ __forceinline__ uint32_t block_exclusive_scan32(uint32_t v, uint32_t* lds32, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan<DppAdd>(v);
+    if (lane == 63) lds32[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        const uint32_t s = lds32[w];
+        wbase += w < wid ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + incl - v;
+}
+
+// pick_bin for u32 LDS counts of PER bins per thread (bins = PER * kScanThreads): true
+// in the one thread whose bins hold the k-th largest key; *bin, *above as pick_bin.
+template <int PER>
+__device__ __forceinline__ bool pick_bin_small(const uint32_t* h, uint32_t k, uint32_t* lds32, int* bin,
+                                               uint32_t* above) {
+    constexpr int bins = PER * kScanThreads;
+    const int t = threadIdx.x;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        c[j] = h[bins - 1 - (PER * t + j)];
+        sum += c[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan32(sum, lds32, &total);
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!hit && run < k && k <= run + c[j]) {
+            hit = true;
+            *bin = bins - 1 - (PER * t + j);
+            *above = run;
+        }
+        run += c[j];
+    }
+    return hit;
+}
+
+// All three passes of one key set of <= kSmallN keys in ONE 1024-thread workgroup
+// (k_rs_small, k_rs_small_multi): x[0..n) -> *out = k-th largest |x| (NaN if any |x|
+// is NaN). Every key load in flight at once (kSmallN / kScanThreads per
+// thread) into LDS, u32 counts and scans, and pass 0 floored. Pass 0's LDS histogram
+// atomics all land in the few bins the keys' exponents span (~n serialised
+// same-address adds), so it first histograms the per-thread maxima (<= 1024 adds) and
+// picks the bin b0 holding their k-th largest: at least k distinct keys (those maxima)
+// are >= b0 << 21, so the k-th largest key is too, and pass 0 need count only the keys
+// >= b0 << 21 — the bins >= b0 are exact, pick_bin picks the same bin. No floor when
+// fewer than k threads hold a key.
+__device__ void rs_small_wg(const float* __restrict__ x, int64_t n, uint64_t k64, float* out) {
+    constexpr int kPer = kSmallN / kScanThreads;
     __shared__ uint32_t h[kRsBins];
-    __shared__ uint64_t lds16[16];
-    __shared__ uint32_t nan_cnt, prefix;
-    __shared__ uint64_t k_rem;
+    __shared__ uint32_t lds32[16];
+    __shared__ uint32_t nan_cnt, prefix, k_rem, sel_above;
     __shared__ int sel_bin;
-    __shared__ uint64_t sel_above;
-    if (threadIdx.x == 0) {
+    const int tid = threadIdx.x;
+    const int nn = (int)n;   // <= kSmallN
+    const uint32_t k = (uint32_t)k64;
+    RS_STAMP(0);
+    for (int b = tid; b < kRsBins; b += kScanThreads) h[b] = 0;
+    if (tid == 0) {
         nan_cnt = 0;
         prefix = 0;
         k_rem = k;
+        sel_bin = -1;
+    }
+    // the thread's keys stay in registers (kPer VGPRs); out-of-range slots hold 0 and
+    // are masked by `in` below
+    uint32_t key[kPer];
+    uint32_t mx = 0, my_nan = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = tid + j * kScanThreads;
+        key[j] = i < nn ? abs_key(x[i]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const bool in = tid + j * kScanThreads < nn;
+        mx = in && key[j] > mx ? key[j] : mx;
+        my_nan += in && key[j] > 0x7F800000u ? 1u : 0u;
+    }
+    __syncthreads();   // h zeroed
+    RS_STAMP(1);
+    if (my_nan) atomicAdd(&nan_cnt, my_nan);
+    if (tid < nn) atomicAdd(&h[mx >> 21], 1u);
+    __syncthreads();
+    {
+        int bin;
+        uint32_t above;
+        if (pick_bin_small<2>(h, k, lds32, &bin, &above)) sel_bin = bin;
     }
     __syncthreads();
-    uint32_t my_nan = 0;
-    for (int i = threadIdx.x; i < n; i += kScanThreads) {
-        const uint32_t key = abs_key(x[i]);
-        keys[i] = key;
-        my_nan += key > 0x7F800000u;
-    }
-    if (my_nan) atomicAdd(&nan_cnt, my_nan);
+    const uint32_t floor = sel_bin >= 0 ? (uint32_t)sel_bin << 21 : 0u;
+    RS_STAMP(2);
     for (int pass = 0; pass < 3; ++pass) {
-        for (int b = threadIdx.x; b < kRsBins; b += kScanThreads) h[b] = 0;
-        if (threadIdx.x == 0) sel_bin = -1;
-        __syncthreads();
+        for (int b = tid; b < kRsBins; b += kScanThreads) h[b] = 0;
+        __syncthreads();   // everyone has read sel_bin / prefix
+        if (tid == 0) sel_bin = -1;
         const uint32_t pmask = rs_pmask(pass), dmask = rs_dmask(pass), pre = prefix;
         const int shift = rs_shift(pass);
-        for (int i = threadIdx.x; i < n; i += kScanThreads) {
-            const uint32_t key = keys[i];
-            if ((key & pmask) == pre) atomicAdd(&h[(key >> shift) & dmask], 1u);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const bool in = tid + j * kScanThreads < nn;
+            if (in && (pass == 0 ? key[j] >= floor : (key[j] & pmask) == pre))
+                atomicAdd(&h[(key[j] >> shift) & dmask], 1u);
         }
         __syncthreads();
+        RS_STAMP(3 + 2 * pass);
         int bin;
-        uint64_t above;
-        if (pick_bin(h, rs_bins(pass), k_rem, lds16, &bin, &above)) {
+        uint32_t above;
+        const bool hit = pass == 2 ? pick_bin_small<1>(h, k_rem, lds32, &bin, &above)
+                                   : pick_bin_small<2>(h, k_rem, lds32, &bin, &above);
+        if (hit) {
             sel_bin = bin;
             sel_above = above;
         }
         __syncthreads();
-        if (threadIdx.x == 0 && sel_bin >= 0) {
+        if (tid == 0 && sel_bin >= 0) {
             prefix |= (uint32_t)sel_bin << shift;
             k_rem -= sel_above;
         }
         __syncthreads();
+        RS_STAMP(4 + 2 * pass);
+        if (sel_bin < 0) break;   // uniform: k exceeds the key count
     }
-    if (threadIdx.x == 0)
-        *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
+    if (tid == 0) *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
     __syncthreads();
 }
 

@@ -137,6 +137,7 @@ struct SelCfg {
     float upper, lower;         // fl32(compress_upper_bound), fl32(compress_lower_bound)
     int32_t max_iters, resample, masking, vdtype, idtype;
     int32_t update_memory;      // 0: none, 1: zero the emitted slots now, 2: deferred to the next K1
+    int32_t tdtype;             // the sparsified tensor's dtype: threshold *= bound rounds to it
 };
 
 // Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
@@ -798,7 +799,7 @@ __device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t, int spec =
                     st->rs_nth = (cnt < 64 * k && cnt <= d.cand_cap) ? 1 : 2;
                     st->tie_rule = DGC_TIES_EXACT;
                 } else {
-                    st->t_cur = __fmul_rn(st->t_cur, p.upper);
+                    st->t_cur = thr_mul(st->t_cur, p.upper, p.tdtype);
                     done = 0;
                 }
             } else {
@@ -810,7 +811,7 @@ __device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t, int spec =
                 st->lower_pending = 1;   // k_lower_counts finds the final threshold in one pass
                 done = 2;
             } else {
-                st->t_cur = __fmul_rn(st->t_cur, p.lower);
+                st->t_cur = thr_mul(st->t_cur, p.lower, p.tdtype);
                 done = 0;
             }
         } else {
@@ -1089,7 +1090,7 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     float th[kMaxLower + 1];
     th[0] = st->t_cur;
 #pragma unroll
-    for (int j = 1; j <= kMaxLower; ++j) th[j] = __fmul_rn(th[j - 1], p.lower);
+    for (int j = 1; j <= kMaxLower; ++j) th[j] = thr_mul(th[j - 1], p.lower, p.tdtype);
     const float tmin = th[m];
     uint32_t c[kMaxLower + 1];
 #pragma unroll
@@ -1159,7 +1160,7 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     float th[kLowerLists + 1];
     th[0] = st->t_cur;
 #pragma unroll
-    for (int j = 1; j <= kLowerLists; ++j) th[j] = __fmul_rn(th[j - 1], p.lower);
+    for (int j = 1; j <= kLowerLists; ++j) th[j] = thr_mul(th[j - 1], p.lower, p.tdtype);
     const float tl = st->t_list;
     int ms = 0;   // thresholds t_1..t_ms are served by the lists (uniform per tensor)
 #pragma unroll
@@ -2259,7 +2260,10 @@ static int validate_select(const dgc_select_params* p, void* values, void* indic
     if (p->num_samples < 1 || p->num_samples > p->numel)
         DGC_FAIL(DGC_ERR_INVALID, "dgc_select: bad num_samples");
     if (p->max_iters < 0) DGC_FAIL(DGC_ERR_INVALID, "dgc_select: max_iters < 0");
-    if (p->vdtype != DGC_F32 && p->vdtype != DGC_F16) DGC_FAIL(DGC_ERR_DTYPE, "dgc_select: value dtype");
+    if (p->vdtype != DGC_F32 && p->vdtype != DGC_F16 && p->vdtype != DGC_BF16)
+        DGC_FAIL(DGC_ERR_DTYPE, "dgc_select: value dtype");
+    if (p->thr_dtype != DGC_F32 && p->thr_dtype != DGC_F16 && p->thr_dtype != DGC_BF16)
+        DGC_FAIL(DGC_ERR_DTYPE, "dgc_select: threshold dtype");
     if (p->idtype != DGC_I64 && p->idtype != DGC_I32) DGC_FAIL(DGC_ERR_DTYPE, "dgc_select: index dtype");
     if (p->idtype == DGC_I32 && p->numel > 2147483647LL)
         DGC_FAIL(DGC_ERR_OVERFLOW, "dgc_select: int32 indices cannot address %lld elements",
@@ -2269,7 +2273,7 @@ static int validate_select(const dgc_select_params* p, void* values, void* indic
 }
 
 static SelCfg cfg_of(const dgc_select_params& p) {
-    return SelCfg{p.upper, p.lower, p.max_iters, p.resample, p.masking, p.vdtype, p.idtype, p.update_memory};
+    return SelCfg{p.upper, p.lower, p.max_iters, p.resample, p.masking, p.vdtype, p.idtype, p.update_memory, p.thr_dtype};
 }
 
 // The selection of every tensor (its K1 lists kept or not), from k_sel_init to the

@@ -1,7 +1,8 @@
 """ctypes binding of ``libdgc_hip.so`` (the C ABI declared in ``include/dgc_hip.h``).
 
 The product path has no CPU fallback: if the library cannot be loaded, or a tensor
-is not an fp32 tensor on an MI355X, every entry point raises.
+is not a float tensor on an MI355X (fp32; bf16 / fp16 on the per-tensor path), every
+entry point raises.
 """
 import ctypes
 import os
@@ -18,7 +19,8 @@ LIB_PATH = os.environ.get(
 DGC_OK = 0
 SPEC_MARGIN = 0.8      # speculative list threshold = 0.8 x the previous final threshold
 SYNC_DEVICE, SYNC_HOST = 0, 1
-VD = {torch.float32: 0, torch.float16: 1}
+VD = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+HALF = (torch.bfloat16, torch.float16)   # 16-bit parameters (dgc_*16 entry points)
 ID = {torch.int64: 0, torch.int32: 1}
 BRANCHES = {0: "direct", 1: "ok", 2: "trunc", 3: "resample", 4: "exhausted"}
 TIE_RULES = {0: "none", 1: "exact"}
@@ -29,7 +31,8 @@ class SelectParams(ctypes.Structure):
                 ("num_samples", ctypes.c_int64), ("upper_count", ctypes.c_int64),
                 ("lower_count", ctypes.c_int64), ("upper", ctypes.c_float), ("lower", ctypes.c_float),
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("masking", ctypes.c_int32),
-                ("vdtype", ctypes.c_int32), ("idtype", ctypes.c_int32), ("update_memory", ctypes.c_int32)]
+                ("vdtype", ctypes.c_int32), ("idtype", ctypes.c_int32), ("update_memory", ctypes.c_int32),
+                ("thr_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class SelectInfo(ctypes.Structure):
@@ -120,6 +123,11 @@ _SIGNATURES = {
     "dgc_batch_compress_finish": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _P, _P, _SZ, _I32, _P]),
     "dgc_batch_flush": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _SZ, _P]),
     "dgc_hbm_probe": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),
+    "dgc_compensate16": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _F, _I32, _I32, _I32, _P]),
+    "dgc_mask_indices16": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _I64, _P, _P]),
+    "dgc_widen16": (ctypes.c_int, [_P, _P, _I64, _I32, _P]),
+    "dgc_decompress16": (ctypes.c_int, [_P, _I32, _P, _I32, ctypes.POINTER(ctypes.c_int64), _I32, _P, _I32, _I64,
+                                        _F, _P, _P]),
     "dgc_sgd_step": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                     ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _P]),
 }
@@ -134,7 +142,12 @@ def _load():
         return _lib
     try:
         handle = ctypes.CDLL(LIB_PATH)
+        # DGC_LIB_PARTIAL=1 (same-box A/B against an older build, tools/ab_bench.py):
+        # symbols the older library lacks stay unbound instead of failing the load
+        partial = os.environ.get("DGC_LIB_PARTIAL") == "1"
         for name, (res, args) in _SIGNATURES.items():
+            if partial and not hasattr(handle, name):
+                continue
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
@@ -169,6 +182,19 @@ def stream_of(device):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def require_cuda_float(t, what, contiguous=True):
+    """A contiguous fp32, bf16 or fp16 tensor on the MI355X (the per-tensor path takes all
+    three; the engines take fp32 only: require_cuda_f32). Returns its dtype."""
+    if not (torch.is_tensor(t) and t.is_cuda):
+        raise RuntimeError(f"{what}: the DGC hot path runs on the MI355X only (got a "
+                           f"{'CPU' if torch.is_tensor(t) else type(t).__name__} tensor)")
+    if t.dtype not in (torch.float32,) + HALF:
+        raise NotImplementedError(f"{what}: fp32, bf16 or fp16 tensors only (got {t.dtype})")
+    if contiguous and not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+    return t.dtype
 
 
 def require_cuda_f32(t, what):

@@ -98,6 +98,7 @@ class DGCCompressor:
         self._ws = _lib.Workspace()
         self._params = {}
         self._payloads = {}
+        self._bad16 = {}       # device -> int32 flag: out-of-range indices (dgc_decompress16)
         self._spec = {}        # name -> device float: speculative list threshold (dgc_compress)
 
     # ------------------------------------------------------------------ host math
@@ -157,8 +158,8 @@ class DGCCompressor:
             self.initialize(self.attributes.items())
 
     # ------------------------------------------------------------------ kernels
-    def _select_params(self, name, masking, update_memory):
-        key = (name, bool(masking), bool(update_memory))
+    def _select_params(self, name, masking, update_memory, dtype=torch.float32):
+        key = (name, bool(masking), bool(update_memory), dtype)
         p = self._params.get(key)
         if p is None:
             numel, _, k, S, _, _ = self.attributes[name]
@@ -171,15 +172,16 @@ class DGCCompressor:
             p.max_iters = int(self.max_adaptation_iters)
             p.resample = int(bool(self.resample))
             p.masking = int(bool(masking))
-            p.vdtype = _lib.VD[torch.float16 if self.fp16_values else torch.float32]
+            p.vdtype = _lib.VD[torch.float16 if self.fp16_values else dtype]
+            p.thr_dtype = _lib.VD[dtype]   # threshold *= bound rounds to the tensor's dtype
             p.idtype = _lib.ID[torch.int32 if self.int32_indices else torch.int64]
             p.update_memory = int(bool(update_memory))
             self._params[key] = p
         return p
 
-    def _new_payload(self, name, device):
+    def _new_payload(self, name, device, dtype=torch.float32):
         k = self.attributes[name][2]
-        vdt = torch.float16 if self.fp16_values else torch.float32
+        vdt = torch.float16 if self.fp16_values else dtype
         idt = torch.int32 if self.int32_indices else torch.int64
         stride, voff, ioff = _layout(k, vdt, idt)
         payload = torch.empty(stride, dtype=torch.uint8, device=device)
@@ -200,9 +202,22 @@ class DGCCompressor:
 
     def _sparsify(self, tensor, name, payload=None, lay=None, update_memory=False):
         """dgc/compression.py:109-153 on an already-compensated tensor. Returns
-        (values, indices, numel, shape, num_selects) with exact-length 1-D outputs."""
-        vec = tensor.view(-1)
-        _lib.require_cuda_f32(vec, "DGCCompressor._sparsify")
+        (values, indices, numel, shape, num_selects) with exact-length 1-D outputs.
+        A bf16 / fp16 tensor is selected on its exact fp32 image (dgc_widen16)."""
+        vec = tensor.reshape(-1)
+        dt = _lib.require_cuda_float(vec, "DGCCompressor._sparsify")
+        if dt in _lib.HALF:
+            if update_memory:
+                raise ValueError("DGCCompressor._sparsify: a 16-bit state is masked by DGCSGDMemory.update")
+            img = self._ws.get(vec.device, 4 * vec.numel(), "img16")[: 4 * vec.numel()].view(torch.float32)
+            _lib.check(_lib.lib().dgc_widen16(_lib.ptr(vec), _lib.ptr(img), vec.numel(), _lib.VD[dt],
+                                              _lib.stream_of(vec.device)), "dgc_widen16")
+            vec = img
+        return self._select_on(vec, name, dt, payload, lay, update_memory)
+
+    def _select_on(self, vec, name, dt, payload, lay, update_memory):
+        """Sample, threshold and select over the fp32 tensor (or 16-bit image) vec of
+        a tensor of dtype dt (dgc/compression.py:113-153)."""
         numel, shape, k, S, ks, stride = self.attributes[name]
         L = _lib.lib()
         dev = vec.device
@@ -227,10 +242,10 @@ class DGCCompressor:
         _lib.check(L.dgc_kth_largest(_lib.ptr(samples), m, ks, _lib.ptr(thr), _lib.ptr(kbuf), kws, stream),
                    "dgc_kth_largest")
         if payload is None:
-            payload, lay = self._new_payload(name, dev)
+            payload, lay = self._new_payload(name, dev, dt)
         k_, vdt, idt, pstride, voff, ioff = lay
         masking = isinstance(self.memory, DGCSGDMemory) and self.memory.momentum_masking
-        params = self._select_params(name, masking, update_memory)
+        params = self._select_params(name, masking, update_memory, dt)
         # pure selection emits fp32 / int64; the wire casts happen in compress
         sws = L.dgc_select_workspace(numel, k)
         sbuf = self._ws.get(dev, sws, "select")
@@ -251,8 +266,19 @@ class DGCCompressor:
             numel, shape, k, S, ks, stride = self.attributes[name]
             mem = self.memory
             dev = tensor.device
-            payload, lay = self._new_payload(name, dev)
-            if isinstance(mem, DGCSGDMemory) and self.strided_sample:
+            dt = _lib.require_cuda_float(tensor, "DGCCompressor.compress", contiguous=False)
+            payload, lay = self._new_payload(name, dev, dt)
+            if isinstance(mem, DGCSGDMemory) and dt in _lib.HALF:
+                # 16-bit state: K1-16 writes the velocity's fp32 image, the selection runs
+                # on it (pure), then DGCSGDMemory.update masks the 16-bit state
+                grad = mem._clip(tensor).reshape(-1).contiguous()
+                mem._sync()
+                img = self._ws.get(dev, 4 * numel, "img16")[: 4 * numel].view(torch.float32)
+                mem._compensate16(grad, name, True, vec32=img)
+                _, idx, _, _, _ = self._select_on(img, name, dt, payload, lay, False)
+                mem.update(name, (idx,))
+                values, indices = self._views(payload, lay, idx.numel())
+            elif isinstance(mem, DGCSGDMemory) and self.strided_sample:
                 # fused path: K1 (+sample) -> K3 -> K4 (+update) in one library call
                 grad = mem._clip(tensor).reshape(-1)
                 _lib.require_cuda_f32(grad, "DGCCompressor.compress")
@@ -283,7 +309,7 @@ class DGCCompressor:
                 mem.update(name, (idx.to(torch.int64) if idx.dtype != torch.int64 else idx,))
                 values, indices = self._views(payload, lay, idx.numel())
             self._payloads[name] = (payload, lay)
-            ctx = (name, numel, shape, torch.float32, torch.int64, tensor.data.view(numel))
+            ctx = (name, numel, shape, dt, torch.int64, tensor.data.view(numel))
             return (values, indices), ctx
         ctx = (name, None, None, tensor.dtype, None, None)
         if self.fp16_values and tensor.dtype.is_floating_point:
@@ -308,11 +334,13 @@ class DGCCompressor:
         name, numel, shape, vdtype, idtype, grad = ctx
         if self.compress_ratio < 1.0 and name in self.attributes:
             assert isinstance(tensor, (list, tuple))
-            _lib.require_cuda_f32(grad, "DGCCompressor.decompress")
+            gdt = _lib.require_cuda_float(grad, "DGCCompressor.decompress")
             L = _lib.lib()
             dev = grad.device
             scale = 1.0 / self.world_size if self.op == Average else 1.0
             stream = _lib.stream_of(dev)
+            if gdt in _lib.HALF:
+                return self._decompress16(tensor, grad, numel, shape, scale)
             if isinstance(tensor, _Gathered) and tensor.packed is not None:
                 p = tensor
                 wsz = L.dgc_decompress_packed_workspace(numel, p.world, p.capacity)
@@ -355,6 +383,37 @@ class DGCCompressor:
         if self.fp16_values and vdtype.is_floating_point:
             tensor = tensor.type(vdtype)
         return self.memory.compensate(tensor, name, accumulate=False)
+
+    def _decompress16(self, tensor, grad, numel, shape, scale):
+        """dgc/compression.py:179-194 into a bf16 / fp16 gradient (dgc_decompress16):
+        runs (ranks) in rank order, every add and the 1/W scale rounded to its dtype."""
+        import ctypes
+        values, indices = tensor
+        values = values.reshape(-1).contiguous()
+        indices = indices.reshape(-1).contiguous()
+        if values.dtype not in _lib.VD:
+            values = values.to(grad.dtype)
+        if indices.dtype not in _lib.ID:
+            indices = indices.to(torch.int64)
+        offs = getattr(tensor, "run_offsets", None)
+        if offs is None:
+            # reference-format input (ranks' indices may repeat): one stably sorted run,
+            # each index folded in input order (as the fp32 path's unsorted fallback)
+            order = torch.sort(indices, stable=True).indices
+            values, indices = values[order].contiguous(), indices[order].contiguous()
+            offs, nruns = [0, values.numel()], -1
+        else:
+            nruns = len(offs) - 1
+        arr = (ctypes.c_int64 * len(offs))(*[int(o) for o in offs])
+        dev = grad.device
+        bad = self._bad16.get(dev)
+        if bad is None:
+            bad = self._bad16[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().dgc_decompress16(_lib.ptr(values), _lib.VD[values.dtype], _lib.ptr(indices),
+                                               _lib.ID[indices.dtype], arr, nruns, _lib.ptr(grad),
+                                               _lib.VD[grad.dtype], numel, scale, _lib.ptr(bad),
+                                               _lib.stream_of(dev)), "dgc_decompress16")
+        return grad.view(shape)
 
     # ------------------------------------------------------------------ collectives
     def communicate(self, tensor_compressed, name, op):

@@ -60,6 +60,10 @@ class BatchedStep:
         self.comp = compression
         self.mem = compression.memory
         self.named = [(n, p) for n, p in named_parameters if p.requires_grad]
+        bad = sorted({str(p.dtype) for _, p in self.named if p.dtype != torch.float32})
+        if bad:   # the engines (dgc_batch_*) are fp32; 16-bit parameters take the per-tensor path
+            raise NotImplementedError(f"DistributedOptimizer(batch=True): fp32 parameters only (got {', '.join(bad)}); "
+                                      "bf16 / fp16 parameters run with batch=False")
         self._plan = None
         self.mem._before_read.append(self.flush)
 

@@ -9,8 +9,10 @@ The arithmetic runs in ``libdgc_hip.so`` on the MI355X:
 * ``update``      -> ``dgc_mask_indices`` (the same masking that ``dgc_compress``
   fuses into its emit kernel when the compressor drives this memory).
 
-``momentums`` / ``velocities`` stay plain param-shaped fp32 tensors keyed by name,
-so ``state_dict`` / ``load_state_dict`` and checkpoints are unchanged.
+``momentums`` / ``velocities`` stay plain param-shaped tensors of the parameter's dtype
+keyed by name, so ``state_dict`` / ``load_state_dict`` and checkpoints are unchanged.
+bf16 / fp16 parameters run ``dgc_compensate16`` / ``dgc_mask_indices16``: every op of
+the reference rounds to the dtype, as ATen does on a 16-bit tensor.
 """
 import torch
 
@@ -84,11 +86,15 @@ class DGCSGDMemory(Memory):
         self._sync()
         grad = self._clip(grad)
         mmt = self.momentums[name]
-        _lib.require_cuda_f32(grad, "DGCSGDMemory.compensate")
-        _lib.require_cuda_f32(mmt, "DGCSGDMemory.compensate")
         g = grad.contiguous()
+        dt = _lib.require_cuda_float(g, "DGCSGDMemory.compensate")
+        _lib.require_cuda_float(mmt, "DGCSGDMemory.compensate")
+        if mmt.dtype != dt:
+            raise TypeError(f"DGCSGDMemory.compensate: gradient {dt} vs momentum {mmt.dtype}")
         L = _lib.lib()
         stream = _lib.stream_of(g.device)
+        if dt in _lib.HALF:
+            return self._compensate16(g, name, accumulate)
         if accumulate:
             vec = self.velocities[name]
             _lib.check(L.dgc_compensate(_lib.ptr(g), _lib.ptr(mmt), _lib.ptr(vec), None, mmt.numel(),
@@ -101,13 +107,32 @@ class DGCSGDMemory(Memory):
                                     stream), "dgc_compensate")
         return out
 
+    def _compensate16(self, g, name, accumulate, vec32=None):
+        """compensate on a bf16 / fp16 state (K1-16); vec32: optional fp32 image of the
+        new velocity for the selection (the compressor's fused path)."""
+        mmt = self.momentums[name]
+        L = _lib.lib()
+        dt = _lib.VD[g.dtype]
+        stream = _lib.stream_of(g.device)
+        if accumulate:
+            vec = self.velocities[name]
+            _lib.check(L.dgc_compensate16(_lib.ptr(g), _lib.ptr(mmt), _lib.ptr(vec), None, _lib.ptr(vec32),
+                                          mmt.numel(), float(self.momentum), int(bool(self.nesterov)), 1, dt,
+                                          stream), "dgc_compensate16")
+            return vec
+        out = torch.empty_like(mmt)
+        _lib.check(L.dgc_compensate16(_lib.ptr(g), _lib.ptr(mmt), None, _lib.ptr(out), None, mmt.numel(),
+                                      float(self.momentum), int(bool(self.nesterov)), 0, dt, stream),
+                   "dgc_compensate16")
+        return out
+
     def update(self, name, ctx):
         """Zero the transmitted slots (dgc/memory.py:72-77)."""
         self._sync()
         indices = ctx[0]
         vec = self.velocities[name]
         mmt = self.momentums[name]
-        _lib.require_cuda_f32(vec, "DGCSGDMemory.update")
+        dt = _lib.require_cuda_float(vec, "DGCSGDMemory.update")
         idx = indices.reshape(-1)
         if idx.dtype not in _lib.ID:
             idx = idx.to(torch.int64)
@@ -116,9 +141,10 @@ class DGCSGDMemory(Memory):
         if bad is None:
             bad = self._bad[vec.device] = torch.zeros(1, dtype=torch.int32, device=vec.device)
         L = _lib.lib()
-        _lib.check(L.dgc_mask_indices(_lib.ptr(mmt) if self.momentum_masking else None, _lib.ptr(vec),
-                                      vec.numel(), _lib.ptr(idx), _lib.ID[idx.dtype], idx.numel(),
-                                      _lib.ptr(bad), _lib.stream_of(vec.device)), "dgc_mask_indices")
+        fn = L.dgc_mask_indices16 if dt in _lib.HALF else L.dgc_mask_indices
+        _lib.check(fn(_lib.ptr(mmt) if self.momentum_masking else None, _lib.ptr(vec),
+                      vec.numel(), _lib.ptr(idx), _lib.ID[idx.dtype], idx.numel(),
+                      _lib.ptr(bad), _lib.stream_of(vec.device)), "dgc_mask_indices")
 
     def state_dict(self):
         self._sync()

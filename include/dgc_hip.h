@@ -24,6 +24,10 @@
  *                         previous call's result (zero_() as a sparse re-zero);
  *                         dgc_clear_packed + dgc_scatter_packed_cleared: its two halves
  *   dgc_sgd_step          DGCSGD.step (weight-decay momentum + update) dgc/optim/sgd.py:42-68
+ *   dgc_compensate16, dgc_mask_indices16, dgc_widen16, dgc_decompress16
+ *                         the same memory / decompress for bf16 / fp16 parameters
+ *                         (dgc/memory.py:43-77, dgc/compression.py:179-194 on a
+ *                         16-bit tensor: every op rounds to the dtype)
  *
  * Conventions
  *   - All tensor pointers are DEVICE pointers owned by the caller (PyTorch's caching
@@ -57,7 +61,8 @@ enum dgc_status {
     DGC_ERR_UNSORTED = 6      /* decompress input has more descending runs than supported */
 };
 
-enum dgc_vdtype { DGC_F32 = 0, DGC_F16 = 1 };   /* wire value dtype  (fp16_values)   */
+enum dgc_vdtype { DGC_F32 = 0, DGC_F16 = 1, DGC_BF16 = 2 };   /* value / parameter dtype; wire values:
+                                                 fp16_values -> F16, else the param dtype */
 enum dgc_idtype { DGC_I64 = 0, DGC_I32 = 1 };   /* wire index dtype  (int32_indices) */
 
 enum dgc_sync_mode {
@@ -104,6 +109,11 @@ typedef struct dgc_select_params {
                               /*    zeroes them while it streams vec/mmt;   */
                               /*    dgc_compress_flush applies it on demand */
                               /* 0: pure selection, vec/mmt untouched       */
+    int32_t thr_dtype;        /* dtype of the tensor being sparsified        */
+                              /* (DGC_F32 / DGC_BF16 / DGC_F16): the        */
+                              /* threshold *= bound products round to it,   */
+                              /* as the 0-dim threshold tensor does          */
+    int32_t reserved;
 } dgc_select_params;
 
 /* Device-resident result record written by dgc_select / dgc_compress. */
@@ -341,6 +351,32 @@ int dgc_hbm_probe(const float* a, const float* b, const float* c, float* d, floa
 int dgc_sgd_step(float* const* params, const float* const* grads, float* const* bufs, const int64_t* numels,
                  const int32_t* first, int32_t count, float lr, float momentum, float dampening,
                  float weight_decay, int32_t nesterov, void* stream);
+
+/* ---- 16-bit parameters (bf16 / fp16, dtype = DGC_BF16 / DGC_F16) ----
+ * The reference's memory and compressor on a bf16 / fp16 parameter
+ * (dgc/memory.py:43-77, dgc/compression.py:109-198): each ATen op computes in fp32 and
+ * rounds to the dtype. Arrays are 16-bit device arrays of that dtype.
+ * dgc_compensate16: DGCSGDMemory.compensate (dgc/memory.py:50-70), rounding after
+ *   each op; with accumulate, vec32 (may be NULL) receives the new velocity's exact
+ *   fp32 image, which dgc_sample_strided / dgc_kth_largest / dgc_select then take as
+ *   the tensor (thr_dtype = dtype, vdtype = DGC_F16 for fp16_values else dtype).
+ * dgc_mask_indices16: DGCSGDMemory.update (dgc/memory.py:72-77).
+ * dgc_widen16: y = fp32 image of x (a 16-bit tensor handed to the selection).
+ * dgc_decompress16: grad.zero_().index_put_([idx], values.type(dtype),
+ *   accumulate=True).mul_(scale) (dgc/compression.py:179-194): runs (ranks) in order,
+ *   each add rounded to the dtype; indices distinct within a run (as DGC payloads
+ *   are); the mul_ is skipped for scale == 1. run_offsets: host array, nruns + 1.
+ *   nruns = -1: ONE run, indices stably sorted (duplicates in their input order),
+ *   run_offsets = {begin, end}: each index's entries are folded in order — input
+ *   that does not come as distinct-index runs (index_put_'s serial order). */
+int dgc_compensate16(const void* grad, void* mmt, void* vec, void* out, float* vec32, int64_t n, float momentum,
+                     int32_t nesterov, int32_t accumulate, int32_t dtype, void* stream);
+int dgc_mask_indices16(void* mmt, void* vec, int64_t n, const void* indices, int32_t idtype, int64_t count,
+                       int32_t* bad_flag, void* stream);
+int dgc_widen16(const void* x, float* y, int64_t n, int32_t dtype, void* stream);
+int dgc_decompress16(const void* values, int32_t vdtype, const void* indices, int32_t idtype,
+                     const int64_t* run_offsets, int32_t nruns, void* grad, int32_t dtype, int64_t n, float scale,
+                     int32_t* bad_flag, void* stream);
 
 #ifdef __cplusplus
 }

@@ -42,3 +42,8 @@ def golden_attributes():
 @pytest.fixture(scope="session")
 def golden_optimizer():
     return load_json("optimizer.json"), np.load(os.path.join(GOLDEN, "optimizer.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_half():
+    return load_json("half.json"), np.load(os.path.join(GOLDEN, "half.npz"))

@@ -496,7 +496,90 @@ def gen_optimizer_trace(C, M, H, O):
     print(f"optimizer_trace: {len(meta)} (step, rank) call sequences")
 
 
-GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20", "optimizer_trace")
+# 16-bit parameters: the reference's memory + compressor on bf16 / fp16 tensors (every
+# ATen op rounds to the dtype). (name, N, ratio, dtype, kind, scale, nesterov, masking,
+# fp16_values, int32, resample, steps, W)
+HALF_CASES = [
+    ("bf16_n200k_nest", 200000, 0.001, "bfloat16", "normal", 1.0, True, True, False, False, True, 3, 1),
+    ("bf16_n100k_plain_fp16v_i32", 100000, 0.01, "bfloat16", "normal", 1.0, False, True, True, True, True, 3, 1),
+    ("bf16_n30000_ties_nm", 30000, 0.01, "bfloat16", "ties", 1.0, True, False, False, False, True, 3, 1),
+    ("bf16_n50k_noresample", 50000, 0.01, "bfloat16", "layered", 1.0, True, True, False, False, False, 4, 1),
+    ("fp16_n200k_nest", 200000, 0.001, "float16", "normal", 1e-2, True, True, False, False, True, 3, 1),
+    ("fp16_n100k_plain_fp16v", 100000, 0.01, "float16", "layered", 1.0, False, True, True, False, True, 3, 1),
+    ("fp16_n65537_overflow", 65537, 0.01, "float16", "normal", 3000.0, False, True, False, False, True, 2, 1),
+    ("bf16_n2001_stride1", 2001, 0.001, "bfloat16", "normal", 1.0, False, True, False, False, True, 3, 1),
+    ("bf16_w3", 20000, 0.01, "bfloat16", "normal", 1.0, True, True, False, False, True, 2, 3),
+    ("fp16_w2_fp16v_i32", 20000, 0.01, "float16", "normal", 1e-2, True, True, True, True, True, 2, 2),
+    ("bf16_w4_fp16v", 30000, 0.01, "bfloat16", "layered", 1.0, True, True, True, False, True, 2, 4),
+]
+HALF_FULL_STATE_MAX = 50000
+
+
+def gen_half(C, M, rec):
+    """Per step and rank: the indices and values the reference transmits, its
+    thresholds / counts, the 16-bit state (N <= HALF_FULL_STATE_MAX) and the
+    decompressed gradient of the rank-order concatenation (W ranks emulated as in
+    gen_decompress: identical ``random`` state per rank)."""
+    torch.set_num_threads(1)
+    meta, arrays = {}, {}
+    for ci, (name, N, r, dts, kind, scale, nest, mask, fp16, i32, resample, steps, W) in enumerate(HALF_CASES):
+        dt = getattr(torch, dts)
+        _World.size = W
+        comps, mems = [], []
+        for q in range(W):
+            _World.rank = q
+            mem = M.DGCSGDMemory(momentum=0.9, nesterov=nest, momentum_masking=mask)
+            comp = _quiet(C.DGCCompressor, r, memory=mem, fp16_values=fp16, int32_indices=i32, resample=resample)
+            prm = torch.zeros(N, dtype=dt)
+            _quiet(mem.initialize, [("w", prm)])
+            _quiet(comp.initialize, [("w", prm)])
+            comps.append(comp)
+            mems.append(mem)
+        random.seed(42)
+        case = dict(N=N, ratio=r, dtype=dts, kind=kind, scale=scale, nesterov=nest, masking=mask, fp16=fp16,
+                    int32=i32, resample=resample, steps=steps, W=W,
+                    attrs=[comps[0].attributes["w"][i] for i in (0, 2, 3, 4, 5)], per_step=[])
+        for s in range(steps):
+            rstate = random.getstate()
+            payloads, ctxs, ranks = [], [], []
+            for q in range(W):
+                random.setstate(rstate)
+                _World.rank = q
+                seed = 70000 + 100 * ci + 10 * s + q
+                g = torch.from_numpy(synth.gradient(seed, N, kind, scale).copy()).to(dt)
+                rec.reset()
+                with rec:
+                    (v, i), ctx = comps[q].compress(g, "w")
+                payloads.append((v, i))
+                ctxs.append(ctx)
+                key = f"{name}/s{s}/r{q}"
+                arrays[key + "/indices"] = i.view(-1).numpy().copy()
+                arrays[key + "/values"] = v.view(-1).float().numpy().copy()
+                if N <= HALF_FULL_STATE_MAX:
+                    arrays[key + "/mmt"] = mems[q].momentums["w"].float().numpy().copy()
+                    arrays[key + "/vec"] = mems[q].velocities["w"].float().numpy().copy()
+                ranks.append(dict(seed=seed, thresholds=[float(t) for t in rec.thresholds], counts=rec.counts,
+                                  topk_calls=rec.topk_calls, n=int(i.numel()), values_dtype=str(v.dtype),
+                                  mmt_sha=synth.digest(mems[q].momentums["w"].float().numpy()),
+                                  vec_sha=synth.digest(mems[q].velocities["w"].float().numpy())))
+            _World.rank = 0
+            cat_v = torch.cat([p[0] for p in payloads])
+            cat_i = torch.cat([p[1] for p in payloads])
+            out = comps[0].decompress((cat_v, cat_i), ctxs[0])
+            flat = out.view(-1).float().numpy()
+            nz = np.flatnonzero(flat.view(np.uint32))
+            arrays[f"{name}/s{s}/dec_nz_idx"] = nz.astype(np.int64)
+            arrays[f"{name}/s{s}/dec_nz_val"] = flat[nz].copy()
+            case["per_step"].append(dict(ranks=ranks, out_dtype=str(out.dtype), dense_sha=synth.digest(flat)))
+        meta[name] = case
+        print(f"half {name}: " + ", ".join(f"{len(p['ranks'][0]['counts'])}c/{p['ranks'][0]['topk_calls']}t"
+                                           for p in case["per_step"]))
+    np.savez_compressed(os.path.join(HERE, "half.npz"), **arrays)
+    with open(os.path.join(HERE, "half.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20", "optimizer_trace", "half")
 
 
 def main(which=GENERATORS):
@@ -514,6 +597,8 @@ def main(which=GENERATORS):
         gen_optimizer_resnet20(C, M, H, O)
     if "optimizer_trace" in which:
         gen_optimizer_trace(C, M, H, O)
+    if "half" in which:
+        gen_half(C, M, rec)
 
 
 if __name__ == "__main__":

@@ -23,7 +23,7 @@ def main():
                 env, root = dict(os.environ), os.path.abspath(lib)
                 env.pop("DGC_HIP_LIB", None)
             else:
-                env, root = dict(os.environ, DGC_HIP_LIB=os.path.abspath(lib)), REPO
+                env, root = dict(os.environ, DGC_HIP_LIB=os.path.abspath(lib), DGC_LIB_PARTIAL="1"), REPO
             out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--workload", wl, "--no-cpu",
                                   "--steps", "20", "--warmup", "5"], env=env, check=True, capture_output=True,
                                  text=True).stdout

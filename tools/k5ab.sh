@@ -1,18 +1,15 @@
 #!/bin/bash
-# K5 A/B: tools/k5_bench-style select timings with the multi-workgroup global phase vs one workgroup
+# Same-box A/B of K5 timings (tools/k5_bench.py select_ms, min of 3) and the model-set
+# bench steps: this tree's library vs adam-compression_amd/lib/ab_old (a previous
+# revision: make -C <old csrc> OUT_DIR=<repo>/adam-compression_amd/lib/ab_old).
 set -o pipefail
-for r in 1 2; do for m in multi wg; do
-  if [ $m = wg ]; then export DGC_K5_GLOBAL=wg; else unset DGC_K5_GLOBAL; fi
-  timeout -k 10 120 python tools/k5_bench.py > gpurun_out/k5_${m}_$r.log 2>&1 || exit $?
-  echo "== $m $r"; grep -v amdgpu.ids gpurun_out/k5_${m}_$r.log
-done; done
-for r in 1 2; do for wl in resnet50 vgg16_bn; do for m in multi wg; do
-  if [ $m = wg ]; then export DGC_K5_GLOBAL=wg; else unset DGC_K5_GLOBAL; fi
-  timeout -k 10 200 python bench.py --workload $wl --no-cpu --steps 20 --warmup 5 > gpurun_out/k5ab_${wl}_${m}_$r.json 2>/dev/null || exit $?
-  python -c "import json;d=json.load(open('gpurun_out/k5ab_${wl}_${m}_$r.json'));print('$wl','$m',round(d['ms_per_step'],4))"
-done; done; done
-for m in multi wg; do
-  if [ $m = wg ]; then export DGC_K5_GLOBAL=wg; else unset DGC_K5_GLOBAL; fi
-  timeout -k 10 200 python bench.py --workload flat-1B --no-cpu --steps 20 --warmup 5 > gpurun_out/k5ab_flat_${m}.json 2>/dev/null || exit $?
-  python -c "import json;d=json.load(open('gpurun_out/k5ab_flat_${m}.json'));print('flat-1B','$m',round(d['ms_per_step'],4))"
+mkdir -p gpurun_out/k5ab
+export TMPDIR=/tmp
+for r in 1 2; do
+  for lib in adam-compression_amd/lib/libdgc_hip.so adam-compression_amd/lib/ab_old/libdgc_hip.so; do
+    DGC_HIP_LIB=$PWD/$lib DGC_LIB_PARTIAL=1 K5_MODELS=0 timeout -k 10 200 python tools/k5_bench.py > gpurun_out/k5ab/k5_${r}_$(basename $(dirname $lib)).txt 2>&1 || exit 1
+  done
+done
+for wl in ${K5AB_WL:-resnet50 vgg16_bn}; do
+  timeout -k 10 600 python tools/ab_bench.py $wl adam-compression_amd/lib/libdgc_hip.so adam-compression_amd/lib/ab_old/libdgc_hip.so 2 > gpurun_out/k5ab/ab_$wl.txt 2>&1 || exit 1
 done
