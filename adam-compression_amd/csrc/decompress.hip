@@ -322,12 +322,7 @@ __device__ void tile_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__
             cnt = b1 - b0;
             if (c == 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);   // idx < 0 or >= n
         }
-        long long incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const long long y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        const long long incl = (long long)wave_incl_scan64((uint64_t)cnt);   // the whole wave 0 is here
         if (tid < nr) roff[tid] = (int)(incl - cnt);
         if (tid == nr - 1) roff[nr] = (int)incl;
     }

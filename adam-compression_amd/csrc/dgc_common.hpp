@@ -188,14 +188,36 @@ __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan<Op>(v), 63);
 }
 
+// 64-bit inclusive add-scan: the same DPP steps on both halves, carry propagated.
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define DGC_SCAN64_STEP(CTRL, ROWS)                                    \
+    {                                                                  \
+        const uint32_t l2 = dpp_src<CTRL, ROWS>(lo, 0u);               \
+        const uint32_t h2 = dpp_src<CTRL, ROWS>(hi, 0u);               \
+        const uint32_t nl = lo + l2;                                   \
+        hi = hi + h2 + (nl < lo ? 1u : 0u);                            \
+        lo = nl;                                                       \
+    }
+    DGC_SCAN64_STEP(0x111, 0xf)
+    DGC_SCAN64_STEP(0x112, 0xf)
+    DGC_SCAN64_STEP(0x114, 0xf)
+    DGC_SCAN64_STEP(0x118, 0xf)
+    DGC_SCAN64_STEP(0x142, 0xa)
+    DGC_SCAN64_STEP(0x143, 0xc)
+#undef DGC_SCAN64_STEP
+    return ((uint64_t)hi << 32) | lo;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
     if constexpr (sizeof(T) == 4) {
         return (T)wave_reduce<DppAdd>((uint32_t)v);
     } else {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        return v;
+        const uint64_t s = wave_incl_scan64((uint64_t)v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s, 63);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s >> 32), 63);
+        return (T)(((uint64_t)hi << 32) | lo);
     }
 }
 
@@ -262,12 +284,7 @@ __device__ __forceinline__ void store_index(void* out, int64_t pos, int64_t idx,
 // <= 1024); returns the exclusive prefix and writes the block total to *total.
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds16, uint64_t* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    const uint64_t incl = wave_incl_scan64(v);
     if (lane == 63) lds16[wid] = incl;
     __syncthreads();
     uint64_t wbase = 0, tot = 0;
