@@ -1,6 +1,6 @@
 // K3's one-workgroup radix select (rs_small_wg, the model sets' sampled threshold),
-// 54 tensors per launch like ResNet-50's k_rs_small_multi (v0 and v1 both run the
-// product body; edit one to A/B a candidate). Prints us per launch and checks that the two
+// 54 tensors per launch like ResNet-50's k_rs_small_multi (v0: a previous body kept
+// here, v1: the product body). Prints us per launch and checks that the two
 // bodies agree on every case (ties, NaN, inf, tiny n, large k).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I adam-compression_amd/csrc -I include
 //        tools/rsbench.hip -o tools/rsbench
@@ -17,6 +17,89 @@
 __device__ unsigned long long g_st[16];
 #define RS_STAMP(i) do { __syncthreads(); if (blockIdx.x == 0 && threadIdx.x == 0) g_st[i] = wall_clock64(); } while (0)
 #include "radix_select.hpp"
+#define RS_STAMP_PREV(i) do { } while (0)
+namespace dgc {
+__device__ void rs_small_prev(const float* __restrict__ x, int64_t n, uint64_t k64, float* out) {
+    constexpr int kPer = kSmallN / kScanThreads;
+    __shared__ uint32_t h[kRsBins];
+    __shared__ uint32_t lds32[16];
+    __shared__ uint32_t nan_cnt, prefix, k_rem, sel_above;
+    __shared__ int sel_bin;
+    const int tid = threadIdx.x;
+    const int nn = (int)n;   // <= kSmallN
+    const uint32_t k = (uint32_t)k64;
+    RS_STAMP_PREV(0);
+    for (int b = tid; b < kRsBins; b += kScanThreads) h[b] = 0;
+    if (tid == 0) {
+        nan_cnt = 0;
+        prefix = 0;
+        k_rem = k;
+        sel_bin = -1;
+    }
+    // the thread's keys stay in registers (kPer VGPRs); out-of-range slots hold 0 and
+    // are masked by `in` below
+    uint32_t key[kPer];
+    uint32_t mx = 0, my_nan = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = tid + j * kScanThreads;
+        key[j] = i < nn ? abs_key(x[i]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const bool in = tid + j * kScanThreads < nn;
+        mx = in && key[j] > mx ? key[j] : mx;
+        my_nan += in && key[j] > 0x7F800000u ? 1u : 0u;
+    }
+    __syncthreads();   // h zeroed
+    RS_STAMP_PREV(1);
+    if (my_nan) atomicAdd(&nan_cnt, my_nan);
+    if (tid < nn) atomicAdd(&h[mx >> 21], 1u);
+    __syncthreads();
+    {
+        int bin;
+        uint32_t above;
+        if (pick_bin_small<2>(h, k, lds32, &bin, &above)) sel_bin = bin;
+    }
+    __syncthreads();
+    const uint32_t floor = sel_bin >= 0 ? (uint32_t)sel_bin << 21 : 0u;
+    RS_STAMP_PREV(2);
+    for (int pass = 0; pass < 3; ++pass) {
+        for (int b = tid; b < kRsBins; b += kScanThreads) h[b] = 0;
+        __syncthreads();   // everyone has read sel_bin / prefix
+        if (tid == 0) sel_bin = -1;
+        const uint32_t pmask = rs_pmask(pass), dmask = rs_dmask(pass), pre = prefix;
+        const int shift = rs_shift(pass);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const bool in = tid + j * kScanThreads < nn;
+            if (in && (pass == 0 ? key[j] >= floor : (key[j] & pmask) == pre))
+                atomicAdd(&h[(key[j] >> shift) & dmask], 1u);
+        }
+        __syncthreads();
+        RS_STAMP_PREV(3 + 2 * pass);
+        int bin;
+        uint32_t above;
+        const bool hit = pass == 2 ? pick_bin_small<1>(h, k_rem, lds32, &bin, &above)
+                                   : pick_bin_small<2>(h, k_rem, lds32, &bin, &above);
+        if (hit) {
+            sel_bin = bin;
+            sel_above = above;
+        }
+        __syncthreads();
+        if (tid == 0 && sel_bin >= 0) {
+            prefix |= (uint32_t)sel_bin << shift;
+            k_rem -= sel_above;
+        }
+        __syncthreads();
+        RS_STAMP_PREV(4 + 2 * pass);
+        if (sel_bin < 0) break;   // uniform: k exceeds the key count
+    }
+    if (tid == 0) *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
+    __syncthreads();
+}
+
+}  // namespace dgc
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -24,7 +107,7 @@ using namespace dgc;
 
 __global__ void __launch_bounds__(kScanThreads) k_v0(const float* x, const int64_t* n, const uint64_t* k, float* out,
                                                      int64_t stride) {
-    rs_small_wg(x + blockIdx.x * stride, n[blockIdx.x], k[blockIdx.x], out + blockIdx.x);
+    rs_small_prev(x + blockIdx.x * stride, n[blockIdx.x], k[blockIdx.x], out + blockIdx.x);
 }
 __global__ void __launch_bounds__(kScanThreads) k_v1(const float* x, const int64_t* n, const uint64_t* k, float* out,
                                                      int64_t stride) {
