@@ -38,6 +38,7 @@ class _Gathered(list):
     rank_stride = 0
     capacity = 0
     run_offsets = None
+    distinct_runs = False   # every run's indices distinct (payloads this compressor emitted)
 
 
 class _PackedHandle:
@@ -50,6 +51,7 @@ class _PackedHandle:
         self.stride = stride
         self.voff = voff
         self.ioff = ioff
+        self.distinct = False   # the payload came from compress (distinct indices per rank)
 
 
 def _layout(capacity, vdtype, idtype):
@@ -396,9 +398,10 @@ class DGCCompressor:
         if indices.dtype not in _lib.ID:
             indices = indices.to(torch.int64)
         offs = getattr(tensor, "run_offsets", None)
-        if offs is None:
-            # reference-format input (ranks' indices may repeat): one stably sorted run,
-            # each index folded in input order (as the fp32 path's unsorted fallback)
+        if offs is None or not getattr(tensor, "distinct_runs", False):
+            # input whose runs may repeat an index (the reference's list format, or
+            # foreign payloads): one stably sorted run, each index folded in input order
+            # (index_put_'s serial order; as the fp32 path's unsorted fallback)
             order = torch.sort(indices, stable=True).indices
             values, indices = values[order].contiguous(), indices[order].contiguous()
             offs, nruns = [0, values.numel()], -1
@@ -424,11 +427,14 @@ class DGCCompressor:
             values, indices = tensor_compressed
             packed = self._payloads.get(name)
             payload, lay = packed if packed is not None else (None, None)
-            if payload is None or values.data_ptr() != payload.data_ptr() + lay[4]:
+            ours = payload is not None and values.data_ptr() == payload.data_ptr() + lay[4]
+            if not ours:
                 payload, lay = self._pack_foreign(name, values, indices)
             k, vdt, idt, stride, voff, ioff = lay
             handle = comm.allgather_packed_async(payload)
-            return _PackedHandle(handle, name, k, vdt, idt, stride, voff, ioff)
+            h = _PackedHandle(handle, name, k, vdt, idt, stride, voff, ioff)
+            h.distinct = ours   # every rank runs this same code: all payloads are compress's
+            return h
         return comm.allreduce_async_(tensor_compressed, name=name, op=op)
 
     def _pack_foreign(self, name, values, indices):
@@ -462,6 +468,7 @@ class DGCCompressor:
             for c in counts:
                 offs.append(offs[-1] + c)
             out.run_offsets = offs
+            out.distinct_runs = handle.distinct
             return out
         if isinstance(handle, (tuple, list)):
             return [comm.synchronize(h) for h in handle]

@@ -365,3 +365,56 @@ def batch_worker(rank, world, port, fill, kind, queue):
         queue.put((rank, [("error", repr(e), traceback.format_exc())]))
     finally:
         dist.destroy_process_group()
+
+
+def half_worker(rank, world, port, case_name, queue):
+    """A 16-bit golden case (tests/golden/half.*) at its own world size over gloo: each
+    rank compresses its own gradient (DGCSGDMemory / DGCCompressor on bf16 / fp16),
+    communicate -> synchronize (the packed allgather) -> decompress; the payload, the
+    16-bit state and the decompressed gradient must equal the reference's."""
+    _init(rank, world, port)
+    problems = []
+    try:
+        from dgc.compression import DGCCompressor
+        from dgc.memory import DGCSGDMemory
+        from dgc.comm import Average
+        from oracle import synth
+        with open(os.path.join(GOLDEN, "half.json")) as f:
+            case = json.load(f)[case_name]
+        arrays = np.load(os.path.join(GOLDEN, "half.npz"))
+        assert case["W"] == world
+        dt = getattr(torch, case["dtype"])
+        dev = torch.device("cuda:0")
+        N = case["N"]
+        mem = DGCSGDMemory(momentum=0.9, nesterov=case["nesterov"], momentum_masking=case["masking"])
+        with contextlib.redirect_stdout(io.StringIO()):
+            comp = DGCCompressor(case["ratio"], memory=mem, fp16_values=case["fp16"], int32_indices=case["int32"],
+                                 resample=case["resample"])
+            prm = torch.zeros(N, dtype=dt, device=dev)
+            mem.initialize([("w", prm)])
+            comp.initialize([("w", prm)])
+        random.seed(42)
+        for s, step in enumerate(case["per_step"]):
+            rk = step["ranks"][rank]
+            g = torch.from_numpy(synth.gradient(rk["seed"], N, case["kind"], case["scale"]).copy()).to(dt).to(dev)
+            (vals, idx), ctx = comp.compress(g, "w")
+            key = f"{case_name}/s{s}/r{rank}"
+            if not np.array_equal(idx.view(-1).cpu().numpy(), arrays[key + "/indices"]):
+                problems.append((s, "indices"))
+            if not np.array_equal(vals.view(-1).float().cpu().numpy().view(np.uint32),
+                                  arrays[key + "/values"].view(np.uint32)):
+                problems.append((s, "values"))
+            h = comp.communicate((vals, idx), "w", Average)
+            out = comp.decompress(comp.synchronize(h), ctx)
+            want = np.zeros(N, np.float32)
+            nz = arrays[f"{case_name}/s{s}/dec_nz_idx"]
+            want[nz] = arrays[f"{case_name}/s{s}/dec_nz_val"]
+            got = out.view(-1).float().cpu().numpy()
+            if out.dtype != dt or not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                problems.append((s, "decompress"))
+            if synth.digest(mem.velocities["w"].float().cpu().numpy()) != rk["vec_sha"]:
+                problems.append((s, "vec"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        problems.append(("exception", traceback.format_exc()[-600:]))
+    queue.put((rank, problems))

@@ -90,6 +90,7 @@ def test_half_dropin_against_reference_goldens(L, golden_half, decomp):
             if decomp == "offsets":   # as our synchronize hands it over: one run per rank
                 gath = _Gathered([cat_v, cat_i])
                 gath.run_offsets = list(np.cumsum([0] + [p[0].numel() for p in payload]))
+                gath.distinct_runs = True
             else:                     # the reference's list of two concatenations
                 gath = [cat_v, cat_i]
             ctxs[0][5].fill_(7.0)     # decompress overwrites the gradient buffer

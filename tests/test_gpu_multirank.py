@@ -102,3 +102,14 @@ def test_bucket_w4_matches_oracle(fill):
     for rank, res in out.items():
         problems = [r for r in res if r[0] != "branches"]
         assert problems == [], (rank, res)
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("case", ["fp16_w2_fp16v_i32"])
+def test_half_w2_communicate_matches_reference(case):
+    """bf16 / fp16 parameters through the real exchange (compress -> communicate ->
+    synchronize -> decompress, gloo) at the golden case's world size: payloads, 16-bit
+    velocity and decompressed gradient equal the reference's (tests/golden/half.*)."""
+    out = run(G.half_worker, 2, case)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)
