@@ -780,6 +780,103 @@ __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* xl, DGC_
     return ln < rs ? ln : rs;
 }
 
+// ---------------------------------------------------------------- register tail
+// The last steps (range <= 64 entries): entry i of the range in lane i's registers, so
+// a step is ballots, mbcnt and one cross-lane move — no LDS round trip at all. The
+// median of three comes from readlanes; L_t's partner is the R stopper with t right
+// stoppers after it, i.e. bit TR-1-t of the right-stopper ballot, R's partner with u
+// right stoppers after it is bit u of the left-stopper ballot (select_bit).
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Position of the k-th (0-based) set bit of m (k < popcount(m)).
+__device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t k) {
+    uint32_t pos = 0, c = (uint32_t)__popc((uint32_t)m);
+    uint32_t w = (uint32_t)m;
+    if (k >= c) {
+        k -= c;
+        w = (uint32_t)(m >> 32);
+        pos = 32;
+    }
+#pragma unroll
+    for (int b = 16; b >= 1; b >>= 1) {
+        c = (uint32_t)__popc(w & ((1u << b) - 1u));
+        if (k >= c) {
+            k -= c;
+            w >>= b;
+            pos += (uint32_t)b;
+        }
+    }
+    return pos;
+}
+
+// Range q[f, l) of <= 64 entries; returns after the entries are back in q and the
+// final insertion sort ran; depth as in nth_tail_wave.
+__device__ void nth_tail_regs(DGC_LDS uint64_t* q, int64_t f, int64_t l, int64_t depth, int64_t nth) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n = (uint32_t)(l - f);
+    uint64_t x = lane < n ? q[f + lane] : 0ull;
+    uint32_t F = 0, Lr = n;
+    const int64_t nr = nth - f;
+    bool heap = false;
+    while (Lr - F > 3) {
+        if (depth == 0) {
+            heap = true;
+            break;
+        }
+        depth -= 1;
+        K5_STEP(2);
+        // std::__move_median_to_first(F, F+1, mid, Lr-1), as nth_median
+        const uint32_t a = F + 1, b = F + (Lr - F) / 2, c = Lr - 1;
+        const uint64_t ea = readlane64(x, a), eb = readlane64(x, b), ec = readlane64(x, c), ef = readlane64(x, F);
+        const uint32_t ka = qkey(ea), kb = qkey(eb), kc = qkey(ec);
+        uint32_t m;
+        uint64_t em;
+        if (ka > kb) {
+            if (kb > kc) { m = b; em = eb; }
+            else if (ka > kc) { m = c; em = ec; }
+            else { m = a; em = ea; }
+        } else if (ka > kc) { m = a; em = ea; }
+        else if (kb > kc) { m = c; em = ec; }
+        else { m = b; em = eb; }
+        x = lane == F ? em : lane == m ? ef : x;
+        const uint32_t P = qkey(em);
+        // the Hoare partition of [F+1, Lr) around P (nth_step_wave's tests)
+        const bool inr = lane > F && lane < Lr;
+        const bool isl = inr && qkey(x) <= P, isr = inr && qkey(x) >= P;
+        const uint64_t BL = __ballot(isl), BR = __ballot(isr);
+        const uint32_t TR = (uint32_t)__popcll(BR);
+        const uint32_t rl = mbcnt64(BL, 0u);
+        const uint32_t ur = TR - (mbcnt64(BR, 0u) + (isr ? 1u : 0u));
+        const bool swl = isl && ur >= rl + 1;
+        const bool swr = isr && rl >= ur + 1;
+        const uint32_t src = swl ? select_bit(BR, TR - 1u - rl) : swr ? select_bit(BL, ur) : lane;
+        const uint64_t y = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(x >> 32), (int)src) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)x, (int)src);
+        const uint64_t msl = __ballot(swl), mln = __ballot(isl && !swl), msr = __ballot(swr);
+        x = (swl || swr) ? y : x;
+        const uint32_t s = (uint32_t)__popcll(msl);
+        const uint32_t ln = mln ? (uint32_t)__builtin_ctzll(mln) : 0xFFFFFFFFu;
+        const uint32_t rs = s ? (uint32_t)__builtin_ctzll(msr) : Lr;
+        const uint32_t cut = ln < rs ? ln : rs;
+        if ((int64_t)cut <= nr)
+            F = cut;
+        else
+            Lr = cut;
+    }
+    if (lane < n) q[f + lane] = x;
+    wave_sync();
+    if (heap) {
+        if (lane == 0) nth_heap_select(q + f + F, nth + 1 - (f + F), (int64_t)(Lr - F), nth - (f + F));
+    } else if (lane == 0) {
+        nth_insertion_sort(q, f + F, f + Lr);
+    }
+    wave_sync();
+}
+
 // Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
 // slots: >= kNthWave + kWave u64 of LDS (the pair slots and the dummy words).
 __device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* slots, NthShared& sh, int64_t nth) {
@@ -790,6 +887,10 @@ __device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* slots, NthS
     DGC_LDS uint64_t* dummy = slots + kNthWave;
     K5_WSUB_BEGIN();
     while (l - f > 3) {
+        if (l - f <= kWave) {   // the rest in registers
+            nth_tail_regs(q, f, l, depth, nth);
+            return;
+        }
         if (depth == 0) {
             if (lane == 0) nth_heap_select(q + f, nth + 1 - f, l - f, nth - f);
             wave_sync();
