@@ -634,7 +634,7 @@ __device__ __forceinline__ void nth_advance(NthShared& sh, int64_t nth) {
 // in gpos_l / gpos_r); otherwise mk / mk_tiles and the plain LDS slots lpos / rpos.
 // Pointers typed by address space (dgc_common.hpp: DGC_GLB / DGC_LDS).
 template <int kNthBatch, int kSwapBatch, bool GLOBAL, class QP, class SP>
-__device__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& sh, int64_t nth, int64_t stop,
+__device__ __forceinline__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& sh, int64_t nth, int64_t stop,
                             DGC_LDS uint8_t* mk, int64_t mk_tiles, size_t arena_bytes = 0) {
     // thread 0 prepares a step: depth check, median, reset of the step's results
     auto prepare = [&]() -> bool {
@@ -815,7 +815,7 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t k) {
 
 // Range q[f, l) of <= 64 entries; returns after the entries are back in q and the
 // final insertion sort ran; depth as in nth_tail_wave.
-__device__ void nth_tail_regs(DGC_LDS uint64_t* q, int64_t f, int64_t l, int64_t depth, int64_t nth) {
+__device__ __forceinline__ void nth_tail_regs(DGC_LDS uint64_t* q, int64_t f, int64_t l, int64_t depth, int64_t nth) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t n = (uint32_t)(l - f);
     uint64_t x = lane < n ? q[f + lane] : 0ull;
@@ -879,7 +879,7 @@ __device__ void nth_tail_regs(DGC_LDS uint64_t* q, int64_t f, int64_t l, int64_t
 
 // Wave 0 finishes the introselect from sh.f/l/depth (range <= kNthWave, in LDS).
 // slots: >= kNthWave + kWave u64 of LDS (the pair slots and the dummy words).
-__device__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* slots, NthShared& sh, int64_t nth) {
+__device__ __forceinline__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* slots, NthShared& sh, int64_t nth) {
     int64_t f = sh.f, l = sh.l, depth = sh.depth;
     const int lane = threadIdx.x & 63;
     DGC_LDS uint64_t* xl = slots;

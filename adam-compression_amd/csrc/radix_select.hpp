@@ -348,7 +348,7 @@ __device__ __forceinline__ bool pick_bin_small(const uint32_t* h, uint32_t k, ui
 // are >= b0 << 21, so the k-th largest key is too, and pass 0 need count only the keys
 // >= b0 << 21 — the bins >= b0 are exact, pick_bin picks the same bin. No floor when
 // fewer than k threads hold a key.
-__device__ void rs_small_wg(const float* __restrict__ x, int64_t n, uint64_t k64, float* out) {
+__device__ __forceinline__ void rs_small_wg(const float* __restrict__ x, int64_t n, uint64_t k64, float* out) {
     constexpr int kPer = kSmallN / kScanThreads;
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t lds32[16];
