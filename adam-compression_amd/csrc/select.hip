@@ -1126,21 +1126,21 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         if (v) atomicAdd(&st->lower_cnt[j], (unsigned long long)v);
     }
     if (!last_block_arrival(&st->tickets[0], (uint32_t)nb)) return;
-    if (threadIdx.x == 0) {
-        int js = m;
-        for (int j = 1; j <= m; ++j) {
-            const long long nj = (long long)load_count(&st->lower_cnt[j]);
-            if (nj >= d.lower_count) {
-                js = j;
-                break;
-            }
-        }
+    if (threadIdx.x < kWave) {
+        // the m counts loaded together, one lane each (a loop of dependent agent-scope
+        // loads paid an L2 round trip per threshold); j* = the first reaching lower*k
+        const int j = lane + 1;
+        const bool hit = j <= m && (long long)load_count(&st->lower_cnt[j]) >= d.lower_count;
+        const uint64_t hb = __ballot(hit);
+        const int js = hb ? __builtin_ctzll(hb) + 1 : m;
+        if (threadIdx.x == 0) {
         st->t_cur = th[js];
         st->iter = js;
         st->recounts = js;
         st->overflow = 0;
         st->lower_pending = 0;
         st->active = 1;   // count pass + decide at t_{j*}
+        }
     }
 }
 
@@ -1226,14 +1226,13 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         atomicAdd(&st->lower_cnt[threadIdx.x], (unsigned long long)bsum[threadIdx.x]);
     const uint32_t nb = (uint32_t)(w.bt[BT_SEG][t + 1] - w.bt[BT_SEG][t]);
     if (!last_block_arrival(&st->tickets[2], nb)) return;
-    if (threadIdx.x == 0) {
-        int js = 0;
-        for (int j = 1; j <= ms; ++j) {
-            if ((long long)load_count(&st->lower_cnt[j]) >= d.lower_count) {
-                js = j;
-                break;
-            }
-        }
+    if (threadIdx.x < kWave) {
+        // the ms counts loaded together, one lane each (see k_lower_counts)
+        const int jl = (int)(threadIdx.x & 63) + 1;
+        const bool hit = jl <= ms && (long long)load_count(&st->lower_cnt[jl]) >= d.lower_count;
+        const uint64_t hb = __ballot(hit);
+        int js = hb ? __builtin_ctzll(hb) + 1 : 0;
+        if (threadIdx.x == 0) {
         // every t_j served and none reaches lower*k: t_(max_iters), as k_lower_counts picks
         if (!js && ms == p.max_iters) js = ms;
         if (js) {
@@ -1245,6 +1244,7 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
             st->active = 1;   // count pass + decide at t_{j*}
         } else {
             for (int j = 1; j <= ms; ++j) st->lower_cnt[j] = 0;   // k_lower_counts recounts every t_j
+        }
         }
     }
 }
