@@ -772,7 +772,16 @@ __device__ void decide_tensor(const SelWS& w, const SelCfg& p, int t, int spec =
     __shared__ uint64_t lds16[16];
     __shared__ int finished;
     uint64_t local = 0;
-    for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) local += load_count(&w.grp_cnt[d.grp0 + i]);
+    // 8 loads in flight per thread: a 7B tensor has ~6700 groups, 26 per thread of a
+    // 256-thread workgroup — one agent-scope round trip each when issued one by one
+    const int64_t bd = blockDim.x;
+    for (int64_t i0 = threadIdx.x; i0 < d.ngrp; i0 += 8 * bd) {
+        uint64_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = i0 + u * bd < d.ngrp ? load_count(&w.grp_cnt[d.grp0 + i0 + u * bd]) : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) local += v[u];
+    }
     uint64_t n;
     block_exclusive_scan(local, lds16, &n);
     if (threadIdx.x == 0) {
