@@ -16,6 +16,8 @@
 // one float4 per lane in one-shot block chunks. The sample |vec[start + q*stride]|
 // is written from registers, saving a strided re-read of vec (which would touch
 // ~1/3 of its lines).
+#include <algorithm>
+
 #include "dgc_common.hpp"
 
 namespace dgc {
@@ -168,6 +170,188 @@ static int launch_comp(const float* g, float* m, float* v, float* o, int64_t n, 
     return DGC_OK;
 }
 
+// ---- the dense tensors of a step (dgc/compression.py:173-177, 195-198) ----
+// Multi-tensor gather with the wire cast: dst[off_t + i] = cast(src_t[i]) for up to
+// kMtMax tensors per launch (their table rides in the kernel arguments): the dense
+// gradients of a step, wherever autograd put them, into one allreduce buffer — fp16
+// when the compressor casts (`tensor.type(torch.float16)`), else fp32. One launch where
+// a copy per parameter was one ATen launch each (107 for ResNet-50).
+constexpr int kMtMax = 64;
+constexpr int kMtPerThread = 4;
+struct MtChunk {
+    int32_t count, dtype;                // dtype: DGC_F32 / DGC_F16 / DGC_BF16 of dst
+    int32_t bstart[kMtMax + 1];          // first workgroup of each tensor (prefix)
+    const float* src[kMtMax];
+    int64_t n[kMtMax];
+    int64_t off[kMtMax];
+};
+
+__global__ void __launch_bounds__(kBlock) k_gather_cast(MtChunk c, void* __restrict__ dst) {
+    int lo = 0, hi = c.count - 1;   // the tensor of this workgroup: bstart[t] <= b < bstart[t + 1]
+    const int b = (int)blockIdx.x;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (c.bstart[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const int t = lo;
+    const float* __restrict__ src = c.src[t];
+    const int64_t n = c.n[t], off = c.off[t];
+    const int64_t e0 = ((int64_t)(b - c.bstart[t]) * kBlock) * kMtPerThread + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kMtPerThread; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        if (e >= n) break;
+        const float x = src[e];
+        if (c.dtype == DGC_F16)
+            static_cast<uint16_t*>(dst)[off + e] = f32_to_f16(x);
+        else if (c.dtype == DGC_BF16)
+            static_cast<uint16_t*>(dst)[off + e] = f32_to_bf16(x);
+        else
+            static_cast<float*>(dst)[off + e] = x;
+    }
+}
+
+// compensate(accumulate=False) of the exchanged dense gradient (dgc/memory.py:50-70 on
+// what decompress hands it, dgc/compression.py:195-198): the source is the allreduce
+// buffer — fp32, or fp16 widened exactly as `tensor.type(vdtype)` does — or, ROUND16, an
+// fp32 gradient rounded to fp16 and back (a one-rank exchange of an fp16 wire, with no
+// buffer in between). Four elements per thread; the dense tensors are small.
+template <bool NEST, int SRC>   // SRC: 0 fp32, 1 fp16, 2 fp32 rounded through fp16
+__global__ void __launch_bounds__(kBlock)
+k_compensate_wire(const void* __restrict__ src, float* __restrict__ mmt, float* __restrict__ out, int64_t n,
+                  float mom) {
+    const int64_t e0 = (int64_t)blockIdx.x * kBlock * 4 + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        if (e >= n) break;
+        float g;
+        if (SRC == 1)
+            g = f16_to_f32(static_cast<const uint16_t*>(src)[e]);
+        else if (SRC == 2)
+            g = f16_to_f32(f32_to_f16(static_cast<const float*>(src)[e]));
+        else
+            g = static_cast<const float*>(src)[e];
+        float m = mmt[e], v = 0.f;
+        const float o = comp1<NEST, false>(g, m, v, mom);
+        mmt[e] = m;
+        out[e] = o;
+    }
+}
+
+// compensate(accumulate=False) of up to kMtMax tensors per launch straight from their
+// gradients (a one-rank exchange: nothing to gather for an allreduce), mmt and out at
+// the tensors' offsets of two flat buffers; ROUND16: each gradient rounded to fp16 and
+// back first (the fp16 wire's cast and decompress's widening).
+template <bool NEST, bool ROUND16>
+__global__ void __launch_bounds__(kBlock) k_compensate_mt(MtChunk c, float* __restrict__ mmt, float* __restrict__ out,
+                                                          float mom) {
+    int lo = 0, hi = c.count - 1;
+    const int b = (int)blockIdx.x;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (c.bstart[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const int t = lo;
+    const float* __restrict__ src = c.src[t];
+    const int64_t n = c.n[t], off = c.off[t];
+    const int64_t e0 = ((int64_t)(b - c.bstart[t]) * kBlock) * kMtPerThread + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kMtPerThread; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        if (e >= n) break;
+        const float g = ROUND16 ? f16_to_f32(f32_to_f16(src[e])) : src[e];
+        float m = mmt[off + e], v = 0.f;
+        const float o = comp1<NEST, false>(g, m, v, mom);
+        mmt[off + e] = m;
+        out[off + e] = o;
+    }
+}
+
+// The tensor table of one launch: tensors [t0, t0 + count) of the host arrays.
+static int mt_chunk(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t t0,
+                    int32_t total, MtChunk& c, int64_t& blocks, const char* who) {
+    c = MtChunk{};
+    c.count = std::min<int32_t>(kMtMax, total - t0);
+    blocks = 0;
+    for (int i = 0; i < c.count; ++i) {
+        const int64_t n = numels[t0 + i];
+        if (n < 0 || offsets[t0 + i] < 0 || (n > 0 && !srcs[t0 + i]))
+            DGC_FAIL(DGC_ERR_INVALID, "%s: tensor %d: bad pointer, size or offset", who, t0 + i);
+        c.bstart[i] = (int32_t)blocks;
+        c.src[i] = srcs[t0 + i];
+        c.n[i] = n;
+        c.off[i] = offsets[t0 + i];
+        blocks += ceil_div(n, (int64_t)kBlock * kMtPerThread);
+        if (blocks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "%s: too many elements", who);
+    }
+    c.bstart[c.count] = (int32_t)blocks;
+    return DGC_OK;
+}
+
+int compensate_multi(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count,
+                     int32_t round_to, float* mmt, float* out, float mom, bool nesterov, hipStream_t st) {
+    if (count < 0 || (count > 0 && (!srcs || !numels || !offsets || !mmt || !out)))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_multi: null argument");
+    if (round_to != DGC_F32 && round_to != DGC_F16) DGC_FAIL(DGC_ERR_DTYPE, "dgc_compensate_multi: round_to");
+    for (int32_t t0 = 0; t0 < count; t0 += kMtMax) {
+        MtChunk c;
+        int64_t blocks;
+        DGC_TRY(mt_chunk(srcs, numels, offsets, t0, count, c, blocks, "dgc_compensate_multi"));
+        if (blocks == 0) continue;
+        const dim3 gd((unsigned)blocks), bd(kBlock);
+        if (nesterov) {
+            if (round_to == DGC_F16) hipLaunchKernelGGL((k_compensate_mt<true, true>), gd, bd, 0, st, c, mmt, out, mom);
+            else hipLaunchKernelGGL((k_compensate_mt<true, false>), gd, bd, 0, st, c, mmt, out, mom);
+        } else {
+            if (round_to == DGC_F16) hipLaunchKernelGGL((k_compensate_mt<false, true>), gd, bd, 0, st, c, mmt, out, mom);
+            else hipLaunchKernelGGL((k_compensate_mt<false, false>), gd, bd, 0, st, c, mmt, out, mom);
+        }
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
+}
+
+int gather_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count, void* dst,
+                int32_t dtype, hipStream_t st) {
+    if (count < 0 || (count > 0 && (!srcs || !numels || !offsets || !dst)))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_gather_cast: null argument");
+    if (dtype != DGC_F32 && dtype != DGC_F16 && dtype != DGC_BF16) DGC_FAIL(DGC_ERR_DTYPE, "dgc_gather_cast: dtype");
+    for (int32_t t0 = 0; t0 < count; t0 += kMtMax) {
+        MtChunk c;
+        int64_t blocks;
+        DGC_TRY(mt_chunk(srcs, numels, offsets, t0, count, c, blocks, "dgc_gather_cast"));
+        c.dtype = dtype;
+        if (blocks == 0) continue;
+        hipLaunchKernelGGL(k_gather_cast, dim3((unsigned)blocks), dim3(kBlock), 0, st, c, dst);
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
+}
+
+int compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float* mmt, float* out, int64_t n,
+                    float mom, bool nesterov, hipStream_t st) {
+    if (n < 0 || (n > 0 && (!src || !mmt || !out))) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_wire: bad arguments");
+    if (n == 0) return DGC_OK;
+    int mode;
+    if (src_dtype == DGC_F16 && round_to == DGC_F32) mode = 1;
+    else if (src_dtype == DGC_F32 && round_to == DGC_F16) mode = 2;
+    else if (src_dtype == DGC_F32 && round_to == DGC_F32) mode = 0;
+    else DGC_FAIL(DGC_ERR_DTYPE, "dgc_compensate_wire: source fp32 (round_to fp32 / fp16) or fp16 (round_to fp32)");
+    const int64_t grid = ceil_div(n, (int64_t)kBlock * 4);
+    if (grid > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_wire: n too large");
+    const dim3 gd((unsigned)grid), bd(kBlock);
+#define DGC_WIRE(NE, M) hipLaunchKernelGGL((k_compensate_wire<NE, M>), gd, bd, 0, st, src, mmt, out, n, mom)
+    if (nesterov) {
+        if (mode == 0) DGC_WIRE(true, 0); else if (mode == 1) DGC_WIRE(true, 1); else DGC_WIRE(true, 2);
+    } else {
+        if (mode == 0) DGC_WIRE(false, 0); else if (mode == 1) DGC_WIRE(false, 1); else DGC_WIRE(false, 2);
+    }
+#undef DGC_WIRE
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
 int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n, float momentum,
                bool nesterov, bool accumulate, float* samples, int64_t s_start, int64_t s_stride,
                int64_t s_count, hipStream_t st) {
@@ -242,6 +426,24 @@ extern "C" int dgc_compensate(const float* grad, float* mmt, float* vec, float* 
     return dgc::compensate(grad, mmt, vec, out, n, momentum, nesterov != 0, accumulate != 0, samples,
                            sample_start, sample_stride, num_samples,
                            static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_gather_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets,
+                               int32_t count, void* dst, int32_t dst_dtype, void* stream) {
+    return dgc::gather_cast(srcs, numels, offsets, count, dst, dst_dtype, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_compensate_multi(const float* const* srcs, const int64_t* numels, const int64_t* offsets,
+                                    int32_t count, int32_t round_to, float* mmt, float* out, float momentum,
+                                    int32_t nesterov, void* stream) {
+    return dgc::compensate_multi(srcs, numels, offsets, count, round_to, mmt, out, momentum, nesterov != 0,
+                                 static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float* mmt, float* out,
+                                   int64_t n, float momentum, int32_t nesterov, void* stream) {
+    return dgc::compensate_wire(src, src_dtype, round_to, mmt, out, n, momentum, nesterov != 0,
+                                static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dgc_sample_strided(const float* vec, int64_t n, int64_t start, int64_t stride,

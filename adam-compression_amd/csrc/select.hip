@@ -151,6 +151,7 @@ struct SelWS {
     float* thr;                // [T] sampled thresholds
     float* spec;               // [2T] speculative list thresholds (null: none), persistent
     int64_t* starts;           // [T] sample starts of this call
+    const float** gptr;        // [T] per-tensor gradient pointers of this call (K1 from a pointer table)
     int64_t* scnt;             // [T] strided sample counts of this call
     float* samples;            // flat sample buffer
     int32_t* bt[BT_COUNT];     // block tables
@@ -299,6 +300,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.thr = c.take<float>(L.T);
     w.spec = c.take<float>(2 * L.T);
     w.starts = c.take<int64_t>(L.T);
+    w.gptr = c.take<const float*>(L.T);
     w.scnt = c.take<int64_t>(L.T);
     for (int which = 0; which < BT_COUNT; ++which) w.bt[which] = c.take<int32_t>(L.T + 1);
     w.small = c.take<int32_t>(L.T);
@@ -341,10 +343,14 @@ __global__ void k_put_one(SelWS w, OneTable o) {
 }
 
 // Per-call sample starts of a batch (random.randint per tensor, drawn on the host),
-// 64 per launch in the kernel arguments; also the sample counts.
+// 64 per launch in the kernel arguments; also the sample counts. ptrs: K1 reads tensor
+// t's gradient from grad[t] (a pointer table: the parameters' own p.grad tensors, no
+// copy into the flat buffer) instead of the flat buffer at its offset.
 struct StartChunk {
     int32_t first, count;
+    int32_t ptrs, pad;
     int64_t start[64];
+    const float* grad[64];
 };
 
 __global__ void k_put_starts(SelWS w, StartChunk c) {
@@ -354,6 +360,14 @@ __global__ void k_put_starts(SelWS w, StartChunk c) {
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     w.starts[t] = c.start[i];
     w.scnt[t] = d.samp_off < 0 ? d.n : ceil_div(d.n - c.start[i], d.stride);
+    if (c.ptrs) w.gptr[t] = c.grad[i];
+}
+
+// The float4 at element e0 of a gradient of n elements that may end inside it (a
+// pointer-table gradient is exactly n floats long): elements past n read as 0.
+__device__ __forceinline__ float4 ld_tail4(const float* __restrict__ g, int64_t e0, int64_t n) {
+    if (e0 + 3 < n) return ld_nt(reinterpret_cast<const float4*>(g + e0));
+    return make_float4(g[e0], e0 + 1 < n ? g[e0 + 1] : 0.f, e0 + 2 < n ? g[e0 + 2] : 0.f, 0.f);
 }
 
 // ------------------------------------------------------------------ tile helpers
@@ -558,7 +572,10 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_K1][t]) * kSegPerBlock4 + wave;   // local segment
-    const float4* g = reinterpret_cast<const float4*>(g_flat + d.off);
+    // sample starts (and gradient pointers) of the first sc.count tensors ride in the arguments
+    const bool arg_start = t < sc.count;
+    const float* gsrc = !sc.ptrs ? g_flat + d.off : (arg_start ? sc.grad[t] : w.gptr[t]);
+    const float4* g = reinterpret_cast<const float4*>(gsrc);
     float4* mmt = reinterpret_cast<float4*>(mmt_flat + d.off);
     float4* vec = reinterpret_cast<float4*>(vec_flat + d.off);
     const int64_t n4 = d.nv4, n = d.n;
@@ -566,8 +583,6 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     SelState* st = w.st + t;
     if (blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) st->t_list = tl;
     const bool sample = d.samp_off >= 0;
-    // sample starts of the first sc.count tensors ride in the arguments (no k_put_starts)
-    const bool arg_start = t < sc.count;
     const int64_t start = !sample ? 0 : (arg_start ? sc.start[t] : w.starts[t]);
     const int64_t scount = !sample ? 0 : (arg_start ? ceil_div(d.n - start, d.stride) : w.scnt[t]);
     if (arg_start && blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) {
@@ -589,7 +604,7 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     for (int u = 0; u < kSegTiles; ++u) {
         const int64_t v = ls * (kSeg / 4) + u * 64 + lane;
         if (v < n4) {
-            gv[u] = ld_nt(g + v);
+            gv[u] = sc.ptrs && 4 * v + 3 >= n ? ld_tail4(gsrc, 4 * v, n) : ld_nt(g + v);
             mv[u] = ld_nt(mmt + v);
             vv[u] = ld_nt(vec + v);
         }
@@ -1806,6 +1821,11 @@ struct FinishArgs {
     float margin;
     int32_t defer, mask_mmt;
     int32_t on;   // k_nth_select: its last workgroup runs the finish (no k_sel_finish launch)
+    // Host-mapped (pinned) word of the engine, may be null: a call whose resample replay
+    // broke (DGC_K5_BROKEN) stores its status there — a plain system-scope store, only
+    // then — so an engine that never synchronises sees it on its next step, for free.
+    int32_t* sink;
+    uint32_t force;   // DGC_K5_FORCE_BROKEN (tests): status bits added to every resampled tensor
 };
 
 __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
@@ -1814,11 +1834,17 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
     const float margin = f.margin;
     const int defer = f.defer, mask_mmt = f.mask_mmt;
     __shared__ unsigned long long total;
-    if (threadIdx.x == 0) total = 0;
+    __shared__ uint32_t broken;
+    if (threadIdx.x == 0) {
+        total = 0;
+        broken = 0;
+    }
     __syncthreads();
     for (int t = threadIdx.x; t < w.T; t += blockDim.x) {
         SelState* st = w.st + t;
         st->epoch += 1;
+        const uint32_t k5 = w.nthg[t].status | (st->branch == DGC_BRANCH_RESAMPLE ? f.force : 0u);
+        if (k5 & DGC_K5_BROKEN) atomicOr(&broken, k5);
         const long long cnt = final_count(*st, w.td[t].k);
         // what the next K1 must zero (first-k branches of a deferring engine only)
         st->def_mode = (defer && st->branch != DGC_BRANCH_RESAMPLE && !w.td[t].tail && cnt > 0) ? 1 : 0;
@@ -1838,7 +1864,7 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             r.full_passes = st->full_passes;
             r.tie_rule = st->tie_rule;
             r.window_keys = st->win_keys;
-            r.k5_status = (int32_t)w.nthg[t].status;
+            r.k5_status = (int32_t)k5;
             r.reserved = 0;
         }
         if (w.spec) {
@@ -1865,6 +1891,8 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
     }
     __syncthreads();
     if (threadIdx.x == 0 && count_out) *count_out = (int64_t)total;
+    if (threadIdx.x == 0 && broken && f.sink)
+        __hip_atomic_store(f.sink, (int32_t)broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_sel_finish(SelWS w, FinishArgs f) { sel_finish_body(w, f); }
@@ -2261,6 +2289,24 @@ __global__ void k_spec_reset(float* spec, int32_t T) {
 }
 
 // ------------------------------------------------------------------ host driver
+// The resample replays pack what they move into 64-bit entries: K5's queue holds
+// (key << 32 | candidate position), K5b's heap (key31 << 33 | element index). A tensor
+// whose candidates or elements do not fit those widths is refused up front — torch's
+// topk takes any n (dgc/compression.py:124-137), and a truncated position would be a
+// wrong payload, not an error.
+static int check_replay_width(int64_t n, int64_t k, const char* who) {
+    if (nth_cand_cap(n, k) > (int64_t)0xFFFFFFFFLL)
+        DGC_FAIL(DGC_ERR_OVERFLOW,
+                 "%s: the resample replay addresses at most 2^32 - 1 candidates; numel %lld with num_selects %lld "
+                 "can have %lld (use resample=False or a smaller tensor)",
+                 who, (long long)n, (long long)k, (long long)nth_cand_cap(n, k));
+    if (n >= ((int64_t)1 << kHeapKeyShift))
+        DGC_FAIL(DGC_ERR_OVERFLOW,
+                 "%s: the partial_sort resample replay addresses elements below 2^33; numel %lld "
+                 "(use resample=False or a smaller tensor)", who, (long long)n);
+    return DGC_OK;
+}
+
 static int validate_select(const dgc_select_params* p, void* values, void* indices) {
     if (!p) DGC_FAIL(DGC_ERR_INVALID, "dgc_select: null params");
     if (p->numel < 1 || p->num_selects < 1 || p->num_selects > p->numel)
@@ -2277,6 +2323,7 @@ static int validate_select(const dgc_select_params* p, void* values, void* indic
     if (p->idtype == DGC_I32 && p->numel > 2147483647LL)
         DGC_FAIL(DGC_ERR_OVERFLOW, "dgc_select: int32 indices cannot address %lld elements",
                  (long long)p->numel);
+    if (p->resample) DGC_TRY(check_replay_width(p->numel, p->num_selects, "dgc_select"));
     if (!values || !indices) DGC_FAIL(DGC_ERR_INVALID, "dgc_select: null outputs");
     return DGC_OK;
 }
@@ -2342,7 +2389,7 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
 
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
                        int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists, int sync_mode,
-                       float margin, hipStream_t s) {
+                       float margin, int32_t* sink, hipStream_t s) {
     // keep_lists: a compress call, whose K3 kernels already reset every tensor's state
     // (sel_init_tensor) when they produced its threshold; a pure selection resets here
     if (!keep_lists) {
@@ -2392,7 +2439,11 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0};
+    // DGC_K5_FORCE_BROKEN=1 (parity tests only): report every resampled tensor as broken,
+    // to exercise the engines' raise without a barrier actually timing out
+    const uint32_t force = std::getenv("DGC_K5_FORCE_BROKEN") ? (uint32_t)DGC_K5_BROKEN : 0u;
+    const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
+                         sink, force};
     bool finished = false;   // the payload count and records are written
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
@@ -2526,7 +2577,8 @@ int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p
     w.thr = const_cast<float*>(thr0);
     hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
     DGC_LAUNCHED();
-    return select_core(vec, mmt, cfg_of(*p), L, values, indices, count_out, info, w, 0, sync_mode, 1.f, s);
+    return select_core(vec, mmt, cfg_of(*p), L, values, indices, count_out, info, w, 0, sync_mode, 1.f,
+                       p->status_sink, s);
 }
 
 // ------------------------------------------------------------------ threshold
@@ -2575,6 +2627,7 @@ static int compress_check(const dgc_select_params* p, void* values, void* indice
                           int64_t s_stride, int64_t top_k_samples, bool need_outputs) {
     if (need_outputs) DGC_TRY(validate_select(p, values, indices));
     else if (!p) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: null params");
+    else if (p->resample) DGC_TRY(check_replay_width(p->numel, p->num_selects, "dgc_compress"));
     const bool sampled = p->numel != p->num_samples;
     if (sampled && (s_stride < 2 || s_start < 0 || s_start >= s_stride))
         DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: sample_start must be in [0, stride)");
@@ -2666,7 +2719,8 @@ int compress_finish(float* vec, float* mmt, int64_t s_start, int64_t s_stride, i
     dgc_select_params q = *p;
     // DGCSGDMemory.update fused into the emit (1), or deferred into the next K1 (2)
     q.update_memory = p->update_memory == 2 ? 2 : 1;
-    return select_core(vec, mmt, cfg_of(q), L, values, indices, count_out, info, w, 1, sync_mode, margin, s);
+    return select_core(vec, mmt, cfg_of(q), L, values, indices, count_out, info, w, 1, sync_mode, margin,
+                       p->status_sink, s);
 }
 
 // ------------------------------------------------------------------ batch
@@ -2690,6 +2744,11 @@ static int batch_layout(const dgc_batch_desc* b, Layout& L, std::vector<TDesc>& 
         x.samples = true;
         if (x.n < 1 || x.k < 1 || x.k > x.n || x.S < 1 || x.S > x.n || x.ks < 1 || x.ks > x.S)
             DGC_FAIL(DGC_ERR_INVALID, "dgc_batch: tensor %d: bad numel/num_selects/num_samples/top_k_samples", t);
+        if (b->resample) {
+            char who[48];
+            std::snprintf(who, sizeof(who), "dgc_batch: tensor %d", t);
+            DGC_TRY(check_replay_width(x.n, x.k, who));
+        }
         if (x.n != x.S && (x.stride < 4 || x.stride >= (1LL << 30)))
             DGC_FAIL(DGC_ERR_INVALID, "dgc_batch: tensor %d: sample stride %lld outside [4, 2^30)", t,
                      (long long)x.stride);
@@ -2761,30 +2820,44 @@ static int batch_ws(const dgc_batch_desc* b, void* ws, size_t ws_bytes, const ch
     return DGC_OK;
 }
 
-// K1 over every tensor (+ fused strided samples + speculative candidate lists).
-int batch_compress_begin(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
-                         void* ws, size_t ws_bytes, hipStream_t s) {
+// K1 over every tensor (+ fused strided samples + speculative candidate lists), the
+// gradients from the flat buffer (grads == null) or from a host table of T device
+// pointers (grads[t]: numel[t] contiguous floats, 16-B aligned).
+int batch_compress_begin(const dgc_batch_desc* b, const float* grad, const float* const* grads, float* mmt,
+                         float* vec, const int64_t* starts, void* ws, size_t ws_bytes, hipStream_t s) {
     Layout L;
     std::vector<TDesc> td;
     SelWS w;
     DGC_TRY(batch_ws(b, ws, ws_bytes, "dgc_batch_compress", L, td, w));
-    if (!grad || !mmt || !vec || !starts) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
-    if (!aligned16(grad) || !aligned16(mmt) || !aligned16(vec))
+    if ((!grad && !grads) || !mmt || !vec || !starts) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
+    if ((grad && !aligned16(grad)) || !aligned16(mmt) || !aligned16(vec))
         DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: flat buffers must be 16-B aligned");
+    if (grads)
+        for (int32_t t = 0; t < L.T; ++t)
+            if (!grads[t] || !aligned16(grads[t]))
+                DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: gradient %d is null or not 16-B aligned", t);
     for (int32_t t = 0; t < L.T; ++t)
         if (td[t].samp_off >= 0 && (starts[t] < 0 || starts[t] >= td[t].stride))
             DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: tensor %d: sample start outside [0, stride)", t);
     // up to 64 starts go to K1 in its arguments; a larger batch puts them first
     StartChunk arg{};
+    arg.ptrs = grads ? 1 : 0;
     if (L.T <= 64) {
         arg.count = L.T;
-        for (int i = 0; i < L.T; ++i) arg.start[i] = td[i].samp_off >= 0 ? starts[i] : 0;
+        for (int i = 0; i < L.T; ++i) {
+            arg.start[i] = td[i].samp_off >= 0 ? starts[i] : 0;
+            arg.grad[i] = grads ? grads[i] : nullptr;
+        }
     } else {
         for (int32_t t0 = 0; t0 < L.T; t0 += 64) {
             StartChunk c{};
             c.first = t0;
             c.count = std::min<int32_t>(64, L.T - t0);
-            for (int i = 0; i < c.count; ++i) c.start[i] = td[t0 + i].samp_off >= 0 ? starts[t0 + i] : 0;
+            c.ptrs = arg.ptrs;
+            for (int i = 0; i < c.count; ++i) {
+                c.start[i] = td[t0 + i].samp_off >= 0 ? starts[t0 + i] : 0;
+                c.grad[i] = grads ? grads[t0 + i] : nullptr;
+            }
             hipLaunchKernelGGL(k_put_starts, dim3(1), dim3(64), 0, s, w, c);
             DGC_LAUNCHED();
         }
@@ -2816,13 +2889,13 @@ int batch_compress_finish(const dgc_batch_desc* b, float* mmt, float* vec, void*
     payload_layout(cap, cfg.vdtype, cfg.idtype, &voff, &ioff);
     char* pl = static_cast<char*>(payload);
     return select_core(vec, mmt, cfg, L, pl + voff, pl + ioff, reinterpret_cast<int64_t*>(pl), info, w, 1,
-                       sync_mode, b->spec_margin, s);
+                       sync_mode, b->spec_margin, b->status_sink, s);
 }
 
 int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
                    void* payload, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
     if (!payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
-    DGC_TRY(batch_compress_begin(b, grad, mmt, vec, starts, ws, ws_bytes, s));
+    DGC_TRY(batch_compress_begin(b, grad, nullptr, mmt, vec, starts, ws, ws_bytes, s));
     return batch_compress_finish(b, mmt, vec, payload, info, ws, ws_bytes, sync_mode, s);
 }
 
@@ -2921,7 +2994,15 @@ extern "C" int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad
 
 extern "C" int dgc_batch_compress_begin(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
                                         const int64_t* sample_starts, void* ws, size_t ws_bytes, void* stream) {
-    return dgc::batch_compress_begin(batch, grad, mmt, vec, sample_starts, ws, ws_bytes,
+    return dgc::batch_compress_begin(batch, grad, nullptr, mmt, vec, sample_starts, ws, ws_bytes,
+                                     static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_batch_compress_begin_ptrs(const dgc_batch_desc* batch, const float* const* grads, float* mmt,
+                                             float* vec, const int64_t* sample_starts, void* ws, size_t ws_bytes,
+                                             void* stream) {
+    if (!grads) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress_begin_ptrs: null gradient table");
+    return dgc::batch_compress_begin(batch, nullptr, grads, mmt, vec, sample_starts, ws, ws_bytes,
                                      static_cast<hipStream_t>(stream));
 }
 

@@ -32,7 +32,8 @@ class SelectParams(ctypes.Structure):
                 ("lower_count", ctypes.c_int64), ("upper", ctypes.c_float), ("lower", ctypes.c_float),
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("masking", ctypes.c_int32),
                 ("vdtype", ctypes.c_int32), ("idtype", ctypes.c_int32), ("update_memory", ctypes.c_int32),
-                ("thr_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("thr_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("status_sink", ctypes.c_void_p)]
 
 
 class SelectInfo(ctypes.Structure):
@@ -63,6 +64,34 @@ def info_dict(i, what):
 INFO_BYTES = ctypes.sizeof(SelectInfo)
 
 
+class StatusSink:
+    """The engines' per-step check of the resample replay (DGC_K5_BROKEN) without a host
+    synchronisation: a pinned host int32 whose address goes to the library as
+    ``status_sink``; a finish whose replay broke stores its k5_status there (nothing is
+    written otherwise). ``check()`` reads the host word — free — and raises once it is set,
+    i.e. at the first step the host issues after the GPU finished the broken call (a host
+    that runs ahead of the GPU sees it that many steps later; ``check(sync=True)``
+    waits for the stream first)."""
+
+    def __init__(self, what, device):
+        self.what = what
+        self.device = device
+        self.word = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+
+    @property
+    def address(self):
+        return self.word.data_ptr()
+
+    def check(self, sync=False):
+        if sync:
+            torch.cuda.current_stream(self.device).synchronize()
+        v = int(self.word[0])
+        if v & K5_BROKEN:
+            raise RuntimeError(f"{self.what}: the resample replay's multi-workgroup phase timed out at a barrier after "
+                               f"it started (k5_status {v}; workgroups not co-resident?); the selection of that step "
+                               "is not reliable")
+
+
 class BatchDesc(ctypes.Structure):
     """dgc_batch_desc (include/dgc_hip.h): a batch's tensors and shared settings."""
     _fields_ = [("count", ctypes.c_int32), ("numel", ctypes.POINTER(ctypes.c_int64)),
@@ -73,7 +102,8 @@ class BatchDesc(ctypes.Structure):
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("momentum_masking", ctypes.c_int32),
                 ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
                 ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float),
-                ("deferred_masking", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("deferred_masking", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("status_sink", ctypes.c_void_p)]
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -120,6 +150,13 @@ _SIGNATURES = {
                                           _SZ, _I32, _P]),
     "dgc_batch_compress_begin": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, ctypes.POINTER(_I64), _P,
                                                 _SZ, _P]),
+    "dgc_batch_compress_begin_ptrs": (ctypes.c_int, [ctypes.POINTER(BatchDesc), ctypes.POINTER(_P), _P, _P,
+                                                     ctypes.POINTER(_I64), _P, _SZ, _P]),
+    "dgc_gather_cast": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32, _P, _I32,
+                                       _P]),
+    "dgc_compensate_wire": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _F, _I32, _P]),
+    "dgc_compensate_multi": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32,
+                                            _I32, _P, _P, _F, _I32, _P]),
     "dgc_batch_compress_finish": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _P, _P, _SZ, _I32, _P]),
     "dgc_batch_flush": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _SZ, _P]),
     "dgc_hbm_probe": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),

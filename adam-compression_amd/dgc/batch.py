@@ -85,6 +85,7 @@ class DGCBatch:
         self.out_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
         self._L = _lib.lib()
         self.info = torch.zeros(len(self.names) * _lib.INFO_BYTES, dtype=torch.uint8, device=dev)
+        self.status = _lib.StatusSink("DGCBatch", dev)   # DGC_K5_BROKEN, checked every step
         self.set_ratio(compress_ratio)
 
     # ---------------------------------------------------------------- layout
@@ -109,6 +110,7 @@ class DGCBatch:
         d.fp16_values, d.int32_indices = int(self.vdtype == torch.float16), int(self.idtype == torch.int32)
         d.nesterov, d.momentum, d.spec_margin = int(self.nesterov), self.momentum, _lib.SPEC_MARGIN
         d.deferred_masking = int(self.deferred_masking)
+        d.status_sink = self.status.address
         self.desc = d
         L = self._L
         wsz = L.dgc_batch_workspace(ctypes.byref(d))
@@ -186,17 +188,27 @@ class DGCBatch:
             starts.append(self.rng.randint(0, stride - 1) if n != S else 0)
         return starts
 
-    def compensate(self, starts=None):
+    def compensate(self, starts=None, grad_ptrs=None):
         """K1 over every tensor: compensate + strided samples + candidate lists (and any
-        masking the previous select left pending)."""
+        masking the previous select left pending). The gradients come from ``grad_flat``,
+        or — ``grad_ptrs``, a ctypes array of T device pointers, each to the tensor's
+        numel contiguous fp32 elements, 16-B aligned — from wherever they are (the
+        batched optimizer's p.grad tensors, read in place). Raises first if a previous
+        step's resample replay reported DGC_K5_BROKEN (``status``)."""
+        self.status.check()
         starts = self.draw_starts() if starts is None else starts
         self.starts = starts
         self._par += 1   # a step starts: the other payload / gather buffer
         arr = (ctypes.c_int64 * len(starts))(*starts)
-        _lib.check(self._L.dgc_batch_compress_begin(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
-                                                    self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
-                                                    self.ws.data_ptr(), self.ws.numel(),
-                                                    _lib.stream_of(self.device)), "dgc_batch_compress_begin")
+        L, st = self._L, _lib.stream_of(self.device)
+        if grad_ptrs is None:
+            _lib.check(L.dgc_batch_compress_begin(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
+                                                  self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
+                                                  self.ws.data_ptr(), self.ws.numel(), st), "dgc_batch_compress_begin")
+        else:
+            _lib.check(L.dgc_batch_compress_begin_ptrs(ctypes.byref(self.desc), grad_ptrs, self._mmt_flat.data_ptr(),
+                                                       self._vec_flat.data_ptr(), arr, self.ws.data_ptr(),
+                                                       self.ws.numel(), st), "dgc_batch_compress_begin_ptrs")
         self._pending = False
 
     def select(self):
@@ -260,6 +272,7 @@ class DGCBatch:
 
     # ---------------------------------------------------------------- results
     def infos(self):
+        self.status.check(sync=True)
         raw = self.info.cpu().numpy().tobytes()
         out = []
         for t in range(len(self.names)):

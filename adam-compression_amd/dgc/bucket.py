@@ -87,6 +87,8 @@ class DGCBucket:
         # next step's K1, which streams vec/mmt anyway (mmt/vec below flush it on read)
         p.vdtype, p.idtype = _lib.VD[self.vdtype], _lib.ID[self.idtype]
         p.update_memory = 2 if deferred_masking else 1
+        self.status = _lib.StatusSink("DGCBucket", self.device)   # DGC_K5_BROKEN, checked every step
+        p.status_sink = self.status.address
         self.params = p
 
         dev = self.device
@@ -154,7 +156,9 @@ class DGCBucket:
 
     # ---------------------------------------------------------------- phases
     def compensate(self, grad):
-        """K1: compensate + fused strided sample + speculative candidate lists."""
+        """K1: compensate + fused strided sample + speculative candidate lists. Raises
+        first if a previous step's resample replay reported DGC_K5_BROKEN (``status``)."""
+        self.status.check()
         L = self._L
         self._par += 1   # a step starts: the other payload / gather buffer
         self.start = self.rng.randint(0, self.stride - 1) if self.sampled else 0
@@ -272,5 +276,6 @@ class DGCBucket:
                     self._fill_on_side(out)
 
     def last_info(self):
+        self.status.check(sync=True)
         raw = self.info.cpu().numpy().tobytes()
         return _lib.info_dict(_lib.SelectInfo.from_buffer_copy(raw), "DGCBucket")

@@ -51,7 +51,9 @@ class _PackedHandle:
         self.stride = stride
         self.voff = voff
         self.ioff = ioff
-        self.distinct = False   # the payload came from compress (distinct indices per rank)
+
+
+_OURS = 0x444743454D495454   # payload header word 1 of a compress-emitted payload ("DGCEMITT")
 
 
 def _layout(capacity, vdtype, idtype):
@@ -102,6 +104,7 @@ class DGCCompressor:
         self._payloads = {}
         self._bad16 = {}       # device -> int32 flag: out-of-range indices (dgc_decompress16)
         self._spec = {}        # name -> device float: speculative list threshold (dgc_compress)
+        self.layout_epoch = 0  # bumped by initialize(): the batched step re-derives its layout
 
     # ------------------------------------------------------------------ host math
     @staticmethod
@@ -124,6 +127,7 @@ class DGCCompressor:
         (dgc/compression.py:56-89)."""
         if comm.rank() == 0:
             print("=> initializing dgc compressor")
+        self.layout_epoch += 1
         for name, param in named_parameters:
             if torch.is_tensor(param):
                 numel, shape = param.numel(), list(param.size())
@@ -275,6 +279,7 @@ class DGCCompressor:
                 # on it (pure), then DGCSGDMemory.update masks the 16-bit state
                 grad = mem._clip(tensor).reshape(-1).contiguous()
                 mem._sync()
+                mem.state_of(name, grad, True, "DGCCompressor.compress")
                 img = self._ws.get(dev, 4 * numel, "img16")[: 4 * numel].view(torch.float32)
                 mem._compensate16(grad, name, True, vec32=img)
                 _, idx, _, _, _ = self._select_on(img, name, dt, payload, lay, False)
@@ -284,8 +289,8 @@ class DGCCompressor:
                 # fused path: K1 (+sample) -> K3 -> K4 (+update) in one library call
                 grad = mem._clip(tensor).reshape(-1)
                 _lib.require_cuda_f32(grad, "DGCCompressor.compress")
-                mmt, vec = mem.momentums[name], mem.velocities[name]
-                _lib.require_cuda_f32(vec, "DGCCompressor.compress")
+                mem._sync()
+                mmt, vec = mem.state_of(name, grad, True, "DGCCompressor.compress")
                 start = self._sample_start(name)
                 params = self._select_params(name, mem.momentum_masking, True)
                 L = _lib.lib()
@@ -310,6 +315,9 @@ class DGCCompressor:
                 _, idx, _, _, _ = self._sparsify(compensated, name, payload, lay, update_memory=False)
                 mem.update(name, (idx.to(torch.int64) if idx.dtype != torch.int64 else idx,))
                 values, indices = self._views(payload, lay, idx.numel())
+            # header word 1: "emitted by compress" (distinct indices), read by every rank's
+            # synchronize with the counts, so a peer's foreign payload is never taken for one
+            payload[8:16].view(torch.int64).fill_(_OURS)
             self._payloads[name] = (payload, lay)
             ctx = (name, numel, shape, dt, torch.int64, tensor.data.view(numel))
             return (values, indices), ctx
@@ -401,7 +409,9 @@ class DGCCompressor:
         if offs is None or not getattr(tensor, "distinct_runs", False):
             # input whose runs may repeat an index (the reference's list format, or
             # foreign payloads): one stably sorted run, each index folded in input order
-            # (index_put_'s serial order; as the fp32 path's unsorted fallback)
+            # (index_put_'s serial order; as the fp32 path's unsorted fallback). Negative
+            # indices wrap as in index_put_: normalised first, so -1 and n - 1 fold together
+            indices = torch.where(indices < 0, indices + numel, indices)
             order = torch.sort(indices, stable=True).indices
             values, indices = values[order].contiguous(), indices[order].contiguous()
             offs, nruns = [0, values.numel()], -1
@@ -432,16 +442,14 @@ class DGCCompressor:
                 payload, lay = self._pack_foreign(name, values, indices)
             k, vdt, idt, stride, voff, ioff = lay
             handle = comm.allgather_packed_async(payload)
-            h = _PackedHandle(handle, name, k, vdt, idt, stride, voff, ioff)
-            h.distinct = ours   # every rank runs this same code: all payloads are compress's
-            return h
+            return _PackedHandle(handle, name, k, vdt, idt, stride, voff, ioff)
         return comm.allreduce_async_(tensor_compressed, name=name, op=op)
 
     def _pack_foreign(self, name, values, indices):
         """Pack (values, indices) that did not come from this compressor's compress."""
         payload, lay = self._new_payload(name, values.device)
         n = values.numel()
-        payload[:8].view(torch.int64).fill_(n)
+        payload[:16].view(torch.int64).copy_(torch.tensor([n, 0], dtype=torch.int64))
         v, i = self._views(payload, lay, n)
         v.copy_(values.reshape(-1, 1))
         i.copy_(indices.reshape(-1, 1))
@@ -453,7 +461,8 @@ class DGCCompressor:
             gathered = handle.handle.wait()
             W = gathered.numel() // handle.stride
             rows = gathered.view(W, handle.stride)
-            counts = rows[:, :8].contiguous().view(torch.int64).view(-1).tolist()
+            head = rows[:, :16].contiguous().view(torch.int64).view(W, 2).tolist()
+            counts = [c for c, _ in head]
             vb = torch.empty(0, dtype=handle.vdtype).element_size()
             ib = torch.empty(0, dtype=handle.idtype).element_size()
             vals = [rows[r, handle.voff: handle.voff + c * vb].view(handle.vdtype) for r, c in enumerate(counts)]
@@ -468,7 +477,9 @@ class DGCCompressor:
             for c in counts:
                 offs.append(offs[-1] + c)
             out.run_offsets = offs
-            out.distinct_runs = handle.distinct
+            # every rank's run came from compress (distinct indices): the per-run scatter;
+            # a foreign payload anywhere sends the 16-bit decompress to its sorted fold
+            out.distinct_runs = all(mark == _OURS for _, mark in head)
             return out
         if isinstance(handle, (tuple, list)):
             return [comm.synchronize(h) for h in handle]

@@ -6,33 +6,43 @@ Horovod allgathers and a decompress; per dense tensor an allreduce and a
 ``compensate(accumulate=False)`` (dgc/compression.py:155-212). ``BatchedStep`` keeps
 those numerics and runs the whole step as
 
-    compressed tensors   dgc.batch.DGCBatch: ONE K1 launch over all of them, the
-                         selections together, ONE packed payload -> ONE allgather
-                         (RCCL over xGMI) -> ONE decompress, written back into the
-                         gradients (the reference's decompress writes into p.grad)
-    dense tensors        ONE flat allreduce (Average; fp16 on the wire when the
-                         compressor casts) -> ONE compensate(accumulate=False)
+    compressed tensors   dgc.batch.DGCBatch: ONE K1 launch over all of them, reading
+                         every gradient where autograd left it (a table of p.grad
+                         pointers in the kernel arguments, no copy), the selections
+                         together, ONE packed payload -> ONE allgather (RCCL over xGMI)
+                         -> ONE decompress into the batch's output buffer, whose views
+                         become the new p.grad (the reference's decompress writes into
+                         p.grad, dgc/compression.py:191-194)
+    dense tensors        W = 1: ONE multi-tensor compensate(accumulate=False) straight
+                         from the gradients (the fp16 wire's rounding fused); W > 1: ONE
+                         gather (+ fp16 cast) into the allreduce buffer -> ONE allreduce
+                         (Average) -> ONE compensate from the buffer (fp16 widened in it)
 
-with no host synchronisation. It does so by laying the parameters' state out flat:
+with no host synchronisation and no per-parameter launch. The momentums and
+velocities become views of the batch's flat buffers (``memory.momentums[name]`` /
+``velocities[name]``); anything that rebinds them (``memory.load_state_dict``,
+``compressor.initialize``) is detected at the next step and copied back in.
 
-* every compressed parameter's ``p.grad``, ``memory.momentums[name]`` and
-  ``memory.velocities[name]`` become views of the batch's three flat buffers;
-* every dense parameter's ``p.grad`` and momentum become views of two dense flat
-  buffers; the dense result goes to a second gradient buffer (the reference's
-  ``p.grad.set_(compensate(...))`` of a new tensor), and the two alternate by step.
+Gradients: whatever ``p.grad`` is at ``step()`` — a fresh tensor from backward after
+the default ``zero_grad(set_to_none=True)``, or the previous step's output view zeroed
+in place and accumulated into (``set_to_none=False``) — is read in place when it is a
+contiguous, 16-B aligned fp32 tensor on the device (else copied into the batch's flat
+gradient buffer first; a missing one counts as zeros).
 
-Anything that rebinds those tensors (``zero_grad(set_to_none=True)`` followed by a
-backward, ``memory.load_state_dict``, ``compressor.initialize``) is detected at the
-next step and copied back into the flat layout, so the results never depend on it;
-keeping the views (``zero_grad(set_to_none=False)``; torch's and so the wrapper's
-default is ``set_to_none=True``) just avoids that copy.
+The zero_() before the scatter (dgc/compression.py:191): ``fill="inline"`` (the
+default) zeroes the whole output, as the reference does. ``fill="sparse"`` re-zeroes
+only the previous step's gathered indices of the output when nothing wrote it since
+(same storage, torch version counter unchanged — an in-place op on a p.grad view bumps
+it); writes through ``p.grad.data`` or raw pointers do not, so only a training loop
+that never writes the gradients that way (torch's optimizers, clip_grad_norm_ and
+zero_grad do not) should opt in.
 
 Sample starts: one ``random.randint(0, stride - 1)`` per sampled compressed tensor,
 drawn from Python's global ``random`` in the order the hooks fired — the order in
 which the reference's hooks call ``compress`` (dgc/compression.py:118) — so the
 selections, and the weights, are the reference's bit for bit.
 """
-import math
+import ctypes
 import random
 
 import torch
@@ -55,10 +65,18 @@ def supported(compression):
             and compression.strided_sample and mem.gradient_clipping is None)
 
 
+def _readable(g, dev):
+    """A gradient K1 / the dense kernels may read in place."""
+    return (g.dtype == torch.float32 and g.device == dev and g.is_contiguous() and g.data_ptr() % 16 == 0)
+
+
 class BatchedStep:
-    def __init__(self, compression, named_parameters):
+    def __init__(self, compression, named_parameters, fill="inline"):
+        if fill not in ("inline", "sparse"):
+            raise ValueError(f"batched DGC: fill must be 'inline' or 'sparse', not {fill!r}")
         self.comp = compression
         self.mem = compression.memory
+        self.fill = fill
         self.named = [(n, p) for n, p in named_parameters if p.requires_grad]
         bad = sorted({str(p.dtype) for _, p in self.named if p.dtype != torch.float32})
         if bad:   # the engines (dgc_batch_*) are fp32; 16-bit parameters take the per-tensor path
@@ -70,28 +88,27 @@ class BatchedStep:
     # ------------------------------------------------------------------ layout
     def _plan_key(self):
         c = self.comp
-        names = tuple(n for n, _ in self.named if c.compress_ratio < 1.0 and n in c.attributes)
-        return (c.compress_ratio, names)
+        return (c.compress_ratio, c.layout_epoch, len(c.attributes))
 
     def _build(self, key):
-        """(Re)lays out the flat buffers, moving the current momentum / velocity / grad
-        contents in (a no-op copy when they already live there)."""
+        """(Re)lays out the flat buffers, moving the current momentum / velocity contents
+        in (a no-op copy when they already live there)."""
         c, mem = self.comp, self.mem
-        ratio, comp_names = key
         old_batch = self._plan["batch"] if self._plan else None
         if old_batch is not None:
             old_batch.flush()
+        comp_names = [n for n, _ in self.named if c.compress_ratio < 1.0 and n in c.attributes]
         params = dict(self.named)
         dev = self.named[0][1].device
-        plan = {"key": key, "batch": None, "comp": [], "dense": [], "parity": 0}
+        plan = {"key": key, "batch": None, "comp": [], "dense": [], "dev": dev, "state": [], "dense_state": []}
         if comp_names:
             shapes = [(n, tuple(params[n].shape)) for n in comp_names]
-            b = DGCBatch(shapes, compress_ratio=ratio, momentum=mem.momentum, nesterov=mem.nesterov,
+            b = DGCBatch(shapes, compress_ratio=c.compress_ratio, momentum=mem.momentum, nesterov=mem.nesterov,
                          momentum_masking=mem.momentum_masking, sample_ratio=c.sample_ratio,
                          compress_upper_bound=c.compress_upper_bound, compress_lower_bound=c.compress_lower_bound,
                          max_adaptation_iters=c.max_adaptation_iters, resample=c.resample,
                          fp16_values=c.fp16_values, int32_indices=c.int32_indices, device=dev,
-                         world_size=comm.size(), deferred_masking=True)
+                         world_size=comm.size(), deferred_masking=True, fill=self.fill)
             for i, n in enumerate(comp_names):
                 numel, _, k, S, ks, stride = c.attributes[n]
                 if (k, S, ks, stride) != tuple(b.attrs[i]):
@@ -99,33 +116,38 @@ class BatchedStep:
             plan["batch"] = b
             for n in comp_names:
                 p = params[n]
-                mv, vv, gv = b._view(b._mmt_flat, n), b._view(b._vec_flat, n), b._view(b.grad_flat, n)
+                mv, vv = b._view(b._mmt_flat, n), b._view(b._vec_flat, n)
                 mv.copy_(mem.momentums[n])
                 vv.copy_(mem.velocities[n])
-                if p.grad is not None:
-                    gv.copy_(p.grad)
                 mem.momentums[n], mem.velocities[n] = mv, vv
-                p.grad = gv
-                plan["comp"].append((n, p))
+                plan["comp"].append((n, p, b.out(n), b.grad(n)))
+                plan["state"].append((n, mv, vv))
+            plan["index"] = {n: i for i, n in enumerate(b.names)}
+            plan["ptrs"] = (ctypes.c_void_p * len(comp_names))()
         dense = [(n, p) for n, p in self.named if n not in set(comp_names)]
         if dense:
             offs, end = [], 0
             for _, p in dense:
                 offs.append(end)
                 end += -(-p.numel() // 4) * 4   # 16-B aligned views
-            bufs = [torch.zeros(end, dtype=torch.float32, device=dev) for _ in range(3)]   # grad A, grad B, mmt
-            plan["dense_bufs"], plan["dense_numel"] = bufs, end
+            out = torch.zeros(end, dtype=torch.float32, device=dev)
+            mmt = torch.zeros(end, dtype=torch.float32, device=dev)
             for (n, p), o in zip(dense, offs):
-                mv = bufs[2][o: o + p.numel()].view(p.shape)
+                mv = mmt[o: o + p.numel()].view(p.shape)
                 mv.copy_(mem.momentums[n])
                 mem.momentums[n] = mv
-                gv = bufs[0][o: o + p.numel()].view(p.shape)
-                if p.grad is not None:
-                    gv.copy_(p.grad)
-                p.grad = gv
-                plan["dense"].append((n, p, o))
-            if c.fp16_values:
-                plan["dense_wire"] = torch.empty(end, dtype=torch.float16, device=dev)
+                plan["dense"].append((n, p, o, out[o: o + p.numel()].view(p.shape)))
+                plan["dense_state"].append((n, mv))
+            plan["dense_out"], plan["dense_mmt"], plan["dense_numel"] = out, mmt, end
+            T = len(dense)
+            plan["dense_ptrs"] = (ctypes.c_void_p * T)()
+            plan["dense_numels"] = (ctypes.c_int64 * T)(*[p.numel() for _, p in dense])
+            plan["dense_offs"] = (ctypes.c_int64 * T)(*offs)
+            if comm.size() > 1:
+                plan["dense_wire"] = torch.empty(end, dtype=torch.float16 if c.fp16_values else torch.float32,
+                                                 device=dev)
+            plan["zeros"] = torch.zeros(max((p.numel() for _, p in dense), default=1), dtype=torch.float32,
+                                        device=dev)
         self._plan = plan
 
     def flush(self):
@@ -133,38 +155,21 @@ class BatchedStep:
         if self._plan and self._plan["batch"] is not None:
             self._plan["batch"].flush()
 
-    def _rebind(self):
-        """Moves back into the flat layout whatever was rebound since the last step."""
+    def _rebind_state(self):
+        """Moves back into the flat layout whatever state was rebound since the last step
+        (``load_state_dict`` puts the checkpoint's tensors into the memory's dicts)."""
         plan, mem = self._plan, self.mem
-        b = plan["batch"]
-        if b is not None:
-            for n, p in plan["comp"]:
-                for store, flat in ((mem.momentums, b._mmt_flat), (mem.velocities, b._vec_flat)):
-                    view = b._view(flat, n)
-                    if store[n].data_ptr() != view.data_ptr():
-                        b.flush()
-                        view.copy_(store[n])
-                        store[n] = view
-                gv = b._view(b.grad_flat, n)
-                self._own_grad(p, gv)
-        if plan["dense"]:
-            cur = plan["dense_bufs"][plan["parity"]]
-            for n, p, o in plan["dense"]:
-                mv = plan["dense_bufs"][2][o: o + p.numel()].view(p.shape)
-                if mem.momentums[n].data_ptr() != mv.data_ptr():
-                    mv.copy_(mem.momentums[n])
-                    mem.momentums[n] = mv
-                self._own_grad(p, cur[o: o + p.numel()].view(p.shape))
-
-    @staticmethod
-    def _own_grad(p, view):
-        if p.grad is None:
-            view.zero_()
-        elif p.grad.data_ptr() != view.data_ptr():
-            view.copy_(p.grad)
-        else:
-            return
-        p.grad = view
+        moms, vels = mem.momentums, mem.velocities
+        for n, mv, vv in plan["state"]:
+            for store, view in ((moms, mv), (vels, vv)):
+                if store[n] is not view:
+                    plan["batch"].flush()
+                    view.copy_(store[n])
+                    store[n] = view
+        for n, mv in plan["dense_state"]:
+            if moms[n] is not mv:
+                mv.copy_(moms[n])
+                moms[n] = mv
 
     # ------------------------------------------------------------------ step
     def step(self, hook_order):
@@ -173,57 +178,99 @@ class BatchedStep:
         key = self._plan_key()
         if self._plan is None or self._plan["key"] != key:
             self._build(key)
-        self._rebind()
+        self._rebind_state()
         plan = self._plan
         b = plan["batch"]
+        dev = plan["dev"]
         handle = None
         if b is not None:
-            index = {n: i for i, n in enumerate(b.names)}
+            index = plan["index"]
             starts = [0] * len(b.names)
             seen = set()
-            for n in list(hook_order) + [n for n, _ in plan["comp"]]:
+            attrs = self.comp.attributes
+            for n in list(hook_order) + [e[0] for e in plan["comp"]]:
                 i = index.get(n)
                 if i is None or i in seen:
                     continue
                 seen.add(i)
-                numel, _, _, S, _, stride = self.comp.attributes[n]
+                numel, _, _, S, _, stride = attrs[n]
                 if numel != S:
                     starts[i] = random.randint(0, stride - 1)   # dgc/compression.py:118
-            b.compensate(starts)
+            ptrs = plan["ptrs"]
+            for i, (n, p, _, gflat) in enumerate(plan["comp"]):
+                g = p.grad
+                if g is None:
+                    gflat.zero_()   # no gradient this step: zeros
+                    g = gflat
+                elif not _readable(g, dev):
+                    gflat.copy_(g)
+                    g = gflat
+                ptrs[i] = g.data_ptr()
+            b.compensate(starts, grad_ptrs=ptrs)
             b.select()
             if b.world > 1:
                 handle = comm.allgather_packed_async(b.payload, out=b.gathered)
         dense_handle = None
         if plan["dense"]:
-            cur = plan["dense_bufs"][plan["parity"]]
+            dptrs = plan["dense_ptrs"]
+            zeros = plan["zeros"]
+            for i, (n, p, o, _) in enumerate(plan["dense"]):
+                g = p.grad
+                if g is None:
+                    g = zeros
+                elif g.dtype != torch.float32 or g.device != dev or not g.is_contiguous():
+                    g = g.to(device=dev, dtype=torch.float32).contiguous()
+                    plan.setdefault("keep", []).append(g)
+                dptrs[i] = g.data_ptr()
             wire = plan.get("dense_wire")
-            if wire is not None:
-                wire.copy_(cur)   # compress: tensor.type(float16) (dgc/compression.py:175-177)
-            dense_handle = comm.allreduce_async_(wire if wire is not None else cur, op=Average)
+            L = _lib.lib()
+            st = _lib.stream_of(dev)
+            if wire is not None:   # compress: tensor.type(float16) (dgc/compression.py:175-177)
+                _lib.check(L.dgc_gather_cast(dptrs, plan["dense_numels"], plan["dense_offs"], len(plan["dense"]),
+                                             _lib.ptr(wire), _lib.VD[wire.dtype], st), "dgc_gather_cast")
+                dense_handle = comm.allreduce_async_(wire, op=Average)
         if b is not None:
             if handle is not None:
                 handle.wait()
-            b.decompress(out_flat=b.grad_flat)   # into p.grad, as dgc/compression.py:191-194
-        if dense_handle is not None:
-            red = comm.synchronize(dense_handle)
-            src = red.float() if red.dtype != torch.float32 else red
-            nxt = plan["dense_bufs"][1 - plan["parity"]]
+            b.decompress()   # into the batch's output, then p.grad (dgc/compression.py:191-194)
+            for _, p, out, _ in plan["comp"]:
+                if p.grad is not out:
+                    p.grad = out
+        if plan["dense"]:
             mem = self.mem
             L = _lib.lib()
-            _lib.check(L.dgc_compensate(_lib.ptr(src), _lib.ptr(plan["dense_bufs"][2]), None, _lib.ptr(nxt),
-                                        plan["dense_numel"], float(mem.momentum), int(bool(mem.nesterov)), 0,
-                                        None, 0, 1, 0, _lib.stream_of(nxt.device)), "dgc_compensate")
-            for n, p, o in plan["dense"]:   # p.grad.set_(compensate(accumulate=False)) (:195-198)
-                p.grad = nxt[o: o + p.numel()].view(p.shape)
-            plan["parity"] = 1 - plan["parity"]
+            st = _lib.stream_of(dev)
+            out, mmt = plan["dense_out"], plan["dense_mmt"]
+            if dense_handle is not None:
+                red = comm.synchronize(dense_handle)
+                _lib.check(L.dgc_compensate_wire(_lib.ptr(red), _lib.VD[red.dtype], _lib.VD[torch.float32],
+                                                 _lib.ptr(mmt), _lib.ptr(out), plan["dense_numel"],
+                                                 float(mem.momentum), int(bool(mem.nesterov)), st),
+                           "dgc_compensate_wire")
+            else:   # one rank: the allreduce is the identity, the fp16 wire a rounding
+                rnd = torch.float16 if self.comp.fp16_values else torch.float32
+                _lib.check(L.dgc_compensate_multi(plan["dense_ptrs"], plan["dense_numels"], plan["dense_offs"],
+                                                  len(plan["dense"]), _lib.VD[rnd], _lib.ptr(mmt), _lib.ptr(out),
+                                                  float(mem.momentum), int(bool(mem.nesterov)), st),
+                           "dgc_compensate_multi")
+            for _, p, _, view in plan["dense"]:   # p.grad.set_(compensate(accumulate=False)) (:195-198)
+                if p.grad is not view:
+                    p.grad = view
+            plan.pop("keep", None)
 
     def zero_grads(self):
-        """zero_() of every gradient in place (the views stay bound)."""
+        """zero_() of every gradient in place (the output views stay bound)."""
         plan = self._plan
         if plan is None:
             return False
         if plan["batch"] is not None:
-            plan["batch"].grad_flat.zero_()
+            plan["batch"].out_flat.zero_()
         if plan["dense"]:
-            plan["dense_bufs"][plan["parity"]].zero_()
+            plan["dense_out"].zero_()
+        for _, p, out, _ in plan["comp"]:     # anything rebound since: zeroed in place too
+            if p.grad is not None and p.grad is not out:
+                p.grad.zero_()
+        for _, p, _, view in plan["dense"]:
+            if p.grad is not None and p.grad is not view:
+                p.grad.zero_()
         return True

@@ -62,6 +62,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self.op = op
         self._handles = {}
         self._grad_accs = []
+        self._hook_fns = []   # (parameter, hook) in registration order (bench.py fires them directly)
         self._requires_update = set()
         self._synchronized = False
         self._should_synchronize = True
@@ -72,7 +73,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             if not batched.supported(compression):
                 raise ValueError("batch=True needs a DGCCompressor driving a DGCSGDMemory with strided sampling "
                                  "and no gradient clipping")
-            self._batched = batched.BatchedStep(compression, named_parameters)
+            self._batched = batched.BatchedStep(compression, named_parameters,
+                                                fill="sparse" if batch == "sparse" else "inline")
         if comm.size() > 1 or os.environ.get("HOROVOD_ELASTIC") == "1":
             self._register_hooks()
 
@@ -96,8 +98,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                     p.grad = p.data.new(p.size()).zero_()
                     self._requires_update.add(p)
                     grad_acc = p.expand_as(p).grad_fn.next_functions[0][0]
-                    grad_acc.register_hook(self._make_hook(p))
+                    hook = self._make_hook(p)
+                    grad_acc.register_hook(hook)
                     self._grad_accs.append(grad_acc)
+                    self._hook_fns.append((p, hook))
 
     def _allreduce_grad_async(self, p):
         name = self._parameter_names.get(p)
@@ -190,10 +194,14 @@ def DistributedOptimizer(optimizer, named_parameters=None, compression=Compressi
     decompressed before it steps (dgc/horovod/optimizer.py:370-417).
 
     ``batch=True`` (not in the reference; DGCCompressor + DGCSGDMemory only) exchanges
-    every gradient of a step at once in ``synchronize()``: one K1 launch, one packed
-    allgather and one decompress for all compressed tensors, one allreduce for the
-    dense ones, no host synchronisation (dgc/horovod/batched.py). The numerics, the
-    sample-start draws and so the weights are those of the per-tensor path."""
+    every gradient of a step at once in ``synchronize()``: one K1 launch reading the
+    gradients where autograd left them, one packed allgather and one decompress for all
+    compressed tensors, one allreduce for the dense ones, no host synchronisation and no
+    per-parameter launch (dgc/horovod/batched.py). The numerics, the sample-start draws
+    and so the weights are those of the per-tensor path. ``batch="sparse"`` also
+    replaces decompress's dense ``zero_()`` by a re-zero of the previous step's entries
+    when the gradients were not written in between (see dgc/horovod/batched.py for what
+    it cannot see)."""
     if op == Adasum and comm.size() > 1:
         raise NotImplementedError("Adasum is not part of the DGC path (dgc/horovod/optimizer.py:197-367)")
     if batch and op != Average:

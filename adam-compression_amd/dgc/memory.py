@@ -78,6 +78,26 @@ class DGCSGDMemory(Memory):
     def _clip(self, grad):
         return self.gradient_clipping(grad) if self.gradient_clipping is not None else grad
 
+    def state_of(self, name, like, accumulate=True, what="DGCSGDMemory.compensate"):
+        """(momentum, velocity or None) of ``name``, checked before their pointers reach a
+        kernel: contiguous tensors of ``like``'s dtype, device and size. ``load_state_dict``
+        rebinds them to whatever the checkpoint holds (a CPU map_location, fp32 state for a
+        16-bit parameter); the reference's ATen ops would raise on the device mismatch and
+        promote the dtype, the kernels would fault or misread — so this raises instead."""
+        out = []
+        for kind, store in (("momentum", self.momentums), ("velocity", self.velocities if accumulate else None)):
+            if store is None:
+                out.append(None)
+                continue
+            t = store[name]
+            _lib.require_cuda_float(t, f"{what} ({kind} of {name})")
+            if t.dtype != like.dtype or t.device != like.device or t.numel() != like.numel():
+                raise TypeError(f"{what}: {kind} of {name} is {t.dtype} [{t.numel()}] on {t.device}, the gradient "
+                                f"{like.dtype} [{like.numel()}] on {like.device}; load the state with the "
+                                "parameter's dtype and device")
+            out.append(t)
+        return out[0], out[1]
+
     def compensate(self, grad, name, accumulate=True):
         """Momentum correction + local accumulation (dgc/memory.py:50-70).
 
@@ -85,12 +105,9 @@ class DGCSGDMemory(Memory):
         accumulate=False (dense tensors) returns a new tensor."""
         self._sync()
         grad = self._clip(grad)
-        mmt = self.momentums[name]
         g = grad.contiguous()
         dt = _lib.require_cuda_float(g, "DGCSGDMemory.compensate")
-        _lib.require_cuda_float(mmt, "DGCSGDMemory.compensate")
-        if mmt.dtype != dt:
-            raise TypeError(f"DGCSGDMemory.compensate: gradient {dt} vs momentum {mmt.dtype}")
+        mmt, _ = self.state_of(name, g, accumulate)
         L = _lib.lib()
         stream = _lib.stream_of(g.device)
         if dt in _lib.HALF:
@@ -110,7 +127,7 @@ class DGCSGDMemory(Memory):
     def _compensate16(self, g, name, accumulate, vec32=None):
         """compensate on a bf16 / fp16 state (K1-16); vec32: optional fp32 image of the
         new velocity for the selection (the compressor's fused path)."""
-        mmt = self.momentums[name]
+        mmt, _ = self.state_of(name, g, accumulate)
         L = _lib.lib()
         dt = _lib.VD[g.dtype]
         stream = _lib.stream_of(g.device)
@@ -131,8 +148,8 @@ class DGCSGDMemory(Memory):
         self._sync()
         indices = ctx[0]
         vec = self.velocities[name]
-        mmt = self.momentums[name]
         dt = _lib.require_cuda_float(vec, "DGCSGDMemory.update")
+        mmt, _ = self.state_of(name, vec, False, "DGCSGDMemory.update")
         idx = indices.reshape(-1)
         if idx.dtype not in _lib.ID:
             idx = idx.to(torch.int64)

@@ -20,6 +20,9 @@ with HIP events on the stream it runs on; ``step_hbm`` is the whole step's algor
 HBM rate. With ``--gpus N`` and no torchrun, N ranks are spawned on 127.0.0.1.
 """
 import argparse
+import contextlib
+import ctypes
+import io
 import json
 import os
 import sys
@@ -61,6 +64,10 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the dense-fill pass and (W = 1) the drop-in DistributedOptimizer comparison")
+    ap.add_argument("--dropin-model", default="resnet50", choices=["resnet50", "vgg16_bn"],
+                    help="model set of the drop-in comparison of a flat workload's run")
     ap.add_argument("--fill", default="sparse", choices=["inline", "allgather", "sparse"],
                     help="decompress zero_(): sparse = re-zero only the previous step's entries of the bench's "
                          "persistent output (the bench owns it and never writes it; dgc/bucket.py)")
@@ -304,6 +311,7 @@ class ModelRun:
         self.dense_mmt = torch.zeros(self.n_dense, device=dev)
         self.dense_out = torch.empty(self.n_dense, device=dev)
         self.dense_wire = torch.empty(self.n_dense, dtype=torch.float16 if wl["fp16"] else torch.float32, device=dev)
+        self._one = (ctypes.c_int64 * 1)(self.n_dense), (ctypes.c_int64 * 1)(0)
         self.elements = self.n_comp + self.n_dense
         self.k, self.S = self.b.capacity, sum(a[1] for a in self.b.attrs)
         self.payload = self.b.rank_stride
@@ -326,20 +334,26 @@ class ModelRun:
             if pair:
                 pair[1].record()
         # dense tensors: (fp16 wire cast) -> allreduce Average -> compensate(accumulate=False)
-        # (dgc/compression.py:173-177, 195-198). An fp32 wire at W = 1 is the gradient
-        # itself (the reference allreduces p.grad in place; one rank leaves it as is);
-        # otherwise the wire buffer keeps the bench's fixed gradient buffers intact.
-        if self.dense_wire.dtype == torch.float32 and self.world == 1:
-            src = gd
-        else:
-            self.dense_wire.copy_(gd)
-            if self.world > 1:
-                from dgc import comm
-                comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Average))
-            src = self.dense_wire if self.dense_wire.dtype == torch.float32 else self.dense_wire.float()
-        self._lib.check(L.dgc_compensate(src.data_ptr(), self.dense_mmt.data_ptr(), None, self.dense_out.data_ptr(),
-                                         self.n_dense, 0.9, int(self.nesterov), 0, None, 0, 1, 0,
-                                         self._lib.stream_of(g.device)), "dgc_compensate")
+        # (dgc/compression.py:173-177, 195-198), no ATen kernel: at W = 1 the allreduce is
+        # the identity and the wire cast a rounding, fused into the compensate
+        # (dgc_compensate_wire, round_to fp16); at W > 1 dgc_gather_cast fills the wire
+        # buffer and the compensate widens it
+        st = self._lib.stream_of(g.device)
+        wt = self._lib.VD[self.dense_wire.dtype]
+        f32 = self._lib.VD[torch.float32]
+        if self.world == 1:
+            self._lib.check(L.dgc_compensate_wire(gd.data_ptr(), f32, wt, self.dense_mmt.data_ptr(),
+                                                  self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov),
+                                                  st), "dgc_compensate_wire")
+            return
+        from dgc import comm
+        src = (ctypes.c_void_p * 1)(gd.data_ptr())
+        self._lib.check(L.dgc_gather_cast(src, self._one[0], self._one[1], 1, self.dense_wire.data_ptr(), wt, st),
+                        "dgc_gather_cast")
+        comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Average))
+        self._lib.check(L.dgc_compensate_wire(self.dense_wire.data_ptr(), wt, f32, self.dense_mmt.data_ptr(),
+                                              self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov), st),
+                        "dgc_compensate_wire")
 
     def probe_buffers(self):
         b = self.b
@@ -361,6 +375,112 @@ class ModelRun:
     def config(self):
         return {"compressed_tensors": len(self.b.names), "compressed_elements": self.n_comp,
                 "dense_elements": self.n_dense, "num_selects_total": self.b.capacity, "fill": self.b.fill}
+
+
+class DropinRun:
+    """A model's step through the drop-in API, as the reference's training loop drives it
+    (dgc/horovod/optimizer.py:91-187, train.py:137-140): nn.Parameters of the model's
+    shapes, DGCSGDMemory + DGCCompressor (initialised on the dim > 1 tensors), and
+    dgc.horovod.DistributedOptimizer around a torch optimizer — ``batch`` True (one grouped
+    step, dense zero_()), "sparse" (its re-zero of the previous entries) or False (the
+    reference's per-tensor hooks: a compress with one host sync per tensor). One step =
+    fresh p.grad tensors as backward hands them over (a distinct gradient set per step,
+    the values of ModelRun's two sets), the grad-accumulator hooks fired in backward's
+    (reverse) order, ``synchronize()`` (compress -> exchange -> decompress -> p.grad), and
+    ``zero_grad()`` (set_to_none=True, torch's default). The wrapped optimizer's own update
+    is not on the DGC path and is not run. W = 1 needs HOROVOD_ELASTIC=1 for the hooks
+    (dgc/horovod/optimizer.py:79-80)."""
+
+    def __init__(self, wl, rank, world, dev, batch, steps):
+        import random
+        from dgc import workloads
+        from dgc.compression import DGCCompressor
+        from dgc.horovod import DistributedOptimizer
+        from dgc.memory import DGCSGDMemory
+        os.environ.setdefault("HOROVOD_ELASTIC", "1")
+        shapes = getattr(workloads, wl["model"])()
+        comp_shapes, dense_shapes = workloads.split(shapes)
+        self.named = [(n, torch.nn.Parameter(torch.zeros(s, device=dev))) for n, s in shapes]
+        params = dict(self.named)
+        compression = DGCCompressor(wl["ratio"], memory=DGCSGDMemory(momentum=0.9, nesterov=wl["nesterov"]),
+                                    fp16_values=wl["fp16"], int32_indices=wl["int32"])
+        with contextlib.redirect_stdout(io.StringIO()):
+            compression.memory.initialize(self.named)
+            compression.initialize([(n, params[n]) for n, _ in comp_shapes])
+        random.seed(42)
+        inner = torch.optim.SGD([p for _, p in self.named], lr=0.0)
+        self.opt = DistributedOptimizer(inner, named_parameters=self.named, compression=compression, batch=batch)
+        # ModelRun's two gradient sets, value for value, as per-parameter tensors; then a
+        # distinct copy per step (the per-tensor path decompresses into p.grad in place)
+        gen = torch.Generator(device=dev)
+        base = []
+        for s_ in range(2):
+            gen.manual_seed(0xD6C + 1000 * rank + s_)
+            g = {n: torch.randn(workloads.numel(sh), generator=gen, device=dev).mul_(1e-3).view(sh)
+                 for n, sh in comp_shapes}
+            nd = sum(workloads.numel(sh) for _, sh in dense_shapes)
+            d = torch.randn(nd, generator=gen, device=dev).mul_(1e-3)
+            o = 0
+            for n, sh in dense_shapes:
+                g[n] = d[o: o + workloads.numel(sh)].clone().view(sh)
+                o += workloads.numel(sh)
+            base.append([g[n] for n, _ in self.named])
+        self.sets = [[t.clone() for t in base[i % 2]] for i in range(steps)]
+        self.elements = sum(p.numel() for _, p in self.named)
+        self.hooks = list(reversed(self.opt._hook_fns))
+
+    def step(self, i, ev=None):
+        for (_, p), g in zip(self.named, self.sets[i % len(self.sets)]):
+            p.grad = g
+        for _, hook in self.hooks:
+            hook()
+        self.opt.synchronize()
+        self.opt.zero_grad()
+
+
+def timed_steps(run, steps, warmup, world):
+    """ms per step of ``run.step`` over ``steps`` steps after ``warmup`` (barrier +
+    synchronize on both sides, max over ranks)."""
+    for i in range(warmup):
+        run.step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run.step(warmup + i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    return el * 1e3 / steps
+
+
+def dropin_compare(model, rank, world, dev, steps, warmup):
+    """The drop-in training step against the engine it wraps, same box, same gradients:
+    DGCBatch alone (ModelRun, both fills), DistributedOptimizer(batch=True / "sparse"),
+    and the reference's per-tensor hook path (few steps: it syncs per tensor)."""
+    wl = dict(WORKLOADS[model])
+    res = {"model": model, "steps": steps, "warmup": warmup}
+    for fill in ("inline", "sparse"):
+        run = ModelRun(wl, rank, world, dev, fill)
+        res[f"dgcbatch_{fill}_ms"] = round(timed_steps(run, steps, warmup, world), 4)
+        del run
+    for label, batch, n in (("optimizer_batch_ms", True, steps), ("optimizer_batch_sparse_ms", "sparse", steps),
+                            ("optimizer_per_tensor_ms", False, max(3, steps // 4))):
+        run = DropinRun(wl, rank, world, dev, batch, n + warmup)
+        res[label] = round(timed_steps(run, n, warmup, world), 4)
+        del run
+        torch.cuda.empty_cache()
+    res["batch_vs_dgcbatch"] = round(res["optimizer_batch_ms"] / res["dgcbatch_inline_ms"], 3)
+    res["batch_sparse_vs_dgcbatch"] = round(res["optimizer_batch_sparse_ms"] / res["dgcbatch_sparse_ms"], 3)
+    res["note"] = ("ms per step; dgcbatch = the engine alone (gradients planted in its flat buffer); optimizer = "
+                   "dgc.horovod.DistributedOptimizer: fresh p.grad tensors, hooks in backward order, synchronize(), "
+                   "zero_grad(set_to_none=True); inline = the reference's dense zero_(), sparse = re-zero of the "
+                   "previous entries")
+    return res
 
 
 def hbm_probe(reads, writes, reps=5):
@@ -456,6 +576,16 @@ def main():
         elapsed = t.item()
     ms = {p: sum(e[p][0].elapsed_time(e[p][1]) for e in evs) / args.steps for p in timed}
     info = run.info()
+    extras = {}
+    if not args.no_extras and run.b.fill == "sparse":
+        # the same steps with the reference's dense zero_() (dgc/compression.py:191) before
+        # the scatter, on the same state: what the persistent output's re-zero saves
+        run.b.fill = "inline"
+        extras["dense_fill"] = {"ms_per_step": round(timed_steps(run, args.steps, 2, world), 4),
+                                "steps": args.steps, "warmup": 2,
+                                "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
+                                        "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
+        run.b.fill = "sparse"
     probe = hbm_probe(*run.probe_buffers())   # after the timed steps: overwrites the state
     ms_step = elapsed * 1e3 / args.steps
     full_passes = info.get("full_passes", 0)
@@ -515,6 +645,14 @@ def main():
         res["allgather"] = {"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
                             "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS)}
     log(f"{args.workload}: {ms_step:.3f} ms/step on the GPU")
+    if world == 1 and not args.no_extras:
+        model = wl["model"] if wl["kind"] == "model" else args.dropin_model
+        try:
+            log(f"drop-in DistributedOptimizer comparison on {model}")
+            res["dropin"] = dropin_compare(model, rank, world, dev, 20, 5)
+        except Exception as e:   # an extra must not cost the headline line
+            res["dropin"] = {"error": f"{type(e).__name__}: {e}"}
+    res.update(extras)
     if world == 1 and not args.no_cpu:
         cores = cpu_cores()
         log(f"CPU baseline on {cores} threads, then 1 thread")

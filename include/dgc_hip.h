@@ -55,7 +55,10 @@ enum dgc_status {
     DGC_OK = 0,
     DGC_ERR_INVALID = 1,      /* bad argument (null pointer, k > n, ...) */
     DGC_ERR_DTYPE = 2,        /* unsupported value / index dtype */
-    DGC_ERR_OVERFLOW = 3,     /* int32 indices requested for n > 2^31 - 1 */
+    DGC_ERR_OVERFLOW = 3,     /* int32 indices requested for n > 2^31 - 1, or a    */
+                              /* resample replay that cannot address the tensor:   */
+                              /* more than 2^32 - 1 candidates (min(64k - 1, n))   */
+                              /* or n >= 2^33 elements (resample = 1 only)         */
     DGC_ERR_HIP = 4,          /* a HIP runtime call failed */
     DGC_ERR_WORKSPACE = 5,    /* workspace too small or misaligned */
     DGC_ERR_UNSORTED = 6      /* decompress input has more descending runs than supported */
@@ -114,6 +117,12 @@ typedef struct dgc_select_params {
                               /* threshold *= bound products round to it,   */
                               /* as the 0-dim threshold tensor does          */
     int32_t reserved;
+    int32_t* status_sink;     /* NULL, or a host-mapped (pinned) int32: a call  */
+                              /* whose resample replay broke stores its       */
+                              /* dgc_select_info.k5_status there (with        */
+                              /* DGC_K5_BROKEN set) — nothing is written      */
+                              /* otherwise — so a DGC_SYNC_DEVICE caller can  */
+                              /* check every step without synchronising       */
 } dgc_select_params;
 
 /* Device-resident result record written by dgc_select / dgc_compress. */
@@ -249,6 +258,7 @@ typedef struct dgc_batch_desc {
                                     /*   streams vec/mmt anyway); dgc_batch_flush    */
                                     /*   applies it before vec/mmt are read elsewhere */
     int32_t pad;
+    int32_t* status_sink;           /* as dgc_select_params.status_sink (NULL: none)   */
 } dgc_batch_desc;
 
 size_t dgc_batch_workspace(const dgc_batch_desc* batch);
@@ -266,6 +276,13 @@ int dgc_batch_compress(const dgc_batch_desc* batch, const float* grad, float* mm
  * payload. Nothing may touch grad/mmt/vec between them. */
 int dgc_batch_compress_begin(const dgc_batch_desc* batch, const float* grad, float* mmt, float* vec,
                              const int64_t* sample_starts, void* ws, size_t ws_bytes, void* stream);
+/* dgc_batch_compress_begin with the gradients taken where they are: grads is a HOST
+ * array of `count` device pointers, grads[t] holding numel[t] contiguous floats, 16-B
+ * aligned (the parameters' own p.grad tensors as autograd left them — the batched
+ * DistributedOptimizer, dgc/horovod/optimizer.py:116-155, without a copy into the flat
+ * buffer). A tensor that ends inside a float4 is read to its last element only. */
+int dgc_batch_compress_begin_ptrs(const dgc_batch_desc* batch, const float* const* grads, float* mmt, float* vec,
+                                  const int64_t* sample_starts, void* ws, size_t ws_bytes, void* stream);
 int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt, float* vec, void* payload,
                               dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
                               void* stream);
@@ -342,6 +359,25 @@ int dgc_decompress_status(const void* ws, int32_t* status, void* stream);
  * non-temporal 16-B writes per float4 — to measure the streaming rate of the box at
  * hand next to K1. Not part of the reference's interface. */
 int dgc_hbm_probe(const float* a, const float* b, const float* c, float* d, float* e, int64_t n, void* stream);
+
+/* ---- the dense (uncompressed) tensors of a step (dgc/compression.py:173-177, 195-198) ----
+ * dgc_gather_cast: dst[offsets[t] + i] = (dst_dtype) srcs[t][i] for count tensors (HOST
+ *   arrays; srcs[t]: numels[t] device floats, any alignment) — the dense gradients into
+ *   one allreduce buffer, with compress's `tensor.type(torch.float16)` when dst_dtype is
+ *   DGC_F16 (DGC_BF16 and DGC_F32 too), in one launch per 64 tensors.
+ * dgc_compensate_wire: out = DGCSGDMemory.compensate(g, accumulate=False) (mmt updated),
+ *   g = the exchanged gradient: src_dtype DGC_F16 (widened exactly, decompress's
+ *   `tensor.type(vdtype)`) or DGC_F32; round_to = DGC_F16 with an fp32 src rounds it to
+ *   fp16 and back first (a one-rank exchange of an fp16 wire without the buffer).
+ * dgc_compensate_multi: the same from each tensor's own gradient (srcs[t], numels[t];
+ *   HOST arrays) into mmt / out at offsets[t] of two flat buffers, round_to as above:
+ *   a one-rank step's dense tensors in one launch per 64 tensors. */
+int dgc_gather_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count,
+                    void* dst, int32_t dst_dtype, void* stream);
+int dgc_compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float* mmt, float* out, int64_t n,
+                        float momentum, int32_t nesterov, void* stream);
+int dgc_compensate_multi(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count,
+                         int32_t round_to, float* mmt, float* out, float momentum, int32_t nesterov, void* stream);
 
 /* ---- K7: DGCSGD.step over `count` parameters of one group (dgc/optim/sgd.py:42-68) ----
  * params[i], grads[i] (and bufs[i], the momentum_buffer, when weight_decay != 0 and

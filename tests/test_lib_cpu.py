@@ -96,3 +96,39 @@ def test_batch_desc_validation_without_gpu(L):
     assert b"multiple of 1024" in L.dgc_last_error()
     d, keep = desc([5000, 3000], [0, 5120], 8000)          # past flat_numel
     assert L.dgc_batch_workspace(ctypes.byref(d)) == 0
+
+
+def test_resample_replay_width_refusals_without_gpu(L):
+    """The resample replays pack candidate positions in 32 bits (K5's queue) and element
+    indices in 33 bits (K5b's heap): a tensor past either width is refused with
+    DGC_ERR_OVERFLOW before anything runs, on every entry point — never a truncated
+    payload. resample=False takes any size."""
+    from dgc import _lib
+    OVERFLOW = 3
+    # more than 2^32 - 1 candidates: n >= 2^32, k > 2^26 (a 7B bucket at a warmup ratio)
+    # ... and n >= 2^33 for the partial_sort path
+    for n, k, what in ((2 ** 32 + 4096, 2 ** 26 + 1, b"2^32 - 1 candidates"), (2 ** 33, 1000, b"below 2^33")):
+        p = _lib.SelectParams()
+        p.numel, p.num_selects, p.num_samples = n, k, n // 100
+        p.max_iters, p.resample = 10, 1
+        out = ctypes.c_void_p(256)
+        rc = L.dgc_select(None, None, None, ctypes.byref(p), out, out, None, None, None, 0, 0, None)
+        assert rc == OVERFLOW and what in L.dgc_last_error(), L.dgc_last_error()
+        rc = L.dgc_compress_begin(None, None, None, 0.9, 0, 0, 100, ctypes.byref(p), None, None, 0, None)
+        assert rc == OVERFLOW and what in L.dgc_last_error()
+        T = 1
+        arr = lambda xs: (ctypes.c_int64 * T)(*xs)   # noqa: E731
+        keep = [arr([n]), arr([0]), arr([k]), arr([n // 100]), arr([max(1, n // 100000)]), arr([100])]
+        d = _lib.BatchDesc()
+        d.count = T
+        d.numel, d.offset, d.num_selects, d.num_samples, d.top_k_samples, d.sample_stride = keep
+        d.flat_numel, d.upper_bound, d.lower_bound, d.max_iters, d.resample = n + 4, 1.3, 0.8, 10, 1
+        assert L.dgc_batch_workspace(ctypes.byref(d)) == 0 and what in L.dgc_last_error()
+        d.resample = 0                                     # no replay: no limit of its own
+        assert L.dgc_batch_workspace(ctypes.byref(d)) > 0
+    # the largest tensor the replays take passes the width check (and fails on the null vec after it)
+    p = _lib.SelectParams()
+    p.numel, p.num_selects, p.num_samples, p.max_iters, p.resample = 2 ** 33 - 1, 2 ** 26, 2 ** 26, 10, 1
+    out = ctypes.c_void_p(256)
+    rc = L.dgc_select(None, None, None, ctypes.byref(p), out, out, None, None, None, 0, 0, None)
+    assert rc == 1 and b"null vec" in L.dgc_last_error()

@@ -31,9 +31,12 @@ def main():
     L = _lib.lib()
     L.dgc_k5_prof.restype = ctypes.c_int
     L.dgc_k5_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    cases = [(400_000, 400, 2_000), (1_000_000, 1000, 6_000), (2_000_000, 2000, 12_000),
-             (4_000_000, 2360, 30_000), (4_000_000, 2360, 57_000), (10_000_000, 10_000, 100_000),
-             (100_000_000, 102_761, 1_000_000)]
+    cases = [(400_000, 400, 2_000), (262_144, 263, 8_200), (1_000_000, 1000, 6_000), (589_824, 590, 18_700),
+             (2_000_000, 2000, 12_000), (4_000_000, 2360, 30_000), (2_359_296, 2360, 72_000),
+             (10_000_000, 10_000, 100_000), (100_000_000, 102_761, 1_000_000)]
+    if len(sys.argv) > 1:   # only the cases whose target candidate count is listed
+        keep = {int(a) for a in sys.argv[1:]}
+        cases = [c for c in cases if c[2] in keep]
     for n, k, target in cases:
         select_case(L, n, k, target, reps=1)
         best = None
