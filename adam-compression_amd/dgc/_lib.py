@@ -77,6 +77,7 @@ class StatusSink:
         self.what = what
         self.device = device
         self.word = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+        self._view = self.word.numpy()   # the same host word, read without a tensor op
 
     @property
     def address(self):
@@ -85,7 +86,7 @@ class StatusSink:
     def check(self, sync=False):
         if sync:
             torch.cuda.current_stream(self.device).synchronize()
-        v = int(self.word[0])
+        v = int(self._view[0])
         if v & K5_BROKEN:
             raise RuntimeError(f"{self.what}: the resample replay's multi-workgroup phase timed out at a barrier after "
                                f"it started (k5_status {v}; workgroups not co-resident?); the selection of that step "
@@ -192,6 +193,28 @@ def _load():
     except OSError as e:   # pragma: no cover - reported through lib()
         _load_error = e
     return _lib
+
+
+_glue = None
+
+
+def glue():
+    """The batched optimizer's host glue (csrc/glue.cpp, lib/_dgc_glue.so: p.grad pointer
+    tables and rebinding over torch's tensor objects); raises if it was not built."""
+    global _glue
+    if _glue is None:
+        import importlib.util
+        path = os.path.join(os.path.dirname(LIB_PATH), "_dgc_glue.so")
+        if not os.path.exists(path):
+            path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "_dgc_glue.so")
+        try:
+            spec = importlib.util.spec_from_file_location("_dgc_glue", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+        except (ImportError, OSError, AttributeError) as e:
+            raise RuntimeError(f"{path} could not be loaded ({e}); build it with `make -C adam-compression_amd/csrc`")
+        _glue = mod
+    return _glue
 
 
 def available():

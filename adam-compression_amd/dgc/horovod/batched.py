@@ -49,6 +49,7 @@ import torch
 
 from .. import _lib
 from .. import comm
+from .._lib import glue as _glue
 from ..batch import DGCBatch
 from ..comm import Average
 from ..compression import DGCCompressor
@@ -65,9 +66,13 @@ def supported(compression):
             and compression.strided_sample and mem.gradient_clipping is None)
 
 
-def _readable(g, dev):
-    """A gradient K1 / the dense kernels may read in place."""
-    return (g.dtype == torch.float32 and g.device == dev and g.is_contiguous() and g.data_ptr() % 16 == 0)
+def _draw():
+    """random.randint(0, stride - 1) of dgc/compression.py:118, as the function that
+    consumes the generator the same way (randint(0, b) = randrange(0, b + 1) = the
+    generator's _randbelow(b + 1)) at a third of the call cost; randint where the
+    module lacks it."""
+    rb = getattr(getattr(random, "_inst", None), "_randbelow", None)
+    return rb if rb is not None else (lambda s: random.randint(0, s - 1))
 
 
 class BatchedStep:
@@ -84,6 +89,7 @@ class BatchedStep:
                                       "bf16 / fp16 parameters run with batch=False")
         self._plan = None
         self.mem._before_read.append(self.flush)
+        _lib.glue()   # the host glue must be there (fails loudly, like the library)
 
     # ------------------------------------------------------------------ layout
     def _plan_key(self):
@@ -122,8 +128,12 @@ class BatchedStep:
                 mem.momentums[n], mem.velocities[n] = mv, vv
                 plan["comp"].append((n, p, b.out(n), b.grad(n)))
                 plan["state"].append((n, mv, vv))
+            plan["comp_params"] = [e[1] for e in plan["comp"]]
+            plan["comp_views"] = [e[2] for e in plan["comp"]]
             plan["index"] = {n: i for i, n in enumerate(b.names)}
             plan["ptrs"] = (ctypes.c_void_p * len(comp_names))()
+            plan["sampled"] = {n: c.attributes[n][5] for n in comp_names if c.attributes[n][0] != c.attributes[n][3]}
+            plan["order"] = None
         dense = [(n, p) for n, p in self.named if n not in set(comp_names)]
         if dense:
             offs, end = [], 0
@@ -139,6 +149,8 @@ class BatchedStep:
                 plan["dense"].append((n, p, o, out[o: o + p.numel()].view(p.shape)))
                 plan["dense_state"].append((n, mv))
             plan["dense_out"], plan["dense_mmt"], plan["dense_numel"] = out, mmt, end
+            plan["dense_params"] = [e[1] for e in plan["dense"]]
+            plan["dense_views"] = [e[3] for e in plan["dense"]]
             T = len(dense)
             plan["dense_ptrs"] = (ctypes.c_void_p * T)()
             plan["dense_numels"] = (ctypes.c_int64 * T)(*[p.numel() for _, p in dense])
@@ -175,6 +187,7 @@ class BatchedStep:
     def step(self, hook_order):
         """compress -> exchange -> decompress for every parameter; ``hook_order`` lists
         the parameters in the order their hooks fired (the reference's compress order)."""
+        glue = _glue()
         key = self._plan_key()
         if self._plan is None or self._plan["key"] != key:
             self._build(key)
@@ -184,28 +197,31 @@ class BatchedStep:
         dev = plan["dev"]
         handle = None
         if b is not None:
-            index = plan["index"]
-            starts = [0] * len(b.names)
-            seen = set()
-            attrs = self.comp.attributes
-            for n in list(hook_order) + [e[0] for e in plan["comp"]]:
-                i = index.get(n)
-                if i is None or i in seen:
-                    continue
-                seen.add(i)
-                numel, _, _, S, _, stride = attrs[n]
-                if numel != S:
-                    starts[i] = random.randint(0, stride - 1)   # dgc/compression.py:118
+            if plan["order"] != hook_order:
+                # the sample-start draw sequence of this hook order (backward's order is
+                # the same step after step): the hooked tensors in their order, then the
+                # rest in the model's order (synchronize() compresses those after)
+                index, sampled, seq, seen = plan["index"], plan["sampled"], [], set()
+                for n in list(hook_order) + [e[0] for e in plan["comp"]]:
+                    if n in index and n not in seen:
+                        seen.add(n)
+                        if n in sampled:
+                            seq.append((index[n], sampled[n]))
+                plan["order"], plan["seq"] = list(hook_order), seq
+            starts = [0] * len(plan["comp"])
+            draw = _draw()
+            for i, stride in plan["seq"]:
+                starts[i] = draw(stride)   # dgc/compression.py:118
             ptrs = plan["ptrs"]
-            for i, (n, p, _, gflat) in enumerate(plan["comp"]):
-                g = p.grad
-                if g is None:
+            # autograd (and the p.grad setter) keep dtype, device and size those of the
+            # parameter: only the layout needs a look (K1 reads 16-B aligned rows)
+            for i in glue.grad_table(plan["comp_params"], ctypes.addressof(ptrs), 16):
+                _, p, _, gflat = plan["comp"][i]
+                if p.grad is None:
                     gflat.zero_()   # no gradient this step: zeros
-                    g = gflat
-                elif not _readable(g, dev):
-                    gflat.copy_(g)
-                    g = gflat
-                ptrs[i] = g.data_ptr()
+                else:
+                    gflat.copy_(p.grad)
+                ptrs[i] = gflat.data_ptr()
             b.compensate(starts, grad_ptrs=ptrs)
             b.select()
             if b.world > 1:
@@ -213,13 +229,12 @@ class BatchedStep:
         dense_handle = None
         if plan["dense"]:
             dptrs = plan["dense_ptrs"]
-            zeros = plan["zeros"]
-            for i, (n, p, o, _) in enumerate(plan["dense"]):
-                g = p.grad
+            for i in glue.grad_table(plan["dense_params"], ctypes.addressof(dptrs), 4):
+                g = plan["dense"][i][1].grad
                 if g is None:
-                    g = zeros
-                elif g.dtype != torch.float32 or g.device != dev or not g.is_contiguous():
-                    g = g.to(device=dev, dtype=torch.float32).contiguous()
+                    g = plan["zeros"]
+                else:
+                    g = g.contiguous()
                     plan.setdefault("keep", []).append(g)
                 dptrs[i] = g.data_ptr()
             wire = plan.get("dense_wire")
@@ -233,9 +248,7 @@ class BatchedStep:
             if handle is not None:
                 handle.wait()
             b.decompress()   # into the batch's output, then p.grad (dgc/compression.py:191-194)
-            for _, p, out, _ in plan["comp"]:
-                if p.grad is not out:
-                    p.grad = out
+            glue.bind_grads(plan["comp_params"], plan["comp_views"])
         if plan["dense"]:
             mem = self.mem
             L = _lib.lib()
@@ -253,10 +266,19 @@ class BatchedStep:
                                                   len(plan["dense"]), _lib.VD[rnd], _lib.ptr(mmt), _lib.ptr(out),
                                                   float(mem.momentum), int(bool(mem.nesterov)), st),
                            "dgc_compensate_multi")
-            for _, p, _, view in plan["dense"]:   # p.grad.set_(compensate(accumulate=False)) (:195-198)
-                if p.grad is not view:
-                    p.grad = view
+            # p.grad.set_(compensate(accumulate=False)) (dgc/compression.py:195-198)
+            glue.bind_grads(plan["dense_params"], plan["dense_views"])
             plan.pop("keep", None)
+
+    def release_grads(self, param_groups):
+        """zero_grad(set_to_none=True): every gradient of the wrapped optimizer's params
+        dropped (torch's zero_grad does the same, per call with a profiler scope)."""
+        key = (id(param_groups), len(param_groups), sum(len(g["params"]) for g in param_groups))
+        if getattr(self, "_params_key", None) != key:
+            self._params_key = key
+            self._params = [p for g in param_groups for p in g["params"]]
+        _glue().release_grads(self._params)
+        return True
 
     def zero_grads(self):
         """zero_() of every gradient in place (the output views stay bound)."""

@@ -68,6 +68,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._should_synchronize = True
         self._batched = None
         self._order = []
+        self._cells = {}        # batch mode: name -> [backward passes left]
+        self._fired = [False]   # batch mode: a hook fired since the last synchronize()
         if batch:
             from dgc.horovod import batched
             if not batched.supported(compression):
@@ -84,12 +86,20 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._should_synchronize = True
         for p in self._allreduce_delay:
             self._allreduce_delay[p] = self.backward_passes_per_step
+        self._reset_cells()
         super(self.__class__, self).load_state_dict(*args, **kwargs)
 
     def set_backward_passes_per_step(self, passes):
         self.backward_passes_per_step = passes
         for p in self._allreduce_delay:
             self._allreduce_delay[p] = passes
+        self._reset_cells()
+
+    def _reset_cells(self):
+        bpps = self.backward_passes_per_step
+        for c in self._cells.values():
+            c[0] = bpps
+        self._fired[0] = False
 
     def _register_hooks(self):
         for group in self.param_groups:
@@ -98,7 +108,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                     p.grad = p.data.new(p.size()).zero_()
                     self._requires_update.add(p)
                     grad_acc = p.expand_as(p).grad_fn.next_functions[0][0]
-                    hook = self._make_hook(p)
+                    hook = self._make_hook(p) if self._batched is None else self._make_batched_hook(p)
                     grad_acc.register_hook(hook)
                     self._grad_accs.append(grad_acc)
                     self._hook_fns.append((p, hook))
@@ -129,13 +139,33 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._handles[p] = (handle, ctx)
         return hook
 
+    def _make_batched_hook(self, p):
+        """The hook of batch mode: the reference's bookkeeping (the backward_passes_per_step
+        countdown and its errors, dgc/horovod/optimizer.py:105-129) on a per-parameter cell
+        instead of tensor-keyed dicts, and the parameter's name appended to the hook order
+        when its countdown ends — the exchange itself is synchronize()'s."""
+        name = self._parameter_names.get(p)
+        cell = self._cells[name] = [self.backward_passes_per_step]
+        order, fired = self._order, self._fired
+
+        def hook(*ignore):
+            if cell[0] <= 0:
+                raise AssertionError("Gradients were computed more than backward_passes_per_step times "
+                                     "before call to step(). Increase backward_passes_per_step to "
+                                     "accumulate gradients locally.")
+            assert not p.grad.requires_grad
+            cell[0] -= 1
+            fired[0] = True
+            if cell[0] == 0:   # exchanged with all the others in synchronize()
+                order.append(name)
+        return hook
+
     def synchronize(self):
         if self._batched is not None:
             if self._requires_update:
                 # one grouped compress -> allgather -> decompress (+ one dense allreduce)
                 self._batched.step(self._order)
-                for p in self._requires_update:
-                    self._allreduce_delay[p] = self.backward_passes_per_step
+            self._reset_cells()
             self._order.clear()
             self._handles.clear()
             self._synchronized = True
@@ -173,17 +203,16 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         return super(self.__class__, self).step(closure)
 
     def zero_grad(self, *args, **kwargs):
-        if self._handles:
+        if self._handles or self._fired[0]:
             raise AssertionError("optimizer.zero_grad() was called after loss.backward() but before "
                                  "optimizer.step() or optimizer.synchronize(). This is prohibited as it "
                                  "can cause a race condition.")
         # torch >= 2: zero_grad(set_to_none=True) by default, as the wrapped optimizer does
         set_to_none = kwargs.get("set_to_none", args[0] if args else True)
-        if self._batched is not None and not set_to_none:
-            # zero_grad(set_to_none=False): the gradients stay views of the flat buffers
-            # and are zeroed in place; with None (the default) the next step copies the
-            # new gradients back into the flat layout (dgc/horovod/batched.py)
-            if self._batched.zero_grads():
+        if self._batched is not None:
+            # set_to_none=False: the gradients (the batched step's output views) zeroed in
+            # place; True: released, as torch does it, without its per-call profiling scaffold
+            if self._batched.zero_grads() if not set_to_none else self._batched.release_grads(self.param_groups):
                 return None
         return super(self.__class__, self).zero_grad(*args, **kwargs)
 

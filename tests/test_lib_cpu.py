@@ -132,3 +132,28 @@ def test_resample_replay_width_refusals_without_gpu(L):
     out = ctypes.c_void_p(256)
     rc = L.dgc_select(None, None, None, ctypes.byref(p), out, out, None, None, None, 0, 0, None)
     assert rc == 1 and b"null vec" in L.dgc_last_error()
+
+
+def test_host_glue_tables_and_rebinding():
+    """The batched optimizer's host glue (lib/_dgc_glue.so) on CPU tensors: the pointer
+    table with its fallback positions (no gradient, misaligned, non-contiguous), the
+    rebinding of p.grad to given views, and the release of every gradient."""
+    import torch
+    from dgc import _lib
+    g = _lib.glue()
+    ps = [torch.nn.Parameter(torch.zeros(8, 4)) for _ in range(5)]
+    buf = torch.zeros(5 * 32 + 1)
+    grads = [torch.randn(8, 4), None, buf[1:33].view(8, 4), torch.randn(4, 8).t(), torch.randn(8, 4)]
+    for p, gr in zip(ps, grads):
+        p.grad = gr
+    tab = (ctypes.c_void_p * 5)()
+    assert g.grad_table(ps, ctypes.addressof(tab), 16) == [1, 2, 3]
+    assert tab[0] == grads[0].data_ptr() and tab[4] == grads[4].data_ptr()
+    assert g.grad_table(ps, ctypes.addressof(tab), 4) == [1, 3]
+    views = [buf[i * 32: (i + 1) * 32].view(8, 4) for i in range(5)]
+    g.bind_grads(ps, views)
+    assert all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(ps, views))
+    views[2].fill_(3.0)     # the same storage: p.grad sees it
+    assert float(ps[2].grad[0, 0]) == 3.0
+    g.release_grads(ps)
+    assert all(p.grad is None for p in ps)
