@@ -43,11 +43,11 @@ k_compensate4(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __
     ov.y = comp1<NEST, ACC>(gv.y, mv.y, vv.y, mom);
     ov.z = comp1<NEST, ACC>(gv.z, mv.z, vv.z, mom);
     ov.w = comp1<NEST, ACC>(gv.w, mv.w, vv.w, mom);
-    st_nt(mmt + v, mv);
+    st_stream(mmt + v, mv);
     if (ACC)
-        st_nt(vec + v, vv);
+        st_stream(vec + v, vv);
     else
-        st_nt(out + v, ov);
+        st_stream(out + v, ov);
     if (SAMPLE) {
         int64_t q0, r0;
         floor_divmod_fast(4 * ((int64_t)blockIdx.x * kBlock) - sp.start, sp.stride, sp.inv_stride, q0, r0);

@@ -832,7 +832,7 @@ int clear_packed(const void* prev, int32_t world, int64_t rank_stride, int64_t c
 // decompress's status words (ZeroWords), which saves the scatter two memset packets.
 __global__ void __launch_bounds__(kBlock) k_fill_zero(float4* __restrict__ x, int64_t n4, ZeroWords z) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n4) x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n4) st_stream(x + i, make_float4(0.f, 0.f, 0.f, 0.f));
     if (blockIdx.x == 0) {
 #pragma unroll
         for (int q = 0; q < 3; ++q)

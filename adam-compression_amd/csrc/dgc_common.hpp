@@ -315,6 +315,29 @@ __device__ __forceinline__ void st_nt(float4* p, const float4& v) {
     const f4v x = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
 }
+
+// The streaming stores of the big passes (K1's momentum / velocity, the dense zero
+// fill): 16-B global stores with the sc1 policy — write-through, the line dropped from
+// the XCD's L2 — so no dirty line is left behind when the kernel ends. An nt / plain
+// store keeps its line dirty in L2, and the kernel boundary then writes the XCD L2s
+// back before the next kernel starts: + dirty bytes / ~6 TB/s (MI355X_MICROARCH.md,
+// "boundary"), ~5 us of idle GPU after K1 (8 x 4 MB of L2 full of dirty lines).
+// DGC_STREAM_STORE (A/B builds): 0 nt, 1 sc1 (default), 2 sc1 nt.
+#ifndef DGC_STREAM_STORE
+#define DGC_STREAM_STORE 1
+#endif
+__device__ __forceinline__ void st_stream(float4* p, const float4& v) {
+#if DGC_STREAM_STORE == 0
+    st_nt(p, v);
+#else
+    const f4v x = {v.x, v.y, v.z, v.w};
+#if DGC_STREAM_STORE == 1
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(x) : "memory");
+#else
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" : : "v"(p), "v"(x) : "memory");
+#endif
+#endif
+}
 }  // namespace dgc
 
 namespace dgc {

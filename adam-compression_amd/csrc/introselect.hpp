@@ -292,9 +292,12 @@ struct SplitSlots {
 // The step's swaps L_t <-> R_t, t < s (disjoint positions), by threads tid of nt:
 // kNthSwapBatch pairs per thread with all their loads in flight before any store
 // (8 for the global-memory phase, 2 in LDS where latency is short and registers count).
+// left_only: the step's cut is above nth, so the introselect goes on in [f, cut) and
+// never reads a position >= cut again (they are >= k: not output either) — every
+// swapped R_t is >= cut, so only q[L_t] = q[R_t] is written (half the loads and stores).
 template <int kNthSwapBatch, class Slots, class QP>
 __device__ __forceinline__ void nth_swaps(QP q, const Slots& sl, int64_t f, uint32_t s, uint32_t tid,
-                                          uint32_t nt) {
+                                          uint32_t nt, bool left_only = false) {
     for (uint32_t t0 = tid; t0 < s; t0 += nt * kNthSwapBatch) {
         uint32_t li[kNthSwapBatch], ri[kNthSwapBatch];
 #pragma unroll
@@ -307,7 +310,7 @@ __device__ __forceinline__ void nth_swaps(QP q, const Slots& sl, int64_t f, uint
 #pragma unroll
         for (int j = 0; j < kNthSwapBatch; ++j) {
             if (t0 + j * nt < s) {
-                a[j] = q[f + li[j]];
+                if (!left_only) a[j] = q[f + li[j]];
                 b[j] = q[f + ri[j]];
             }
         }
@@ -315,10 +318,18 @@ __device__ __forceinline__ void nth_swaps(QP q, const Slots& sl, int64_t f, uint
         for (int j = 0; j < kNthSwapBatch; ++j) {
             if (t0 + j * nt < s) {
                 q[f + li[j]] = b[j];
-                q[f + ri[j]] = a[j];
+                if (!left_only) q[f + ri[j]] = a[j];
             }
         }
     }
+}
+
+// The cut of a finished step (after its pass 2): min(first unswapped left stopper,
+// last swapped right stopper), or the range end when nothing swapped.
+__device__ __forceinline__ int64_t nth_cut(uint32_t s, unsigned long long r_min, unsigned long long l_next, int64_t l) {
+    const int64_t rs = s ? (int64_t)r_min : l;
+    const int64_t ln = l_next == ~0ull ? INT64_MAX : (int64_t)l_next;
+    return ln < rs ? ln : rs;
 }
 
 __device__ __forceinline__ void stopper_masks(const uint64_t (&x)[4], uint32_t valid, uint32_t P, uint32_t& pl,
@@ -459,7 +470,7 @@ struct NthShared {
 // lane's stopper bits of each tile in mk (one byte, LDS) when the step's tiles fit
 // mk_tiles, so pass 2 reads bytes instead of the entries; otherwise it reloads them.
 template <int kNthBatch, int kSwapBatch, class Slots, class QP, class MP>
-__device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t mk_tiles) {
+__device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t mk_tiles, int64_t nth) {
     const int64_t f = uniform64(sh.f), l = uniform64(sh.l);
     const int lane = threadIdx.x & 63, wv = wave_id();
     const uint32_t P = uniform32(sh.pivot);
@@ -610,17 +621,17 @@ __device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t
     }
     __syncthreads();
     K5_SUB(1, kNthBatch == 8);
-    // pass 3: the swaps L_t <-> R_t, t < s (disjoint positions)
-    nth_swaps<kSwapBatch>(q, sl, f, sh.s, threadIdx.x, kNthThreads);
+    // pass 3: the swaps L_t <-> R_t, t < s (disjoint positions); only the left half of
+    // each when the introselect goes on left of the cut
+    const bool left_only = nth_cut(sh.s, sh.r_min, sh.l_next, l) > nth;
+    nth_swaps<kSwapBatch>(q, sl, f, sh.s, threadIdx.x, kNthThreads, left_only);
     __syncthreads();
     K5_SUB(2, kNthBatch == 8);
 }
 
 // Thread 0, after a step: the cut and the next range.
 __device__ __forceinline__ void nth_advance(NthShared& sh, int64_t nth) {
-    const int64_t rs = sh.s ? (int64_t)sh.r_min : sh.l;
-    const int64_t ln = sh.l_next == ~0ull ? INT64_MAX : (int64_t)sh.l_next;
-    const int64_t cut = ln < rs ? ln : rs;
+    const int64_t cut = nth_cut(sh.s, sh.r_min, sh.l_next, sh.l);
     if (cut <= nth)
         sh.f = cut;
     else
@@ -665,9 +676,9 @@ __device__ __forceinline__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& s
             const uint32_t cap = (uint32_t)((arena_bytes - off) / 8);
             DGC_LDS uint32_t* ll = reinterpret_cast<DGC_LDS uint32_t*>(mk + off);
             const SplitSlots sl{ll, ll + cap, cap, lpos, rpos, lds(dummy)};
-            nth_step_wg<kNthBatch, kSwapBatch>(q, sl, sh, mk, mk_bytes ? tiles : 0);
+            nth_step_wg<kNthBatch, kSwapBatch>(q, sl, sh, mk, mk_bytes ? tiles : 0, nth);
         } else {
-            nth_step_wg<kNthBatch, kSwapBatch>(q, plain_slots(lpos, rpos, lds(dummy)), sh, mk, mk_tiles);
+            nth_step_wg<kNthBatch, kSwapBatch>(q, plain_slots(lpos, rpos, lds(dummy)), sh, mk, mk_tiles, nth);
         }
         K5_SUB_BEGIN();
         if (threadIdx.x == 0) {
@@ -695,7 +706,7 @@ __device__ __forceinline__ void nth_loop_wg(QP q, SP lpos, SP rpos, NthShared& s
 // branch per store otherwise). The pivot key P comes from the median in a register.
 // xl / xr / dummy: >= kNthWave / 2, kNthWave / 2 and kWave u64 of LDS.
 __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* xl, DGC_LDS uint64_t* xr,
-                                 DGC_LDS uint64_t* dummy, int64_t f, int64_t l, uint32_t P) {
+                                 DGC_LDS uint64_t* dummy, int64_t f, int64_t l, uint32_t P, int64_t nth) {
     constexpr int kTiles = kNthWave / 256 + 1;   // the range <= kNthWave, from a base <= a0
     K5_WSUB_BEGIN();
     const int lane = threadIdx.x & 63;
@@ -751,12 +762,18 @@ __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* xl, DGC_
     const uint32_t s = uniform32(wave_sum(nsw));
     lnext = uniform32(wave_min_u32(lnext));
     rmin = uniform32(wave_min_u32(rmin));
+    const int64_t rs = s ? f + (int64_t)rmin : l;
+    const int64_t ln = lnext == UINT32_MAX ? INT64_MAX : f + (int64_t)lnext;
+    const int64_t cut = ln < rs ? ln : rs;
+    // going on left of the cut: the swapped right stoppers (all >= cut) are never read again
+    const uint32_t keep = cut > nth ? 0x0Fu : 0xFFu;
     wave_sync();   // the pair slots are written
     K5_WSUB(5);
     uint64_t y[kTiles][4];
 #pragma unroll
     for (int u = 0; u < kTiles; ++u) {
         if (u >= nt) break;
+        sw[u] &= keep;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool swl = (sw[u] >> j) & 1u, swr = (sw[u] >> (4 + j)) & 1u;
@@ -775,9 +792,7 @@ __device__ int64_t nth_step_wave(DGC_LDS uint64_t* q, DGC_LDS uint64_t* xl, DGC_
     }
     wave_sync();   // the swaps are done
     K5_WSUB(6);
-    const int64_t rs = s ? f + (int64_t)rmin : l;
-    const int64_t ln = lnext == UINT32_MAX ? INT64_MAX : f + (int64_t)lnext;
-    return ln < rs ? ln : rs;
+    return cut;
 }
 
 // ---------------------------------------------------------------- register tail
@@ -904,7 +919,7 @@ __device__ __forceinline__ void nth_tail_wave(DGC_LDS uint64_t* q, DGC_LDS uint6
         const uint32_t P = uniform32(p);   // lane 0's (every lane is active here)
         wave_sync();
         K5_WSUB(4);
-        const int64_t cut = nth_step_wave(q, xl, xr, dummy, f, l, P);
+        const int64_t cut = nth_step_wave(q, xl, xr, dummy, f, l, P, nth);
         if (cut <= nth)
             f = cut;
         else
@@ -1190,15 +1205,21 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
             if (rmin != UINT32_MAX) atomicMin(&g->r_min, (unsigned long long)(f + rmin));
         }
         nthg_barrier(g, G);
-        // pass 3: the swaps L_t <-> R_t, t < s, over all G workgroups
-        if (threadIdx.x == 0) s_sh = __hip_atomic_load(&g->s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // pass 3: the swaps L_t <-> R_t, t < s, over all G workgroups (the left halves only
+        // when the introselect goes on left of the cut)
+        __shared__ int s_left;
+        if (threadIdx.x == 0) {
+            s_sh = __hip_atomic_load(&g->s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long rm = __hip_atomic_load(&g->r_min, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long ln = __hip_atomic_load(&g->l_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_left = nth_cut(s_sh, rm, ln, l) > nth;
+        }
         __syncthreads();
-        nth_swaps<8>(q, plain_slots(lpos, rpos), f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads);
+        nth_swaps<8>(q, plain_slots(lpos, rpos), f, s_sh, b * kNthThreads + threadIdx.x, G * kNthThreads,
+                     s_left != 0);
         // the last arriver: the cut, the next range and the next median (all swaps visible)
         nthg_barrier(g, G, [&] {
-            const int64_t rs = g->s ? (int64_t)g->r_min : g->l;
-            const int64_t ln = g->l_next == ~0ull ? INT64_MAX : (int64_t)g->l_next;
-            const int64_t cut = ln < rs ? ln : rs;
+            const int64_t cut = nth_cut(g->s, g->r_min, g->l_next, g->l);
             if (cut <= nth)
                 g->f = cut;
             else
@@ -1263,7 +1284,9 @@ __device__ __forceinline__ void nth_element_wg(DGC_GLB uint64_t* q, int64_t n, i
         nth_tail_wave(lq, reinterpret_cast<DGC_LDS uint64_t*>(llp), sh, nth - f);
     __syncthreads();
     K5_STAMP(4);
-    for (int64_t i = threadIdx.x; i < m; i += kNthThreads) q[f + i] = lq[i];
+    // back to the queue: the positions below k = nth + 1 only (the rest is not output)
+    const int64_t mo = nth + 1 - f < m ? nth + 1 - f : m;
+    for (int64_t i = threadIdx.x; i < mo; i += kNthThreads) q[f + i] = lq[i];
     __syncthreads();
     K5_STAMP(5);
     K5_PROF_END();

@@ -78,6 +78,7 @@ constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgrou
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
 constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
 constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
+constexpr int kSpecWords = 4;                   // per-tensor speculation state (dgc_compress_begin: spec)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
@@ -298,7 +299,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.st = c.take<SelState>(L.T);
     w.rs = c.take<RSState>(L.T);
     w.thr = c.take<float>(L.T);
-    w.spec = c.take<float>(2 * L.T);
+    w.spec = c.take<float>(kSpecWords * L.T);
     w.starts = c.take<int64_t>(L.T);
     w.gptr = c.take<const float*>(L.T);
     w.scnt = c.take<int64_t>(L.T);
@@ -579,7 +580,7 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     float4* mmt = reinterpret_cast<float4*>(mmt_flat + d.off);
     float4* vec = reinterpret_cast<float4*>(vec_flat + d.off);
     const int64_t n4 = d.nv4, n = d.n;
-    const float tl = w.spec ? w.spec[2 * t] : __builtin_huge_valf();
+    const float tl = w.spec ? w.spec[kSpecWords * t] : __builtin_huge_valf();
     SelState* st = w.st + t;
     if (blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) st->t_list = tl;
     const bool sample = d.samp_off >= 0;
@@ -627,8 +628,8 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
             x[1] = comp1<NEST, true>(gv[u].y, mv[u].y, vv[u].y, mom);
             x[2] = comp1<NEST, true>(gv[u].z, mv[u].z, vv[u].z, mom);
             x[3] = comp1<NEST, true>(gv[u].w, mv[u].w, vv[u].w, mom);
-            st_nt(mmt + v, mv[u]);
-            st_nt(vec + v, vv[u]);
+            st_stream(mmt + v, mv[u]);
+            st_stream(vec + v, vv[u]);
             const int64_t e = 4 * v;
             valid = e + 3 < n ? 0xFu : (e + 2 < n ? 7u : (e + 1 < n ? 3u : (e < n ? 1u : 0u)));
             if (sample) {
@@ -1865,28 +1866,41 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             r.tie_rule = st->tie_rule;
             r.window_keys = st->win_keys;
             r.k5_status = (int32_t)k5;
-            r.reserved = 0;
+            r.list_threshold = w.spec ? w.spec[kSpecWords * t] : __builtin_huge_valf();   // (updated below)
         }
         if (w.spec) {
-            // spec[0]: next call's list threshold = m * t * growth, growth = 2 - spec[1] / t
-            // (linear extrapolation from the previous final threshold spec[1]) clamped to
-            // [1, 1.5]; spec[1] := t. The ratio t / spec[1] overshoots while the growth
-            // decelerates — the accumulating velocity's threshold grows ~linearly, and on the
-            // bench the ratio extrapolation missed at step 5 (a full pass). The margin m adapts:
-            // after a call whose threshold landed at or above its list threshold (a hit),
-            // m = 1.05 x that call's list/final ratio, within [margin, kSpecMarginMax] — the
-            // lists shrink towards the selection while the threshold moves predictably (at
-            // 1B on the bench's dynamics 4 % of the elements at 0.8 vs 0.7 % at 0.95); a
-            // miss (the threshold fell below it: a full select pass ran) resets m to margin.
-            float* spec = w.spec + 2 * t;
-            const float tc = st->t_cur;
+            // spec[0]: next call's list threshold = m x (predicted final threshold), from
+            //   the SAMPLED threshold t0 = thr[t] (spec[1]: the previous call's) and the
+            //   final one t: prediction = t0 x growth x r, growth = 2 - spec[1] / t0 (linear
+            //   extrapolation of the t0 series) clamped to [1, 1.5], r = min(t / t0, spec[2])
+            //   (spec[2]: the previous call's t / t0). The t0 series is smooth where the
+            //   final one zigzags: a model set's tensors lower their threshold to 0.8 t0
+            //   every other step (the synthetic velocities turn bimodal), and extrapolating
+            //   the finals put the lists above the lowered threshold — two full passes over
+            //   vec for ~20 of ResNet-50's 54 tensors per step; with the lower of the last two
+            //   ratios the lists hold the lowered threshold's candidates. A flat bucket never
+            //   lowers (t = t0, r = 1): the same prediction as the final-threshold series.
+            //   The accumulating velocity's threshold grows ~linearly (the ratio
+            //   extrapolation overshot). The margin m adapts: after a call whose threshold
+            //   landed at or above its list threshold (a hit), m = 1.05 x that call's
+            //   list/final ratio, within [margin, kSpecMarginMax] — the lists shrink towards
+            //   the selection while the threshold moves predictably (at 1B on the bench's
+            //   dynamics 4 % of the elements at 0.8 vs 0.7 % at 0.95); a miss (the threshold
+            //   fell below it: a full select pass ran) resets m to margin.
+            float* spec = w.spec + kSpecWords * t;
+            const float tc = st->t_cur, t0 = st->t0;
             const float used = spec[0];
-            const float gr = fminf(fmaxf(2.f - spec[1] / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
+            const bool finite = tc == tc && tc > 0.f && tc < __builtin_huge_valf() && t0 == t0 && t0 > 0.f &&
+                                t0 < __builtin_huge_valf();
+            const float gr = fminf(fmaxf(2.f - spec[1] / t0, 1.f), 1.5f);   // first call: 2 - inf -> 1
+            const float r = finite ? tc / t0 : 1.f;
+            const float rp = fminf(r, spec[2]);                             // first call: min(r, inf)
             float m = margin;
             if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
                 m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
-            spec[0] = (tc == tc && tc > 0.f && tc < __builtin_huge_valf()) ? tc * m * gr : __builtin_huge_valf();
-            spec[1] = tc;
+            spec[0] = finite ? t0 * gr * rp * m : __builtin_huge_valf();
+            spec[1] = finite ? t0 : __builtin_huge_valf();
+            spec[2] = finite ? r : __builtin_huge_valf();
         }
     }
     __syncthreads();
@@ -2285,7 +2299,7 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
 }
 
 __global__ void k_spec_reset(float* spec, int32_t T) {
-    for (int i = threadIdx.x; i < 2 * T; i += blockDim.x) spec[i] = __builtin_huge_valf();
+    for (int i = threadIdx.x; i < kSpecWords * T; i += blockDim.x) spec[i] = __builtin_huge_valf();
 }
 
 // ------------------------------------------------------------------ host driver
@@ -2647,7 +2661,7 @@ static int one_ws(const dgc_select_params* p, int64_t s_start, int64_t s_stride,
     if (!ws || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 255))
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_compress: workspace needs %zu bytes, 256-B aligned", need);
     w = carve_select(ws, L);
-    w.spec = spec;   // the caller's per-tensor float[2] (null: no speculative lists)
+    w.spec = spec;   // the caller's per-tensor float[kSpecWords] (null: no speculative lists)
     return DGC_OK;
 }
 

@@ -42,7 +42,7 @@ class SelectInfo(ctypes.Structure):
                 ("branch", ctypes.c_int32), ("recounts", ctypes.c_int32),
                 ("overflow_segments", ctypes.c_int32), ("full_passes", ctypes.c_int32),
                 ("tie_rule", ctypes.c_int32), ("window_keys", ctypes.c_int32),
-                ("k5_status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("k5_status", ctypes.c_int32), ("list_threshold", ctypes.c_float)]
 
 
 K5_FALLBACK, K5_BROKEN = 1, 2
@@ -58,6 +58,7 @@ def info_dict(i, what):
                 branch=BRANCHES.get(i.branch, i.branch), recounts=i.recounts,
                 overflow_segments=i.overflow_segments, full_passes=i.full_passes,
                 tie_rule=TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys,
+                list_threshold=i.list_threshold,
                 k5_fallback=bool(i.k5_status & K5_FALLBACK))
 
 

@@ -145,7 +145,8 @@ typedef struct dgc_select_info {
                                  (exact, slower); bit 1 (DGC_K5_BROKEN) a barrier of that
                                  phase timed out after it had started: the selection of
                                  this tensor is NOT reliable (the engines raise)       */
-    int32_t reserved;
+    float list_threshold;     /* the K1 candidate lists' threshold this call used (+inf:
+                                 none); diagnostics of the speculative listing       */
 } dgc_select_info;
 
 enum { DGC_K5_FALLBACK = 1, DGC_K5_BROKEN = 2 };
@@ -193,15 +194,17 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
 
 /* ---- fused compress: compensate + sample + threshold + select ----
  * Speculative listing: K1 also lists every element with |vec_new| >= spec_threshold[0]
- * into the selection workspace. spec_threshold is a device float[2], in/out, per
- * tensor (NULL = off); initialise both to +inf. When the sampled threshold comes out
+ * into the selection workspace. spec_threshold is a device float[4], in/out, per
+ * tensor (NULL = off); initialise all four to +inf. When the sampled threshold comes out
  * >= spec[0] and few segment lists overflowed, every count and selection is served
  * from the lists and the separate re-read of vec is skipped; otherwise one full pass
  * runs. Results are identical either way (spec only chooses the work).
- * On return spec[1] = the final threshold t and spec[0] = m x t x growth, growth =
- * 2 - (previous t) / t (linear extrapolation) clamped to [1, 1.5]; m = spec_margin (0.8 is a good one) after a
- * call whose t fell below its list threshold, else 1.05 x (list threshold / t) of
- * that call, within [spec_margin, 0.95]: the lists shrink while t moves predictably.
+ * On return spec[1] = the sampled threshold t0, spec[2] = t / t0 (t the final threshold)
+ * and spec[0] = m x t0 x growth x min(t / t0, previous t / t0), growth = 2 -
+ * (previous t0) / t0 (linear extrapolation) clamped to [1, 1.5]; m = spec_margin (0.8
+ * is a good one) after a call whose t fell below its list threshold, else 1.05 x (list
+ * threshold / t) of that call, within [spec_margin, 0.95]: the lists shrink while t
+ * moves predictably.
  * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
  * one workspace and must see the same sample_start/stride/params. The workspace
  * carries per-tensor state from call to call (a deferred masking, the K1 list-spill

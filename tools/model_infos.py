@@ -34,7 +34,7 @@ def main():
                 continue
             rows.append(dict(t=t, n=b.numels[t], k=b.attrs[t][0], **{k: inf[k] for k in (
                 "branch", "candidates", "full_passes", "recounts", "overflow_segments", "threshold0",
-                "threshold")}))
+                "threshold", "list_threshold")}))
         print(json.dumps({"step": i, "tensors": len(b.names), "notable": rows}), flush=True)
 
 
