@@ -17,7 +17,10 @@
 //          order (indices within one rank's payload are distinct, as DGC emits them),
 //          then one pass scales.
 // HBM: K1-16 moves 10 B/elem (+4 for the image). Not a BASELINE configuration (every
-// benched config is fp32); the engines (DGCBucket, DGCBatch) stay fp32-only.
+// benched config is fp32). The batch (DGCBatch / DistributedOptimizer(batch=True) on
+// 16-bit parameters) runs K1-16 over its flat 16-bit buffers, dgc_batch_select on the
+// image, k_mask_packed16 / k_scatter_packed16 from the packed payloads (their counts
+// read on the device), k_gather16 for the optimizer's p.grad tensors.
 #include "dgc_common.hpp"
 
 namespace dgc {
@@ -142,6 +145,78 @@ template <int DT>
 __global__ void __launch_bounds__(kBlock) k_scale16(uint16_t* __restrict__ x, int64_t n, float scale) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
         x[i] = f32_to_h16<DT>(__fmul_rn(h16_to_f32<DT>(x[i]), scale));
+}
+
+// ---- the 16-bit batch (dgc_batch_desc.dtype): packed payloads, device counts ----
+int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
+
+// DGCSGDMemory.update of one packed payload's entries (its count in the header).
+template <typename I>
+__global__ void __launch_bounds__(kBlock)
+k_mask_packed16(const char* __restrict__ payload, int64_t ioff, uint16_t* __restrict__ mmt,
+                uint16_t* __restrict__ vec, int64_t n) {
+    const int64_t count = *reinterpret_cast<const int64_t*>(payload);
+    const I* idx = reinterpret_cast<const I*>(payload + ioff);
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < count; q += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = (int64_t)idx[q];
+        if (i < 0 || i >= n) continue;   // our own payload: never out of range
+        if (mmt) mmt[i] = 0;
+        vec[i] = 0;
+    }
+}
+
+// One rank's run of a packed payload: out[i] = DT(out[i] + DT(v)) (k_scatter16 with the
+// run's count read on the device).
+template <int DT, int VD, typename I>
+__global__ void __launch_bounds__(kBlock)
+k_scatter_packed16(const char* __restrict__ run, int64_t voff, int64_t ioff, uint16_t* __restrict__ out, int64_t n,
+                   int32_t* bad) {
+    const int64_t count = *reinterpret_cast<const int64_t*>(run);
+    const I* idx = reinterpret_cast<const I*>(run + ioff);
+    const void* values = run + voff;
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < count; q += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = (int64_t)idx[q];
+        if (i < 0 || i >= n) {
+            atomicOr(bad, 1);
+            continue;
+        }
+        float v;
+        if (VD == DGC_F32)
+            v = static_cast<const float*>(values)[q];
+        else if (VD == DGC_F16)
+            v = f16_to_f32(static_cast<const uint16_t*>(values)[q]);
+        else
+            v = bf16_to_f32(static_cast<const uint16_t*>(values)[q]);
+        v = round16<DT>(v);
+        out[i] = f32_to_h16<DT>(__fadd_rn(h16_to_f32<DT>(out[i]), v));
+    }
+}
+
+// 2-byte multi-tensor gather (the 16-bit gradients into the batch's flat buffer).
+constexpr int kG16Max = 64;
+struct G16Chunk {
+    int32_t count, pad;
+    int32_t bstart[kG16Max + 1];
+    const uint16_t* src[kG16Max];
+    int64_t n[kG16Max];
+    int64_t off[kG16Max];
+};
+
+__global__ void __launch_bounds__(kBlock) k_gather16(G16Chunk c, uint16_t* __restrict__ dst) {
+    int lo = 0, hi = c.count - 1;
+    const int b = (int)blockIdx.x;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (c.bstart[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const int64_t n = c.n[lo], off = c.off[lo];
+    const uint16_t* __restrict__ src = c.src[lo];
+    const int64_t e0 = (int64_t)(b - c.bstart[lo]) * kBlock * 4 + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        if (e < n) dst[off + e] = src[e];
+    }
 }
 
 static bool is16(int32_t dt) { return dt == DGC_BF16 || dt == DGC_F16; }
@@ -298,6 +373,115 @@ extern "C" int dgc_decompress16(const void* values, int32_t vdtype, const void* 
             hipLaunchKernelGGL(k_scale16<DGC_BF16>, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n, scale);
         else
             hipLaunchKernelGGL(k_scale16<DGC_F16>, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n, scale);
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
+}
+
+extern "C" int dgc_mask_packed16(const void* payload, int64_t capacity, int32_t vdtype, int32_t idtype, void* mmt,
+                                 void* vec, int64_t n, void* stream) {
+    using namespace dgc;
+    if (!payload || !vec || capacity < 0 || n < 0) DGC_FAIL(DGC_ERR_INVALID, "dgc_mask_packed16: bad arguments");
+    if (idtype != DGC_I64 && idtype != DGC_I32) DGC_FAIL(DGC_ERR_DTYPE, "dgc_mask_packed16: index dtype");
+    if (capacity == 0) return DGC_OK;
+    int64_t voff = 0, ioff = 0;
+    payload_layout(capacity, vdtype, idtype, &voff, &ioff);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = grid_for(capacity);
+    auto p = static_cast<const char*>(payload);
+    auto m = static_cast<uint16_t*>(mmt);
+    auto v = static_cast<uint16_t*>(vec);
+    if (idtype == DGC_I32)
+        hipLaunchKernelGGL(k_mask_packed16<int32_t>, dim3(grid), dim3(kBlock), 0, s, p, ioff, m, v, n);
+    else
+        hipLaunchKernelGGL(k_mask_packed16<int64_t>, dim3(grid), dim3(kBlock), 0, s, p, ioff, m, v, n);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+namespace dgc {
+template <int DT, typename I>
+static int scatter_packed16_t(const char* p, int32_t world, int64_t stride, int64_t capacity, int32_t vd, int64_t voff,
+                              int64_t ioff, uint16_t* out, int64_t n, int32_t* bad, hipStream_t s) {
+    const int grid = grid_for(capacity);
+    for (int32_t r = 0; r < world; ++r) {   // rank order: one launch per run
+        const char* run = p + (int64_t)r * stride;
+        if (vd == DGC_F32)
+            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_F32, I>), dim3(grid), dim3(kBlock), 0, s, run, voff, ioff, out, n, bad);
+        else if (vd == DGC_F16)
+            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_F16, I>), dim3(grid), dim3(kBlock), 0, s, run, voff, ioff, out, n, bad);
+        else
+            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_BF16, I>), dim3(grid), dim3(kBlock), 0, s, run, voff, ioff, out, n, bad);
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
+}
+}  // namespace dgc
+
+extern "C" int dgc_decompress_packed16(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                                       int32_t vdtype, int32_t idtype, void* grad, int32_t dtype, int64_t n,
+                                       float scale, int32_t* bad_flag, void* stream) {
+    using namespace dgc;
+    if (!is16(dtype)) DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress_packed16: grad dtype must be DGC_BF16 or DGC_F16");
+    if (vdtype != DGC_F32 && vdtype != DGC_F16 && vdtype != DGC_BF16)
+        DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress_packed16: value dtype");
+    if (idtype != DGC_I64 && idtype != DGC_I32) DGC_FAIL(DGC_ERR_DTYPE, "dgc_decompress_packed16: index dtype");
+    if (!payload || !grad || !bad_flag || world < 1 || capacity < 0 || n < 0)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed16: bad arguments");
+    int64_t voff = 0, ioff = 0;
+    const int64_t min_stride = payload_layout(capacity, vdtype, idtype, &voff, &ioff);
+    if (rank_stride < min_stride) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_packed16: rank_stride < %lld",
+                                           (long long)min_stride);
+    if (n == 0) return DGC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto out = static_cast<uint16_t*>(grad);
+    hipLaunchKernelGGL(k_zero16, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n);   // grad.zero_()
+    DGC_LAUNCHED();
+    auto p = static_cast<const char*>(payload);
+    if (capacity > 0) {
+        if (dtype == DGC_BF16 && idtype == DGC_I32)
+            DGC_TRY((scatter_packed16_t<DGC_BF16, int32_t>(p, world, rank_stride, capacity, vdtype, voff, ioff, out, n, bad_flag, s)));
+        else if (dtype == DGC_BF16)
+            DGC_TRY((scatter_packed16_t<DGC_BF16, int64_t>(p, world, rank_stride, capacity, vdtype, voff, ioff, out, n, bad_flag, s)));
+        else if (idtype == DGC_I32)
+            DGC_TRY((scatter_packed16_t<DGC_F16, int32_t>(p, world, rank_stride, capacity, vdtype, voff, ioff, out, n, bad_flag, s)));
+        else
+            DGC_TRY((scatter_packed16_t<DGC_F16, int64_t>(p, world, rank_stride, capacity, vdtype, voff, ioff, out, n, bad_flag, s)));
+    }
+    if (scale != 1.0f) {   // grad.mul_(1 / W), rounded to the dtype
+        if (dtype == DGC_BF16)
+            hipLaunchKernelGGL(k_scale16<DGC_BF16>, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n, scale);
+        else
+            hipLaunchKernelGGL(k_scale16<DGC_F16>, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n, scale);
+        DGC_LAUNCHED();
+    }
+    return DGC_OK;
+}
+
+extern "C" int dgc_gather16(const void* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count,
+                            void* dst, void* stream) {
+    using namespace dgc;
+    if (count < 0 || (count > 0 && (!srcs || !numels || !offsets || !dst)))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_gather16: null argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    for (int32_t t0 = 0; t0 < count; t0 += kG16Max) {
+        G16Chunk c{};
+        c.count = count - t0 < kG16Max ? count - t0 : kG16Max;
+        int64_t blocks = 0;
+        for (int i = 0; i < c.count; ++i) {
+            const int64_t n = numels[t0 + i];
+            if (n < 0 || offsets[t0 + i] < 0 || (n > 0 && !srcs[t0 + i]))
+                DGC_FAIL(DGC_ERR_INVALID, "dgc_gather16: tensor %d: bad pointer, size or offset", t0 + i);
+            c.bstart[i] = (int32_t)blocks;
+            c.src[i] = static_cast<const uint16_t*>(srcs[t0 + i]);
+            c.n[i] = n;
+            c.off[i] = offsets[t0 + i];
+            blocks += ceil_div(n, (int64_t)kBlock * 4);
+            if (blocks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_gather16: too many elements");
+        }
+        c.bstart[c.count] = (int32_t)blocks;
+        if (blocks == 0) continue;
+        hipLaunchKernelGGL(k_gather16, dim3((unsigned)blocks), dim3(kBlock), 0, s, c, static_cast<uint16_t*>(dst));
         DGC_LAUNCHED();
     }
     return DGC_OK;

@@ -2775,14 +2775,21 @@ static int batch_layout(const dgc_batch_desc* b, Layout& L, std::vector<TDesc>& 
     }
     if (b->int32_indices && b->flat_numel > 2147483647LL)
         DGC_FAIL(DGC_ERR_OVERFLOW, "dgc_batch: int32 indices cannot address %lld elements", (long long)b->flat_numel);
+    if (b->dtype != DGC_F32 && b->dtype != DGC_BF16 && b->dtype != DGC_F16)
+        DGC_FAIL(DGC_ERR_DTYPE, "dgc_batch: dtype must be DGC_F32, DGC_BF16 or DGC_F16");
     build_layout(in.data(), b->count, true, L, td, bt, small);
     return DGC_OK;
 }
 
+// A 16-bit batch (dtype bf16 / fp16) selects on the velocities' fp32 image without
+// touching it (update_memory 0; the 16-bit state is masked from the payload,
+// dgc_mask_packed16), its wire values in the parameter dtype unless fp16_values, and its
+// threshold *= bound products rounded to the dtype.
 static SelCfg cfg_of_batch(const dgc_batch_desc* b) {
+    const bool half = b->dtype == DGC_BF16 || b->dtype == DGC_F16;
     return SelCfg{(float)b->upper_bound, (float)b->lower_bound, b->max_iters, b->resample, b->momentum_masking,
-                  b->fp16_values ? DGC_F16 : DGC_F32, b->int32_indices ? DGC_I32 : DGC_I64,
-                  b->deferred_masking ? 2 : 1};
+                  b->fp16_values ? DGC_F16 : (half ? b->dtype : DGC_F32), b->int32_indices ? DGC_I32 : DGC_I64,
+                  half ? 0 : (b->deferred_masking ? 2 : 1), half ? b->dtype : DGC_F32};
 }
 
 size_t batch_ws_bytes(const dgc_batch_desc* b) {
@@ -2906,6 +2913,64 @@ int batch_compress_finish(const dgc_batch_desc* b, float* mmt, float* vec, void*
                        sync_mode, b->spec_margin, b->status_sink, s);
 }
 
+// The strided samples |x[start + q * stride]| of every sampled tensor from a flat fp32
+// buffer (K1 writes them on the fp32 path); grid: (chunks, T).
+__global__ void __launch_bounds__(kBlock) k_batch_sample(SelWS w, const float* __restrict__ x_flat) {
+    const int t = blockIdx.y;
+    const TDesc d = w.td[t];
+    if (d.samp_off < 0) return;
+    const int64_t start = w.starts[t], cnt = w.scnt[t];
+    const float* x = x_flat + d.off + start;
+    float* out = w.samples + d.samp_off;
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < cnt; q += (int64_t)gridDim.x * kBlock)
+        out[q] = fabsf(x[q * d.stride]);
+}
+
+// The selection of a batch over a flat fp32 buffer vec32 that no K1 of this library
+// produced (a 16-bit batch's velocity image, dgc_compensate16): the strided samples,
+// then dgc_batch_compress_finish's thresholds and selection (no candidate lists: the
+// first count is a full pass). With dtype = DGC_F32 and update_memory (the desc's
+// deferred_masking off) it masks vec32 like the fused path; a 16-bit batch never
+// writes vec32.
+int batch_select(const dgc_batch_desc* b, float* vec32, float* mmt32, const int64_t* starts, void* payload,
+                 dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
+    Layout L;
+    std::vector<TDesc> td;
+    SelWS w;
+    DGC_TRY(batch_ws(b, ws, ws_bytes, "dgc_batch_select", L, td, w));
+    if (!vec32 || !starts || !payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_select: null pointer");
+    const SelCfg cfg = cfg_of_batch(b);
+    if (cfg.update_memory && cfg.masking && !mmt32) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_select: masking needs mmt");
+    for (int32_t t = 0; t < L.T; ++t)
+        if (td[t].samp_off >= 0 && (starts[t] < 0 || starts[t] >= td[t].stride))
+            DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_select: tensor %d: sample start outside [0, stride)", t);
+    for (int32_t t0 = 0; t0 < L.T; t0 += 64) {
+        StartChunk c{};
+        c.first = t0;
+        c.count = std::min<int32_t>(64, L.T - t0);
+        for (int i = 0; i < c.count; ++i) c.start[i] = td[t0 + i].samp_off >= 0 ? starts[t0 + i] : 0;
+        hipLaunchKernelGGL(k_put_starts, dim3(1), dim3(64), 0, s, w, c);
+        DGC_LAUNCHED();
+    }
+    int64_t smax = 0;
+    for (const TDesc& d : td) smax = std::max(smax, d.samp_off >= 0 ? d.S + 1 : 0);
+    if (smax > 0) {
+        hipLaunchKernelGGL(k_batch_sample, dim3((unsigned)std::min<int64_t>(ceil_div(smax, (int64_t)kBlock), 1024),
+                                                (unsigned)L.T), dim3(kBlock), 0, s, w, vec32);
+        DGC_LAUNCHED();
+    }
+    hipLaunchKernelGGL(k_no_lists, dim3(1), dim3(256), 0, s, w);   // t_list = +inf: no K1 lists
+    DGC_LAUNCHED();
+    DGC_TRY(thresholds(w, L, vec32, s));
+    int64_t cap = 0;
+    for (const TDesc& d : td) cap += d.k;
+    int64_t voff = 0, ioff = 0;
+    payload_layout(cap, cfg.vdtype, cfg.idtype, &voff, &ioff);
+    char* pl = static_cast<char*>(payload);
+    return select_core(vec32, mmt32, cfg, L, pl + voff, pl + ioff, reinterpret_cast<int64_t*>(pl), info, w, 1,
+                       sync_mode, b->spec_margin, b->status_sink, s);
+}
+
 int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,
                    void* payload, dgc_select_info* info, void* ws, size_t ws_bytes, int sync_mode, hipStream_t s) {
     if (!payload) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: null pointer");
@@ -3010,6 +3075,13 @@ extern "C" int dgc_batch_compress_begin(const dgc_batch_desc* batch, const float
                                         const int64_t* sample_starts, void* ws, size_t ws_bytes, void* stream) {
     return dgc::batch_compress_begin(batch, grad, nullptr, mmt, vec, sample_starts, ws, ws_bytes,
                                      static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_batch_select(const dgc_batch_desc* batch, float* vec32, float* mmt32, const int64_t* sample_starts,
+                                void* payload, dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
+                                void* stream) {
+    return dgc::batch_select(batch, vec32, mmt32, sample_starts, payload, info_out, ws, ws_bytes, sync_mode,
+                             static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dgc_batch_compress_begin_ptrs(const dgc_batch_desc* batch, const float* const* grads, float* mmt,

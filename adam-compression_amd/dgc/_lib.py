@@ -104,7 +104,7 @@ class BatchDesc(ctypes.Structure):
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("momentum_masking", ctypes.c_int32),
                 ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
                 ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float),
-                ("deferred_masking", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("deferred_masking", ctypes.c_int32), ("dtype", ctypes.c_int32),
                 ("status_sink", ctypes.c_void_p)]
 
 _P = ctypes.c_void_p
@@ -159,6 +159,11 @@ _SIGNATURES = {
     "dgc_compensate_wire": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _F, _I32, _P]),
     "dgc_compensate_multi": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32,
                                             _I32, _P, _P, _F, _I32, _P]),
+    "dgc_batch_select": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, ctypes.POINTER(_I64), _P, _P, _P, _SZ, _I32,
+                                         _P]),
+    "dgc_mask_packed16": (ctypes.c_int, [_P, _I64, _I32, _I32, _P, _P, _I64, _P]),
+    "dgc_decompress_packed16": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I32, _I64, _F, _P, _P]),
+    "dgc_gather16": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32, _P, _P]),
     "dgc_batch_compress_finish": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _P, _P, _SZ, _I32, _P]),
     "dgc_batch_flush": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, _SZ, _P]),
     "dgc_hbm_probe": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P]),

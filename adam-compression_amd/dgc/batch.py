@@ -52,10 +52,14 @@ class DGCBatch:
     def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
                  resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
-                 deferred_masking=True, fill="auto"):
+                 deferred_masking=True, fill="auto", dtype=torch.float32):
         if fill not in ("auto", "inline", "sparse"):
             raise ValueError(f"fill must be 'auto', 'inline' or 'sparse', not {fill!r}")
-        if fill == "auto":   # the dense zero_() is always right; the re-zero is opt-in
+        if dtype not in (torch.float32,) + _lib.HALF:
+            raise NotImplementedError(f"DGCBatch: fp32, bf16 or fp16 parameters (got {dtype})")
+        self.dtype = dtype
+        self.half = dtype in _lib.HALF
+        if fill == "auto" or self.half:   # the dense zero_() is always right; the re-zero is opt-in (fp32)
             fill = "inline"
         self.fill = fill
         self.device = torch.device(device or "cuda")
@@ -66,7 +70,7 @@ class DGCBatch:
         self.sample_ratio = min(max(sample_ratio, 0.01), 1.0)
         self.upper, self.lower = float(compress_upper_bound), float(compress_lower_bound)
         self.max_iters, self.resample = int(max_adaptation_iters), bool(resample)
-        self.vdtype = torch.float16 if fp16_values else torch.float32
+        self.vdtype = torch.float16 if fp16_values else dtype
         self.idtype = torch.int32 if int32_indices else torch.int64
         self.world = world_size or (dist.get_world_size() if dist.is_initialized() else 1)
         self.rng = random.Random(seed) if seed is not None else random   # the reference draws from `random`
@@ -77,12 +81,17 @@ class DGCBatch:
         self.offsets = offs
         self.flat_numel = max(end, SEG)
         dev = self.device
-        self.grad_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
-        self._mmt_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
-        self._vec_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
-        self.deferred_masking = bool(deferred_masking)
+        self.grad_flat = torch.zeros(self.flat_numel, dtype=dtype, device=dev)
+        self._mmt_flat = torch.zeros(self.flat_numel, dtype=dtype, device=dev)
+        self._vec_flat = torch.zeros(self.flat_numel, dtype=dtype, device=dev)
+        # 16-bit: K1-16 (dgc_compensate16) rounds every op to the dtype and writes the new
+        # velocity's exact fp32 image, which the selection reads (dgc_batch_select); the
+        # 16-bit state is masked from the payload (dgc_mask_packed16)
+        self._vec32 = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev) if self.half else None
+        self._bad16 = torch.zeros(1, dtype=torch.int32, device=dev) if self.half else None
+        self.deferred_masking = bool(deferred_masking) and not self.half
         self._pending = False
-        self.out_flat = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev)
+        self.out_flat = torch.zeros(self.flat_numel, dtype=dtype, device=dev)
         self._L = _lib.lib()
         self.info = torch.zeros(len(self.names) * _lib.INFO_BYTES, dtype=torch.uint8, device=dev)
         self.status = _lib.StatusSink("DGCBatch", dev)   # DGC_K5_BROKEN, checked every step
@@ -110,6 +119,7 @@ class DGCBatch:
         d.fp16_values, d.int32_indices = int(self.vdtype == torch.float16), int(self.idtype == torch.int32)
         d.nesterov, d.momentum, d.spec_margin = int(self.nesterov), self.momentum, _lib.SPEC_MARGIN
         d.deferred_masking = int(self.deferred_masking)
+        d.dtype = _lib.VD[self.dtype]
         d.status_sink = self.status.address
         self.desc = d
         L = self._L
@@ -188,6 +198,12 @@ class DGCBatch:
             starts.append(self.rng.randint(0, stride - 1) if n != S else 0)
         return starts
 
+    def _arrays16(self):
+        if not hasattr(self, "_g16"):
+            T = len(self.names)
+            self._g16 = ((ctypes.c_int64 * T)(*self.numels), (ctypes.c_int64 * T)(*self.offsets))
+        return self._g16
+
     def compensate(self, starts=None, grad_ptrs=None):
         """K1 over every tensor: compensate + strided samples + candidate lists (and any
         masking the previous select left pending). The gradients come from ``grad_flat``,
@@ -200,7 +216,18 @@ class DGCBatch:
         self.starts = starts
         self._par += 1   # a step starts: the other payload / gather buffer
         arr = (ctypes.c_int64 * len(starts))(*starts)
+        self._starts_arr = arr
         L, st = self._L, _lib.stream_of(self.device)
+        if self.half:
+            if grad_ptrs is not None:   # the 16-bit gradients into the flat buffer (2-B gather)
+                numels, offs = self._arrays16()
+                _lib.check(L.dgc_gather16(grad_ptrs, numels, offs, len(self.names), self.grad_flat.data_ptr(), st),
+                           "dgc_gather16")
+            _lib.check(L.dgc_compensate16(self.grad_flat.data_ptr(), self._mmt_flat.data_ptr(),
+                                          self._vec_flat.data_ptr(), None, self._vec32.data_ptr(), self.flat_numel,
+                                          self.momentum, int(self.nesterov), 1, _lib.VD[self.dtype], st),
+                       "dgc_compensate16")
+            return
         if grad_ptrs is None:
             _lib.check(L.dgc_batch_compress_begin(ctypes.byref(self.desc), self.grad_flat.data_ptr(),
                                                   self._mmt_flat.data_ptr(), self._vec_flat.data_ptr(), arr,
@@ -213,6 +240,16 @@ class DGCBatch:
 
     def select(self):
         """K3 thresholds + selection / adaptation / resample / pack / masking of every tensor."""
+        if self.half:
+            L, st = self._L, _lib.stream_of(self.device)
+            _lib.check(L.dgc_batch_select(ctypes.byref(self.desc), self._vec32.data_ptr(), None, self._starts_arr,
+                                          self.payload.data_ptr(), self.info.data_ptr(), self.ws.data_ptr(),
+                                          self.ws.numel(), _lib.SYNC_DEVICE, st), "dgc_batch_select")
+            _lib.check(L.dgc_mask_packed16(self.payload.data_ptr(), self.capacity, _lib.VD[self.vdtype],
+                                           _lib.ID[self.idtype],
+                                           self._mmt_flat.data_ptr() if self.momentum_masking else None,
+                                           self._vec_flat.data_ptr(), self.flat_numel, st), "dgc_mask_packed16")
+            return
         _lib.check(self._L.dgc_batch_compress_finish(ctypes.byref(self.desc), self._mmt_flat.data_ptr(),
                                                      self._vec_flat.data_ptr(), self.payload.data_ptr(),
                                                      self.info.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
@@ -239,13 +276,20 @@ class DGCBatch:
         step's gathered indices (dgc_decompress_packed_over) instead of the whole
         buffer: identical result, W * capacity slots instead of flat_numel."""
         out = self.out_flat if out_flat is None else out_flat
-        _lib.require_cuda_f32(out, "DGCBatch.decompress")
-        if out.numel() != self.flat_numel or out.device != self.device:
-            raise ValueError(f"DGCBatch.decompress: out_flat must be a contiguous fp32 tensor of {self.flat_numel} "
-                             f"elements on {self.device} (got {out.numel()} on {out.device})")
+        if _lib.require_cuda_float(out, "DGCBatch.decompress") != self.dtype or out.numel() != self.flat_numel \
+                or out.device != self.device:
+            raise ValueError(f"DGCBatch.decompress: out_flat must be a contiguous {self.dtype} tensor of "
+                             f"{self.flat_numel} elements on {self.device} (got {out.dtype} [{out.numel()}] on "
+                             f"{out.device})")
         L = self._L
         st = _lib.stream_of(self.device)
         cur = self.gathered
+        if self.half:   # zero_(), the runs in rank order (each add rounded), the 1/W scale
+            _lib.check(L.dgc_decompress_packed16(cur.data_ptr(), self.world, self.rank_stride, self.capacity,
+                                                 _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
+                                                 _lib.VD[self.dtype], self.flat_numel, 1.0 / self.world,
+                                                 self._bad16.data_ptr(), st), "dgc_decompress_packed16")
+            return out
         args = (self.world, self.rank_stride, self.capacity, _lib.VD[self.vdtype], _lib.ID[self.idtype],
                 out.data_ptr(), self.flat_numel, 1.0 / self.world, self.dec_ws.data_ptr(), self.dec_ws.numel(), st)
         aliased = out.untyped_storage().data_ptr() == self.grad_flat.untyped_storage().data_ptr()

@@ -83,10 +83,13 @@ class BatchedStep:
         self.mem = compression.memory
         self.fill = fill
         self.named = [(n, p) for n, p in named_parameters if p.requires_grad]
-        bad = sorted({str(p.dtype) for _, p in self.named if p.dtype != torch.float32})
-        if bad:   # the engines (dgc_batch_*) are fp32; 16-bit parameters take the per-tensor path
-            raise NotImplementedError(f"DistributedOptimizer(batch=True): fp32 parameters only (got {', '.join(bad)}); "
-                                      "bf16 / fp16 parameters run with batch=False")
+        dts = sorted({str(p.dtype) for _, p in self.named})
+        if len(dts) > 1 or any(p.dtype not in (torch.float32,) + _lib.HALF for _, p in self.named):
+            # one flat layout per step: fp32, or bf16 / fp16 throughout (mixed dtypes: batch=False)
+            raise NotImplementedError(f"DistributedOptimizer(batch=True): the parameters must share one dtype of "
+                                      f"fp32, bf16 or fp16 (got {', '.join(dts)}); mixed dtypes run with batch=False")
+        self.dtype = self.named[0][1].dtype if self.named else torch.float32
+        self.half = self.dtype in _lib.HALF
         self._plan = None
         self.mem._before_read.append(self.flush)
         _lib.glue()   # the host glue must be there (fails loudly, like the library)
@@ -114,7 +117,7 @@ class BatchedStep:
                          compress_upper_bound=c.compress_upper_bound, compress_lower_bound=c.compress_lower_bound,
                          max_adaptation_iters=c.max_adaptation_iters, resample=c.resample,
                          fp16_values=c.fp16_values, int32_indices=c.int32_indices, device=dev,
-                         world_size=comm.size(), deferred_masking=True, fill=self.fill)
+                         world_size=comm.size(), deferred_masking=True, fill=self.fill, dtype=self.dtype)
             for i, n in enumerate(comp_names):
                 numel, _, k, S, ks, stride = c.attributes[n]
                 if (k, S, ks, stride) != tuple(b.attrs[i]):
@@ -140,8 +143,8 @@ class BatchedStep:
             for _, p in dense:
                 offs.append(end)
                 end += -(-p.numel() // 4) * 4   # 16-B aligned views
-            out = torch.zeros(end, dtype=torch.float32, device=dev)
-            mmt = torch.zeros(end, dtype=torch.float32, device=dev)
+            out = torch.zeros(end, dtype=self.dtype, device=dev)
+            mmt = torch.zeros(end, dtype=self.dtype, device=dev)
             for (n, p), o in zip(dense, offs):
                 mv = mmt[o: o + p.numel()].view(p.shape)
                 mv.copy_(mem.momentums[n])
@@ -155,10 +158,12 @@ class BatchedStep:
             plan["dense_ptrs"] = (ctypes.c_void_p * T)()
             plan["dense_numels"] = (ctypes.c_int64 * T)(*[p.numel() for _, p in dense])
             plan["dense_offs"] = (ctypes.c_int64 * T)(*offs)
-            if comm.size() > 1:
+            if comm.size() > 1 and not self.half:
                 plan["dense_wire"] = torch.empty(end, dtype=torch.float16 if c.fp16_values else torch.float32,
                                                  device=dev)
-            plan["zeros"] = torch.zeros(max((p.numel() for _, p in dense), default=1), dtype=torch.float32,
+            if self.half:   # the gathered 16-bit gradients (K1-16's dense branch reads one buffer)
+                plan["dense_in"] = torch.zeros(end, dtype=self.dtype, device=dev)
+            plan["zeros"] = torch.zeros(max((p.numel() for _, p in dense), default=1), dtype=self.dtype,
                                         device=dev)
         self._plan = plan
 
@@ -215,7 +220,7 @@ class BatchedStep:
             ptrs = plan["ptrs"]
             # autograd (and the p.grad setter) keep dtype, device and size those of the
             # parameter: only the layout needs a look (K1 reads 16-B aligned rows)
-            for i in glue.grad_table(plan["comp_params"], ctypes.addressof(ptrs), 16):
+            for i in glue.grad_table(plan["comp_params"], ctypes.addressof(ptrs), 2 if self.half else 16):
                 _, p, _, gflat = plan["comp"][i]
                 if p.grad is None:
                     gflat.zero_()   # no gradient this step: zeros
@@ -229,7 +234,7 @@ class BatchedStep:
         dense_handle = None
         if plan["dense"]:
             dptrs = plan["dense_ptrs"]
-            for i in glue.grad_table(plan["dense_params"], ctypes.addressof(dptrs), 4):
+            for i in glue.grad_table(plan["dense_params"], ctypes.addressof(dptrs), 2 if self.half else 4):
                 g = plan["dense"][i][1].grad
                 if g is None:
                     g = plan["zeros"]
@@ -240,7 +245,9 @@ class BatchedStep:
             wire = plan.get("dense_wire")
             L = _lib.lib()
             st = _lib.stream_of(dev)
-            if wire is not None:   # compress: tensor.type(float16) (dgc/compression.py:175-177)
+            if self.half:
+                dense_handle = self._dense16_exchange(plan, L, st)
+            elif wire is not None:   # compress: tensor.type(float16) (dgc/compression.py:175-177)
                 _lib.check(L.dgc_gather_cast(dptrs, plan["dense_numels"], plan["dense_offs"], len(plan["dense"]),
                                              _lib.ptr(wire), _lib.VD[wire.dtype], st), "dgc_gather_cast")
                 dense_handle = comm.allreduce_async_(wire, op=Average)
@@ -254,7 +261,14 @@ class BatchedStep:
             L = _lib.lib()
             st = _lib.stream_of(dev)
             out, mmt = plan["dense_out"], plan["dense_mmt"]
-            if dense_handle is not None:
+            if self.half:
+                src = plan["dense_in"]
+                if dense_handle is not None:   # decompress: tensor.type(vdtype) (dgc/compression.py:196-197)
+                    src = comm.synchronize(dense_handle).to(self.dtype)
+                _lib.check(L.dgc_compensate16(_lib.ptr(src), _lib.ptr(mmt), None, _lib.ptr(out), None,
+                                              plan["dense_numel"], float(mem.momentum), int(bool(mem.nesterov)), 0,
+                                              _lib.VD[self.dtype], st), "dgc_compensate16")
+            elif dense_handle is not None:
                 red = comm.synchronize(dense_handle)
                 _lib.check(L.dgc_compensate_wire(_lib.ptr(red), _lib.VD[red.dtype], _lib.VD[torch.float32],
                                                  _lib.ptr(mmt), _lib.ptr(out), plan["dense_numel"],
@@ -269,6 +283,22 @@ class BatchedStep:
             # p.grad.set_(compensate(accumulate=False)) (dgc/compression.py:195-198)
             glue.bind_grads(plan["dense_params"], plan["dense_views"])
             plan.pop("keep", None)
+
+    def _dense16_exchange(self, plan, L, st):
+        """16-bit dense tensors: the gradients gathered into one buffer (2-B copies),
+        then compress's wire cast (fp16 for fp16_values, dgc/compression.py:175-177) and
+        the allreduce, or at W = 1 the cast's rounding alone (the allreduce is the
+        identity). Returns the allreduce handle (None at W = 1). Not on a benched path:
+        the casts are ATen's."""
+        dense_in = plan["dense_in"]
+        _lib.check(L.dgc_gather16(plan["dense_ptrs"], plan["dense_numels"], plan["dense_offs"], len(plan["dense"]),
+                                  _lib.ptr(dense_in), st), "dgc_gather16")
+        wire = dense_in.to(torch.float16) if self.comp.fp16_values else dense_in
+        if comm.size() > 1:
+            return comm.allreduce_async_(wire, op=Average)
+        if wire is not dense_in:
+            dense_in.copy_(wire)   # the fp16 round trip of a bf16 gradient
+        return None
 
     def release_grads(self, param_groups):
         """zero_grad(set_to_none=True): every gradient of the wrapped optimizer's params

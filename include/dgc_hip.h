@@ -260,7 +260,11 @@ typedef struct dgc_batch_desc {
                                     /*   zeroing to the next compress's K1 (which    */
                                     /*   streams vec/mmt anyway); dgc_batch_flush    */
                                     /*   applies it before vec/mmt are read elsewhere */
-    int32_t pad;
+    int32_t dtype;                  /* parameter dtype: DGC_F32 (0: dgc_batch_compress*), */
+                                    /*   DGC_BF16 / DGC_F16 (dgc_batch_select over the  */
+                                    /*   dgc_compensate16 image, 16-bit wire values     */
+                                    /*   unless fp16_values, dgc_mask_packed16,         */
+                                    /*   dgc_decompress_packed16)                       */
     int32_t* status_sink;           /* as dgc_select_params.status_sink (NULL: none)   */
 } dgc_batch_desc;
 
@@ -289,6 +293,15 @@ int dgc_batch_compress_begin_ptrs(const dgc_batch_desc* batch, const float* cons
 int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt, float* vec, void* payload,
                               dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
                               void* stream);
+/* The selection of a batch over a flat fp32 buffer that no dgc_batch_compress_begin
+ * produced — a 16-bit batch's velocity image from dgc_compensate16 (vec32 = its
+ * vec32 output over the flat 16-bit buffers): the strided samples, the thresholds and
+ * the selection into the payload, as dgc_batch_compress_finish (no candidate lists).
+ * A 16-bit batch (desc dtype) leaves vec32 untouched (mmt32 may be NULL); mask its
+ * state with dgc_mask_packed16. */
+int dgc_batch_select(const dgc_batch_desc* batch, float* vec32, float* mmt32, const int64_t* sample_starts,
+                     void* payload, dgc_select_info* info_out, void* ws, size_t ws_bytes, int32_t sync_mode,
+                     void* stream);
 /* Pending deferred masking (deferred_masking = 1) applied now; no-op when none is. */
 int dgc_batch_flush(const dgc_batch_desc* batch, float* mmt, float* vec, void* ws, size_t ws_bytes, void* stream);
 
@@ -416,6 +429,19 @@ int dgc_widen16(const void* x, float* y, int64_t n, int32_t dtype, void* stream)
 int dgc_decompress16(const void* values, int32_t vdtype, const void* indices, int32_t idtype,
                      const int64_t* run_offsets, int32_t nruns, void* grad, int32_t dtype, int64_t n, float scale,
                      int32_t* bad_flag, void* stream);
+/* The 16-bit batch (dgc_batch_desc.dtype): DGCSGDMemory.update of the entries of one
+ * packed payload (its device count) on the flat 16-bit state — mmt may be NULL
+ * (momentum_masking off); the decompress of W packed payloads into a flat 16-bit
+ * gradient (zero fill, the runs in rank order with every add rounded, then the 1/W
+ * scale rounded, as dgc_decompress16); and the 2-byte multi-tensor gather of 16-bit
+ * gradients into the flat buffer (srcs / numels / offsets: HOST arrays). */
+int dgc_mask_packed16(const void* payload, int64_t capacity, int32_t vdtype, int32_t idtype, void* mmt, void* vec,
+                      int64_t n, void* stream);
+int dgc_decompress_packed16(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
+                            int32_t vdtype, int32_t idtype, void* grad, int32_t dtype, int64_t n, float scale,
+                            int32_t* bad_flag, void* stream);
+int dgc_gather16(const void* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count, void* dst,
+                 void* stream);
 
 #ifdef __cplusplus
 }

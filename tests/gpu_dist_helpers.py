@@ -418,3 +418,57 @@ def half_worker(rank, world, port, case_name, queue):
         import traceback
         problems.append(("exception", traceback.format_exc()[-600:]))
     queue.put((rank, problems))
+
+
+HALF_SHAPES = [("conv.weight", (64, 3, 7, 7)), ("bn.weight", (64,)), ("bn.bias", (64,)), ("odd.weight", (333, 7)),
+               ("fc.weight", (1000, 512)), ("fc.bias", (1000,))]
+
+
+def _half_run(batch, dtype, fp16, rank, dev, steps=4):
+    from dgc.compression import DGCCompressor
+    from dgc.horovod import DistributedOptimizer
+    from dgc.memory import DGCSGDMemory
+    named = [(n, torch.nn.Parameter(torch.zeros(s, device=dev, dtype=dtype))) for n, s in HALF_SHAPES]
+    with contextlib.redirect_stdout(io.StringIO()):
+        comp = DGCCompressor(0.01, memory=DGCSGDMemory(momentum=0.9), fp16_values=fp16, int32_indices=fp16)
+        comp.memory.initialize(named)
+        comp.initialize([(n, p) for n, p in named if p.dim() > 1])
+    dopt = DistributedOptimizer(torch.optim.SGD([p for _, p in named], lr=0.0), named_parameters=named,
+                                compression=comp, batch=batch)
+    random.seed(5)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    out = []
+    for s in range(steps):
+        for i, (n, p) in enumerate(named):
+            g = torch.randn(p.shape, generator=gen, device=dev) * (1e-3 * (1 + i))
+            if s % 2:   # heavy-tailed: the adaptation loop and the resample run
+                g = g * torch.rand(p.shape, generator=gen, device=dev).pow(8) * 50
+            p.grad = g.to(dtype)
+        for _, hook in reversed(dopt._hook_fns):
+            hook()
+        dopt.synchronize()
+        torch.cuda.synchronize()
+        st = comp.memory.state_dict()
+        out.append({n: p.grad.clone() for n, p in named} | {f"m:{n}": t.clone() for n, t in st["momentums"].items()}
+                   | {f"v:{n}": t.clone() for n, t in st["velocities"].items()})
+        dopt.zero_grad()
+    return out
+
+
+def half_batch_worker(rank, world, port, dtype_name, fp16, q):
+    """W ranks: DistributedOptimizer(batch=True) on bf16 / fp16 parameters (the 16-bit
+    batch engine, one packed allgather, the 16-bit decompress and dense allreduce) equals
+    the per-tensor path (pinned to the reference's 16-bit fixtures) bit for bit."""
+    _init(rank, world, port)
+    dev = torch.device("cuda:0")
+    dtype = getattr(torch, dtype_name)
+    want = _half_run(False, dtype, fp16, rank, dev)
+    got = _half_run(True, dtype, fp16, rank, dev)
+    problems = []
+    for s, (w, g) in enumerate(zip(want, got)):
+        for k in w:
+            if not torch.equal(w[k].view(torch.int16), g[k].view(torch.int16)):
+                problems.append((s, k))
+    q.put((rank, problems))
+    import torch.distributed as dist
+    dist.destroy_process_group()

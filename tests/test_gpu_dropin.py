@@ -25,12 +25,12 @@ SHAPES = [("conv.weight", (64, 3, 7, 7)), ("bn.weight", (64,)), ("bn.bias", (64,
           ("big.weight", (512, 512, 3, 3)), ("late.weight", (16, 16))]
 
 
-def _run(batch, fp16, modes, monkeypatch):
+def _run(batch, fp16, modes, monkeypatch, dtype=torch.float32):
     from dgc.compression import DGCCompressor
     from dgc.horovod import DistributedOptimizer
     from dgc.memory import DGCSGDMemory
     monkeypatch.setenv("HOROVOD_ELASTIC", "1")
-    named = [(n, torch.nn.Parameter(torch.zeros(s, device=DEV))) for n, s in SHAPES]
+    named = [(n, torch.nn.Parameter(torch.zeros(s, device=DEV, dtype=dtype))) for n, s in SHAPES]
     comp = DGCCompressor(0.01, memory=DGCSGDMemory(momentum=0.9, nesterov=True), fp16_values=fp16,
                          int32_indices=fp16)
     comp.memory.initialize(named)
@@ -47,10 +47,11 @@ def _run(batch, fp16, modes, monkeypatch):
             g = torch.randn(p.shape, generator=gen, device=DEV) * (1e-3 * (1 + i))
             if step % 2:   # a heavy-tailed step: the adaptation loop and the resample run
                 g = g * torch.rand(p.shape, generator=gen, device=DEV).pow(8) * 50
+            g = g.to(dtype)
             if mode == "inplace" and p.grad is not None:
                 p.grad.add_(g)          # zero_grad(set_to_none=False) then backward's accumulation
             elif mode == "unaligned" and n in ("fc.weight", "bn.bias"):
-                buf = torch.empty(p.numel() + 1, device=DEV)
+                buf = torch.empty(p.numel() + 1, device=DEV, dtype=dtype)
                 buf[1:].copy_(g.view(-1))
                 p.grad = buf[1:].view(p.shape)   # 4-B aligned only
             else:
@@ -70,18 +71,23 @@ def _run(batch, fp16, modes, monkeypatch):
 
 
 def _bits(t):
-    return t.contiguous().view(torch.int32)
+    return t.contiguous().view(torch.int32 if t.element_size() == 4 else torch.int16)
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fp16", [False, True], ids=["fp32-int64", "fp16-int32"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["fp32", "bf16", "f16"])
+@pytest.mark.parametrize("fp16", [False, True], ids=["wire-dtype-int64", "wire-fp16-int32"])
 @pytest.mark.parametrize("batch", [True, "sparse"], ids=["batch", "batch-sparse"])
-def test_batched_optimizer_equals_per_tensor(batch, fp16, monkeypatch):
+def test_batched_optimizer_equals_per_tensor(batch, fp16, dtype, monkeypatch):
+    """16-bit parameters (bf16 / fp16) run the batch's 16-bit engine (K1-16, the
+    selection on the velocity's fp32 image, the 16-bit masking and decompress; "sparse"
+    falls back to the dense zero_() there); the per-tensor path they are compared with is
+    pinned to the reference's own 16-bit fixtures (test_gpu_half.py)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     modes = ["fresh", "fresh", "inplace", "inplace", "unaligned", "fresh", "fresh"]
-    want = _run(False, fp16, modes, monkeypatch)
-    got = _run(batch, fp16, modes, monkeypatch)
+    want = _run(False, fp16, modes, monkeypatch, dtype)
+    got = _run(batch, fp16, modes, monkeypatch, dtype)
     for step, (w, g) in enumerate(zip(want, got)):
         assert w.keys() == g.keys()
         for k in w:

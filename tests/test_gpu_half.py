@@ -123,14 +123,58 @@ def test_half_dense_branch_and_state_dict(L):
             assert sd["momentums"]["b"].dtype == dt
 
 
-def test_half_batch_mode_refuses(L):
+def test_half_batch_mixed_dtypes_refuse(L):
     import torch.nn as nn
     from dgc.compression import DGCCompressor
     from dgc.memory import DGCSGDMemory
     from dgc.horovod.optimizer import DistributedOptimizer
-    model = nn.Linear(64, 64).to(DEV).to(torch.bfloat16)
+    model = nn.Sequential(nn.Linear(64, 64), nn.Linear(64, 64).to(torch.bfloat16)).to(DEV)
     mem = DGCSGDMemory(momentum=0.9)
     comp = quiet(DGCCompressor, 0.01, memory=mem)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
-    with pytest.raises(NotImplementedError, match="fp32 parameters only"):
+    with pytest.raises(NotImplementedError, match="share one dtype"):
         DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp, batch=True)
+
+
+def test_half_batch_against_reference_goldens(L, golden_half):
+    """DGCBatch on a 16-bit tensor (the engine of DistributedOptimizer(batch=True) on
+    bf16 / fp16 parameters): K1-16 over the flat 16-bit buffers, the selection on the
+    fp32 image (dgc_batch_select), the 16-bit masking from the payload and the packed
+    16-bit decompress, one DGCBatch per rank — against the reference's own fixtures, every
+    case and step, W = 1 to 4: indices in order, values, 16-bit state, dense output."""
+    from dgc.batch import DGCBatch
+    meta, arrays = golden_half
+    for name, case in meta.items():
+        dt = getattr(torch, case["dtype"])
+        N, W = case["N"], case["W"]
+        bs = [DGCBatch([("w", (N,))], compress_ratio=case["ratio"], momentum=0.9, nesterov=case["nesterov"],
+                       momentum_masking=case["masking"], resample=case["resample"], fp16_values=case["fp16"],
+                       int32_indices=case["int32"], device=DEV, world_size=W, dtype=dt) for _ in range(W)]
+        assert tuple(bs[0].attrs[0]) == tuple(case["attrs"][1:]), name
+        stride = bs[0].attrs[0][3]
+        random.seed(42)
+        for s, step in enumerate(case["per_step"]):
+            rstate = random.getstate()
+            for q, rk in enumerate(step["ranks"]):
+                random.setstate(rstate)
+                start = random.randint(0, stride - 1) if N != bs[q].attrs[0][1] else 0
+                g = torch.from_numpy(synth.gradient(rk["seed"], N, case["kind"], case["scale"]).copy()).to(dt)
+                bs[q].grad("w").copy_(g.to(DEV))
+                bs[q].compress([start])
+                key = f"{name}/s{s}/r{q}"
+                vals, idx = bs[q].transmitted()["w"]
+                assert vals.dtype == getattr(torch, rk["values_dtype"].split(".")[1]), key
+                assert np.array_equal(idx.cpu().numpy(), arrays[key + "/indices"]), key
+                assert np.array_equal(bits(vals.float().cpu().numpy()), bits(arrays[key + "/values"])), key
+                assert synth.digest(bs[q].momentum_of("w").float().cpu().numpy()) == rk["mmt_sha"], key
+                assert synth.digest(bs[q].velocity_of("w").float().cpu().numpy()) == rk["vec_sha"], key
+            gathered = torch.cat([b.payload for b in bs])   # the allgather: rank order
+            b0 = bs[0]
+            b0._gathers = [gathered] * len(b0._gathers) if W > 1 else b0._gathers
+            out = b0.decompress().view(-1)[:N]
+            assert out.dtype == dt
+            got = out.float().cpu().numpy()
+            want = np.zeros(N, np.float32)
+            want[arrays[f"{name}/s{s}/dec_nz_idx"]] = arrays[f"{name}/s{s}/dec_nz_val"]
+            assert np.array_equal(bits(got), bits(want)), (name, s)
+            assert synth.digest(got) == step["dense_sha"], (name, s)

@@ -113,3 +113,15 @@ def test_half_w2_communicate_matches_reference(case):
     out = run(G.half_worker, 2, case)
     for rank, problems in out.items():
         assert problems == [], (rank, problems)
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("fp16", [False, True], ids=["wire-dtype", "wire-fp16"])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_half_batched_optimizer_w2_equals_per_tensor(dtype, fp16):
+    """bf16 / fp16 parameters through DistributedOptimizer(batch=True) at W = 2 (two
+    processes on one MI355X over gloo): the per-tensor path's gradients and 16-bit state
+    (that path is pinned to the reference's 16-bit fixtures) bit for bit, 4 steps."""
+    out = run(G.half_batch_worker, 2, dtype, fp16)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)
