@@ -322,7 +322,10 @@ __device__ __forceinline__ void st_nt(float4* p, const float4& v) {
 // store keeps its line dirty in L2, and the kernel boundary then writes the XCD L2s
 // back before the next kernel starts: + dirty bytes / ~6 TB/s (MI355X_MICROARCH.md,
 // "boundary"), ~5 us of idle GPU after K1 (8 x 4 MB of L2 full of dirty lines).
-// DGC_STREAM_STORE (A/B builds): 0 nt, 1 sc1 (default), 2 sc1 nt.
+// DGC_STREAM_STORE (A/B builds): 0 nt, 1 sc1 (default), 2 sc1 nt. The asm store ends
+// with s_nop 1: hipcc does not pad an asm statement, and its next instruction could
+// otherwise overwrite the data registers before the store has read them
+// (cdna_hip_programming.md §5.7 item 1).
 #ifndef DGC_STREAM_STORE
 #define DGC_STREAM_STORE 1
 #endif
@@ -332,9 +335,9 @@ __device__ __forceinline__ void st_stream(float4* p, const float4& v) {
 #else
     const f4v x = {v.x, v.y, v.z, v.w};
 #if DGC_STREAM_STORE == 1
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(x) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
 #else
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" : : "v"(p), "v"(x) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
 #endif
 #endif
 }

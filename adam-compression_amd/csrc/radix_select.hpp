@@ -41,7 +41,9 @@ struct RSState {
     uint64_t nan_count;
     uint32_t tickets[4];
     uint32_t win_n;                    // > 0: the passes read the K1 sample window list of
-    uint32_t win_pad;                  // win_n keys instead of the samples (select.hip)
+                                       // win_n keys instead of the samples (select.hip)
+    uint32_t small_done;               // select.hip: a window of <= kSmallN keys was selected
+                                       // in one workgroup; the passes skip the task
     unsigned long long hist[3][kRsBins];
 };
 

@@ -193,6 +193,7 @@ struct Layout {
     int64_t nseg = 0, ngrp = 0, nsamp = 0, ncand = 0, ngpos = 0;
     int64_t max_cand = 0;       // the largest K5 candidate capacity of a tensor
     int32_t nsmall = 0;
+    int32_t nwins = 0;          // tensors with a K1 sample window (their ids follow the small ones)
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool tail_any = false;      // some tensor is compensated partly outside K1 (unpadded tail)
     int64_t grid[BT_COUNT] = {};
@@ -277,6 +278,10 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
     L.ncand = cand;
     L.ngpos = gpos;
     L.nsmall = (int32_t)small.size();
+    // the windowed tensors after the small ones: k_rs_small_multi tries their windows
+    for (int32_t t = 0; t < T; ++t)
+        if (td[t].win_cap > 0 && !td[t].tail) small.push_back(t);
+    L.nwins = (int32_t)small.size() - L.nsmall;
     for (int which = 0; which < BT_COUNT; ++which) {
         bt[which].assign(T + 1, 0);
         int64_t acc = 0;
@@ -883,7 +888,10 @@ struct SampleKeys {
         const uint32_t wn = w.rs[t].win_n;
         return wn ? min(all, (int)((wn + 4095u) / 4096u)) : all;
     }
-    __device__ __forceinline__ bool active(int) const { return true; }
+    // a windowed task whose window k_rs_small_multi selected in one workgroup is done
+    __device__ __forceinline__ bool active(int t) const {
+        return !(w.td[t].win_cap > 0 && !w.td[t].tail && w.rs[t].small_done);
+    }
     __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
     __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
     // the final pass's last workgroup: the threshold is known, reset the selection state
@@ -916,6 +924,7 @@ __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w, int64_t ks
     const int t = blockIdx.x;
     if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    if (d.win_cap > 0 && !d.tail && w.rs[t].small_done) return;   // k_rs_small_multi selected its window
     const int64_t ks = ks_of(d, t, ks1);
     RSState* rs = w.rs + t;
     rs_reset(rs, (uint64_t)ks);
@@ -927,12 +936,32 @@ __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w, int64_t ks
 }
 
 // One workgroup per small tensor: all three passes from LDS, then the tensor's
-// selection state reset (sel_init_tensor).
-__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat, int64_t ks1) {
+// selection state reset (sel_init_tensor). Workgroups nsmall.. take the windowed
+// tensors (K1 appended every sample >= the list threshold to a window list): a
+// complete window of ks..kSmallN keys is selected the same way, in ONE workgroup, and
+// the multi-workgroup passes skip the tensor (small_done) — the ks-th largest sample is
+// the ks-th largest of its window (SampleKeys); for VGG-16-BN's big tensors ~3 ks keys,
+// where the passes were four launches. A window that does not qualify is left to them.
+__global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat, int64_t ks1,
+                                                                 int32_t nsmall) {
     const int t = w.small[blockIdx.x];
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const uint64_t ks = (uint64_t)ks_of(d, t, ks1);
+    if ((int32_t)blockIdx.x >= nsmall) {
+        const SelState* st = w.st + t;
+        const uint32_t cnt = st->win_cnt[st->epoch & 1];
+        const bool take = cnt >= ks && cnt <= (uint64_t)d.win_cap && cnt <= (uint32_t)kSmallN;
+        if (threadIdx.x == 0) {
+            w.rs[t].small_done = take ? 1u : 0u;
+            w.rs[t].win_n = take ? cnt : 0u;   // the record's window_keys (sel_init_tensor)
+        }
+        if (!take) return;   // uniform
+        rs_small_wg(w.samples + d.win_off, cnt, ks, w.thr + t);
+        sel_init_tensor(w, t, 1);
+        return;
+    }
     const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
-    rs_small_wg(x, w.scnt[t], (uint64_t)ks_of(d, t, ks1), w.thr + t);
+    rs_small_wg(x, w.scnt[t], ks, w.thr + t);
     sel_init_tensor(w, t, 1);
 }
 
@@ -2618,8 +2647,9 @@ int kth_largest(const float* x, int64_t n, int64_t k, float* out, void* ws, size
 // K3 of every tensor of the call: the small ones in one workgroup each, the rest in
 // three multi-block passes.
 static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStream_t s, int64_t ks1 = 0) {
-    if (L.nsmall) {
-        hipLaunchKernelGGL(k_rs_small_multi, dim3((unsigned)L.nsmall), dim3(kScanThreads), 0, s, w, vec, ks1);
+    if (L.nsmall + L.nwins) {
+        hipLaunchKernelGGL(k_rs_small_multi, dim3((unsigned)(L.nsmall + L.nwins)), dim3(kScanThreads), 0, s, w, vec,
+                           ks1, L.nsmall);
         DGC_LAUNCHED();
     }
     if (L.grid[BT_SAMP] > 0) {
@@ -2818,8 +2848,9 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
     DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
     for (int which = 0; which < BT_COUNT; ++which)
         DGC_HIP(hipMemcpyAsync(w.bt[which], bt[which].data(), sizeof(int32_t) * (L.T + 1), hipMemcpyHostToDevice, s));
-    if (L.nsmall)
-        DGC_HIP(hipMemcpyAsync(w.small, small.data(), sizeof(int32_t) * L.nsmall, hipMemcpyHostToDevice, s));
+    if (L.nsmall + L.nwins)
+        DGC_HIP(hipMemcpyAsync(w.small, small.data(), sizeof(int32_t) * (L.nsmall + L.nwins), hipMemcpyHostToDevice,
+                               s));
     hipLaunchKernelGGL(k_spec_reset, dim3(1), dim3(256), 0, s, w.spec, L.T);
     DGC_LAUNCHED();
     // the host tables are pageable and local: let the copies finish first
