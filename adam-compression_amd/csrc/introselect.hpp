@@ -248,6 +248,9 @@ struct PlainSlotsT {
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return l[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return r[t]; }
     __device__ __forceinline__ bool fast(uint32_t) const { return true; }
+    __device__ __forceinline__ bool gfast(uint32_t) const { return false; }
+    __device__ __forceinline__ void gl_(bool, uint32_t, uint32_t) const {}
+    __device__ __forceinline__ void gr_(bool, uint32_t, uint32_t) const {}
     __device__ __forceinline__ void fl(bool on, uint32_t t, uint32_t v) const {
         *(on ? l + t : d + (threadIdx.x & 63)) = v;
     }
@@ -281,6 +284,15 @@ struct SplitSlots {
     __device__ __forceinline__ uint32_t get_l(uint32_t t) const { return t < cap ? ll[t] : gl[t]; }
     __device__ __forceinline__ uint32_t get_r(uint32_t t) const { return t < cap ? lr[t] : gr[t]; }
     __device__ __forceinline__ bool fast(uint32_t end) const { return end <= cap; }
+    // every slot from `begin` on is a global one: exec-masked global stores, no LDS / global
+    // choice per element
+    __device__ __forceinline__ bool gfast(uint32_t begin) const { return begin >= cap; }
+    __device__ __forceinline__ void gl_(bool on, uint32_t t, uint32_t v) const {
+        if (on) gl[t] = v;
+    }
+    __device__ __forceinline__ void gr_(bool on, uint32_t t, uint32_t v) const {
+        if (on) gr[t] = v;
+    }
     __device__ __forceinline__ void fl(bool on, uint32_t t, uint32_t v) const {
         *(on ? ll + t : d + (threadIdx.x & 63)) = v;
     }
@@ -549,6 +561,9 @@ __device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t
                     if (sl.fast(runl + tl)) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) sl.fl((pl >> j) & 1u, r0 + __popc(pl & below[j]), rel0 + (uint32_t)j);
+                    } else if (sl.gfast(runl)) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) sl.gl_((pl >> j) & 1u, r0 + __popc(pl & below[j]), rel0 + (uint32_t)j);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
@@ -565,6 +580,10 @@ __device__ void nth_step_wg(QP q, const Slots& sl, NthShared& sh, MP mk, int64_t
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
                             sl.fr((pr >> j) & 1u, TR - 1u - r0 - __popc(pr & below[j]), rel0 + (uint32_t)j);
+                    } else if (sl.gfast((uint32_t)(from - tr))) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            sl.gr_((pr >> j) & 1u, TR - 1u - r0 - __popc(pr & below[j]), rel0 + (uint32_t)j);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
