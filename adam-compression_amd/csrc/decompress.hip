@@ -88,7 +88,10 @@ __device__ __forceinline__ long long load_idx(const void* p, long long e) {
 
 // Where the runs come from: a table in the workspace (concatenated input), or the
 // packed allgather buffer itself (rank r's header holds its count) — the latter
-// needs no setup launch.
+// needs no setup launch. A split exchange (dgc_payload_split) gathers each rank's
+// payload as `parts` part buffers, part-major (part p of rank r at p * pstride +
+// r * stride): run q = r * parts + p, so the runs stay in rank order (an index is in
+// at most one part of a rank); parts >= `ready` have not landed yet and are empty.
 struct RunSrc {
     const Run* table;
     const int32_t* nruns_dev;
@@ -97,17 +100,34 @@ struct RunSrc {
     int32_t world;
     const int32_t* unsorted;      // regrouped runs (null: none): read them from `sorted`
     const Run* sorted;
-    __device__ __forceinline__ int count() const { return payload ? world : *nruns_dev; }
+    int32_t parts = 1, ready = 1;
+    int64_t pstride = 0;
+    __host__ __device__ __forceinline__ int count() const { return payload ? world * parts : *nruns_dev; }
     __device__ __forceinline__ Run get(int r) const {
         if (unsorted && unsorted[r]) return sorted[r];
         return get_raw(r);
     }
-    __device__ __forceinline__ Run get_raw(int r) const {
-        if (!payload) return table[r];
-        const char* base = payload + (int64_t)r * stride;
+    __device__ __forceinline__ const char* base_of(int q) const {
+        const int r = q / parts, p = q - r * parts;
+        return payload + (int64_t)p * pstride + (int64_t)r * stride;
+    }
+    __device__ __forceinline__ Run get_raw(int q) const {
+        if (!payload) return table[q];
+        const char* base = base_of(q);
+        if (parts > 1 && q % parts >= ready) return Run{base + voff, base + ioff, 0};
         long long c = *reinterpret_cast<const long long*>(base);
         c = c < 0 ? 0 : (c > capacity ? capacity : c);
         return Run{base + voff, base + ioff, c};
+    }
+    // split exchange: min over ranks of the smallest index in the parts after part p
+    // (header word 1, dgc_payload_split); every index below it has landed with parts <= p
+    __device__ __forceinline__ long long landed_below(int p) const {
+        long long m = LLONG_MAX;
+        for (int r = 0; r < world; ++r) {
+            const long long b = reinterpret_cast<const long long*>(base_of(r * parts + p))[1];
+            m = b < m ? b : m;
+        }
+        return m;
     }
 };
 
@@ -179,8 +199,8 @@ __device__ __forceinline__ long long chunk_rank(long long v, int64_t n, int64_t 
 
 template <int ID>
 __global__ void __launch_bounds__(kBlock)
-k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap) {
-    const int r = blockIdx.y;
+k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap, int ystep, int yoff) {
+    const int r = (int)blockIdx.y * ystep + yoff;   // the run (a split exchange: one part's runs)
     const int64_t stride = w.nchunks + 1;
     if (r >= rs.count()) return;   // uniform per workgroup
     const Run run = rs.get_raw(r);
@@ -194,6 +214,7 @@ k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap) {
             const long long ic = e < run.count ? load_idx<ID>(run.idx, e) : 0;
             lo = e > 0 ? chunk_rank(ip, n, w.nchunks) : 0;
             hi = e < run.count ? chunk_rank(ic, n, w.nchunks) : stride;
+            if (e < run.count && (ic < 0 || ic >= n)) atomicOr(w.status, 1);
             if (e > 0 && e < run.count && ic < ip) {
                 atomicOr(w.status, 2);
                 if (w.sort_cap) atomicOr(&w.unsorted[r], 1);
@@ -234,8 +255,8 @@ __device__ __forceinline__ void chunk_range(const long long* bnd, int64_t c, lon
 constexpr int kRegroupThreads = 1024;
 
 template <int VD, int ID>
-__global__ void __launch_bounds__(kRegroupThreads) k_regroup(DecWS w, RunSrc rs, int64_t n) {
-    const int r = blockIdx.x;
+__global__ void __launch_bounds__(kRegroupThreads) k_regroup(DecWS w, RunSrc rs, int64_t n, int ystep, int yoff) {
+    const int r = (int)blockIdx.x * ystep + yoff;
     if (r >= rs.count() || !w.unsorted[r]) return;   // uniform per workgroup
     const Run run = rs.get_raw(r);
     const int64_t stride = w.nchunks + 1;
@@ -429,150 +450,162 @@ k_scatter_waves(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float s
     __shared__ uint32_t dup_bits[kSegWaves][kChunk / 32];
     __shared__ uint32_t gran_cnt[kSegWaves][kGranules];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t sc0 = (xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv) * kSCB;
     uint32_t* bits = dup_bits[wv];
     uint32_t* gcnt = gran_cnt[wv];
     for (int q = lane; q < kChunk / 32; q += 64) bits[q] = 0;
     for (int q = lane; q < kGranules; q += 64) gcnt[q] = 0;
-    if (sc0 * m >= w.nchunks) return;
     const int nr = rs.count();
     const int64_t stride = w.nchunks + 1;
-    // run bounds at the kSCB + 1 super-chunk edges, lanes < nr (one run each)
-    long long bb[kSCB + 1];
-    uintptr_t rv = 0, ri = 0;
-    if (lane < nr) {
-        const Run run = rs.get(lane);
-        rv = reinterpret_cast<uintptr_t>(run.vals);
-        ri = reinterpret_cast<uintptr_t>(run.idx);
-        const long long* bnd = w.bnd + (int64_t)lane * stride;
-#pragma unroll
-        for (int j = 0; j <= kSCB; ++j) {
-            const int64_t c = (sc0 + j) * m < w.nchunks ? (sc0 + j) * m : w.nchunks;
-            bb[j] = bnd[c];
-        }
-        long long prev = 0;
-#pragma unroll
-        for (int j = 0; j <= kSCB; ++j) {   // clamp: stale bounds of an unsorted run stay in range
-            bb[j] = bb[j] < prev ? prev : (bb[j] > run.count ? run.count : bb[j]);
-            prev = bb[j];
-        }
-        // entries below 0 or at/after n are in no chunk: flag them once
-        if (sc0 == 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);
-    } else {
-#pragma unroll
-        for (int j = 0; j <= kSCB; ++j) bb[j] = 0;
+    // the super-chunks [lo, hi) of this call: all of them, or — one phase of a split
+    // exchange, parts < ready landed — those every index of which has landed and that
+    // no earlier phase took (landed_below is non-decreasing in the part)
+    const int64_t nsc = ceil_div(w.nchunks, (int64_t)m), span = (int64_t)m * kChunk;
+    int64_t lo = 0, hi = nsc;
+    if (rs.parts > 1) {
+        const int p = rs.ready - 1;
+        if (p > 0) lo = rs.landed_below(p - 1) / span;
+        if (p < rs.parts - 1) hi = rs.landed_below(p) / span;
+        lo = lo < 0 ? 0 : (lo > nsc ? nsc : lo);
+        hi = hi < lo ? lo : (hi > nsc ? nsc : hi);
     }
-    // Lane l takes entry l of each super-chunk: its run r = #{q : roff[q+1] <= l},
-    // found with scalar run offsets (readlane) — no cross-lane shuffles.
-    int T[kSCB], off[kSCB];
-    float v[kSCB];
+    const int64_t nwaves = (int64_t)gridDim.x * kSegWaves;
+    for (int64_t sc0 = lo + (xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv) * kSCB; sc0 < hi;
+         sc0 += nwaves * kSCB) {
+        // run bounds at the kSCB + 1 super-chunk edges, lanes < nr (one run each)
+        long long bb[kSCB + 1];
+        uintptr_t rv = 0, ri = 0;
+        if (lane < nr) {
+            const Run run = rs.get(lane);
+            rv = reinterpret_cast<uintptr_t>(run.vals);
+            ri = reinterpret_cast<uintptr_t>(run.idx);
+            const long long* bnd = w.bnd + (int64_t)lane * stride;
 #pragma unroll
-    for (int j = 0; j < kSCB; ++j) {
-        const long long c64 = bb[j + 1] - bb[j];
-        const int cnt = c64 > 65 ? 65 : (int)c64;   // > 64 entries overflow anyway
-        int roff = 0, r = 0, first = 0;
-        long long e0 = 0;
-        uintptr_t pv = 0, pi = 0;
-        for (int q = 0; q < nr; ++q) {   // uniform loop, scalar bookkeeping
-            const int cq = __builtin_amdgcn_readlane(cnt, q);
-            if (lane >= roff) {
-                r = q;
-                first = roff;
+            for (int j = 0; j <= kSCB; ++j) {
+                const int64_t c = (sc0 + j) * m < w.nchunks ? (sc0 + j) * m : w.nchunks;
+                bb[j] = bnd[c];
             }
-            roff += cq;
-        }
-        T[j] = roff;
-        for (int q = 0; q < nr; ++q) {
-            const long long bq = ((long long)__builtin_amdgcn_readlane((int)(bb[j] >> 32), q) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)bb[j], q);
-            const uintptr_t vq = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(rv >> 32), q) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)rv, q);
-            const uintptr_t iq = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(ri >> 32), q) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)ri, q);
-            if (r == q) {
-                e0 = bq;
-                pv = vq;
-                pi = iq;
-            }
-        }
-        off[j] = -1;
-        v[j] = 0.f;
-        if (T[j] <= 64 && lane < T[j]) {
-            const long long e = e0 + (lane - first);
-            v[j] = load_val<VD>(reinterpret_cast<const void*>(pv), e);
-            const long long i = load_idx<ID>(reinterpret_cast<const void*>(pi), e);
-            const long long lo_i = (sc0 + j) * m * (long long)kChunk;
-            const long long hi_i = (sc0 + j + 1) * m < w.nchunks ? (sc0 + j + 1) * m * (long long)kChunk : n;
-            if (i >= lo_i && i < hi_i)
-                off[j] = (int)(i - lo_i);
-            else
-                atomicOr(w.status, 2);   // only an unsorted run lands outside its chunks
-        }
-    }
+            long long prev = 0;
 #pragma unroll
-    for (int j = 0; j < kSCB; ++j) {
-        if ((sc0 + j) * m >= w.nchunks || T[j] == 0) continue;   // uniform
-        if (T[j] > 64) {
-            if (lane == 0) w.ovf_list[atomicAdd(w.ovf_cnt, 1)] = (int32_t)(sc0 + j);
-            continue;
-        }
-        // an index in two runs (rare: ~W*ratio per entry) sets a bit another lane set
-        bool dup = false;
-        if (off[j] >= 0) {
-            const uint32_t bit = 1u << (off[j] & 31);
-            dup = (atomicOr(&bits[(off[j] & (kChunk - 1)) >> 5], bit) & bit) != 0;
-        }
-        const bool any_dup = __ballot(dup) != 0;
-        if (off[j] >= 0) bits[(off[j] & (kChunk - 1)) >> 5] = 0;   // clean for the next super-chunk
-        bool head = off[j] >= 0;
-        float a = v[j];
-        if (any_dup) {   // slow path: the first occurrence sums all of them in lane order
-            a = 0.f;
-            for (int q = 0; q < T[j]; ++q) {
-                const int oq = __shfl(off[j], q);
-                const float vq = __shfl(v[j], q);
-                if (head && oq == off[j]) {
-                    if (q < lane)
-                        head = false;
-                    else
-                        a = __fadd_rn(a, vq);
-                }
+            for (int j = 0; j <= kSCB; ++j) {   // clamp: stale bounds of an unsorted run stay in range
+                bb[j] = bb[j] < prev ? prev : (bb[j] > run.count ? run.count : bb[j]);
+                prev = bb[j];
             }
         } else {
-            a = __fadd_rn(0.f, a);   // index_put_ onto +0.0 (-0.0 -> +0.0)
-        }
-        // gran: an entry alone in its 64-B granule writes the whole granule (its value,
-        // +0.0 around it — what the granule holds after the zero fill / re-zero):
-        // full-granule stores instead of 4-B partial writes, 1.7x the line rate at 8M
-        // lines (tools/scatterbench.hip). Shared granules (counted in LDS, mod kGranules,
-        // so a false share only costs the fast path) keep the word store.
-        // the granule must lie inside this super-chunk (which only this wave writes) and
-        // inside grad: with an unaligned grad, granules straddle chunk edges
-        const long long c_lo = (sc0 + j) * m * (long long)kChunk;
-        const long long c_hi = (sc0 + j + 1) * m * (long long)kChunk < n ? (sc0 + j + 1) * m * (long long)kChunk : n;
-        float* dst = grad + c_lo + off[j];
-        const uintptr_t g = reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)63;
-        const uint32_t gslot = (uint32_t)(g >> 6) & (kGranules - 1);
-        if (gran && head) atomicAdd(&gcnt[gslot], 1u);
-        if (gran) wave_sync_lds();
-        const bool alone = gran && head && gcnt[gslot] == 1 && g >= reinterpret_cast<uintptr_t>(grad + c_lo) &&
-                           g + 64 <= reinterpret_cast<uintptr_t>(grad + c_hi);
-        const float val = scale != 1.0f ? __fmul_rn(a, scale) : a;
-        if (alone) {
-            const int pos = (int)((reinterpret_cast<uintptr_t>(dst) - g) >> 2);
-            DGC_GLB f4v* g4 = (DGC_GLB f4v*)g;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                f4v v = {0.f, 0.f, 0.f, 0.f};
-                if (pos >> 2 == q) v[pos & 3] = val;
-                g4[q] = v;
-            }
-        } else if (head) {
-            *dst = val;
+            for (int j = 0; j <= kSCB; ++j) bb[j] = 0;
         }
-        if (gran) {
-            wave_sync_lds();
-            if (head) gcnt[gslot] = 0;   // clean for the next super-chunk
+        // Lane l takes entry l of each super-chunk: its run r = #{q : roff[q+1] <= l},
+        // found with scalar run offsets (readlane) — no cross-lane shuffles.
+        int T[kSCB], off[kSCB];
+        float v[kSCB];
+#pragma unroll
+        for (int j = 0; j < kSCB; ++j) {
+            const long long c64 = bb[j + 1] - bb[j];
+            const int cnt = c64 > 65 ? 65 : (int)c64;   // > 64 entries overflow anyway
+            int roff = 0, r = 0, first = 0;
+            long long e0 = 0;
+            uintptr_t pv = 0, pi = 0;
+            for (int q = 0; q < nr; ++q) {   // uniform loop, scalar bookkeeping
+                const int cq = __builtin_amdgcn_readlane(cnt, q);
+                if (lane >= roff) {
+                    r = q;
+                    first = roff;
+                }
+                roff += cq;
+            }
+            T[j] = roff;
+            for (int q = 0; q < nr; ++q) {
+                const long long bq = ((long long)__builtin_amdgcn_readlane((int)(bb[j] >> 32), q) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)bb[j], q);
+                const uintptr_t vq = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(rv >> 32), q) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)rv, q);
+                const uintptr_t iq = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(ri >> 32), q) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)ri, q);
+                if (r == q) {
+                    e0 = bq;
+                    pv = vq;
+                    pi = iq;
+                }
+            }
+            off[j] = -1;
+            v[j] = 0.f;
+            if (T[j] <= 64 && lane < T[j]) {
+                const long long e = e0 + (lane - first);
+                v[j] = load_val<VD>(reinterpret_cast<const void*>(pv), e);
+                const long long i = load_idx<ID>(reinterpret_cast<const void*>(pi), e);
+                const long long lo_i = (sc0 + j) * m * (long long)kChunk;
+                const long long hi_i = (sc0 + j + 1) * m < w.nchunks ? (sc0 + j + 1) * m * (long long)kChunk : n;
+                if (i >= lo_i && i < hi_i)
+                    off[j] = (int)(i - lo_i);
+                else
+                    atomicOr(w.status, 2);   // only an unsorted run lands outside its chunks
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kSCB; ++j) {
+            if (sc0 + j >= hi || T[j] == 0) continue;   // uniform
+            if (T[j] > 64) {
+                if (lane == 0) w.ovf_list[atomicAdd(w.ovf_cnt, 1)] = (int32_t)(sc0 + j);
+                continue;
+            }
+            // an index in two runs (rare: ~W*ratio per entry) sets a bit another lane set
+            bool dup = false;
+            if (off[j] >= 0) {
+                const uint32_t bit = 1u << (off[j] & 31);
+                dup = (atomicOr(&bits[(off[j] & (kChunk - 1)) >> 5], bit) & bit) != 0;
+            }
+            const bool any_dup = __ballot(dup) != 0;
+            if (off[j] >= 0) bits[(off[j] & (kChunk - 1)) >> 5] = 0;   // clean for the next super-chunk
+            bool head = off[j] >= 0;
+            float a = v[j];
+            if (any_dup) {   // slow path: the first occurrence sums all of them in lane order
+                a = 0.f;
+                for (int q = 0; q < T[j]; ++q) {
+                    const int oq = __shfl(off[j], q);
+                    const float vq = __shfl(v[j], q);
+                    if (head && oq == off[j]) {
+                        if (q < lane)
+                            head = false;
+                        else
+                            a = __fadd_rn(a, vq);
+                    }
+                }
+            } else {
+                a = __fadd_rn(0.f, a);   // index_put_ onto +0.0 (-0.0 -> +0.0)
+            }
+            // gran: an entry alone in its 64-B granule writes the whole granule (its value,
+            // +0.0 around it — what the granule holds after the zero fill / re-zero):
+            // full-granule stores instead of 4-B partial writes, 1.7x the line rate at 8M
+            // lines (tools/scatterbench.hip). Shared granules (counted in LDS, mod kGranules,
+            // so a false share only costs the fast path) keep the word store.
+            // the granule must lie inside this super-chunk (which only this wave writes) and
+            // inside grad: with an unaligned grad, granules straddle chunk edges
+            const long long c_lo = (sc0 + j) * m * (long long)kChunk;
+            const long long c_hi = (sc0 + j + 1) * m * (long long)kChunk < n ? (sc0 + j + 1) * m * (long long)kChunk : n;
+            float* dst = grad + c_lo + off[j];
+            const uintptr_t g = reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)63;
+            const uint32_t gslot = (uint32_t)(g >> 6) & (kGranules - 1);
+            if (gran && head) atomicAdd(&gcnt[gslot], 1u);
+            if (gran) wave_sync_lds();
+            const bool alone = gran && head && gcnt[gslot] == 1 && g >= reinterpret_cast<uintptr_t>(grad + c_lo) &&
+                               g + 64 <= reinterpret_cast<uintptr_t>(grad + c_hi);
+            const float val = scale != 1.0f ? __fmul_rn(a, scale) : a;
+            if (alone) {
+                const int pos = (int)((reinterpret_cast<uintptr_t>(dst) - g) >> 2);
+                DGC_GLB f4v* g4 = (DGC_GLB f4v*)g;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f4v v = {0.f, 0.f, 0.f, 0.f};
+                    if (pos >> 2 == q) v[pos & 3] = val;
+                    g4[q] = v;
+                }
+            } else if (head) {
+                *dst = val;
+            }
+            if (gran) {
+                wave_sync_lds();
+                if (head) gcnt[gslot] = 0;   // clean for the next super-chunk
+            }
         }
     }
 }
@@ -653,22 +686,29 @@ static ZeroWords status_words(const DecWS& w) {
 
 template <int ID>
 static int launch_clear(const RunSrc& prev, const DecWS& w, float* grad, int64_t n, hipStream_t s) {
-    const dim3 grid((unsigned)grid_for(4 * prev.capacity, kBlock, kMaxGrid / 2), (unsigned)prev.world);
+    const dim3 grid((unsigned)grid_for(4 * prev.capacity, kBlock, kMaxGrid / 2), (unsigned)prev.count());
     hipLaunchKernelGGL(k_clear_packed<ID>, grid, dim3(kBlock), 0, s, prev, grad, n, status_words(w));
     DGC_LAUNCHED();
     return DGC_OK;
 }
 
-// prev: the previous payload (kZeroPrev only).
+// prev: the previous payload (kZeroPrev only). A phase of a split exchange (rs.parts >
+// 1: the runs of part rs.ready - 1 just landed) bounds and regroups only those runs and
+// scatters the super-chunks whose indices have all landed; zmode applies to phase 0.
 template <int VD, int ID>
 static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n, float scale, int max_runs,
                        int zmode, int64_t entries, int64_t run_cap, int runs, hipStream_t s,
                        const RunSrc* prev = nullptr) {
     if (w.nchunks > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress: n too large");
+    const bool split = rs.payload && rs.parts > 1;
+    const int part = split ? rs.ready - 1 : 0;
     // status, the overflow queue count and the unsorted flags are reset before any
     // kernel of this call can set them: by the dense fill's (or the sparse re-zero's)
-    // first block, or memsets
-    if (zmode == kZeroPrev) {
+    // first block, or memsets; a later phase of a split exchange only restarts the
+    // overflow queue (the previous phase's queued super-chunks are done)
+    if (part > 0) {
+        DGC_HIP(hipMemsetAsync(w.ovf_cnt, 0, sizeof(int32_t), s));
+    } else if (zmode == kZeroPrev) {
         DGC_TRY(launch_clear<ID>(*prev, w, grad, n, s));
     } else if (zmode == kZeroDense) {
         DGC_TRY(fill_zero(grad, n, s, status_words(w)));
@@ -686,11 +726,13 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
         return DGC_OK;
     }
     const unsigned bx = (unsigned)grid_for(run_cap + 1, kBlock, kMaxGrid / 2);
-    hipLaunchKernelGGL(k_bounds<ID>, dim3(bx, (unsigned)max_runs), dim3(kBlock), 0, s, w, rs, n, run_cap);
+    const int ystep = split ? rs.parts : 1, yruns = split ? rs.world : max_runs;
+    hipLaunchKernelGGL(k_bounds<ID>, dim3(bx, (unsigned)yruns), dim3(kBlock), 0, s, w, rs, n, run_cap, ystep, part);
     DGC_LAUNCHED();
     if (w.sort_cap) {
         if (run_cap > w.sort_cap) DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_decompress: run capacity above the regroup area");
-        hipLaunchKernelGGL((k_regroup<VD, ID>), dim3((unsigned)max_runs), dim3(kRegroupThreads), 0, s, w, rs, n);
+        hipLaunchKernelGGL((k_regroup<VD, ID>), dim3((unsigned)yruns), dim3(kRegroupThreads), 0, s, w, rs, n, ystep,
+                           part);
         DGC_LAUNCHED();
     }
     // super-chunk of m chunks holding ~32 entries on average
@@ -698,7 +740,8 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
     const double per_chunk = (double)kChunk * (double)entries / (double)n;
     while (m < 64 && per_chunk * (2 * m) <= 32.0) m *= 2;
     const int64_t nsc = ceil_div(w.nchunks, (int64_t)m);
-    const dim3 grid((unsigned)ceil_div(nsc, (int64_t)kSegWaves * kSCB));
+    // a split phase covers ~1/parts of the super-chunks (its waves loop over its window)
+    const dim3 grid((unsigned)ceil_div(nsc, (int64_t)kSegWaves * kSCB * (split ? rs.parts : 1)));
     // whole-granule stores pay for their LDS bookkeeping from ~24 entries per chunk on
     // (measured at 1B: W = 8 scatter 0.39 -> 0.33 ms; W = 2 and 4 a few % slower with it)
     const int gran = per_chunk >= 24.0 ? 1 : 0;
@@ -786,6 +829,157 @@ int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t*
     if (voff) *voff = v;
     if (ioff) *ioff = i;
     return (int64_t)align_up(i + capacity * ibytes(id), 256);
+}
+
+// ---------------------------------------------------------------- split exchange
+// The allgather in `parts` collectives, so the scatter of what has landed runs while
+// the rest is in flight (the W-dependent decompress under the exchange). A rank's
+// packed payload is re-laid out as `parts` part buffers, each a packed payload of
+// part_cap = ceil(capacity / parts) entries (dgc_payload_layout) whose header holds
+// [0] its count and [1] the smallest index in the parts after it (INT64_MAX: none).
+// Part p of every rank has landed => every entry below min_r bound(r, p) has: the
+// scatter of phase p takes the super-chunks below that (and above phase p-1's).
+constexpr int kMaxParts = 8;
+constexpr int64_t kSplitScratch = 256;   // after the parts: per-part minima, arrival tickets
+
+int64_t split_layout(int64_t capacity, int parts, int vd, int id, int64_t* part_cap, int64_t* voff, int64_t* ioff) {
+    const int64_t pc = capacity > 0 ? ceil_div(capacity, (int64_t)parts) : 0;
+    if (part_cap) *part_cap = pc;
+    return payload_layout(pc, vd, id, voff, ioff);
+}
+
+// One pass over the payload's entries: each copied to its part, the per-part minimum
+// index kept as max(~idx) (0 at rest: the scratch is zero between calls); the last
+// workgroup writes the part headers and resets the scratch.
+template <int VB, int IB>
+__global__ void __launch_bounds__(kBlock)
+k_payload_split(const char* __restrict__ src, int64_t cap, int64_t voff, int64_t ioff, char* __restrict__ dst,
+                int parts, int64_t pc, int64_t pbytes, int64_t pvoff, int64_t pioff, uint64_t* pmin, uint32_t* tk) {
+    __shared__ unsigned long long smin[kMaxParts];
+    if (threadIdx.x < kMaxParts) smin[threadIdx.x] = 0;
+    __syncthreads();
+    long long cnt = *reinterpret_cast<const long long*>(src);
+    cnt = cnt < 0 ? 0 : (cnt > cap ? cap : cnt);
+    for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < cnt; e += (long long)gridDim.x * kBlock) {
+        const int p = (int)(e / pc);
+        const long long j = e - (long long)p * pc;
+        char* part = dst + p * pbytes;
+        long long idx;
+        if (IB == 4) {
+            const int32_t x = reinterpret_cast<const int32_t*>(src + ioff)[e];
+            reinterpret_cast<int32_t*>(part + pioff)[j] = x;
+            idx = x;
+        } else {
+            const int64_t x = reinterpret_cast<const int64_t*>(src + ioff)[e];
+            reinterpret_cast<int64_t*>(part + pioff)[j] = x;
+            idx = x;
+        }
+        if (VB == 2)
+            reinterpret_cast<uint16_t*>(part + pvoff)[j] = reinterpret_cast<const uint16_t*>(src + voff)[e];
+        else
+            reinterpret_cast<uint32_t*>(part + pvoff)[j] = reinterpret_cast<const uint32_t*>(src + voff)[e];
+        atomicMax(&smin[p], ~(unsigned long long)(idx < 0 ? 0 : idx));
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)parts && smin[threadIdx.x])
+        __hip_atomic_fetch_max(reinterpret_cast<unsigned long long*>(pmin) + threadIdx.x, smin[threadIdx.x],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!last_block_arrival8(tk, blockIdx.x, gridDim.x)) return;
+    if (threadIdx.x == 0) {
+        long long bound = LLONG_MAX;
+        for (int p = parts - 1; p >= 0; --p) {
+            long long* h = reinterpret_cast<long long*>(dst + p * pbytes);
+            const long long c = cnt - (long long)p * pc;
+            h[0] = c < 0 ? 0 : (c > pc ? pc : c);
+            h[1] = bound;
+            const uint64_t v = __hip_atomic_exchange(reinterpret_cast<unsigned long long*>(pmin) + p, 0ull,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long mn = v ? (long long)~v : LLONG_MAX;
+            bound = mn < bound ? mn : bound;
+        }
+    }
+}
+
+int payload_split(const void* payload, int64_t capacity, int parts, int vd, int id, void* split, hipStream_t s) {
+    if ((vd != DGC_F32 && vd != DGC_F16 && vd != DGC_BF16) || (id != DGC_I64 && id != DGC_I32))
+        DGC_FAIL(DGC_ERR_DTYPE, "dgc_payload_split: unsupported value/index dtype (%d, %d)", vd, id);
+    if (!payload || !split || capacity < 0 || parts < 1 || parts > kMaxParts)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_payload_split: null buffer, capacity < 0 or parts outside 1..%d", kMaxParts);
+    if ((reinterpret_cast<uintptr_t>(payload) | reinterpret_cast<uintptr_t>(split)) & 255)
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_payload_split: buffers must be 256-B aligned");
+    int64_t voff, ioff, pc, pvoff, pioff;
+    payload_layout(capacity, vd, id, &voff, &ioff);
+    const int64_t pbytes = split_layout(capacity, parts, vd, id, &pc, &pvoff, &pioff);
+    char* dst = static_cast<char*>(split);
+    auto* pmin = reinterpret_cast<uint64_t*>(dst + parts * pbytes);
+    auto* tk = reinterpret_cast<uint32_t*>(pmin + kMaxParts);
+    const unsigned g = (unsigned)grid_for(capacity, kBlock * 4);
+    const char* src = static_cast<const char*>(payload);
+    const int vb = vbytes(vd);
+    if (pc == 0) {   // no entries: headers only
+        DGC_HIP(hipMemsetAsync(dst, 0, (size_t)parts * pbytes, s));
+        return DGC_OK;
+    }
+    if (vb == 2 && id == DGC_I32)
+        hipLaunchKernelGGL((k_payload_split<2, 4>), dim3(g), dim3(kBlock), 0, s, src, capacity, voff, ioff, dst, parts, pc,
+                           pbytes, pvoff, pioff, pmin, tk);
+    else if (vb == 2)
+        hipLaunchKernelGGL((k_payload_split<2, 8>), dim3(g), dim3(kBlock), 0, s, src, capacity, voff, ioff, dst, parts, pc,
+                           pbytes, pvoff, pioff, pmin, tk);
+    else if (id == DGC_I32)
+        hipLaunchKernelGGL((k_payload_split<4, 4>), dim3(g), dim3(kBlock), 0, s, src, capacity, voff, ioff, dst, parts, pc,
+                           pbytes, pvoff, pioff, pmin, tk);
+    else
+        hipLaunchKernelGGL((k_payload_split<4, 8>), dim3(g), dim3(kBlock), 0, s, src, capacity, voff, ioff, dst, parts, pc,
+                           pbytes, pvoff, pioff, pmin, tk);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+static RunSrc split_src(const void* gathered, int32_t world, int parts, int ready, int64_t pbytes, int64_t pc,
+                        int64_t voff, int64_t ioff, const DecWS* w) {
+    RunSrc r{nullptr, nullptr, static_cast<const char*>(gathered), pbytes, voff, ioff, pc, world,
+             w ? w->unsorted : nullptr, w ? w->sorted : nullptr};
+    r.parts = parts;
+    r.ready = ready;
+    r.pstride = (int64_t)world * pbytes;
+    return r;
+}
+
+static int check_split(const void* gathered, int32_t world, int parts, int64_t capacity, int vd, int id,
+                       const char* fn) {
+    if (!gathered || world < 1 || parts < 2 || parts > kMaxParts || capacity < 0 || world * parts > kMaxRuns)
+        DGC_FAIL(DGC_ERR_INVALID, "%s: null buffer, parts outside 2..%d or world * parts > %d", fn, kMaxParts, kMaxRuns);
+    if ((vd != DGC_F32 && vd != DGC_F16) || (id != DGC_I64 && id != DGC_I32))
+        DGC_FAIL(DGC_ERR_DTYPE, "%s: unsupported value/index dtype (%d, %d)", fn, vd, id);
+    return DGC_OK;
+}
+
+// Phase `part` of the split decompress (parts < part landed and scattered by the
+// earlier phases, in order, on this workspace). grad holds +0.0 (zeroed before phase 0
+// — cleared: by dgc_clear_split on this workspace, which also reset its status words).
+int scatter_split(const void* gathered, int32_t world, int parts, int part, int64_t capacity, int vd, int id,
+                  float* grad, int64_t n, float scale, int cleared, void* ws, size_t ws_bytes, hipStream_t s) {
+    DGC_TRY(check_split(gathered, world, parts, capacity, vd, id, "dgc_scatter_split"));
+    if (part < 0 || part >= parts) DGC_FAIL(DGC_ERR_INVALID, "dgc_scatter_split: part %d outside 0..%d", part, parts - 1);
+    int64_t pc, voff, ioff;
+    const int64_t pbytes = split_layout(capacity, parts, vd, id, &pc, &voff, &ioff);
+    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world * parts, pc));
+    const DecWS w = carve_dec(ws, n, world * parts, pc);
+    const RunSrc rs = split_src(gathered, world, parts, part + 1, pbytes, pc, voff, ioff, &w);
+    return dispatch_scatter(vd, id, w, rs, grad, n, scale, world * parts, cleared ? kZeroDone : kZeroNone,
+                            (int64_t)world * parts * pc, pc, world * parts, s);
+}
+
+int clear_split(const void* prev, int32_t world, int parts, int64_t capacity, int vd, int id, float* grad, int64_t n,
+                void* ws, size_t ws_bytes, hipStream_t s) {
+    DGC_TRY(check_split(prev, world, parts, capacity, vd, id, "dgc_clear_split"));
+    int64_t pc, voff, ioff;
+    const int64_t pbytes = split_layout(capacity, parts, vd, id, &pc, &voff, &ioff);
+    DGC_TRY(check_common(vd, id, grad, n, ws, ws_bytes, world * parts, pc));
+    const DecWS w = carve_dec(ws, n, world * parts, pc);
+    const RunSrc pr = split_src(prev, world, parts, parts, pbytes, pc, voff, ioff, nullptr);
+    return id == DGC_I32 ? launch_clear<DGC_I32>(pr, w, grad, n, s) : launch_clear<DGC_I64>(pr, w, grad, n, s);
 }
 
 int decompress_packed(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity, int vd,
@@ -948,6 +1142,43 @@ extern "C" int dgc_scatter_packed(const void* payload, int32_t world, int64_t ra
                                   size_t ws_bytes, void* stream) {
     return dgc::decompress_packed(payload, world, rank_stride, capacity, vdtype, idtype, grad, n, scale, ws,
                                   ws_bytes, static_cast<hipStream_t>(stream), dgc::kZeroNone);
+}
+
+extern "C" int64_t dgc_payload_split_layout(int64_t capacity, int32_t parts, int32_t vdtype, int32_t idtype,
+                                            int64_t* part_capacity) {
+    if (parts < 1 || parts > dgc::kMaxParts || capacity < 0) return 0;
+    return dgc::split_layout(capacity, parts, vdtype, idtype, part_capacity, nullptr, nullptr);
+}
+
+extern "C" int64_t dgc_payload_split_bytes(int64_t capacity, int32_t parts, int32_t vdtype, int32_t idtype) {
+    if (parts < 1 || parts > dgc::kMaxParts || capacity < 0) return 0;
+    return parts * dgc::split_layout(capacity, parts, vdtype, idtype, nullptr, nullptr, nullptr) + dgc::kSplitScratch;
+}
+
+extern "C" int dgc_payload_split(const void* payload, int64_t capacity, int32_t parts, int32_t vdtype, int32_t idtype,
+                                 void* split, void* stream) {
+    return dgc::payload_split(payload, capacity, parts, vdtype, idtype, split, static_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t dgc_decompress_split_workspace(int64_t n, int32_t world, int32_t parts, int64_t capacity) {
+    if (parts < 1 || parts > dgc::kMaxParts || world < 1 || world * parts > dgc::kMaxRuns) return 0;
+    size_t b = 0;
+    dgc::carve_dec(nullptr, n, world * parts, capacity > 0 ? dgc::ceil_div(capacity, (int64_t)parts) : 0, &b);
+    return b;
+}
+
+extern "C" int dgc_scatter_split(const void* gathered, int32_t world, int32_t parts, int32_t part, int64_t capacity,
+                                 int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, int32_t cleared,
+                                 void* ws, size_t ws_bytes, void* stream) {
+    return dgc::scatter_split(gathered, world, parts, part, capacity, vdtype, idtype, grad, n, scale, cleared, ws,
+                              ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_clear_split(const void* prev_gathered, int32_t world, int32_t parts, int64_t capacity,
+                               int32_t vdtype, int32_t idtype, float* grad, int64_t n, void* ws, size_t ws_bytes,
+                               void* stream) {
+    return dgc::clear_split(prev_gathered, world, parts, capacity, vdtype, idtype, grad, n, ws, ws_bytes,
+                            static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dgc_decompress_status(const void* ws, int32_t* status, void* stream) {

@@ -165,56 +165,6 @@ __device__ __forceinline__ bool pick_bin(const CountT* counts, int bins, uint64_
     return hit;
 }
 
-// True in every thread of the workgroup that arrives last at `ticket` among
-// `nblocks`. The data handed to the last workgroup is ONLY device-scope atomics
-// (histogram / count adds) that it reads back with agent-scope atomic loads — the
-// "agent atomics both sides" form of cdna_hip_programming.md G16 — so no L2
-// write-back (release) or L1 invalidate (acquire) fence is needed: every wave
-// drains its atomics (vmcnt(0): acknowledged = performed at the coherence point)
-// before the barrier, then one lane draws the ticket.
-__device__ __forceinline__ bool last_block_arrival(uint32_t* ticket, uint32_t nblocks) {
-    __shared__ int is_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = t == nblocks - 1;
-        if (is_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reusable
-    }
-    __syncthreads();
-    return is_last;
-}
-
-// last_block_arrival for many workgroups: arrivals spread over 8 shard counters (lb %
-// 8: one shard per XCD under round-robin placement), and the shard's last arrival
-// arrives at the top counter tk[8] — a ~1000-way arrival on one word costs ~12 us
-// (MI355X_MICROARCH.md "fanin"), eight ~125-way ones run side by side. tk: 9 words,
-// zero at rest (each last arrival resets its word). lb: the block's index among the
-// nblocks of the task.
-__device__ __forceinline__ bool last_block_arrival8(uint32_t* tk, uint32_t lb, uint32_t nblocks) {
-    if (nblocks <= 64) return last_block_arrival(tk + 8, nblocks);
-    __shared__ int is_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t sh = lb & 7u;
-        const uint32_t members = nblocks / 8 + (sh < (nblocks & 7u) ? 1u : 0u);
-        const uint32_t a = __hip_atomic_fetch_add(tk + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int last = 0;
-        if (a == members - 1) {
-            __hip_atomic_store(tk + sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t b = __hip_atomic_fetch_add(tk + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (b == 7u) {
-                __hip_atomic_store(tk + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                last = 1;
-            }
-        }
-        is_last = last;
-    }
-    __syncthreads();
-    return is_last;
-}
-
 // ---------------------------------------------------------------- kernels
 __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
     for (int b = threadIdx.x; b < 3 * kRsBins; b += blockDim.x) (&st->hist[0][0])[b] = 0;

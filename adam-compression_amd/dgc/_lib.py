@@ -144,6 +144,12 @@ _SIGNATURES = {
     "dgc_decompress_packed_over": (ctypes.c_int, [_P, _P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
     "dgc_clear_packed": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _P, _SZ, _P]),
     "dgc_scatter_packed_cleared": (ctypes.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _I64, _F, _P, _SZ, _P]),
+    "dgc_payload_split_layout": (_I64, [_I64, _I32, _I32, _I32, _P]),
+    "dgc_payload_split_bytes": (_I64, [_I64, _I32, _I32, _I32]),
+    "dgc_payload_split": (ctypes.c_int, [_P, _I64, _I32, _I32, _I32, _P, _P]),
+    "dgc_decompress_split_workspace": (_SZ, [_I64, _I32, _I32, _I64]),
+    "dgc_scatter_split": (ctypes.c_int, [_P, _I32, _I32, _I32, _I64, _I32, _I32, _P, _I64, _F, _I32, _P, _SZ, _P]),
+    "dgc_clear_split": (ctypes.c_int, [_P, _I32, _I32, _I64, _I32, _I32, _P, _I64, _P, _SZ, _P]),
     "dgc_fill_zero": (ctypes.c_int, [_P, _I64, _P]),
     "dgc_decompress_status": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
     "dgc_batch_workspace": (_SZ, [ctypes.POINTER(BatchDesc)]),

@@ -35,6 +35,7 @@ import torch.distributed as dist
 
 from . import _lib
 from . import comm
+from .exchange import SplitExchange, split_parts
 
 __all__ = ["DGCBatch"]
 
@@ -52,7 +53,7 @@ class DGCBatch:
     def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
                  resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
-                 deferred_masking=True, fill="auto", dtype=torch.float32):
+                 deferred_masking=True, fill="auto", dtype=torch.float32, exchange_parts="auto"):
         if fill not in ("auto", "inline", "sparse"):
             raise ValueError(f"fill must be 'auto', 'inline' or 'sparse', not {fill!r}")
         if dtype not in (torch.float32,) + _lib.HALF:
@@ -62,6 +63,7 @@ class DGCBatch:
         if fill == "auto" or self.half:   # the dense zero_() is always right; the re-zero is opt-in (fp32)
             fill = "inline"
         self.fill = fill
+        self.exchange_parts = exchange_parts
         self.device = torch.device(device or "cuda")
         self.names = [n for n, _ in named_shapes]
         self.shapes = {n: tuple(s) for n, s in named_shapes}
@@ -136,13 +138,22 @@ class DGCBatch:
         # indices stay readable for the re-zero; a new layout forgets them
         nbuf = 2 if self.fill == "sparse" else 1
         self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(nbuf)]
-        self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=self.device)
-                          for _ in range(nbuf)] if self.world > 1 else self._payloads)
+        # W > 1, fp32: the allgather in parts, each scattered as it lands (dgc/exchange.py)
+        self.parts = 1 if self.half else split_parts(self.world, self.capacity, self.exchange_parts)
+        self.xchg = None
+        self._inflight = None
+        if self.parts > 1:
+            self.xchg = SplitExchange(self.capacity, self.flat_numel, self.world, self.parts, self.vdtype,
+                                      self.idtype, self.device, nbuf)
+            self._gathers = self.xchg.gathers
+        else:
+            self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=self.device)
+                              for _ in range(nbuf)] if self.world > 1 else self._payloads)
         self._par = 0
         self._last_out = None
         self._last_gathered = None
-        self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(self.flat_numel, self.world, self.capacity),
-                                  dtype=torch.uint8, device=self.device)
+        self.dec_ws = (torch.empty(L.dgc_decompress_packed_workspace(self.flat_numel, self.world, self.capacity),
+                                   dtype=torch.uint8, device=self.device) if self.xchg is None else None)
 
     @property
     def payload(self):
@@ -262,9 +273,22 @@ class DGCBatch:
         self.compensate(starts)
         self.select()
 
-    def exchange(self):
+    def send(self):
+        """Issues the exchange of this step's payload (W > 1): one allgather, or one per
+        part (split); ``decompress`` waits for it."""
         if self.world > 1:
-            comm.allgather_packed_async(self.payload, out=self.gathered).wait()
+            if self.xchg is not None:
+                self._inflight = self.xchg.send(self.payload, self.gathered)
+            else:
+                self._inflight = [comm.allgather_packed_async(self.payload, out=self.gathered)]
+
+    def exchange(self):
+        """The exchange; a single allgather is also waited for here, a split one part by
+        part in ``decompress``."""
+        self.send()
+        if self.xchg is None and self._inflight:
+            self._inflight.pop().wait()
+            self._inflight = None
 
     def decompress(self, out_flat=None):
         """out = the rank-order sum of the gathered entries / W, +0.0 elsewhere (every tensor).
@@ -284,24 +308,37 @@ class DGCBatch:
         L = self._L
         st = _lib.stream_of(self.device)
         cur = self.gathered
+        handles, self._inflight = self._inflight or [], None
+        if self.xchg is None:
+            for h in handles:
+                h.wait()
+        elif self.world > 1 and not handles:
+            raise RuntimeError("DGCBatch: decompress of a split exchange before send() / exchange()")
         if self.half:   # zero_(), the runs in rank order (each add rounded), the 1/W scale
             _lib.check(L.dgc_decompress_packed16(cur.data_ptr(), self.world, self.rank_stride, self.capacity,
                                                  _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
                                                  _lib.VD[self.dtype], self.flat_numel, 1.0 / self.world,
                                                  self._bad16.data_ptr(), st), "dgc_decompress_packed16")
             return out
-        args = (self.world, self.rank_stride, self.capacity, _lib.VD[self.vdtype], _lib.ID[self.idtype],
-                out.data_ptr(), self.flat_numel, 1.0 / self.world, self.dec_ws.data_ptr(), self.dec_ws.numel(), st)
         aliased = out.untyped_storage().data_ptr() == self.grad_flat.untyped_storage().data_ptr()
         reusable = (self.fill == "sparse" and not aliased and self._last_gathered is not None
                     and self._last_gathered is not cur
                     and self._last_out == (out.data_ptr(), out.numel(), out._version))
-        if reusable:
-            _lib.check(L.dgc_decompress_packed_over(cur.data_ptr(), self._last_gathered.data_ptr(), *args),
-                       "dgc_decompress_packed_over")
+        if self.xchg is not None:   # zero_() first (it runs under the first part's collective)
+            if reusable:
+                self.xchg.clear(self._last_gathered, out, st)
+            else:
+                _lib.check(L.dgc_fill_zero(out.data_ptr(), self.flat_numel, st), "dgc_fill_zero")
+            self.xchg.scatter(cur, handles, out, 1.0 / self.world, reusable)
         else:
-            # the zero fill and the scatter in one call: the fill also resets the scatter's status words
-            _lib.check(L.dgc_decompress_packed(cur.data_ptr(), *args), "dgc_decompress_packed")
+            args = (self.world, self.rank_stride, self.capacity, _lib.VD[self.vdtype], _lib.ID[self.idtype],
+                    out.data_ptr(), self.flat_numel, 1.0 / self.world, self.dec_ws.data_ptr(), self.dec_ws.numel(), st)
+            if reusable:
+                _lib.check(L.dgc_decompress_packed_over(cur.data_ptr(), self._last_gathered.data_ptr(), *args),
+                           "dgc_decompress_packed_over")
+            else:
+                # the zero fill and the scatter in one call: the fill also resets the scatter's status words
+                _lib.check(L.dgc_decompress_packed(cur.data_ptr(), *args), "dgc_decompress_packed")
         if aliased:
             self._last_out = self._last_gathered = None
         else:

@@ -28,6 +28,9 @@ every decision kept on the device:
   (first step, a new tensor, one modified in place) gets the dense fill. The
   payload (W = 1) / gather buffer (W > 1) alternates between two buffers so the
   previous step's indices survive the current step.
+* at W > 1 with a large step (``exchange_parts``, dgc/exchange.py) the allgather goes
+  out in parts and each part is scattered as it lands, so only the last part's share
+  of the W-dependent scatter is exposed after the exchange.
   **What "sparse" cannot see**: writes through ``out.data`` (the reference's own idiom,
   e.g. ``grad.data.mul_``) and raw-pointer writes do not bump torch's version counter,
   so after one the re-zero would leave stale values. Only a caller that owns ``out``
@@ -47,6 +50,7 @@ import torch.distributed as dist
 
 from . import _lib
 from . import comm
+from .exchange import SplitExchange, split_parts
 
 __all__ = ["DGCBucket", "algorithmic_bytes"]
 
@@ -62,7 +66,7 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42, fill="auto", deferred_masking=True):
+                 device=None, world_size=None, seed=42, fill="auto", deferred_masking=True, exchange_parts="auto"):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)
@@ -112,10 +116,18 @@ class DGCBucket:
         self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
         self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=dev)
                           for _ in range(nbuf)] if self.world > 1 else self._payloads)
+        # W > 1: the allgather in parts, each scattered as it lands (dgc/exchange.py)
+        self.parts = split_parts(self.world, self.k, exchange_parts)
+        self.xchg = None
+        if self.parts > 1:
+            self.xchg = SplitExchange(self.k, N, self.world, self.parts, self.vdtype, self.idtype, dev, nbuf)
+            self._gathers = self.xchg.gathers
+        self._inflight = None
         self._par = 0
         self._last_out = None   # (data_ptr, numel, _version) of the output after the last decompress
         self._last_gathered = None
-        self.dec_ws = torch.empty(L.dgc_decompress_packed_workspace(N, self.world, self.k), dtype=torch.uint8, device=dev)
+        self.dec_ws = (torch.empty(L.dgc_decompress_packed_workspace(N, self.world, self.k), dtype=torch.uint8,
+                                   device=dev) if self.xchg is None else None)
         self.scale = 1.0 / self.world
         self._L = L
         if fill in ("allgather", "sparse"):
@@ -181,15 +193,40 @@ class DGCBucket:
                                          _lib.SYNC_DEVICE, _lib.stream_of(self.device)), "dgc_compress_finish")
 
     def exchange(self):
-        """The packed allgather (RCCL over xGMI; gloo stages through the host)."""
+        """The packed allgather (RCCL over xGMI; gloo stages through the host). Split
+        (``parts`` > 1): the parts' collectives are only issued; decompress waits for
+        each as it scatters it."""
         if self.world > 1:
-            comm.allgather_packed_async(self.payload, out=self.gathered).wait()
+            if self.xchg is not None:
+                self._inflight = self.xchg.send(self.payload, self.gathered)
+            else:
+                comm.allgather_packed_async(self.payload, out=self.gathered).wait()
+
+    def _decompress_split(self, out, dense, cleared=False):
+        """The split exchange's decompress: the zero_() (the dense fill, or the sparse
+        re-zero of the previous step's entries) issued first, so it runs under the
+        first part's collective, then one scatter per part as it lands."""
+        if self._inflight is None:
+            raise RuntimeError("DGCBucket: decompress of a split exchange before exchange()")
+        handles, self._inflight = self._inflight, None
+        cur = self.gathered
+        if dense and not cleared:
+            if self.fill == "sparse" and self._reusable(out) and self._last_gathered is not cur:
+                self.xchg.clear(self._last_gathered, out, _lib.stream_of(self.device))
+                cleared = True
+            else:
+                _lib.check(self._L.dgc_fill_zero(out.data_ptr(), self.numel, _lib.stream_of(self.device)),
+                           "dgc_fill_zero")
+        self.xchg.scatter(cur, handles, out, self.scale, cleared)
+        self._remember(out, cur)
 
     def decompress(self, out, dense=True):
         """dense: out = scale * (rank-order sum of the gathered entries), zeros elsewhere.
         dense=False: out already holds +0.0 (see fill_zero); only the entries are written.
         fill="sparse": a dense decompress into the previous step's untouched output
         re-zeroes only the previous entries (see the module docstring)."""
+        if self.xchg is not None:
+            return self._decompress_split(out, dense)
         L = self._L
         cur = self.gathered
         args = self._dec_args(out)
@@ -219,6 +256,10 @@ class DGCBucket:
         start of the step (ordered after everything already issued, e.g. an optimizer
         reading out), so it runs under K1 instead of before the scatter."""
         self.side.wait_stream(torch.cuda.current_stream(self.device))
+        if self.xchg is not None:
+            self.xchg.clear(self._last_gathered, out, self.side.cuda_stream)
+            self._ev_filled.record(self.side)
+            return
         _lib.check(self._L.dgc_clear_packed(self._last_gathered.data_ptr(), self.world, self.rank_stride, self.k,
                                             _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(), self.numel,
                                             self.dec_ws.data_ptr(), self.dec_ws.numel(), self.side.cuda_stream),
@@ -249,6 +290,9 @@ class DGCBucket:
         def decompress():
             if cleared:   # the entries onto the re-zeroed output
                 torch.cuda.current_stream(self.device).wait_event(self._ev_filled)
+                if self.xchg is not None:
+                    self._decompress_split(out, True, cleared=True)
+                    return
                 cur = self.gathered
                 _lib.check(self._L.dgc_scatter_packed_cleared(cur.data_ptr(), *self._dec_args(out)),
                            "dgc_scatter_packed_cleared")

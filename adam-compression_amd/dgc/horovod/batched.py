@@ -200,7 +200,6 @@ class BatchedStep:
         plan = self._plan
         b = plan["batch"]
         dev = plan["dev"]
-        handle = None
         if b is not None:
             if plan["order"] != hook_order:
                 # the sample-start draw sequence of this hook order (backward's order is
@@ -229,8 +228,7 @@ class BatchedStep:
                 ptrs[i] = gflat.data_ptr()
             b.compensate(starts, grad_ptrs=ptrs)
             b.select()
-            if b.world > 1:
-                handle = comm.allgather_packed_async(b.payload, out=b.gathered)
+            b.send()   # the allgather (or its parts), waited for in b.decompress()
         dense_handle = None
         if plan["dense"]:
             dptrs = plan["dense_ptrs"]
@@ -252,8 +250,6 @@ class BatchedStep:
                                              _lib.ptr(wire), _lib.VD[wire.dtype], st), "dgc_gather_cast")
                 dense_handle = comm.allreduce_async_(wire, op=Average)
         if b is not None:
-            if handle is not None:
-                handle.wait()
             b.decompress()   # into the batch's output, then p.grad (dgc/compression.py:191-194)
             glue.bind_grads(plan["comp_params"], plan["comp_views"])
         if plan["dense"]:

@@ -363,6 +363,34 @@ int dgc_scatter_packed_cleared(const void* payload, int32_t world, int64_t rank_
  * the first 16-B boundary). */
 int dgc_fill_zero(float* grad, int64_t n, void* stream);
 
+/* ---- split exchange: the allgather of dgc/compression.py:200-212 in `parts` collectives
+ * (2..8), the decompress of what has landed running while the rest is in flight ----
+ * dgc_payload_split re-lays a rank's packed payload (capacity entries) out as `parts`
+ * part buffers of dgc_payload_split_layout bytes each, consecutive: part p is a packed
+ * payload (dgc_payload_layout(part_capacity)) of the entries [p * part_capacity,
+ * (p + 1) * part_capacity) whose header holds [0] its count and [1] the smallest index
+ * in the parts after it (INT64_MAX: none). `split` is dgc_payload_split_bytes long
+ * (the parts, then scratch that must be zero before the first call; calls leave it zero).
+ * Part p is allgathered into gathered + p * world * part_bytes (rank r's at + r *
+ * part_bytes: part-major). dgc_scatter_split(part p), called for p = 0, 1, ... in order
+ * on one workspace after part p landed, writes every index below min over ranks of part
+ * p's bound (and not below part p-1's) — such an index has all its entries in parts <= p
+ * — with dgc_scatter_packed's sums: each index's run-order (rank-order) sum * scale, the
+ * last call writing the rest. grad holds +0.0 before part 0: zero-filled (cleared = 0),
+ * or re-zeroed by dgc_clear_split on this workspace (cleared = 1; same precondition as
+ * dgc_clear_packed, over the previous step's split gathered buffer). */
+int64_t dgc_payload_split_layout(int64_t capacity, int32_t parts, int32_t vdtype, int32_t idtype,
+                                 int64_t* part_capacity);
+int64_t dgc_payload_split_bytes(int64_t capacity, int32_t parts, int32_t vdtype, int32_t idtype);
+int dgc_payload_split(const void* payload, int64_t capacity, int32_t parts, int32_t vdtype, int32_t idtype,
+                      void* split, void* stream);
+size_t dgc_decompress_split_workspace(int64_t n, int32_t world, int32_t parts, int64_t capacity);
+int dgc_scatter_split(const void* gathered, int32_t world, int32_t parts, int32_t part, int64_t capacity,
+                      int32_t vdtype, int32_t idtype, float* grad, int64_t n, float scale, int32_t cleared, void* ws,
+                      size_t ws_bytes, void* stream);
+int dgc_clear_split(const void* prev_gathered, int32_t world, int32_t parts, int64_t capacity, int32_t vdtype,
+                    int32_t idtype, float* grad, int64_t n, void* ws, size_t ws_bytes, void* stream);
+
 /* Status word written by the decompress kernels: bit 0 = an index was out of
  * range [0, n) and was ignored; bit 1 = a run was not non-decreasing. Packed runs
  * are then regrouped and summed exactly (indices unique within a run); a run given by

@@ -265,9 +265,10 @@ def resume_worker(rank, world, port, label, batch, mode, resume_at, queue):
         dist.destroy_process_group()
 
 
-def bucket_worker(rank, world, port, fill, kind, queue):
+def bucket_worker(rank, world, port, fill, kind, *rest):   # rest: ([parts,] queue)
     """DGCBucket at W=2 (fixed-capacity packed payload, allgather, sparse or dense
     decompress) against the oracle over both ranks' payloads, step by step."""
+    parts, queue = rest if len(rest) == 2 else ("auto",) + rest
     import torch.distributed as dist
     _init(rank, world, port)
     problems = []
@@ -278,7 +279,9 @@ def bucket_worker(rank, world, port, fill, kind, queue):
         dev = torch.device("cuda:0")
         N, ratio = 3_000_017, 0.001
         b = DGCBucket(N, compress_ratio=ratio, momentum=0.9, nesterov=True, device=dev, world_size=world,
-                      seed=42, fill=fill)
+                      seed=42, fill=fill, exchange_parts=parts)
+        if parts != "auto" and b.parts != parts:
+            problems.append(("parts", b.parts))
         attrs = O.attributes(N, ratio)
         state = [(np.zeros(N, np.float32), np.zeros(N, np.float32)) for _ in range(world)]
         rng = random.Random(42)
@@ -316,11 +319,12 @@ def bucket_worker(rank, world, port, fill, kind, queue):
         dist.destroy_process_group()
 
 
-def batch_worker(rank, world, port, fill, kind, queue):
+def batch_worker(rank, world, port, fill, kind, *rest):   # rest: ([parts,] queue)
     """DGCBatch at W ranks (one packed payload of every tensor, allgather, decompress
     into the batch's persistent output — fill "sparse" re-zeroes only the previous
     step's gathered indices) against the oracle over all ranks' payloads, per tensor
     and step."""
+    parts, queue = rest if len(rest) == 2 else ("auto",) + rest
     import torch.distributed as dist
     _init(rank, world, port)
     problems = []
@@ -332,7 +336,9 @@ def batch_worker(rank, world, port, fill, kind, queue):
         shapes = [("a", (1000, 300)), ("b", (257, 3, 3, 64)), ("c", (70001,)), ("d", (2000, 500))]
         ratio = 0.001
         b = DGCBatch(shapes, compress_ratio=ratio, momentum=0.9, nesterov=False, device=dev, world_size=world,
-                     seed=7, fill=fill)
+                     seed=7, fill=fill, exchange_parts=parts)
+        if parts != "auto" and b.parts != parts:
+            problems.append(("parts", b.parts))
         state = {(q, n): (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
                  for q in range(world) for i, n in enumerate(b.names)}
         branches = []

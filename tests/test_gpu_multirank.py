@@ -104,6 +104,30 @@ def test_bucket_w4_matches_oracle(fill):
         assert problems == [], (rank, res)
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,parts,fill,kind", [(2, 2, "inline", "normal"), (2, 3, "sparse", "layered"),
+                                                   (4, 2, "allgather", "normal"), (4, 4, "sparse", "normal"),
+                                                   (8, 4, "sparse", "normal"), (8, 8, "inline", "layered")])
+def test_bucket_split_exchange_matches_oracle(world, parts, fill, kind):
+    """The allgather in `parts` collectives, each part scattered as it lands
+    (dgc/exchange.py), at W = 2 / 4 / 8 ranks on one MI355X over gloo: every fill form,
+    against the oracle over all ranks' payloads, step by step."""
+    out = run(G.bucket_worker, world, fill, kind, parts)
+    for rank, res in out.items():
+        problems = [r for r in res if r[0] != "branches"]
+        assert problems == [], (rank, res)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,parts,fill,kind", [(2, 2, "sparse", "layered"), (4, 2, "inline", "normal"),
+                                                   (8, 4, "sparse", "normal")])
+def test_batch_split_exchange_matches_oracle(world, parts, fill, kind):
+    out = run(G.batch_worker, world, fill, kind, parts)
+    for rank, res in out.items():
+        problems = [r for r in res if r[0] != "branches"]
+        assert problems == [], (rank, res)
+
+
 @pytest.mark.timeout(200)
 @pytest.mark.parametrize("case", ["fp16_w2_fp16v_i32"])
 def test_half_w2_communicate_matches_reference(case):
