@@ -282,7 +282,7 @@ class FlatRun:
     def config(self):
         b = self.b
         return {"numel": self.N, "num_selects": b.k, "num_samples": b.num_samples, "sample_stride": b.stride,
-                "fill": b.fill}
+                "fill": b.fill, "exchange_parts": b.parts}
 
 
 class ModelRun:
@@ -374,7 +374,8 @@ class ModelRun:
 
     def config(self):
         return {"compressed_tensors": len(self.b.names), "compressed_elements": self.n_comp,
-                "dense_elements": self.n_dense, "num_selects_total": self.b.capacity, "fill": self.b.fill}
+                "dense_elements": self.n_dense, "num_selects_total": self.b.capacity, "fill": self.b.fill,
+                "exchange_parts": self.b.parts}
 
 
 class DropinRun:
@@ -483,6 +484,39 @@ def dropin_compare(model, rank, world, dev, steps, warmup):
     return res
 
 
+def allgather_probe(run, world, reps=5):
+    """The step's exchange alone, after the timed steps: one RCCL allgather of the packed
+    payload (its bus bandwidth), and — split exchange — the parts' collectives issued
+    and waited for together (dgc/exchange.py)."""
+    from dgc import comm
+    b = run.b
+    pay = b.payload
+    out = torch.empty(world * pay.numel(), dtype=torch.uint8, device=pay.device)
+
+    def timed(fn):
+        fn()
+        dist.barrier()
+        torch.cuda.synchronize()
+        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(e) / reps
+
+    res = {"single_ms": timed(lambda: comm.allgather_packed_async(pay, out=out).wait())}
+    if getattr(b, "xchg", None) is not None:
+        x = b.xchg
+        g = torch.empty_like(x.gathers[0])
+
+        def split():
+            for h in x.send(pay, g):
+                h.wait()
+        res.update(parts=x.parts, split_ms=timed(split))
+    return res
+
+
 def hbm_probe(reads, writes, reps=5):
     """This box's streaming rate for K1's access mix, measured in the same run:
     dgc_hbm_probe (3 non-temporal 16-B reads + 2 writes per float4, one-shot blocks,
@@ -586,6 +620,7 @@ def main():
                                 "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
                                         "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
         run.b.fill = "sparse"
+    xgmi = allgather_probe(run, world) if world > 1 else None
     probe = hbm_probe(*run.probe_buffers())   # after the timed steps: overwrites the state
     ms_step = elapsed * 1e3 / args.steps
     full_passes = info.get("full_passes", 0)
@@ -640,10 +675,12 @@ def main():
         "compensate_ms_per_step": [round(e["compensate"][0].elapsed_time(e["compensate"][1]), 3) for e in evs],
         "selection": info,
     }
-    if world > 1 and ms.get("allgather", 0) > 0:
-        bus = (world - 1) * run.payload / (ms["allgather"] * 1e-3) / 1e9
-        res["allgather"] = {"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
-                            "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS)}
+    if xgmi is not None:
+        bus = (world - 1) * run.payload / (xgmi["single_ms"] * 1e-3) / 1e9
+        res["allgather"] = dict({"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
+                                 "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS),
+                                 "note": "one all_gather_into_tensor of the packed payload alone, after the timed "
+                                         "steps (HIP events on the compute stream around issue + wait)"}, **xgmi)
     log(f"{args.workload}: {ms_step:.3f} ms/step on the GPU")
     if world == 1 and not args.no_extras:
         model = wl["model"] if wl["kind"] == "model" else args.dropin_model

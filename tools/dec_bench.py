@@ -8,6 +8,11 @@ and times dgc_fill_zero, dgc_scatter_packed (sparse, onto a zeroed buffer),
 dgc_decompress_packed (dense) and dgc_decompress_packed_over (the sparse re-zero of
 the previous payload's entries + the scatter), `reps` times each; prints the average
 ms of each (HIP events on the current stream).
+
+Split exchange (dgc/exchange.py, --parts 2 4 ...): per part count, the sender's
+dgc_payload_split of one rank's payload, and each phase's dgc_scatter_split on the
+part-major gather buffer; the last phase is what stays exposed after the last
+collective (the earlier phases run while the later parts are in flight).
 """
 import argparse
 import json
@@ -40,6 +45,7 @@ def main():
     ap.add_argument("--W", type=int, default=8)
     ap.add_argument("--numel", type=float, default=1e9)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--parts", type=int, nargs="*", default=[2, 4])
     args = ap.parse_args()
     N, W = int(args.numel), args.W
     k = (N + 999) // 1000
@@ -83,7 +89,46 @@ def main():
     res = {"W": W, "numel": N, "k": k,
            "fill_ms": timeit(fill, args.reps), "scatter_ms": timeit(scatter, args.reps),
            "dense_ms": timeit(dense, args.reps), "over_ms": timeit(over, args.reps)}
+    for P in args.parts:
+        if W * P > 64 or P < 2:
+            continue
+        res[f"split{P}"] = split_times(L, pay, stride, W, P, k, N, out, s, args.reps)
     print(json.dumps(res), flush=True)
+
+
+def split_times(L, pay, stride, W, P, k, N, out, s, reps):
+    import ctypes
+    pc = ctypes.c_int64(0)
+    pb = L.dgc_payload_split_layout(k, P, 0, 0, ctypes.byref(pc))
+    dev = out.device
+    split = torch.zeros(L.dgc_payload_split_bytes(k, P, 0, 0), dtype=torch.uint8, device=dev)
+    g = torch.zeros(P * W * pb, dtype=torch.uint8, device=dev)
+
+    def pack(r):
+        _lib.check(L.dgc_payload_split(pay[r * stride:].data_ptr(), k, P, 0, 0, split.data_ptr(), s),
+                   "dgc_payload_split")
+
+    for r in range(W):
+        pack(r)
+        for p in range(P):
+            g[(p * W + r) * pb:(p * W + r + 1) * pb].copy_(split[p * pb:(p + 1) * pb])
+    ws = torch.empty(L.dgc_decompress_split_workspace(N, W, P, k), dtype=torch.uint8, device=dev)
+
+    def phase(p):
+        _lib.check(L.dgc_scatter_split(g.data_ptr(), W, P, p, k, 0, 0, out.data_ptr(), N, 1.0 / W, 0, ws.data_ptr(),
+                                       ws.numel(), s), "dgc_scatter_split")
+
+    phases = [0.0] * P
+    for _ in range(reps):
+        _lib.check(L.dgc_fill_zero(out.data_ptr(), N, s), "dgc_fill_zero")
+        for p in range(P):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            phase(p)
+            b.record()
+            b.synchronize()
+            phases[p] += a.elapsed_time(b) / reps
+    return {"pack_ms": timeit(lambda: pack(0), reps), "phase_ms": phases, "exposed_ms": phases[-1]}
 
 
 if __name__ == "__main__":
