@@ -139,6 +139,7 @@ struct SelCfg {
     int32_t max_iters, resample, masking, vdtype, idtype;
     int32_t update_memory;      // 0: none, 1: zero the emitted slots now, 2: deferred to the next K1
     int32_t tdtype;             // the sparsified tensor's dtype: threshold *= bound rounds to it
+    int32_t set_order;          // resample_order = 1: an untied resample emits its set in index order (K5s)
 };
 
 // Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
@@ -2287,6 +2288,189 @@ __device__ __forceinline__ void heap_select_wg(const float* __restrict__ vec_fla
 // gathered candidates (introselect.hpp: nth_element), or — partial_sort path — heap
 // select + sort_heap over vec, which also emits. They share one LDS area.
 static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
+// ---------------------------------------------------------------- K5s: a resample's set
+// For an engine (resample_order = 1) a resampled tensor's payload need not list torch's
+// topk order: the exchange's decompress (index_put_ of distinct indices) and
+// DGCSGDMemory.update depend on the SET of the top-k (dgc/compression.py:134-137,
+// 179-194; dgc/memory.py:72-77). When the k-th largest candidate key is not tied
+// across the k boundary (#keys >= kth == k) every top-k is that set, whatever order
+// and tie rule produced it, so it is emitted in index order and the exact replay (K5)
+// skips the tensor (rs_nth = 3). Tied, the replay runs as always.
+//
+// One 1024-thread workgroup per tensor over its K5 queue (the candidates in index
+// order, key << 32 | position): the keys in registers (kSetReg per thread, the rest
+// re-read from L2), a radix select of the k-th largest over key - min in up to three
+// 11-bit passes (the candidates of one tensor span a few octaves: relative to the
+// minimum their top bits spread over the bins instead of piling into the few bins of
+// their exponents), then an order-preserving compaction: per 1024-entry round every
+// wave's ballot count goes to LDS, one workgroup scan over the (round, wave) counts
+// gives each its base, and each selected entry is emitted at base + its rank in the
+// ballot — with the wire casts and the masking of the K5 emit.
+constexpr int kSetReg = 32;                  // keys per thread kept in registers
+constexpr int kSetRounds = 256;              // the set path up to kSetRounds x 1024 candidates
+constexpr int64_t kSetMax = (int64_t)kSetRounds * kScanThreads;
+
+__global__ void __launch_bounds__(kScanThreads)
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+    const int t = blockIdx.x;
+    SelState* st = w.st + t;
+    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const int64_t n64 = st->n_cur;
+    if (n64 > kSetMax || d.k < 1 || n64 <= d.k) return;   // the replay takes it
+    const int n = (int)n64;
+    const uint32_t k = (uint32_t)d.k;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int kWaves = kScanThreads / kWave;
+    __shared__ uint32_t h[kRsBins];
+    __shared__ uint32_t lds32[16];
+    __shared__ uint32_t red[2][kWaves];
+    __shared__ uint32_t prefix, k_rem, sel_above, sel_cnt;
+    __shared__ int sel_bin;
+    __shared__ uint32_t rbase[kSetRounds * kWaves];
+    __shared__ long long obase_s;
+    // queue entry i = tid + r * 1024 (coalesced high-word loads); its key
+    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    auto key_at = [&](int i) -> uint32_t { return qw[2 * i + 1]; };
+    const int rounds = (n + kScanThreads - 1) / kScanThreads;
+    uint32_t key[kSetReg];
+#pragma unroll
+    for (int r = 0; r < kSetReg; ++r) {
+        const int i = tid + r * kScanThreads;
+        key[r] = i < n ? key_at(i) : 0u;
+    }
+    // every key of this thread: registers, then L2 (uniform loop bounds)
+    auto for_keys = [&](auto fn) {
+#pragma unroll
+        for (int r = 0; r < kSetReg; ++r) {
+            const int i = tid + r * kScanThreads;
+            if (i < n) fn(key[r]);
+        }
+        for (int r = kSetReg; r < rounds; ++r) {
+            const int i = tid + r * kScanThreads;
+            if (i < n) fn(key_at(i));
+        }
+    };
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+    for_keys([&](uint32_t x) {
+        mn = x < mn ? x : mn;
+        mx = x > mx ? x : mx;
+    });
+    mn = wave_min_u32(mn);
+    mx = wave_max(mx);
+    if (lane == 0) {
+        red[0][wv] = mn;
+        red[1][wv] = mx;
+    }
+    for (int b = tid; b < kRsBins; b += kScanThreads) h[b] = 0;
+    if (tid == 0) {
+        prefix = 0;
+        k_rem = k;
+    }
+    __syncthreads();
+    mn = red[0][0];
+    mx = red[1][0];
+#pragma unroll
+    for (int i = 1; i < kWaves; ++i) {
+        mn = red[0][i] < mn ? red[0][i] : mn;
+        mx = red[1][i] > mx ? red[1][i] : mx;
+    }
+    // passes over the bits of key - mn, 11 at a time from the top
+    const uint32_t span = mx - mn;
+    const int L = span ? 32 - __builtin_clz(span) : 0;
+    int hi = L;   // bits above hi: matched by prefix (of key - mn)
+    bool found = L == 0;   // every key equal: the k-th largest is mn
+    uint32_t kth = mn, eq = (uint32_t)n;
+    while (!found) {
+        const int lo = hi > 11 ? hi - 11 : 0;
+        const uint32_t pre = prefix;
+        for_keys([&](uint32_t x) {
+            const uint32_t v = x - mn;
+            if (hi >= 32 || (v >> hi) == pre) atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
+        });
+        __syncthreads();
+        if (tid == 0) sel_bin = -1;
+        int bin;
+        uint32_t above;
+        const bool hit = pick_bin_small<2>(h, k_rem, lds32, &bin, &above);
+        if (hit) {
+            sel_bin = bin;
+            sel_above = above;
+            sel_cnt = h[bin];
+        }
+        __syncthreads();
+        if (sel_bin < 0) return;   // (cannot happen: k < n keys) — the replay takes it
+        const uint32_t b = (uint32_t)sel_bin, a = sel_above, c = sel_cnt;
+        __syncthreads();   // every thread has read sel_*
+        if (tid == 0) {
+            prefix = (pre << (hi - lo)) | b;
+            k_rem -= a;
+        }
+        for (int q = tid; q < kRsBins; q += kScanThreads) h[q] = 0;
+        __syncthreads();
+        hi = lo;
+        if (lo == 0) {
+            found = true;
+            kth = mn + prefix;
+            eq = c;
+        }
+    }
+    // tied across the boundary (more keys == kth than the k - #(> kth) still needed):
+    // only torch's exact order of operations knows which ones — the replay
+    if (eq != k_rem) return;
+    // order-preserving compaction: (round, wave) counts, one scan, ranks from ballots
+    auto count_round = [&](int r, uint32_t x) {   // uniform in r
+        const int i = tid + r * kScanThreads;
+        const uint32_t c = (uint32_t)__popcll(__ballot(i < n && x >= kth));
+        if (lane == 0) rbase[r * kWaves + wv] = c;
+    };
+#pragma unroll
+    for (int r = 0; r < kSetReg; ++r)
+        if (r < rounds) count_round(r, key[r]);
+    for (int r = kSetReg; r < rounds; ++r) count_round(r, tid + r * kScanThreads < n ? key_at(tid + r * kScanThreads) : 0u);
+    if (wv == 0) {
+        const long long b = out_base(w, t);
+        if (lane == 0) obase_s = b;
+    }
+    __syncthreads();
+    {
+        constexpr int kPerT = kSetRounds * kWaves / kScanThreads;   // 4 (round, wave) counts per thread
+        uint32_t c[kPerT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kPerT; ++j) {
+            c[j] = kPerT * tid + j < rounds * kWaves ? rbase[kPerT * tid + j] : 0u;
+            sum += c[j];
+        }
+        uint32_t total;
+        uint32_t run = block_exclusive_scan32(sum, lds32, &total);
+#pragma unroll
+        for (int j = 0; j < kPerT; ++j) {
+            if (kPerT * tid + j < rounds * kWaves) rbase[kPerT * tid + j] = run;
+            run += c[j];
+        }
+    }
+    __syncthreads();
+    const long long ob = obase_s;
+    const float* vec = vec_flat + d.off;
+    auto emit_round = [&](int r, uint32_t x) {   // uniform in r
+        const int i = tid + r * kScanThreads;
+        const bool sel = i < n && x >= kth;
+        const uint64_t m = __ballot(sel);
+        if (sel) {
+            const int64_t li = w.cand_idx[d.cand_off + i];
+            emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(m, 0u), li, vec[li]);
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < kSetReg; ++r)
+        if (r < rounds) emit_round(r, key[r]);
+    for (int r = kSetReg; r < rounds; ++r) emit_round(r, tid + r * kScanThreads < n ? key_at(tid + r * kScanThreads) : 0u);
+    if (tid == 0) {
+        st->rs_nth = 3;   // K5's replay and emit skip the tensor
+        st->tie_rule = DGC_TIES_SET;
+    }
+}
+
 // K5's global-memory phase by G workgroups per tensor (grid G x T, a plain launch sized
 // so all of them fit at once; a residency consensus decides whether they run it, see
 // introselect.hpp); k_nth_select goes on from the state it leaves.
@@ -2372,7 +2556,8 @@ static int validate_select(const dgc_select_params* p, void* values, void* indic
 }
 
 static SelCfg cfg_of(const dgc_select_params& p) {
-    return SelCfg{p.upper, p.lower, p.max_iters, p.resample, p.masking, p.vdtype, p.idtype, p.update_memory, p.thr_dtype};
+    return SelCfg{p.upper, p.lower,       p.max_iters,     p.resample,  p.masking,
+                  p.vdtype, p.idtype,     p.update_memory, p.thr_dtype, p.resample_order == 1 ? 1 : 0};
 }
 
 // The selection of every tensor (its K1 lists kept or not), from k_sel_init to the
@@ -2495,6 +2680,10 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         g.queue = w.queue;
         g.cand = w.cand_idx;
         DGC_TRY(launch_emit(L, vec, w, g, s));
+        if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
+            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o);
+            DGC_LAUNCHED();
+        }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
         if (G > 1) {
             // DGC_K5_GLOBAL=multi: every range over several workgroups (parity); =abort: the
@@ -2819,7 +3008,8 @@ static SelCfg cfg_of_batch(const dgc_batch_desc* b) {
     const bool half = b->dtype == DGC_BF16 || b->dtype == DGC_F16;
     return SelCfg{(float)b->upper_bound, (float)b->lower_bound, b->max_iters, b->resample, b->momentum_masking,
                   b->fp16_values ? DGC_F16 : (half ? b->dtype : DGC_F32), b->int32_indices ? DGC_I32 : DGC_I64,
-                  half ? 0 : (b->deferred_masking ? 2 : 1), half ? b->dtype : DGC_F32};
+                  half ? 0 : (b->deferred_masking ? 2 : 1), half ? b->dtype : DGC_F32,
+                  b->resample_order == 1 ? 1 : 0};
 }
 
 size_t batch_ws_bytes(const dgc_batch_desc* b) {

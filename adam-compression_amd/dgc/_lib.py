@@ -23,7 +23,7 @@ VD = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 HALF = (torch.bfloat16, torch.float16)   # 16-bit parameters (dgc_*16 entry points)
 ID = {torch.int64: 0, torch.int32: 1}
 BRANCHES = {0: "direct", 1: "ok", 2: "trunc", 3: "resample", 4: "exhausted"}
-TIE_RULES = {0: "none", 1: "exact"}
+TIE_RULES = {0: "none", 1: "exact", 2: "set"}
 
 
 class SelectParams(ctypes.Structure):
@@ -32,7 +32,7 @@ class SelectParams(ctypes.Structure):
                 ("lower_count", ctypes.c_int64), ("upper", ctypes.c_float), ("lower", ctypes.c_float),
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("masking", ctypes.c_int32),
                 ("vdtype", ctypes.c_int32), ("idtype", ctypes.c_int32), ("update_memory", ctypes.c_int32),
-                ("thr_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("thr_dtype", ctypes.c_int32), ("resample_order", ctypes.c_int32),
                 ("status_sink", ctypes.c_void_p)]
 
 
@@ -105,7 +105,7 @@ class BatchDesc(ctypes.Structure):
                 ("fp16_values", ctypes.c_int32), ("int32_indices", ctypes.c_int32), ("nesterov", ctypes.c_int32),
                 ("momentum", ctypes.c_float), ("spec_margin", ctypes.c_float),
                 ("deferred_masking", ctypes.c_int32), ("dtype", ctypes.c_int32),
-                ("status_sink", ctypes.c_void_p)]
+                ("resample_order", ctypes.c_int32), ("status_sink", ctypes.c_void_p)]
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64

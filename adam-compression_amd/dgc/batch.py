@@ -53,7 +53,8 @@ class DGCBatch:
     def __init__(self, named_shapes, compress_ratio=0.001, momentum=0.9, nesterov=False, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
                  resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
-                 deferred_masking=True, fill="auto", dtype=torch.float32, exchange_parts="auto"):
+                 deferred_masking=True, fill="auto", dtype=torch.float32, exchange_parts="auto",
+                 resample_order="index"):
         if fill not in ("auto", "inline", "sparse"):
             raise ValueError(f"fill must be 'auto', 'inline' or 'sparse', not {fill!r}")
         if dtype not in (torch.float32,) + _lib.HALF:
@@ -64,6 +65,12 @@ class DGCBatch:
             fill = "inline"
         self.fill = fill
         self.exchange_parts = exchange_parts
+        if resample_order not in ("index", "topk"):
+            raise ValueError(f"resample_order must be 'index' or 'topk', not {resample_order!r}")
+        # "index": a resampled tensor whose k-th largest candidate is untied lists its
+        # top-k set in index order (the decompress and the memory update depend on the
+        # set only; dgc_select_params.resample_order); "topk": torch.topk's order always
+        self.resample_order = resample_order
         self.device = torch.device(device or "cuda")
         self.names = [n for n, _ in named_shapes]
         self.shapes = {n: tuple(s) for n, s in named_shapes}
@@ -123,6 +130,7 @@ class DGCBatch:
         d.deferred_masking = int(self.deferred_masking)
         d.dtype = _lib.VD[self.dtype]
         d.status_sink = self.status.address
+        d.resample_order = 1 if self.resample_order == "index" else 0
         self.desc = d
         L = self._L
         wsz = L.dgc_batch_workspace(ctypes.byref(d))

@@ -66,7 +66,8 @@ class DGCBucket:
     def __init__(self, numel, compress_ratio=0.001, momentum=0.9, nesterov=True, momentum_masking=True,
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8,
                  max_adaptation_iters=10, resample=True, fp16_values=False, int32_indices=False,
-                 device=None, world_size=None, seed=42, fill="auto", deferred_masking=True, exchange_parts="auto"):
+                 device=None, world_size=None, seed=42, fill="auto", deferred_masking=True, exchange_parts="auto",
+                 resample_order="topk"):
         from .compression import DGCCompressor, _layout
         self.device = torch.device(device or "cuda")
         self.numel = N = int(numel)
@@ -91,6 +92,12 @@ class DGCBucket:
         # next step's K1, which streams vec/mmt anyway (mmt/vec below flush it on read)
         p.vdtype, p.idtype = _lib.VD[self.vdtype], _lib.ID[self.idtype]
         p.update_memory = 2 if deferred_masking else 1
+        # "index" (opt-in): an untied resample lists its set in index order (DGCBatch's
+        # default); a flat bucket's resample (up to 64k candidates) mostly exceeds the
+        # one-workgroup set path, so it keeps torch.topk's order by default
+        if resample_order not in ("index", "topk"):
+            raise ValueError(f"resample_order must be 'index' or 'topk', not {resample_order!r}")
+        p.resample_order = 1 if resample_order == "index" else 0
         self.status = _lib.StatusSink("DGCBucket", self.device)   # DGC_K5_BROKEN, checked every step
         p.status_sink = self.status.address
         self.params = p

@@ -375,7 +375,7 @@ class ModelRun:
     def config(self):
         return {"compressed_tensors": len(self.b.names), "compressed_elements": self.n_comp,
                 "dense_elements": self.n_dense, "num_selects_total": self.b.capacity, "fill": self.b.fill,
-                "exchange_parts": self.b.parts}
+                "exchange_parts": self.b.parts, "resample_order": self.b.resample_order}
 
 
 class DropinRun:

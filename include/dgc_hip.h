@@ -82,12 +82,15 @@ enum dgc_branch {
     DGC_BRANCH_EXHAUSTED = 4  /* max_adaptation_iters recounts used up    */
 };
 
-/* How a resample chose among the candidates tied at its k-th value: always torch's
- * CPU topk replayed exactly, on both of its paths (nth_element for k*64 > n candidates,
- * partial_sort otherwise) — the reference's indices in the reference's order. */
+/* How a resample chose among the candidates tied at its k-th value: torch's CPU topk
+ * replayed exactly, on both of its paths (nth_element for k*64 > n candidates,
+ * partial_sort otherwise) — the reference's indices in the reference's order; or, for a
+ * caller that asked for index order (resample_order = 1) when the k-th largest key is
+ * not tied across the k boundary, the same SET in ascending index order. */
 enum dgc_tie_rule {
     DGC_TIES_NONE = 0,   /* no resample this call */
-    DGC_TIES_EXACT = 1   /* torch's topk replayed */
+    DGC_TIES_EXACT = 1,  /* torch's topk replayed */
+    DGC_TIES_SET = 2     /* untied boundary: topk's set, index order */
 };
 
 /* Per-tensor selection parameters: DGCCompressor.attributes[name]
@@ -116,7 +119,11 @@ typedef struct dgc_select_params {
                               /* (DGC_F32 / DGC_BF16 / DGC_F16): the        */
                               /* threshold *= bound products round to it,   */
                               /* as the 0-dim threshold tensor does          */
-    int32_t reserved;
+    int32_t resample_order;   /* 0: a resample lists torch.topk's order (the    */
+                              /*    exact replay); 1: index order when the k-th */
+                              /*    largest candidate key is untied (DGC_TIES_  */
+                              /*    SET: the same set, for an engine whose      */
+                              /*    decompress / update depend on the set only)  */
     int32_t* status_sink;     /* NULL, or a host-mapped (pinned) int32: a call  */
                               /* whose resample replay broke stores its       */
                               /* dgc_select_info.k5_status there (with        */
@@ -265,6 +272,7 @@ typedef struct dgc_batch_desc {
                                     /*   dgc_compensate16 image, 16-bit wire values     */
                                     /*   unless fp16_values, dgc_mask_packed16,         */
                                     /*   dgc_decompress_packed16)                       */
+    int32_t resample_order;         /* as dgc_select_params.resample_order             */
     int32_t* status_sink;           /* as dgc_select_params.status_sink (NULL: none)   */
 } dgc_batch_desc;
 

@@ -27,6 +27,18 @@ def _same_or_nan(a, b):
     return bool(np.all((np.isnan(a) & np.isnan(b)) | (bits(a) == bits(b))))
 
 
+def _assert_sent(gi, gv, oi, wv, info, key):
+    """The transmitted (indices, wire values) against the oracle's: in order, or — a
+    resample whose k-th key was untied under resample_order="index" (tie rule "set") —
+    torch.topk's set in ascending index order."""
+    gi, gv = gi.cpu().numpy(), gv.cpu().numpy()
+    if info.get("tie_rule") == "set":
+        o = np.argsort(oi, kind="stable")
+        oi, wv = oi[o], wv[o]
+    assert np.array_equal(gi, oi), (key, info)
+    assert np.array_equal(bits(gv), bits(wv)), (key, info)
+
+
 def _sets():
     from dgc import workloads
     r50, _ = workloads.split(workloads.resnet50())
@@ -40,11 +52,13 @@ def _sets():
 @pytest.mark.parametrize("label,shape", [("mixed", None), ("resnet50", None), ("vgg16_bn", None),
                                          ("mixed", "quarter"), ("resnet50", "quarter"), ("mixed+naninf", None),
                                          ("mixed", "k5multi"), ("resnet50", "k5multi"), ("mixed", "k5abort"),
-                                         ("resnet50", "k5abort")])
+                                         ("resnet50", "k5abort"), ("mixed", "topk"), ("resnet50", "topk")])
 def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
     """shape: the emit kernel (None: the library's choice — k_emit_wide for these few
     groups; "quarter": k_emit, the flat buckets' kernel, forced), or "k5multi": the
-    resample replay's global phase over several workgroups per tensor (k_nth_global). "+naninf": tensor "b"
+    resample replay's global phase over several workgroups per tensor (k_nth_global);
+    "topk": resample_order="topk" (every resample replays torch's order; the K5 shapes
+    too) — otherwise DGCBatch's default "index" (an untied resample: the set). "+naninf": tensor "b"
     gets a NaN at one of its samples on step 1 (its threshold turns NaN, nothing of it
     is selected), "odd" a NaN that is never sampled and "c" +-inf — the other tensors'
     selections must not notice."""
@@ -54,20 +68,21 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
         monkeypatch.setenv("DGC_K5_GLOBAL", "multi")
     elif shape == "k5abort":   # ... whose residency consensus times out: the one-workgroup fallback
         monkeypatch.setenv("DGC_K5_GLOBAL", "abort")
-    elif shape:
+    elif shape and shape != "topk":
         monkeypatch.setenv("DGC_EMIT_SHAPE", shape)
+    order = "topk" if shape in ("k5multi", "k5abort", "topk") else "index"
     from dgc.batch import DGCBatch
     naninf = label.endswith("+naninf")
     label = label.split("+")[0]
     shapes, fp16, int32 = _sets()[label]
     nest = label == "mixed"
     b = DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, nesterov=nest, fp16_values=fp16,
-                 int32_indices=int32, device=DEV, seed=42)
+                 int32_indices=int32, device=DEV, seed=42, resample_order=order)
     ref_rng = random.Random(42)
     state = {n: (np.zeros(b.numels[i], np.float32), np.zeros(b.numels[i], np.float32))
              for i, n in enumerate(b.names)}
     branches = set()
-    fallbacks = replays = 0
+    fallbacks = replays = sets = 0
     steps = 3 if label != "vgg16_bn" else 2
     for s in range(steps):
         # state read on odd and last steps only: reading flushes the deferred masking, so the
@@ -105,12 +120,13 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
             branches.add(info["branch"])
             assert infos[t]["branch"] == info["branch"], key
             replays += infos[t]["branch"] == "resample" and infos[t]["tie_rule"] == "exact"
+            sets += infos[t]["tie_rule"] == "set"
+            assert order == "index" or infos[t]["tie_rule"] != "set", key
             fallbacks += infos[t]["k5_fallback"]
             if shape != "k5abort":
                 assert not infos[t]["k5_fallback"], (key, infos[t])
             gv, gi = sent[name]
-            assert np.array_equal(gi.cpu().numpy(), oi), key
-            assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
+            _assert_sent(gi, gv, oi, wv, infos[t], key)
             if check_state:
                 assert _same_or_nan(b.momentum_of(name).reshape(-1).cpu().numpy(), m_o), key
                 assert _same_or_nan(b.velocity_of(name).reshape(-1).cpu().numpy(), v_o), key
@@ -127,6 +143,8 @@ def test_batch_matches_per_tensor_oracle(label, shape, monkeypatch):
             assert not bool(b.vec_flat[pad].any())
     if label == "mixed":
         assert {"direct", "resample"} <= branches, branches
+        if order == "index":   # the untied resamples took the set path, the "ties" tensor the replay
+            assert sets > 0, (sets, replays)
     if shape == "k5abort":   # every replay that reached the consensus fell back, exactly
         assert replays > 0 and fallbacks > 0, (replays, fallbacks)
 
@@ -156,14 +174,14 @@ def test_batch_warmup_ratio_change():
         out = b.decompress()   # persistent output: sparse re-zero except after a ratio change
         torch.cuda.synchronize()
         sent = b.transmitted()
+        infos = b.infos()
         for t, name in enumerate(b.names):
             attrs = O.attributes(b.numels[t], ratio)
             start = ref_rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
             m_o, v_o = state[name]
             ov, oi, _ = O.compress_step(grads[name], m_o, v_o, attrs, start)
             wv, wi = O.wire_cast(ov, oi, True, True)
-            assert np.array_equal(sent[name][1].cpu().numpy(), oi), (s, name)
-            assert np.array_equal(bits(sent[name][0].cpu().numpy()), bits(wv)), (s, name)
+            _assert_sent(sent[name][1], sent[name][0], oi, wv, infos[t], (s, name))
             dense = O.decompress([wv], [oi], b.numels[t], 1)
             assert np.array_equal(bits(b.out(name).reshape(-1).cpu().numpy()), bits(dense)), (s, name)
         pad = torch.ones(b.flat_numel, dtype=torch.bool, device=DEV)
@@ -195,3 +213,49 @@ def test_batch_sparse_rezero_matches_dense_fill():
             b.compress()
             outs.append(b.decompress())
         assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), s
+
+
+@pytest.mark.timeout(600)
+def test_batch_index_order_equals_topk_order():
+    """resample_order="index" (the set of an untied resample in index order, K5s) against
+    "topk" (torch's order, the exact replay) on the ResNet-50 set with the bench's
+    alternating gradients, whose bimodal velocities resample every other step: the same
+    sets, the same dense outputs and the same memory state, bit for bit, every step."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc import workloads
+    from dgc.batch import DGCBatch
+    shapes, _ = workloads.split(workloads.resnet50())
+    bs = [DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, device=DEV, seed=5, resample_order=o)
+          for o in ("index", "topk")]
+    gen = torch.Generator(device=DEV)
+    sets = 0
+    for s in range(8):
+        gen.manual_seed(0xD6C + s % 2)
+        g = torch.zeros(bs[0].flat_numel, device=DEV)
+        for off, n in zip(bs[0].offsets, bs[0].numels):
+            g[off: off + n] = torch.randn(n, generator=gen, device=DEV) * 1e-3
+        outs = []
+        for b in bs:
+            b.grad_flat.copy_(g)
+            b.compress()
+            outs.append(b.decompress().clone())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), s
+        ia, it = bs[0].infos(), bs[1].infos()
+        sa, st = bs[0].transmitted(), bs[1].transmitted()
+        for t, name in enumerate(bs[0].names):
+            assert ia[t]["branch"] == it[t]["branch"] and ia[t]["count"] == it[t]["count"], (s, name)
+            if ia[t]["tie_rule"] == "set":
+                sets += 1
+                assert it[t]["tie_rule"] == "exact", (s, name)
+                oi = st[name][1].cpu().numpy()
+                o = np.argsort(oi, kind="stable")
+                assert np.array_equal(sa[name][1].cpu().numpy(), oi[o]), (s, name)
+                assert np.array_equal(bits(sa[name][0].cpu().numpy()), bits(st[name][0].cpu().numpy()[o])), (s, name)
+            else:
+                assert torch.equal(sa[name][1], st[name][1]), (s, name)
+    for name in bs[0].names:
+        assert torch.equal(bs[0].velocity_of(name).view(torch.int32), bs[1].velocity_of(name).view(torch.int32))
+        assert torch.equal(bs[0].momentum_of(name).view(torch.int32), bs[1].momentum_of(name).view(torch.int32))
+    assert sets > 0

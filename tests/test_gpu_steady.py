@@ -5,15 +5,18 @@ sets (seeds 0xD6C + buffer), the same sample starts (``random.Random(42)``, one 
 per sampled tensor per step), the same persistent output with the sparse re-zero —
 stepped 25 times and compared with the oracle after EVERY step, tensor by tensor:
 
-* branch, count, transmitted indices (in order) and wire values (fp16/int32 casts);
+* branch, count, transmitted indices (in order) and wire values (fp16/int32 casts) —
+  a resample with an untied k-th key (``DGCBatch``'s default ``resample_order="index"``,
+  tie rule "set") lists torch.topk's SET in index order, so there the indices must be
+  the oracle's set, ascending, with each index's wire value;
 * momentum and velocity as the bench leaves them, i.e. NOT flushed: the first-k
   branches defer ``DGCSGDMemory.update``'s zeroing to the next K1 (so the raw state
   must equal the pre-masking state there), the resample branch masks at once;
 * the decompressed output (W = 1) and the dense tensors' ``compensate(accumulate=False)``.
 
 Reference: dgc/compression.py:109-198, dgc/memory.py:50-77. The run must pass through
-what the bench's ``selection`` record shows — exact resample replays (K5) and full
-select passes — or the test fails."""
+what the bench's ``selection`` record shows — resamples (the set path, and K5's exact
+replay where the k-th key is tied) and full select passes — or the test fails."""
 import importlib.util
 import os
 import random
@@ -59,7 +62,7 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
     state = [(np.zeros(n, np.float32), np.zeros(n, np.float32)) for n in b.numels]
     dense_m = np.zeros(run.n_dense, np.float32)
     ref_rng = random.Random(42)
-    exact = full_pass_steps = resample_max = 0
+    exact = as_set = full_pass_steps = resample_max = 0
     branches = {}
     steps = 25
     for s in range(steps):
@@ -84,8 +87,14 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
             assert info["count"] == oi.size, (key, info)
             wv, wi = O.wire_cast(ov, oi, fp16, int32)
             gv, gi = sent[name]
-            assert np.array_equal(gi.cpu().numpy(), oi), (key, info)
-            assert np.array_equal(bits(gv.cpu().numpy()), bits(wv)), key
+            gi, gv = gi.cpu().numpy(), gv.cpu().numpy()
+            if info["tie_rule"] == "set":   # topk's set, ascending (the oracle lists topk's order)
+                o = np.argsort(oi, kind="stable")
+                assert np.array_equal(gi, oi[o]), (key, info)
+                assert np.array_equal(bits(gv), bits(wv[o])), key
+            else:
+                assert np.array_equal(gi, oi), (key, info)
+                assert np.array_equal(bits(gv), bits(wv)), key
             deferred = info["branch"] != "resample"   # k_sel_finish: first-k branches defer the masking
             if deferred:   # raw state = the pre-masking state
                 assert np.array_equal(bits(raw_v[off: off + N]), bits(v_o)), key
@@ -98,13 +107,14 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
             branches[info["branch"]] = branches.get(info["branch"], 0) + 1
             if info["branch"] == "resample":
                 exact += info["tie_rule"] == "exact"
+                as_set += info["tie_rule"] == "set"
                 resample_max = max(resample_max, info["candidates"])
-                assert info["tie_rule"] == "exact", (key, info)
+                assert info["tie_rule"] in ("exact", "set"), (key, info)
         # dense tensors: wire cast -> (W = 1 allreduce) -> compensate(accumulate=False)
         src = dense_host[s % 2].astype(np.float16).astype(np.float32) if fp16 else dense_host[s % 2]
         want = O.compensate(src, dense_m, None, 0.9, nest, accumulate=False)
         assert np.array_equal(bits(run.dense_out.cpu().numpy()), bits(want)), (workload, s)
-        print(f"{workload} step {s}: branches so far {branches}, exact resamples {exact} "
+        print(f"{workload} step {s}: branches so far {branches}, resamples exact {exact} / set {as_set} "
               f"(max {resample_max} candidates), steps with full passes {full_pass_steps}", file=sys.stderr,
               flush=True)
     # the flushed state at the end equals the oracle's
@@ -112,5 +122,5 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
         m_o, v_o = state[t]
         assert np.array_equal(bits(b.velocity_of(name).reshape(-1).cpu().numpy()), bits(v_o)), name
         assert np.array_equal(bits(b.momentum_of(name).reshape(-1).cpu().numpy()), bits(m_o)), name
-    # the bench's dynamics were exercised: exact resample replays and full select passes
-    assert exact > 0 and full_pass_steps > 0, (branches, exact, full_pass_steps)
+    # the bench's dynamics were exercised: resamples (set path) and full select passes
+    assert as_set > 0 and full_pass_steps > 0, (branches, exact, as_set, full_pass_steps)
