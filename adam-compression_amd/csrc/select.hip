@@ -77,7 +77,16 @@ constexpr int kSpillDiv = 32;                   // lists dropped when > nseg/32 
 constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgroup
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
 constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
-constexpr float kSpecMarginMax = 0.95f;         // the adaptive list margin's ceiling (k_sel_finish)
+constexpr float kSpecMarginMax = 0.95f;
+// K5s, the set path of an untied resample (resample_order = 1; see k_resample_set)
+constexpr int kSetReg = 32;                  // one workgroup: keys per thread kept in registers
+constexpr int kSetRounds = 256;              // one workgroup up to kSetRounds x 1024 candidates
+constexpr int64_t kSetMax = (int64_t)kSetRounds * 1024;
+constexpr int kBigSlice = 32768;             // above: slices of this many candidates per workgroup
+constexpr int kBigSlices = 256;              //   up to this many slices (8M candidates)
+constexpr int kBigMax = 8;                   //   for up to this many tensors of a call
+constexpr int kBigBuf = 65536;               //   keys of the k-th key's coarse bin gathered
+constexpr int kBigShift = 12;                //   coarse bins of 4096 key units above t_cur         // the adaptive list margin's ceiling (k_sel_finish)
 constexpr int kSpecWords = 4;                   // per-tensor speculation state (dgc_compress_begin: spec)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
 
@@ -100,6 +109,7 @@ struct TDesc {
     double inv_stride;
     float inv_stride_f;
     int32_t tail;           // the elements [4*nv4, n) are compensated outside K1 (unpadded)
+    int32_t big;            // its K5s multi-workgroup set state (BigSetWS index), -1: none
 };
 
 struct SelState {
@@ -131,6 +141,18 @@ struct SelState {
     // slot [epoch & 1] like spill (the count runs past win_cap when the list overflows).
     uint32_t win_cnt[2];
     unsigned long long lower_cnt[kMaxLower + 1];   // counts at t_1..t_m (multi-threshold pass)
+};
+
+// K5s over several workgroups (k_bigset_*): one per tensor with d.big >= 0. Zero at
+// rest where noted (the workspace is zero-filled at init).
+struct BigSetWS {
+    uint32_t hist[kRsBins];           // coarse histogram (zero at rest: k_bigset_select re-zeroes it)
+    uint32_t slice_cnt[kBigSlices];   // per slice: keys above the k-th key's coarse bin, then its payload base
+    uint32_t bufn;                    // keys gathered from that bin (reset by k_bigset_hist)
+    int32_t ok;                       // the set path runs (1) or leaves the tensor to the replay (0)
+    uint32_t b0, a0;                  // the coarse bin and the keys above it
+    uint32_t kth;                     // the k-th largest key
+    long long obase;                  // the tensor's first payload slot
 };
 
 // Per-call settings shared by the tensors.
@@ -170,6 +192,7 @@ struct SelWS {
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
+    BigSetWS* bigset;          // [nbig] K5s over several workgroups
     uint32_t* fin_ticket;      // k_nth_select's last-workgroup ticket (zeroed by sel_init_tensor)
     int64_t nseg, ngrp;
 };
@@ -198,6 +221,8 @@ struct Layout {
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool tail_any = false;      // some tensor is compensated partly outside K1 (unpadded tail)
     int64_t grid[BT_COUNT] = {};
+    int32_t nbig = 0;           // tensors whose candidates may exceed one workgroup's set path
+    int32_t big[kBigMax] = {};
 };
 
 // Capped grids serve the launches that are most likely gated no-ops (the list count
@@ -263,6 +288,11 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         L.max_cand = std::max(L.max_cand, d.cand_cap);
         d.gpos_off = gpos;
         gpos += 2 * (d.cand_cap / 2 + 1);
+        d.big = -1;
+        if (d.cand_cap > kSetMax && d.cand_cap <= (int64_t)kBigSlices * kBigSlice && L.nbig < kBigMax) {
+            d.big = L.nbig;
+            L.big[L.nbig++] = t;
+        }
         d.idx_base = T > 1 ? d.off : 0;
         d.nv4 = padded ? ceil_div(d.n, (int64_t)4) : d.n / 4;
         d.tail = (!padded && (d.n & 3)) ? 1 : 0;
@@ -324,6 +354,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.cand_idx = c.take<int64_t>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
     w.nthg = c.take<NthG>(L.T);
+    w.bigset = c.take<BigSetWS>(L.nbig);
     w.fin_ticket = c.take<uint32_t>(16);
     if (bytes) *bytes = c.bytes();
     return w;
@@ -2306,9 +2337,6 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // wave's ballot count goes to LDS, one workgroup scan over the (round, wave) counts
 // gives each its base, and each selected entry is emitted at base + its rank in the
 // ballot — with the wire casts and the masking of the K5 emit.
-constexpr int kSetReg = 32;                  // keys per thread kept in registers
-constexpr int kSetRounds = 256;              // the set path up to kSetRounds x 1024 candidates
-constexpr int64_t kSetMax = (int64_t)kSetRounds * kScanThreads;
 
 __global__ void __launch_bounds__(kScanThreads)
 k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
@@ -2468,6 +2496,279 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     if (tid == 0) {
         st->rs_nth = 3;   // K5's replay and emit skip the tensor
         st->tie_rule = DGC_TIES_SET;
+    }
+}
+
+// ---------------------------------------------------------------- K5s over several workgroups
+// The set path for candidate counts above one workgroup's kSetMax (VGG-16-BN's fc6:
+// up to 64k = 6.5M candidates), in slices of kBigSlice candidates, one workgroup each:
+//   k_bigset_hist    coarse histogram of key - key(t_cur) in 4096-unit bins (the
+//                    candidates are >= t_cur; 2048 bins = the octave above it, the last
+//                    one open-ended), LDS then agent atomics into hist
+//   k_bigset_gather  every workgroup picks the coarse bin b0 of the k-th largest from the
+//                    histogram; counts its slice's keys above b0 and gathers the keys in
+//                    b0 (key, position) into the tensor's K5 pair-slot region
+//   k_bigset_select  one workgroup per tensor: hist re-zeroed for the next call; the exact
+//                    k-th key among the gathered ones (one 4096-bin pass: b0 spans 4096
+//                    key values), the tie check, the slices' payload bases
+//   k_bigset_emit    each slice emits its keys >= the k-th in index order
+// b0 the open-ended bin, more than kBigBuf keys in b0, or a tie across the boundary:
+// the tensor is left to the exact replay (ok = 0), as in k_resample_set.
+struct BigList {
+    int32_t n;
+    int32_t t[kBigMax];
+};
+
+template <int NT>
+__device__ __forceinline__ uint32_t block_exscan_n(uint32_t v, uint32_t* lds, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan<DppAdd>(v);
+    if (lane == 63) lds[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) {
+        const uint32_t x = lds[i];
+        wbase += i < wid ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + incl - v;
+}
+
+// pick_bin_small for NT threads of PER bins each (bins = PER x NT, counts in LDS)
+template <int PER, int NT>
+__device__ __forceinline__ bool pick_bin_n(const uint32_t* h, uint32_t k, uint32_t* lds, int* bin, uint32_t* above) {
+    constexpr int bins = PER * NT;
+    const int t = threadIdx.x;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        c[j] = h[bins - 1 - (PER * t + j)];
+        sum += c[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exscan_n<NT>(sum, lds, &total);
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!hit && run < k && k <= run + c[j]) {
+            hit = true;
+            *bin = bins - 1 - (PER * t + j);
+            *above = run;
+        }
+        run += c[j];
+    }
+    return hit;
+}
+
+// The tensor of launch row j if its resample takes the multi-workgroup set path now.
+__device__ __forceinline__ int bigset_task(const SelWS& w, const BigList& bl, int j, int64_t& cnt) {
+    if (j >= bl.n) return -1;
+    const int t = bl.t[j];
+    const SelState* st = w.st + t;
+    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return -1;
+    cnt = st->n_cur;
+    if (cnt <= kSetMax || cnt > (int64_t)kBigSlices * kBigSlice || cnt <= w.td[t].k) return -1;
+    return t;
+}
+
+__device__ __forceinline__ uint32_t bigset_bin(uint32_t key, uint32_t tkey) {
+    const uint32_t v = (key - tkey) >> kBigShift;
+    return v < (uint32_t)kRsBins - 1 ? v : (uint32_t)kRsBins - 1;
+}
+
+__global__ void __launch_bounds__(kBlock) k_bigset_hist(SelWS w, BigList bl) {
+    int64_t cnt;
+    const int t = bigset_task(w, bl, blockIdx.y, cnt);
+    if (t < 0) return;   // uniform per workgroup
+    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
+    if ((int64_t)blockIdx.x >= nsl) return;
+    const TDesc d = w.td[t];
+    const SelState* st = w.st + t;
+    BigSetWS& b = w.bigset[d.big];
+    const uint32_t tkey = abs_key(st->t_cur);
+    __shared__ uint32_t h[kRsBins];
+    for (int i = threadIdx.x; i < kRsBins; i += kBlock) h[i] = 0;
+    __syncthreads();
+    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
+#pragma unroll 8
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[bigset_bin(qw[2 * i + 1], tkey)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kRsBins; i += kBlock)
+        if (h[i]) atomicAdd(&b.hist[i], h[i]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) b.bufn = 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
+    int64_t cnt;
+    const int t = bigset_task(w, bl, blockIdx.y, cnt);
+    if (t < 0) return;
+    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
+    if ((int64_t)blockIdx.x >= nsl) return;
+    const TDesc d = w.td[t];
+    const SelState* st = w.st + t;
+    BigSetWS& b = w.bigset[d.big];
+    const uint32_t tkey = abs_key(st->t_cur);
+    __shared__ uint32_t h[kRsBins];
+    __shared__ uint32_t lds[kBlock / kWave];
+    __shared__ int sel;
+    __shared__ uint32_t sel_above;
+    for (int i = threadIdx.x; i < kRsBins; i += kBlock) h[i] = b.hist[i];
+    if (threadIdx.x == 0) sel = -1;
+    __syncthreads();
+    int bin;
+    uint32_t above;
+    if (pick_bin_n<kRsBins / kBlock, kBlock>(h, (uint32_t)d.k, lds, &bin, &above)) {
+        sel = bin;
+        sel_above = above;
+    }
+    __syncthreads();
+    const int b0 = sel;
+    const bool ok = b0 >= 0 && b0 < kRsBins - 1 && h[b0] <= (uint32_t)kBigBuf;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        b.ok = ok ? 1 : 0;
+        b.b0 = (uint32_t)b0;
+        b.a0 = sel_above;
+    }
+    if (!ok) return;   // uniform
+    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    DGC_GLB uint32_t* buf = glb(w.gpos + d.gpos_off);   // (key, position) pairs; the replay's pair slots
+    const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
+    const int lane = threadIdx.x & 63;
+    uint32_t above_cnt = 0;
+#pragma unroll 4
+    for (int64_t i0 = lo; i0 < hi; i0 += kBlock) {   // uniform trip count
+        const int64_t i = i0 + threadIdx.x;
+        const uint32_t key = i < hi ? qw[2 * i + 1] : 0u;
+        const uint32_t bb = bigset_bin(key, tkey);
+        above_cnt += i < hi && bb > (uint32_t)b0;
+        const bool in = i < hi && bb == (uint32_t)b0;
+        const uint64_t m = __ballot(in);
+        if (m) {
+            uint32_t slot = 0;
+            if (lane == 0) slot = atomicAdd(&b.bufn, (uint32_t)__popcll(m));
+            slot = __shfl(slot, 0) + mbcnt64(m, 0u);
+            if (in && slot < (uint32_t)kBigBuf) {
+                buf[2 * slot] = key;
+                buf[2 * slot + 1] = (uint32_t)i;
+            }
+        }
+    }
+    uint32_t tot;
+    block_exscan_n<kBlock>(above_cnt, lds, &tot);
+    if (threadIdx.x == 0) b.slice_cnt[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_bigset_select(SelWS w, BigList bl) {
+    int64_t cnt;
+    const int t = bigset_task(w, bl, blockIdx.x, cnt);
+    if (t < 0) return;
+    const TDesc d = w.td[t];
+    SelState* st = w.st + t;
+    BigSetWS& b = w.bigset[d.big];
+    for (int i = threadIdx.x; i < kRsBins; i += kScanThreads) b.hist[i] = 0;   // read by k_bigset_gather
+    if (!b.ok) return;
+    constexpr int kBins = 4096;   // the coarse bin's 4096 key values, one pass
+    __shared__ uint32_t h[kBins];
+    __shared__ uint32_t sc[kBigSlices];
+    __shared__ uint32_t lds32[16];
+    __shared__ int sel;
+    __shared__ uint32_t sel_above, sel_cnt;
+    __shared__ long long ob_s;
+    const int tid = threadIdx.x;
+    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
+    const uint32_t n0 = b.bufn, a0 = b.a0;
+    const uint32_t k = (uint32_t)d.k;
+    const uint32_t base_key = abs_key(st->t_cur) + (b.b0 << kBigShift);
+    const DGC_GLB uint32_t* buf = glb(w.gpos + d.gpos_off);
+    for (int i = tid; i < kBins; i += kScanThreads) h[i] = 0;
+    for (int i = tid; i < kBigSlices; i += kScanThreads) sc[i] = 0;
+    if (tid == 0) sel = -1;
+    __syncthreads();
+    const bool fits = n0 <= (uint32_t)kBigBuf && a0 < k && k - a0 <= n0;
+    if (fits)
+        for (uint32_t i = tid; i < n0; i += kScanThreads) atomicAdd(&h[buf[2 * i] - base_key], 1u);
+    __syncthreads();
+    int bin;
+    uint32_t above;
+    if (fits && pick_bin_small<kBins / kScanThreads>(h, k - a0, lds32, &bin, &above)) {
+        sel = bin;
+        sel_above = above;
+        sel_cnt = h[bin];
+    }
+    __syncthreads();
+    // tied across the boundary (or nothing found): the exact replay
+    if (sel < 0 || sel_cnt != k - a0 - sel_above) {
+        if (tid == 0) b.ok = 0;
+        return;
+    }
+    const uint32_t kth = base_key + (uint32_t)sel;
+    // each slice's selected keys: those above b0 plus its gathered keys >= kth
+    for (uint32_t i = tid; i < n0; i += kScanThreads)
+        if (buf[2 * i] >= kth) atomicAdd(&sc[buf[2 * i + 1] / kBigSlice], 1u);
+    if (tid < kWave) {
+        const long long o = out_base(w, t);
+        if (tid == 0) ob_s = o;
+    }
+    __syncthreads();
+    uint32_t mine = tid < nsl ? sc[tid] + b.slice_cnt[tid] : 0u;   // nsl <= kBigSlices <= kScanThreads
+    uint32_t total;
+    const uint32_t base = block_exclusive_scan32(mine, lds32, &total);
+    if (tid < nsl) b.slice_cnt[tid] = base;
+    if (tid == 0) {
+        b.kth = kth;
+        b.obase = ob_s;
+        st->rs_nth = 3;   // K5's replay and emit skip the tensor; k_bigset_emit writes it
+        st->tie_rule = DGC_TIES_SET;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o) {
+    const int j = blockIdx.y;
+    if (j >= bl.n) return;
+    const int t = bl.t[j];
+    const SelState* st = w.st + t;
+    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 3) return;
+    const TDesc d = w.td[t];
+    const BigSetWS& b = w.bigset[d.big];
+    const int64_t cnt = st->n_cur;
+    if (!b.ok || cnt <= kSetMax) return;   // the one-workgroup path emitted it
+    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
+    if ((int64_t)blockIdx.x >= nsl) return;
+    const uint32_t kth = b.kth;
+    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    const float* vec = vec_flat + d.off;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int kW = kBlock / kWave;
+    __shared__ uint32_t wc[kW];
+    // each wave a contiguous quarter of the slice, 64 keys per round
+    const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
+    const int64_t q = ceil_div(hi - lo, (int64_t)kW);
+    const int64_t qlo = lo + wv * q, qhi = qlo + q < hi ? qlo + q : hi;
+    uint32_t c = 0;
+#pragma unroll 8
+    for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
+        const int64_t i = i0 + lane;
+        c += (uint32_t)__popcll(__ballot(i < qhi && qw[2 * i + 1] >= kth));
+    }
+    if (lane == 0) wc[wv] = c;
+    __syncthreads();
+    long long pos = b.obase + b.slice_cnt[blockIdx.x];
+    for (int i = 0; i < wv; ++i) pos += wc[i];
+#pragma unroll 4
+    for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
+        const int64_t i = i0 + lane;
+        const bool sel = i < qhi && qw[2 * i + 1] >= kth;
+        const uint64_t m = __ballot(sel);
+        if (sel) {
+            const int64_t li = w.cand_idx[d.cand_off + i];
+            emit_one(o, d, pos + mbcnt64(m, 0u), li, vec[li]);
+        }
+        pos += __popcll(m);
     }
 }
 
@@ -2683,6 +2984,23 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
             hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o);
             DGC_LAUNCHED();
+            if (L.nbig > 0) {   // candidate counts above one workgroup's: sliced over workgroups
+                BigList bl{};
+                bl.n = L.nbig;
+                int64_t maxcap = 0;
+                for (int j = 0; j < L.nbig; ++j) bl.t[j] = L.big[j];
+                maxcap = L.max_cand;
+                const dim3 g((unsigned)std::min<int64_t>(ceil_div(maxcap, (int64_t)kBigSlice), kBigSlices),
+                             (unsigned)L.nbig);
+                hipLaunchKernelGGL(k_bigset_hist, g, dim3(kBlock), 0, s, w, bl);
+                DGC_LAUNCHED();
+                hipLaunchKernelGGL(k_bigset_gather, g, dim3(kBlock), 0, s, w, bl);
+                DGC_LAUNCHED();
+                hipLaunchKernelGGL(k_bigset_select, dim3((unsigned)L.nbig), dim3(kScanThreads), 0, s, w, bl);
+                DGC_LAUNCHED();
+                hipLaunchKernelGGL(k_bigset_emit, g, dim3(kBlock), 0, s, vec, w, bl, o);
+                DGC_LAUNCHED();
+            }
         }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
         if (G > 1) {
@@ -3035,6 +3353,7 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_batch_init: workspace needs %zu bytes, 256-B aligned", need);
     SelWS w = carve_select(ws, L);
     DGC_HIP(hipMemsetAsync(w.st, 0, sizeof(SelState) * L.T, s));
+    if (L.nbig) DGC_HIP(hipMemsetAsync(w.bigset, 0, sizeof(BigSetWS) * L.nbig, s));   // zero at rest
     DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
     for (int which = 0; which < BT_COUNT; ++which)
         DGC_HIP(hipMemcpyAsync(w.bt[which], bt[which].data(), sizeof(int32_t) * (L.T + 1), hipMemcpyHostToDevice, s));

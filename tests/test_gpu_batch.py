@@ -259,3 +259,47 @@ def test_batch_index_order_equals_topk_order():
         assert torch.equal(bs[0].velocity_of(name).view(torch.int32), bs[1].velocity_of(name).view(torch.int32))
         assert torch.equal(bs[0].momentum_of(name).view(torch.int32), bs[1].momentum_of(name).view(torch.int32))
     assert sets > 0
+
+
+@pytest.mark.timeout(600)
+def test_batch_index_order_big_resample():
+    """The multi-workgroup set path (k_bigset_*: more candidates than one workgroup's
+    262144) against the exact replay: a 20M-element tensor (k = 20000, up to 64k = 1.28M
+    candidates) stepped with two alternating gradient sets until its resamples pass
+    262144 candidates — the same sets, outputs and state as resample_order="topk"."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc.batch import DGCBatch
+    shapes = [("big", (20_000_000,)), ("small", (300, 1000))]
+    bs = [DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, device=DEV, seed=5, resample_order=o)
+          for o in ("index", "topk")]
+    gen = torch.Generator(device=DEV)
+    big_sets = 0
+    for s in range(16):
+        gen.manual_seed(77 + s % 2)
+        g = torch.zeros(bs[0].flat_numel, device=DEV)
+        for off, n in zip(bs[0].offsets, bs[0].numels):
+            g[off: off + n] = torch.randn(n, generator=gen, device=DEV) * 1e-3
+        outs = []
+        for b in bs:
+            b.grad_flat.copy_(g)
+            b.compress()
+            outs.append(b.decompress().clone())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), s
+        ia, it = bs[0].infos(), bs[1].infos()
+        sa, st = bs[0].transmitted(), bs[1].transmitted()
+        for t, name in enumerate(bs[0].names):
+            assert ia[t]["branch"] == it[t]["branch"] and ia[t]["candidates"] == it[t]["candidates"], (s, name)
+            if ia[t]["tie_rule"] == "set":
+                big_sets += ia[t]["candidates"] > 262144
+                oi = st[name][1].cpu().numpy()
+                o = np.argsort(oi, kind="stable")
+                assert np.array_equal(sa[name][1].cpu().numpy(), oi[o]), (s, name)
+                assert np.array_equal(bits(sa[name][0].cpu().numpy()), bits(st[name][0].cpu().numpy()[o])), (s, name)
+            else:
+                assert torch.equal(sa[name][1], st[name][1]), (s, name)
+    for name in bs[0].names:
+        assert torch.equal(bs[0].velocity_of(name).view(torch.int32), bs[1].velocity_of(name).view(torch.int32))
+        assert torch.equal(bs[0].momentum_of(name).view(torch.int32), bs[1].momentum_of(name).view(torch.int32))
+    assert big_sets > 0
