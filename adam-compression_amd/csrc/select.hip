@@ -1930,38 +1930,30 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             r.list_threshold = w.spec ? w.spec[kSpecWords * t] : __builtin_huge_valf();   // (updated below)
         }
         if (w.spec) {
-            // spec[0]: next call's list threshold = m x (predicted final threshold), from
-            //   the SAMPLED threshold t0 = thr[t] (spec[1]: the previous call's) and the
-            //   final one t: prediction = t0 x growth x r, growth = 2 - spec[1] / t0 (linear
-            //   extrapolation of the t0 series) clamped to [1, 1.5], r = min(t / t0, spec[2])
-            //   (spec[2]: the previous call's t / t0). The t0 series is smooth where the
-            //   final one zigzags: a model set's tensors lower their threshold to 0.8 t0
-            //   every other step (the synthetic velocities turn bimodal), and extrapolating
-            //   the finals put the lists above the lowered threshold — two full passes over
-            //   vec for ~20 of ResNet-50's 54 tensors per step; with the lower of the last two
-            //   ratios the lists hold the lowered threshold's candidates. A flat bucket never
-            //   lowers (t = t0, r = 1): the same prediction as the final-threshold series.
-            //   The accumulating velocity's threshold grows ~linearly (the ratio
-            //   extrapolation overshot). The margin m adapts: after a call whose threshold
-            //   landed at or above its list threshold (a hit), m = 1.05 x that call's
-            //   list/final ratio, within [margin, kSpecMarginMax] — the lists shrink towards
-            //   the selection while the threshold moves predictably (at 1B on the bench's
-            //   dynamics 4 % of the elements at 0.8 vs 0.7 % at 0.95); a miss (the threshold
-            //   fell below it: a full select pass ran) resets m to margin.
+            // spec[0]: next call's list threshold = m x t x growth, growth = 2 - spec[1] / t
+            //   (linear extrapolation from the previous final threshold spec[1]) clamped to
+            //   [1, 1.5]; spec[1] := t. The ratio t / spec[1] overshoots while the growth
+            //   decelerates (the accumulating velocity's threshold grows ~linearly). The
+            //   margin m adapts: after a call whose threshold landed at or above its list
+            //   threshold (a hit), m = 1.05 x that call's list/final ratio, within [margin,
+            //   kSpecMarginMax] — the lists shrink towards the selection while the threshold
+            //   moves predictably (at 1B on the bench's dynamics 4 % of the elements at 0.8
+            //   vs 0.7 % at 0.95); a miss (the threshold fell below it: a full select pass
+            //   ran) resets m to margin. A prediction from the SAMPLED threshold series, with
+            //   the lower of the last two final/sampled ratios (lists that hold a lowered
+            //   threshold's candidates), was measured and dropped: on ResNet-50 its longer
+            //   lists cost the list counts and the lowering 23 + 14 + 25 us where these take
+            //   14 + 5 + 5, and the full passes stayed (same box, 0.372 vs 0.337 ms/step).
             float* spec = w.spec + kSpecWords * t;
-            const float tc = st->t_cur, t0 = st->t0;
+            const float tc = st->t_cur;
             const float used = spec[0];
-            const bool finite = tc == tc && tc > 0.f && tc < __builtin_huge_valf() && t0 == t0 && t0 > 0.f &&
-                                t0 < __builtin_huge_valf();
-            const float gr = fminf(fmaxf(2.f - spec[1] / t0, 1.f), 1.5f);   // first call: 2 - inf -> 1
-            const float r = finite ? tc / t0 : 1.f;
-            const float rp = fminf(r, spec[2]);                             // first call: min(r, inf)
+            const bool finite = tc == tc && tc > 0.f && tc < __builtin_huge_valf();
+            const float gr = fminf(fmaxf(2.f - spec[1] / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
             float m = margin;
             if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
                 m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
-            spec[0] = finite ? t0 * gr * rp * m : __builtin_huge_valf();
-            spec[1] = finite ? t0 : __builtin_huge_valf();
-            spec[2] = finite ? r : __builtin_huge_valf();
+            spec[0] = finite ? tc * m * gr : __builtin_huge_valf();
+            spec[1] = finite ? tc : __builtin_huge_valf();
         }
     }
     __syncthreads();
@@ -2338,6 +2330,8 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // gives each its base, and each selected entry is emitted at base + its rank in the
 // ballot — with the wire casts and the masking of the K5 emit.
 
+constexpr int kSetLds = 32;   // rounds of keys kept in LDS after the register rounds (128 KB)
+
 __global__ void __launch_bounds__(kScanThreads)
 k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const int t = blockIdx.x;
@@ -2350,6 +2344,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     const uint32_t k = (uint32_t)d.k;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int kWaves = kScanThreads / kWave;
+    constexpr int kReg = kSetReg + kSetLds;   // rounds held on chip
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t lds32[16];
     __shared__ uint32_t red[2][kWaves];
@@ -2357,32 +2352,43 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     __shared__ int sel_bin;
     __shared__ uint32_t rbase[kSetRounds * kWaves];
     __shared__ long long obase_s;
+    __shared__ uint32_t kl[kSetLds * kScanThreads];   // rounds kSetReg .. kReg - 1
     // queue entry i = tid + r * 1024 (coalesced high-word loads); its key
     const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
-    auto key_at = [&](int i) -> uint32_t { return qw[2 * i + 1]; };
+    auto key_at = [&](int i) -> uint32_t { return i < n ? qw[2 * i + 1] : 0u; };
     const int rounds = (n + kScanThreads - 1) / kScanThreads;
     uint32_t key[kSetReg];
 #pragma unroll
-    for (int r = 0; r < kSetReg; ++r) {
-        const int i = tid + r * kScanThreads;
-        key[r] = i < n ? key_at(i) : 0u;
+    for (int r = 0; r < kSetReg; ++r) key[r] = key_at(tid + r * kScanThreads);
+    // the LDS rounds: 8 loads in flight per thread
+    for (int r0 = kSetReg; r0 < kReg && r0 < rounds; r0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = r0 + u < rounds ? key_at(tid + (r0 + u) * kScanThreads) : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kl[(r0 + u - kSetReg) * kScanThreads + tid] = v[u];
     }
-    // every key of this thread: registers, then L2 (uniform loop bounds)
+    // every key of this thread with its round (uniform loop bounds): registers, LDS, then
+    // L2 in batches of 8 loads in flight (n > 64K only)
     auto for_keys = [&](auto fn) {
 #pragma unroll
-        for (int r = 0; r < kSetReg; ++r) {
-            const int i = tid + r * kScanThreads;
-            if (i < n) fn(key[r]);
-        }
-        for (int r = kSetReg; r < rounds; ++r) {
-            const int i = tid + r * kScanThreads;
-            if (i < n) fn(key_at(i));
+        for (int r = 0; r < kSetReg; ++r) fn(r, key[r]);
+        for (int r = kSetReg; r < kReg && r < rounds; ++r) fn(r, kl[(r - kSetReg) * kScanThreads + tid]);
+        for (int r0 = kReg; r0 < rounds; r0 += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = r0 + u < rounds ? key_at(tid + (r0 + u) * kScanThreads) : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (r0 + u < rounds) fn(r0 + u, v[u]);
         }
     };
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
-    for_keys([&](uint32_t x) {
-        mn = x < mn ? x : mn;
-        mx = x > mx ? x : mx;
+    for_keys([&](int r, uint32_t x) {
+        if (tid + r * kScanThreads < n) {
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+        }
     });
     mn = wave_min_u32(mn);
     mx = wave_max(mx);
@@ -2412,9 +2418,10 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     while (!found) {
         const int lo = hi > 11 ? hi - 11 : 0;
         const uint32_t pre = prefix;
-        for_keys([&](uint32_t x) {
+        for_keys([&](int r, uint32_t x) {
             const uint32_t v = x - mn;
-            if (hi >= 32 || (v >> hi) == pre) atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
+            if (tid + r * kScanThreads < n && (hi >= 32 || (v >> hi) == pre))
+                atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
         });
         __syncthreads();
         if (tid == 0) sel_bin = -1;
@@ -2447,15 +2454,10 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     // only torch's exact order of operations knows which ones — the replay
     if (eq != k_rem) return;
     // order-preserving compaction: (round, wave) counts, one scan, ranks from ballots
-    auto count_round = [&](int r, uint32_t x) {   // uniform in r
-        const int i = tid + r * kScanThreads;
-        const uint32_t c = (uint32_t)__popcll(__ballot(i < n && x >= kth));
+    for_keys([&](int r, uint32_t x) {   // uniform in r
+        const uint32_t c = (uint32_t)__popcll(__ballot(tid + r * kScanThreads < n && x >= kth));
         if (lane == 0) rbase[r * kWaves + wv] = c;
-    };
-#pragma unroll
-    for (int r = 0; r < kSetReg; ++r)
-        if (r < rounds) count_round(r, key[r]);
-    for (int r = kSetReg; r < rounds; ++r) count_round(r, tid + r * kScanThreads < n ? key_at(tid + r * kScanThreads) : 0u);
+    });
     if (wv == 0) {
         const long long b = out_base(w, t);
         if (lane == 0) obase_s = b;
@@ -2478,21 +2480,37 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         }
     }
     __syncthreads();
+    // the selected queue positions in output order into the tensor's pair-slot region
+    // (free on this path): plain stores, no load waits on them; then the emit reads them
+    // back with every slot's loads independent (a per-round emit waited for the index
+    // and value gathers of each round in turn: two dependent round trips per 1024 keys)
+    DGC_GLB uint32_t* spos = glb(w.gpos + d.gpos_off);
+    for_keys([&](int r, uint32_t x) {   // uniform in r
+        const bool sel = tid + r * kScanThreads < n && x >= kth;
+        const uint64_t m = __ballot(sel);
+        if (sel) spos[rbase[r * kWaves + wv] + mbcnt64(m, 0u)] = (uint32_t)(tid + r * kScanThreads);
+    });
+    __threadfence_block();
+    __syncthreads();
     const long long ob = obase_s;
     const float* vec = vec_flat + d.off;
-    auto emit_round = [&](int r, uint32_t x) {   // uniform in r
-        const int i = tid + r * kScanThreads;
-        const bool sel = i < n && x >= kth;
-        const uint64_t m = __ballot(sel);
-        if (sel) {
-            const int64_t li = w.cand_idx[d.cand_off + i];
-            emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(m, 0u), li, vec[li]);
-        }
-    };
+    const int64_t* cand = w.cand_idx + d.cand_off;
+    for (uint32_t q0 = 0; q0 < k; q0 += 4 * kScanThreads) {
+        int64_t li[4];
+        float x[4];
 #pragma unroll
-    for (int r = 0; r < kSetReg; ++r)
-        if (r < rounds) emit_round(r, key[r]);
-    for (int r = kSetReg; r < rounds; ++r) emit_round(r, tid + r * kScanThreads < n ? key_at(tid + r * kScanThreads) : 0u);
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t q = q0 + u * kScanThreads + tid;
+            li[u] = q < k ? cand[spos[q]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = q0 + u * kScanThreads + tid < k ? vec[li[u]] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t q = q0 + u * kScanThreads + tid;
+            if (q < k) emit_one(o, d, ob + q, li[u], x[u]);
+        }
+    }
     if (tid == 0) {
         st->rs_nth = 3;   // K5's replay and emit skip the tensor
         st->tie_rule = DGC_TIES_SET;

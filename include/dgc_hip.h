@@ -206,12 +206,11 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
  * >= spec[0] and few segment lists overflowed, every count and selection is served
  * from the lists and the separate re-read of vec is skipped; otherwise one full pass
  * runs. Results are identical either way (spec only chooses the work).
- * On return spec[1] = the sampled threshold t0, spec[2] = t / t0 (t the final threshold)
- * and spec[0] = m x t0 x growth x min(t / t0, previous t / t0), growth = 2 -
- * (previous t0) / t0 (linear extrapolation) clamped to [1, 1.5]; m = spec_margin (0.8
+ * On return spec[1] = the final threshold t and spec[0] = m x t x growth, growth =
+ * 2 - (previous t) / t (linear extrapolation) clamped to [1, 1.5]; m = spec_margin (0.8
  * is a good one) after a call whose t fell below its list threshold, else 1.05 x (list
  * threshold / t) of that call, within [spec_margin, 0.95]: the lists shrink while t
- * moves predictably.
+ * moves predictably. spec[2..3] are reserved.
  * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
  * one workspace and must see the same sample_start/stride/params. The workspace
  * carries per-tensor state from call to call (a deferred masking, the K1 list-spill

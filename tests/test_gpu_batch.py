@@ -261,25 +261,51 @@ def test_batch_index_order_equals_topk_order():
     assert sets > 0
 
 
+def designed_big_gradient(n, k, stride, start, seed):
+    """A gradient whose resample has more candidates than one workgroup's set path, its
+    k-th largest magnitude untied and within an octave above the threshold: k distinct
+    magnitudes 1.2 + i * 2e-7 at positions the strided sample (start, stride) misses, a
+    plateau of 500k magnitudes exactly 1.0, N(0, 1e-3) elsewhere, random signs. The
+    samples see only the plateau, so the threshold is 1.0 and its count (~520k) passes
+    1.3k: resample over ~520k candidates, whose top k are the distinct ones."""
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=g) * 1e-3
+    off = (start + stride // 2) % stride                      # a residue the samples never hit
+    slots = torch.arange(off, n, stride)
+    big = slots[torch.randperm(slots.numel(), generator=g)[:k]]
+    x[big] = 1.2 + torch.arange(k, dtype=torch.float64).mul(2e-7).float()
+    rest = torch.ones(n, dtype=torch.bool)
+    rest[big] = False
+    cand = rest.nonzero().view(-1)
+    x[cand[torch.randperm(cand.numel(), generator=g)[:500_000]]] = 1.0
+    sign = torch.randint(0, 2, (n,), generator=g).float().mul(2).sub(1)
+    return x * sign
+
+
 @pytest.mark.timeout(600)
 def test_batch_index_order_big_resample():
     """The multi-workgroup set path (k_bigset_*: more candidates than one workgroup's
     262144) against the exact replay: a 20M-element tensor (k = 20000, up to 64k = 1.28M
-    candidates) stepped with two alternating gradient sets until its resamples pass
-    262144 candidates — the same sets, outputs and state as resample_order="topk"."""
+    candidates) whose first gradient (``designed_big_gradient``) resamples over ~520k
+    candidates, then random steps — the same sets, outputs and state as
+    resample_order="topk"."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    import random
     from dgc.batch import DGCBatch
     shapes = [("big", (20_000_000,)), ("small", (300, 1000))]
     bs = [DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, device=DEV, seed=5, resample_order=o)
           for o in ("index", "topk")]
+    k, _, _, stride = bs[0].attrs[0]
+    start = random.Random(5).randint(0, stride - 1)   # the batch's first draw: tensor 0's sample start
     gen = torch.Generator(device=DEV)
     big_sets = 0
-    for s in range(16):
-        gen.manual_seed(77 + s % 2)
-        g = torch.zeros(bs[0].flat_numel, device=DEV)
-        for off, n in zip(bs[0].offsets, bs[0].numels):
-            g[off: off + n] = torch.randn(n, generator=gen, device=DEV) * 1e-3
+    for s in range(3):
+        gen.manual_seed(77 + s)
+        g = torch.randn(bs[0].flat_numel, generator=gen, device=DEV) * 1e-3
+        if s == 0:
+            g[bs[0].offsets[0]: bs[0].offsets[0] + bs[0].numels[0]] = \
+                designed_big_gradient(bs[0].numels[0], k, stride, start, 100).to(DEV)
         outs = []
         for b in bs:
             b.grad_flat.copy_(g)
@@ -299,6 +325,9 @@ def test_batch_index_order_big_resample():
                 assert np.array_equal(bits(sa[name][0].cpu().numpy()), bits(st[name][0].cpu().numpy()[o])), (s, name)
             else:
                 assert torch.equal(sa[name][1], st[name][1]), (s, name)
+        if s == 0:   # the designed step: a resample of ~520k candidates through the set path
+            assert ia[0]["branch"] == "resample" and ia[0]["candidates"] > 262144, ia[0]
+            assert ia[0]["tie_rule"] == "set", ia[0]
     for name in bs[0].names:
         assert torch.equal(bs[0].velocity_of(name).view(torch.int32), bs[1].velocity_of(name).view(torch.int32))
         assert torch.equal(bs[0].momentum_of(name).view(torch.int32), bs[1].momentum_of(name).view(torch.int32))
