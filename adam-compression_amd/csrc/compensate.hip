@@ -32,7 +32,7 @@ namespace dgc {
 template <bool NEST, bool ACC, bool SAMPLE>
 __global__ void __launch_bounds__(kBlock)
 k_compensate4(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __restrict__ vec,
-              float4* __restrict__ out, int64_t n4, float mom, SampleSpec sp) {
+              float4* __restrict__ out, int64_t n4, float mom, SampleSpec sp, int wt) {
     const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (v >= n4) return;
     const float4 gv = ld_nt(g + v);
@@ -43,11 +43,11 @@ k_compensate4(const float4* __restrict__ g, float4* __restrict__ mmt, float4* __
     ov.y = comp1<NEST, ACC>(gv.y, mv.y, vv.y, mom);
     ov.z = comp1<NEST, ACC>(gv.z, mv.z, vv.z, mom);
     ov.w = comp1<NEST, ACC>(gv.w, mv.w, vv.w, mom);
-    st_stream(mmt + v, mv);
+    st_stream(mmt + v, mv, wt);
     if (ACC)
-        st_stream(vec + v, vv);
+        st_stream(vec + v, vv, wt);
     else
-        st_stream(out + v, ov);
+        st_stream(out + v, ov, wt);
     if (SAMPLE) {
         int64_t q0, r0;
         floor_divmod_fast(4 * ((int64_t)blockIdx.x * kBlock) - sp.start, sp.stride, sp.inv_stride, q0, r0);
@@ -149,10 +149,10 @@ static int launch_comp(const float* g, float* m, float* v, float* o, int64_t n, 
             auto o4 = reinterpret_cast<float4*>(o);
             if (sample)
                 hipLaunchKernelGGL((k_compensate4<NEST, ACC, true>), dim3((unsigned)grid), dim3(kBlock), 0, st,
-                                   g4, m4, v4, o4, n4, mom, sp);
+                                   g4, m4, v4, o4, n4, mom, sp, (int)write_through(n));
             else
                 hipLaunchKernelGGL((k_compensate4<NEST, ACC, false>), dim3((unsigned)grid), dim3(kBlock), 0, st,
-                                   g4, m4, v4, o4, n4, mom, sp);
+                                   g4, m4, v4, o4, n4, mom, sp, (int)write_through(n));
             DGC_LAUNCHED();
         }
         done = n4 * 4;

@@ -341,7 +341,9 @@ __device__ void tile_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__
             rval[tid] = run.vals;
             ridx[tid] = run.idx;
             cnt = b1 - b0;
-            if (c == 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);   // idx < 0 or >= n
+            // idx < 0 or >= n; a split phase's runs that have not landed (count 0) have no
+            // bounds yet (their slots hold an earlier call's)
+            if (c == 0 && run.count > 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);
         }
         const long long incl = (long long)wave_incl_scan64((uint64_t)cnt);   // the whole wave 0 is here
         if (tid < nr) roff[tid] = (int)(incl - cnt);
@@ -1024,9 +1026,9 @@ int clear_packed(const void* prev, int32_t world, int64_t rank_stride, int64_t c
 // plain store per lane — measured 7.0 TB/s on MI355X at 4 GB, vs 5.2-6.2 for
 // grid-stride or non-temporal forms (tools/membench.hip). Block 0 also zeroes the
 // decompress's status words (ZeroWords), which saves the scatter two memset packets.
-__global__ void __launch_bounds__(kBlock) k_fill_zero(float4* __restrict__ x, int64_t n4, ZeroWords z) {
+__global__ void __launch_bounds__(kBlock) k_fill_zero(float4* __restrict__ x, int64_t n4, ZeroWords z, int wt) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n4) st_stream(x + i, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (i < n4) st_stream(x + i, make_float4(0.f, 0.f, 0.f, 0.f), wt);
     if (blockIdx.x == 0) {
 #pragma unroll
         for (int q = 0; q < 3; ++q)
@@ -1061,7 +1063,7 @@ int fill_zero(float* x, int64_t n, hipStream_t s, const ZeroWords& z) {
     if (n4 > 0) {
         if (ceil_div(n4, (int64_t)kBlock) > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_fill_zero: n too large");
         hipLaunchKernelGGL(k_fill_zero, dim3((unsigned)ceil_div(n4, (int64_t)kBlock)), dim3(kBlock), 0, s,
-                           reinterpret_cast<float4*>(x), n4, z);
+                           reinterpret_cast<float4*>(x), n4, z, (int)write_through(4 * n4));
         DGC_LAUNCHED();
         zeroed = true;
     }

@@ -317,29 +317,27 @@ __device__ __forceinline__ void st_nt(float4* p, const float4& v) {
 }
 
 // The streaming stores of the big passes (K1's momentum / velocity, the dense zero
-// fill): 16-B global stores with the sc1 policy — write-through, the line dropped from
-// the XCD's L2 — so no dirty line is left behind when the kernel ends. An nt / plain
-// store keeps its line dirty in L2, and the kernel boundary then writes the XCD L2s
-// back before the next kernel starts: + dirty bytes / ~6 TB/s (MI355X_MICROARCH.md,
-// "boundary"), ~5 us of idle GPU after K1 (8 x 4 MB of L2 full of dirty lines).
-// DGC_STREAM_STORE (A/B builds): 0 nt, 1 sc1 (default), 2 sc1 nt. The asm store ends
-// with s_nop 1: hipcc does not pad an asm statement, and its next instruction could
-// otherwise overwrite the data registers before the store has read them
+// fill), by size. An nt store keeps its line dirty in L2, and the kernel boundary then
+// writes the XCD L2s back before the next kernel starts: + dirty bytes / ~6 TB/s
+// (MI355X_MICROARCH.md, "boundary"), ~5 us of idle GPU after K1 (8 x 4 MB of L2 full
+// of dirty lines). A write-through store (sc1: the line dropped from the XCD's L2)
+// leaves nothing behind, but streams ~10 % slower: same box, flat-1B K1 3.75 ms with
+// sc1 against 3.42 ms nt, VGG-16-BN 0.54 against 0.48 ms, while ResNet-50's 25.5M
+// elements run 0.088 ms sc1 against 0.097 ms nt. So a pass over at most
+// kWriteThroughMax elements writes through (wt), a larger one stores nt. The asm store
+// ends with s_nop 1: hipcc does not pad an asm statement, and its next instruction
+// could otherwise overwrite the data registers before the store has read them
 // (cdna_hip_programming.md §5.7 item 1).
-#ifndef DGC_STREAM_STORE
-#define DGC_STREAM_STORE 1
-#endif
-__device__ __forceinline__ void st_stream(float4* p, const float4& v) {
-#if DGC_STREAM_STORE == 0
-    st_nt(p, v);
-#else
-    const f4v x = {v.x, v.y, v.z, v.w};
-#if DGC_STREAM_STORE == 1
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
-#else
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
-#endif
-#endif
+constexpr int64_t kWriteThroughMax = 48LL << 20;
+inline bool write_through(int64_t elements) { return elements <= kWriteThroughMax; }
+
+__device__ __forceinline__ void st_stream(float4* p, const float4& v, bool wt) {
+    if (wt) {   // uniform
+        const f4v x = {v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
+    } else {
+        st_nt(p, v);
+    }
 }
 }  // namespace dgc
 

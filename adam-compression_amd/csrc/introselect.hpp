@@ -62,6 +62,7 @@ struct K5Prof {
     unsigned long long sub[8];   // global-phase step parts, summed over steps
     unsigned long long bt[64][8];   // per workgroup (tensor) < 64: the same stamps, [6] kernel end
     long long bn[64];               // its candidate count
+    unsigned long long set[64][8];  // K5s k_resample_set per workgroup (tensor) < 64: phase ends
 };
 __device__ K5Prof g_k5prof;
 __shared__ unsigned long long k5_lsub[8];
@@ -79,6 +80,8 @@ __shared__ unsigned int k5_lsteps[4];
          if (blockIdx.x < 64) g_k5prof.bt[blockIdx.x][i] = t_; } } while (0)
 #define K5_STEP(i) \
     do { if (threadIdx.x == 0) k5_lsteps[i] += 1; } while (0)
+#define SET_STAMP(i) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 64) g_k5prof.set[blockIdx.x][i] = wall_clock64(); } while (0)
 #define K5_SUB_BEGIN() unsigned long long k5_t0 = wall_clock64()
 #define K5_SUB(i, global) \
     do { if ((global) && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \
@@ -99,6 +102,7 @@ __shared__ unsigned int k5_lsteps[4];
 #define K5_SUB(i, global) do { } while (0)
 #define K5_STAMP(i) do { } while (0)
 #define K5_STEP(i) do { } while (0)
+#define SET_STAMP(i) do { } while (0)
 #endif
 
 __device__ __forceinline__ void wave_sync() {

@@ -65,6 +65,14 @@ constexpr int kLstTile = 4;
 __host__ __device__ __forceinline__ int64_t lcol(int64_t seg) {
     return (seg / kLstTile) * (kLstTile * kCap) + seg % kLstTile;
 }
+// Slot of entry e of segment seg (every list access goes through it; ntile = tiles of
+// kLstTile segments in the workspace, for layouts that band the entries — one that put
+// entries 0..7 of every tile in one dense array was measured and dropped: flat-1B 3.61 /
+// 3.67 ms against 3.73 / 3.71 ms banded, ResNet-50 unchanged).
+__host__ __device__ __forceinline__ int64_t lslot(int64_t seg, int64_t e, int64_t ntile) {
+    (void)ntile;
+    return lcol(seg) + e * kLstTile;
+}
 constexpr int kSegTiles = kSeg / (kWave * 4);   // 4 float4 per lane per segment
 constexpr int kSuper = 4;                       // segments per wave in the full select pass
 constexpr int kGroupSegs = 1024;                // segments per group (1M elements)
@@ -458,7 +466,7 @@ __device__ __forceinline__ uint32_t ge_mask(const float (&x)[4], uint32_t valid,
 // Append the lanes' flagged elements (element order 4*lane + j) to a segment list
 // (lo / lv: its column, entries kLstTile apart).
 __device__ __forceinline__ void list_append(uint32_t p, const float (&x)[4], int tile_off, uint32_t& c,
-                                            uint16_t* lo, float* lv) {
+                                            uint16_t* lo, float* lv, int64_t seg, int64_t ntile) {
     if (__ballot(p != 0)) {
         uint32_t lb, tot;
         wave_prefix4(p, lb, tot);
@@ -468,8 +476,8 @@ __device__ __forceinline__ void list_append(uint32_t p, const float (&x)[4], int
         for (int j = 0; j < 4; ++j) {
             if (p & (1u << j)) {
                 if (r < (uint32_t)kCap) {
-                    lo[r * kLstTile] = (uint16_t)(tile_off + 4 * lane + j);
-                    lv[r * kLstTile] = x[j];
+                    lo[lslot(seg, r, ntile)] = (uint16_t)(tile_off + 4 * lane + j);
+                    lv[lslot(seg, r, ntile)] = x[j];
                 }
                 ++r;
             }
@@ -605,7 +613,7 @@ static int mask_flush(float* vec, float* mmt, const Layout& L, const SelWS& w, h
 template <bool NEST>
 __global__ void __launch_bounds__(kBlock)
 k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat, float* __restrict__ vec_flat,
-                  float mom, SelWS w, StartChunk sc) {
+                  float mom, SelWS w, StartChunk sc, int wt) {
     const int t = task(w, BT_K1, blockIdx.x);
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -649,8 +657,9 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     }
     uint32_t c = 0, mk = 0;
     const int64_t seg = d.seg0 + ls;
-    uint16_t* lo = w.lst_off + lcol(seg);
-    float* lv = w.lst_val + lcol(seg);
+    uint16_t* lo = w.lst_off;
+    float* lv = w.lst_val;
+    const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
     if (st->def_mode && ls < d.nseg) apply_deferred_mask(*st, w, d, ls, lane, vv, mv);
 #pragma unroll
     for (int u = 0; u < kSegTiles; ++u) {
@@ -665,8 +674,8 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
             x[1] = comp1<NEST, true>(gv[u].y, mv[u].y, vv[u].y, mom);
             x[2] = comp1<NEST, true>(gv[u].z, mv[u].z, vv[u].z, mom);
             x[3] = comp1<NEST, true>(gv[u].w, mv[u].w, vv[u].w, mom);
-            st_stream(mmt + v, mv[u]);
-            st_stream(vec + v, vv[u]);
+            st_stream(mmt + v, mv[u], wt);
+            st_stream(vec + v, vv[u], wt);
             const int64_t e = 4 * v;
             valid = e + 3 < n ? 0xFu : (e + 2 < n ? 7u : (e + 1 < n ? 3u : (e < n ? 1u : 0u)));
             if (sample) {
@@ -694,7 +703,7 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
             const uint32_t pos = base + (uint32_t)__popcll(hb & ((1ull << lane) - 1));
             if (hit && pos < (uint64_t)d.win_cap) win[pos] = hv;
         }
-        list_append(ge_mask(x, valid, tl), x, u * 256, c, lo, lv);
+        list_append(ge_mask(x, valid, tl), x, u * 256, c, lo, lv, seg, ntile);
         mk = max(mk, tile_max_key(x, valid));
     }
     const bool spilled = c > (uint32_t)kCap;
@@ -1010,6 +1019,7 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     const int t = task(w, BT_CNT, blockIdx.x);
     const SelState* st = w.st + t;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
+    const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
@@ -1036,10 +1046,10 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     float a[kCountSegs][kFirst];
 #pragma unroll
     for (int j = 0; j < kCountSegs; ++j) {
-        const float* lv = w.lst_val + lcol(d.seg0 + lseg0 + j * kBlock + threadIdx.x);
+        const int64_t sj = d.seg0 + lseg0 + j * kBlock + threadIdx.x;
 #pragma unroll
         for (int e = 0; e < kFirst; ++e)
-            if ((uint32_t)e < lc[j] && lc[j] <= (uint32_t)kCap) a[j][e] = lv[e * kLstTile];
+            if ((uint32_t)e < lc[j] && lc[j] <= (uint32_t)kCap) a[j][e] = w.lst_val[lslot(sj, e, ntile)];
     }
     uint32_t ctot = 0;
 #pragma unroll
@@ -1056,12 +1066,11 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
 #pragma unroll
         for (int e = 0; e < kFirst; ++e) c += (uint32_t)e < n && fabsf(a[j][e]) >= tc;
         // the rest of a longer list, 16 loads in flight at a time
-        const float* lv = w.lst_val + lcol(seg);
         for (uint32_t e0 = kFirst; e0 < n; e0 += 16) {
             float v[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                if (e0 + q < n) v[q] = lv[(e0 + q) * kLstTile];
+                if (e0 + q < n) v[q] = w.lst_val[lslot(seg, e0 + q, ntile)];
 #pragma unroll
             for (int q = 0; q < 16; ++q) c += e0 + q < n && fabsf(v[q]) >= tc;
         }
@@ -1102,6 +1111,7 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
+    const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int kTiles = kSuper * kSegTiles;   // 16
     __shared__ uint32_t wcnt[kSegPerBlock4];
@@ -1122,14 +1132,14 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
                 const int64_t ls = sup * kSuper + sg;
                 const int64_t seg = d.seg0 + ls;
                 uint32_t c = 0;
-                uint16_t* lo = w.lst_off + lcol(seg);
-                float* lv = w.lst_val + lcol(seg);
+                uint16_t* lo = w.lst_off;
+                float* lv = w.lst_val;
                 if (ls < d.nseg) {   // uniform per wave
                     uint32_t mk = 0;
 #pragma unroll
                     for (int u = 0; u < kSegTiles; ++u) {
                         list_append(ge_mask(x[sg * kSegTiles + u], valid[sg * kSegTiles + u], tc),
-                                    x[sg * kSegTiles + u], u * 256, c, lo, lv);
+                                    x[sg * kSegTiles + u], u * 256, c, lo, lv, seg, ntile);
                         mk = max(mk, tile_max_key(x[sg * kSegTiles + u], valid[sg * kSegTiles + u]));
                     }
                     mk = wave_max(mk);
@@ -1270,12 +1280,12 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         const int64_t seg = d.seg0 + ls;
         const uint32_t lc = lcnt_count(w.seg_lcnt[seg]);
         if (lc <= (uint32_t)kCap) {
-            const float* lv = w.lst_val + lcol(seg);
+            const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
             for (uint32_t e0 = 0; e0 < lc; e0 += 16) {   // 16 loads in flight at a time
                 float v[16];
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
-                    if (e0 + q < lc) v[q] = lv[(e0 + q) * kLstTile];
+                    if (e0 + q < lc) v[q] = w.lst_val[lslot(seg, e0 + q, ntile)];
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
                     if (e0 + q < lc) {
@@ -1485,12 +1495,12 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
         float v[kEmitShort];
         uint16_t e[kEmitShort];
         if (short_list) {
-            const int64_t col = lcol(d.seg0 + ls);
+            const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
 #pragma unroll
             for (int q = 0; q < kEmitShort; ++q)
                 if ((uint32_t)q < lc) {
-                    v[q] = w.lst_val[col + q * kLstTile];
-                    e[q] = w.lst_off[col + q * kLstTile];
+                    v[q] = w.lst_val[lslot(d.seg0 + ls, q, ntile)];
+                    e[q] = w.lst_off[lslot(d.seg0 + ls, q, ntile)];
                 }
         }
         // (earlier quarters' total << 32) | this quarter's counts: one scan gives both
@@ -1535,7 +1545,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
             x[q] = 0.f;
             e[q] = 0;
             if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
-                const int64_t slot = lcol(d.seg0 + lseg0 + j0 + q) + lane * kLstTile;
+                const int64_t slot = lslot(d.seg0 + lseg0 + j0 + q, lane, ceil_div(w.nseg, (int64_t)kLstTile));
                 x[q] = w.lst_val[slot];
                 e[q] = w.lst_off[slot];
             }
@@ -1630,7 +1640,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
             x[q] = 0.f;
             e[q] = 0;
             if (L <= (uint32_t)kCap && (uint32_t)lane < L) {
-                const int64_t slot = lcol(d.seg0 + lseg0 + j0 + q) + lane * kLstTile;
+                const int64_t slot = lslot(d.seg0 + lseg0 + j0 + q, lane, ceil_div(w.nseg, (int64_t)kLstTile));
                 x[q] = w.lst_val[slot];
                 e[q] = w.lst_off[slot];
             }
@@ -1721,15 +1731,16 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
     for (int q = 0; q < kCountSegs; ++q)
         if (n[q] <= (uint32_t)kCap) nmax = max(nmax, n[q]);
     constexpr int kFirst = 8;   // entries 0..7: the four lists' share of one 128-B line
-    const float* lv = w.lst_val + lcol(seg0);
-    const uint16_t* lo = w.lst_off + lcol(seg0);
+    const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
+    const float* lv = w.lst_val;
+    const uint16_t* lo = w.lst_off;
     float4 a[kFirst];
     uint2 ao[kFirst];   // their offsets too: the emit below then needs no second round trip
 #pragma unroll
     for (int e = 0; e < kFirst; ++e)
         if ((uint32_t)e < nmax) {
-            a[e] = *reinterpret_cast<const float4*>(lv + e * kLstTile);
-            ao[e] = *reinterpret_cast<const uint2*>(lo + e * kLstTile);
+            a[e] = *reinterpret_cast<const float4*>(lv + lslot(seg0, e, ntile));
+            ao[e] = *reinterpret_cast<const uint2*>(lo + lslot(seg0, e, ntile));
         }
 #pragma unroll
     for (int e = 0; e < kFirst; ++e) {
@@ -1738,7 +1749,7 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
         for (int q = 0; q < kCountSegs; ++q) c[q] += (uint32_t)e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
     }
     for (uint32_t e = kFirst; e < nmax; ++e) {   // longer lists (rare)
-        const float4 b = *reinterpret_cast<const float4*>(lv + e * kLstTile);
+        const float4 b = *reinterpret_cast<const float4*>(lv + lslot(seg0, e, ntile));
         const float x[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
         for (int q = 0; q < kCountSegs; ++q) c[q] += e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
@@ -1829,8 +1840,8 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
 #pragma unroll
             for (int e = 0; e < kFirst; ++e)
                 if (e0 + e < nmax) {
-                    ob[e] = e0 == 0 ? ao[e] : *reinterpret_cast<const uint2*>(lo + (e0 + e) * kLstTile);
-                    vb[e] = e0 == 0 ? a[e] : *reinterpret_cast<const float4*>(lv + (e0 + e) * kLstTile);
+                    ob[e] = e0 == 0 ? ao[e] : *reinterpret_cast<const uint2*>(lo + lslot(seg0, e0 + e, ntile));
+                    vb[e] = e0 == 0 ? a[e] : *reinterpret_cast<const float4*>(lv + lslot(seg0, e0 + e, ntile));
                 }
 #pragma unroll
             for (int e = 0; e < kFirst; ++e) {
@@ -2332,14 +2343,14 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 
 constexpr int kSetLds = 32;   // rounds of keys kept in LDS after the register rounds (128 KB)
 
-__global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+__device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o) {
     const int t = blockIdx.x;
     SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int64_t n64 = st->n_cur;
     if (n64 > kSetMax || d.k < 1 || n64 <= d.k) return;   // the replay takes it
+    SET_STAMP(0);
     const int n = (int)n64;
     const uint32_t k = (uint32_t)d.k;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2383,6 +2394,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
                 if (r0 + u < rounds) fn(r0 + u, v[u]);
         }
     };
+    SET_STAMP(1);
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
     for_keys([&](int r, uint32_t x) {
         if (tid + r * kScanThreads < n) {
@@ -2409,6 +2421,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         mn = red[0][i] < mn ? red[0][i] : mn;
         mx = red[1][i] > mx ? red[1][i] : mx;
     }
+    SET_STAMP(2);
     // passes over the bits of key - mn, 11 at a time from the top
     const uint32_t span = mx - mn;
     const int L = span ? 32 - __builtin_clz(span) : 0;
@@ -2452,6 +2465,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     }
     // tied across the boundary (more keys == kth than the k - #(> kth) still needed):
     // only torch's exact order of operations knows which ones — the replay
+    SET_STAMP(3);
     if (eq != k_rem) return;
     // order-preserving compaction: (round, wave) counts, one scan, ranks from ballots
     for_keys([&](int r, uint32_t x) {   // uniform in r
@@ -2484,6 +2498,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     // (free on this path): plain stores, no load waits on them; then the emit reads them
     // back with every slot's loads independent (a per-round emit waited for the index
     // and value gathers of each round in turn: two dependent round trips per 1024 keys)
+    SET_STAMP(4);
     DGC_GLB uint32_t* spos = glb(w.gpos + d.gpos_off);
     for_keys([&](int r, uint32_t x) {   // uniform in r
         const bool sel = tid + r * kScanThreads < n && x >= kth;
@@ -2492,6 +2507,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     });
     __threadfence_block();
     __syncthreads();
+    SET_STAMP(5);
     const long long ob = obase_s;
     const float* vec = vec_flat + d.off;
     const int64_t* cand = w.cand_idx + d.cand_off;
@@ -2515,6 +2531,12 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
         st->rs_nth = 3;   // K5's replay and emit skip the tensor
         st->tie_rule = DGC_TIES_SET;
     }
+    SET_STAMP(6);
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+    resample_set_wg(vec_flat, w, o);
 }
 
 // ---------------------------------------------------------------- K5s over several workgroups
@@ -3250,10 +3272,10 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
         const StartChunk none{};   // k_put_one wrote the start
         if (nesterov)
             hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
-                               vec, momentum, w, none);
+                               vec, momentum, w, none, (int)write_through(n));
         else
             hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad,
-                               mmt, vec, momentum, w, none);
+                               mmt, vec, momentum, w, none, (int)write_through(n));
         DGC_LAUNCHED();
     }
     if (n & 3) {   // scalar tail (< 4 elements) incl. its samples; its segment is marked spilled
@@ -3444,10 +3466,10 @@ int batch_compress_begin(const dgc_batch_desc* b, const float* grad, const float
     if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: too many segments");
     if (b->nesterov)
         hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt, vec,
-                           b->momentum, w, arg);
+                           b->momentum, w, arg, (int)write_through(L.nseg * kSeg));
     else
         hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
-                           vec, b->momentum, w, arg);
+                           vec, b->momentum, w, arg, (int)write_through(L.nseg * kSeg));
     DGC_LAUNCHED();
     return DGC_OK;
 }

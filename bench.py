@@ -613,13 +613,18 @@ def main():
     extras = {}
     if not args.no_extras and run.b.fill == "sparse":
         # the same steps with the reference's dense zero_() (dgc/compression.py:191) before
-        # the scatter, on the same state: what the persistent output's re-zero saves
-        run.b.fill = "inline"
-        extras["dense_fill"] = {"ms_per_step": round(timed_steps(run, args.steps, 2, world), 4),
-                                "steps": args.steps, "warmup": 2,
+        # the scatter: what the persistent output's re-zero saves. The flat bucket goes on
+        # from the same state; a model set gets a fresh batch built with fill="inline"
+        # (its step count and gradients as above)
+        if wl["kind"] == "flat":
+            run.b.fill = "inline"
+            dense = timed_steps(run, args.steps, 2, world)
+            run.b.fill = "sparse"
+        else:
+            dense = timed_steps(ModelRun(wl, rank, world, dev, "inline"), args.steps, args.warmup, world)
+        extras["dense_fill"] = {"ms_per_step": round(dense, 4), "steps": args.steps,
                                 "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
                                         "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
-        run.b.fill = "sparse"
     xgmi = allgather_probe(run, world) if world > 1 else None
     probe = hbm_probe(*run.probe_buffers())   # after the timed steps: overwrites the state
     ms_step = elapsed * 1e3 / args.steps
