@@ -90,9 +90,14 @@ constexpr float kSpecMarginMax = 0.95f;
 constexpr int kSetReg = 32;                  // one workgroup: keys per thread kept in registers
 constexpr int kSetRounds = 256;              // one workgroup up to kSetRounds x 1024 candidates
 constexpr int64_t kSetMax = (int64_t)kSetRounds * 1024;
-constexpr int kBigSlice = 32768;             // above: slices of this many candidates per workgroup
-constexpr int kBigSlices = 256;              //   up to this many slices (8M candidates)
-constexpr int kBigMax = 8;                   //   for up to this many tensors of a call
+// One workgroup up to this many candidates, even for a tensor with a sliced-path slot:
+// routing ResNet-50's 72k-candidate sets over workgroups (DGC_SET_ONE=32768) cut
+// k_resample_set 63 -> 20 us but cost 61 us in the four k_bigset_* launches (same box,
+// step 0.286 -> 0.309 ms)
+constexpr int64_t kSetOne = kSetMax;
+constexpr int kBigSlice = 8192;              // above: slices of this many candidates per workgroup
+constexpr int kBigSlices = 1024;             //   up to this many slices (8M candidates)
+constexpr int kBigMax = 64;                  //   for up to this many tensors of a call
 constexpr int kBigBuf = 65536;               //   keys of the k-th key's coarse bin gathered
 constexpr int kBigShift = 12;                //   coarse bins of 4096 key units above t_cur         // the adaptive list margin's ceiling (k_sel_finish)
 constexpr int kSpecWords = 4;                   // per-tensor speculation state (dgc_compress_begin: spec)
@@ -198,6 +203,7 @@ struct SelWS {
     unsigned long long* grp_lb;    // k_count_emit's decoupled look-back words, one per group
     uint64_t* queue;           // K5: (|x| key << 32 | j) for the candidates j, ascending index order
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
+    float* cand_val;           // K5: their values (what the gather read; the set path's emit)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
     BigSetWS* bigset;          // [nbig] K5s over several workgroups
@@ -259,6 +265,13 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, in
     return 0;
 }
 
+// Candidates above which a resample set goes over several workgroups (k_bigset_*) when
+// its tensor has a slot: DGC_SET_ONE=n (A/B runs; results are identical either way).
+static int64_t set_one() {
+    static const int64_t v = std::getenv("DGC_SET_ONE") ? std::atoll(std::getenv("DGC_SET_ONE")) : kSetOne;
+    return v;
+}
+
 static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, std::vector<TDesc>& td,
                          std::vector<int32_t> (&bt)[BT_COUNT], std::vector<int32_t>& small) {
     L = Layout{};
@@ -297,7 +310,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.gpos_off = gpos;
         gpos += 2 * (d.cand_cap / 2 + 1);
         d.big = -1;
-        if (d.cand_cap > kSetMax && d.cand_cap <= (int64_t)kBigSlices * kBigSlice && L.nbig < kBigMax) {
+        if (d.cand_cap > set_one() && d.cand_cap <= (int64_t)kBigSlices * kBigSlice && L.nbig < kBigMax) {
             d.big = L.nbig;
             L.big[L.nbig++] = t;
         }
@@ -360,6 +373,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.lst_val = c.take<float>(ceil_div(L.nseg, (int64_t)kLstTile) * kLstTile * kCap);
     w.queue = c.take<uint64_t>(L.ncand);
     w.cand_idx = c.take<int64_t>(L.ncand);
+    w.cand_val = c.take<float>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
     w.nthg = c.take<NthG>(L.T);
     w.bigset = c.take<BigSetWS>(L.nbig);
@@ -1355,6 +1369,7 @@ struct EmitOut {
     uint64_t* queue;     // non-null: K5 candidate gather (queue[pos] = key << 32 | pos, cand[pos] = index)
     int64_t* cand;
     int32_t defer;       // first-k branches: leave vec/mmt to the next K1 (record seg_off instead)
+    float* cval;         // the K5 gather: cval[pos] = the candidate's value (null: not kept)
 };
 
 // Entries a tensor emits: the first `limit` candidates, or k after a resample.
@@ -1381,6 +1396,7 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long 
     if (o.queue) {
         o.queue[d.cand_off + pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
         o.cand[d.cand_off + pos] = li;
+        if (o.cval) o.cval[d.cand_off + pos] = x;
         return;
     }
     store_value(o.values, pos, x, o.vdtype);
@@ -1991,8 +2007,7 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
     const int64_t q = ((int64_t)blockIdx.x - w.bt[BT_QUEUE][t]) * kQueuePerBlock + threadIdx.x;
     if (q >= d.k) return;
     const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
-    const int64_t li = w.cand_idx[d.cand_off + j];
-    emit_one(o, d, obase_s + q, li, vec_flat[d.off + li]);
+    emit_one(o, d, obase_s + q, w.cand_idx[d.cand_off + j], w.cand_val[d.cand_off + j]);
 }
 
 // K5b: torch's CPU topk on its partial_sort path (k * 64 <= candidates, i.e. a sampled
@@ -2343,13 +2358,15 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 
 constexpr int kSetLds = 32;   // rounds of keys kept in LDS after the register rounds (128 KB)
 
-__device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o) {
+__device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o,
+                                                int64_t one) {
     const int t = blockIdx.x;
     SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int64_t n64 = st->n_cur;
-    if (n64 > kSetMax || d.k < 1 || n64 <= d.k) return;   // the replay takes it
+    // the replay takes it (or, past `one` with a sliced-path slot, k_bigset_*)
+    if (n64 > (d.big >= 0 ? one : kSetMax) || d.k < 1 || n64 <= d.k) return;
     SET_STAMP(0);
     const int n = (int)n64;
     const uint32_t k = (uint32_t)d.k;
@@ -2499,28 +2516,37 @@ __device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_fl
     // back with every slot's loads independent (a per-round emit waited for the index
     // and value gathers of each round in turn: two dependent round trips per 1024 keys)
     SET_STAMP(4);
+    // (n <= 32K: the keys are all in registers and the LDS rounds' area takes them)
     DGC_GLB uint32_t* spos = glb(w.gpos + d.gpos_off);
+    const bool in_lds = rounds <= kSetReg;   // uniform
     for_keys([&](int r, uint32_t x) {   // uniform in r
         const bool sel = tid + r * kScanThreads < n && x >= kth;
         const uint64_t m = __ballot(sel);
-        if (sel) spos[rbase[r * kWaves + wv] + mbcnt64(m, 0u)] = (uint32_t)(tid + r * kScanThreads);
+        if (sel) {
+            const uint32_t q = rbase[r * kWaves + wv] + mbcnt64(m, 0u), i = (uint32_t)(tid + r * kScanThreads);
+            if (in_lds)
+                kl[q] = i;
+            else
+                spos[q] = i;
+        }
     });
-    __threadfence_block();
+    if (!in_lds) __threadfence_block();
     __syncthreads();
     SET_STAMP(5);
     const long long ob = obase_s;
-    const float* vec = vec_flat + d.off;
+    // the index and the value of a slot are independent loads (the gather kept the value)
     const int64_t* cand = w.cand_idx + d.cand_off;
+    const float* cval = w.cand_val + d.cand_off;
     for (uint32_t q0 = 0; q0 < k; q0 += 4 * kScanThreads) {
         int64_t li[4];
         float x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t q = q0 + u * kScanThreads + tid;
-            li[u] = q < k ? cand[spos[q]] : 0;
+            const uint32_t i = q < k ? (in_lds ? kl[q] : spos[q]) : 0u;
+            li[u] = q < k ? cand[i] : 0;
+            x[u] = q < k ? cval[i] : 0.f;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = q0 + u * kScanThreads + tid < k ? vec[li[u]] : 0.f;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t q = q0 + u * kScanThreads + tid;
@@ -2535,8 +2561,8 @@ __device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_fl
 }
 
 __global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
-    resample_set_wg(vec_flat, w, o);
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one) {
+    resample_set_wg(vec_flat, w, o, one);
 }
 
 // ---------------------------------------------------------------- K5s over several workgroups
@@ -2556,6 +2582,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
 // the tensor is left to the exact replay (ok = 0), as in k_resample_set.
 struct BigList {
     int32_t n;
+    int64_t one;   // the one-workgroup path's limit for these tensors (set_one)
     int32_t t[kBigMax];
 };
 
@@ -2610,8 +2637,15 @@ __device__ __forceinline__ int bigset_task(const SelWS& w, const BigList& bl, in
     const SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return -1;
     cnt = st->n_cur;
-    if (cnt <= kSetMax || cnt > (int64_t)kBigSlices * kBigSlice || cnt <= w.td[t].k) return -1;
+    if (cnt <= bl.one || cnt > (int64_t)kBigSlices * kBigSlice || cnt <= w.td[t].k) return -1;
     return t;
+}
+
+// (key, position) pairs of the k-th key's coarse bin, in the tensor's pair-slot region
+// (2 x (cand_cap / 2 + 1) words)
+__device__ __forceinline__ uint32_t bigset_buf_cap(const TDesc& d) {
+    const int64_t c = d.cand_cap / 2 + 1;
+    return (uint32_t)(c < kBigBuf ? c : kBigBuf);
 }
 
 __device__ __forceinline__ uint32_t bigset_bin(uint32_t key, uint32_t tkey) {
@@ -2667,7 +2701,8 @@ __global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
     }
     __syncthreads();
     const int b0 = sel;
-    const bool ok = b0 >= 0 && b0 < kRsBins - 1 && h[b0] <= (uint32_t)kBigBuf;
+    const uint32_t bcap = bigset_buf_cap(d);
+    const bool ok = b0 >= 0 && b0 < kRsBins - 1 && h[b0] <= bcap;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         b.ok = ok ? 1 : 0;
         b.b0 = (uint32_t)b0;
@@ -2691,7 +2726,7 @@ __global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
             uint32_t slot = 0;
             if (lane == 0) slot = atomicAdd(&b.bufn, (uint32_t)__popcll(m));
             slot = __shfl(slot, 0) + mbcnt64(m, 0u);
-            if (in && slot < (uint32_t)kBigBuf) {
+            if (in && slot < bcap) {
                 buf[2 * slot] = key;
                 buf[2 * slot + 1] = (uint32_t)i;
             }
@@ -2728,7 +2763,7 @@ __global__ void __launch_bounds__(kScanThreads) k_bigset_select(SelWS w, BigList
     for (int i = tid; i < kBigSlices; i += kScanThreads) sc[i] = 0;
     if (tid == 0) sel = -1;
     __syncthreads();
-    const bool fits = n0 <= (uint32_t)kBigBuf && a0 < k && k - a0 <= n0;
+    const bool fits = n0 <= bigset_buf_cap(d) && a0 < k && k - a0 <= n0;
     if (fits)
         for (uint32_t i = tid; i < n0; i += kScanThreads) atomicAdd(&h[buf[2 * i] - base_key], 1u);
     __syncthreads();
@@ -2776,12 +2811,11 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
     const TDesc d = w.td[t];
     const BigSetWS& b = w.bigset[d.big];
     const int64_t cnt = st->n_cur;
-    if (!b.ok || cnt <= kSetMax) return;   // the one-workgroup path emitted it
+    if (!b.ok || cnt <= bl.one) return;   // the one-workgroup path emitted it
     const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
     if ((int64_t)blockIdx.x >= nsl) return;
     const uint32_t kth = b.kth;
     const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
-    const float* vec = vec_flat + d.off;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     constexpr int kW = kBlock / kWave;
     __shared__ uint32_t wc[kW];
@@ -2804,10 +2838,7 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
         const int64_t i = i0 + lane;
         const bool sel = i < qhi && qw[2 * i + 1] >= kth;
         const uint64_t m = __ballot(sel);
-        if (sel) {
-            const int64_t li = w.cand_idx[d.cand_off + i];
-            emit_one(o, d, pos + mbcnt64(m, 0u), li, vec[li]);
-        }
+        if (sel) emit_one(o, d, pos + mbcnt64(m, 0u), w.cand_idx[d.cand_off + i], w.cand_val[d.cand_off + i]);
         pos += __popcll(m);
     }
 }
@@ -3020,13 +3051,15 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         EmitOut g = o;
         g.queue = w.queue;
         g.cand = w.cand_idx;
+        g.cval = w.cand_val;
         DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
-            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o);
+            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o, set_one());
             DGC_LAUNCHED();
             if (L.nbig > 0) {   // candidate counts above one workgroup's: sliced over workgroups
                 BigList bl{};
                 bl.n = L.nbig;
+                bl.one = set_one();
                 int64_t maxcap = 0;
                 for (int j = 0; j < L.nbig; ++j) bl.t[j] = L.big[j];
                 maxcap = L.max_cand;

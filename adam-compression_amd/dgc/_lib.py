@@ -17,7 +17,10 @@ LIB_PATH = os.environ.get(
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libdgc_hip.so"))
 
 DGC_OK = 0
-SPEC_MARGIN = 0.8      # speculative list threshold = 0.8 x the previous final threshold
+# speculative list threshold after a miss = SPEC_MARGIN x the predicted final threshold
+# (dgc_hip.h, spec_threshold); DGC_SPEC_MARGIN overrides it for A/B runs (results are
+# identical: it only chooses how much K1 lists ahead)
+SPEC_MARGIN = float(os.environ.get("DGC_SPEC_MARGIN", "0.8"))
 SYNC_DEVICE, SYNC_HOST = 0, 1
 VD = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
 HALF = (torch.bfloat16, torch.float16)   # 16-bit parameters (dgc_*16 entry points)
