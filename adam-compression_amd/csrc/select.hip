@@ -204,6 +204,7 @@ struct SelWS {
     uint64_t* queue;           // K5: (|x| key << 32 | j) for the candidates j, ascending index order
     int64_t* cand_idx;         // K5: the candidates' element indices (within the tensor)
     float* cand_val;           // K5: their values (what the gather read; the set path's emit)
+    uint32_t* cand_key;        // K5: their |x| keys, dense (the set paths read 4 B per candidate, not 8)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
     BigSetWS* bigset;          // [nbig] K5s over several workgroups
@@ -374,6 +375,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.queue = c.take<uint64_t>(L.ncand);
     w.cand_idx = c.take<int64_t>(L.ncand);
     w.cand_val = c.take<float>(L.ncand);
+    w.cand_key = c.take<uint32_t>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
     w.nthg = c.take<NthG>(L.T);
     w.bigset = c.take<BigSetWS>(L.nbig);
@@ -1370,6 +1372,7 @@ struct EmitOut {
     int64_t* cand;
     int32_t defer;       // first-k branches: leave vec/mmt to the next K1 (record seg_off instead)
     float* cval;         // the K5 gather: cval[pos] = the candidate's value (null: not kept)
+    uint32_t* ckey;      //   and ckey[pos] = its key
 };
 
 // Entries a tensor emits: the first `limit` candidates, or k after a resample.
@@ -1396,7 +1399,10 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long 
     if (o.queue) {
         o.queue[d.cand_off + pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
         o.cand[d.cand_off + pos] = li;
-        if (o.cval) o.cval[d.cand_off + pos] = x;
+        if (o.cval) {
+            o.cval[d.cand_off + pos] = x;
+            o.ckey[d.cand_off + pos] = abs_key(x);
+        }
         return;
     }
     store_value(o.values, pos, x, o.vdtype);
@@ -2382,8 +2388,8 @@ __device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_fl
     __shared__ long long obase_s;
     __shared__ uint32_t kl[kSetLds * kScanThreads];   // rounds kSetReg .. kReg - 1
     // queue entry i = tid + r * 1024 (coalesced high-word loads); its key
-    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
-    auto key_at = [&](int i) -> uint32_t { return i < n ? qw[2 * i + 1] : 0u; };
+    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
+    auto key_at = [&](int i) -> uint32_t { return i < n ? qk[i] : 0u; };
     const int rounds = (n + kScanThreads - 1) / kScanThreads;
     uint32_t key[kSetReg];
 #pragma unroll
@@ -2666,10 +2672,10 @@ __global__ void __launch_bounds__(kBlock) k_bigset_hist(SelWS w, BigList bl) {
     __shared__ uint32_t h[kRsBins];
     for (int i = threadIdx.x; i < kRsBins; i += kBlock) h[i] = 0;
     __syncthreads();
-    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
     const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
 #pragma unroll 8
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[bigset_bin(qw[2 * i + 1], tkey)], 1u);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[bigset_bin(qk[i], tkey)], 1u);
     __syncthreads();
     for (int i = threadIdx.x; i < kRsBins; i += kBlock)
         if (h[i]) atomicAdd(&b.hist[i], h[i]);
@@ -2709,7 +2715,7 @@ __global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
         b.a0 = sel_above;
     }
     if (!ok) return;   // uniform
-    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
     DGC_GLB uint32_t* buf = glb(w.gpos + d.gpos_off);   // (key, position) pairs; the replay's pair slots
     const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
     const int lane = threadIdx.x & 63;
@@ -2717,7 +2723,7 @@ __global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
 #pragma unroll 4
     for (int64_t i0 = lo; i0 < hi; i0 += kBlock) {   // uniform trip count
         const int64_t i = i0 + threadIdx.x;
-        const uint32_t key = i < hi ? qw[2 * i + 1] : 0u;
+        const uint32_t key = i < hi ? qk[i] : 0u;
         const uint32_t bb = bigset_bin(key, tkey);
         above_cnt += i < hi && bb > (uint32_t)b0;
         const bool in = i < hi && bb == (uint32_t)b0;
@@ -2815,7 +2821,7 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
     const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
     if ((int64_t)blockIdx.x >= nsl) return;
     const uint32_t kth = b.kth;
-    const DGC_GLB uint32_t* qw = reinterpret_cast<const DGC_GLB uint32_t*>(glb(w.queue + d.cand_off));
+    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     constexpr int kW = kBlock / kWave;
     __shared__ uint32_t wc[kW];
@@ -2827,7 +2833,7 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
 #pragma unroll 8
     for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
         const int64_t i = i0 + lane;
-        c += (uint32_t)__popcll(__ballot(i < qhi && qw[2 * i + 1] >= kth));
+        c += (uint32_t)__popcll(__ballot(i < qhi && qk[i] >= kth));
     }
     if (lane == 0) wc[wv] = c;
     __syncthreads();
@@ -2836,7 +2842,7 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
 #pragma unroll 4
     for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
         const int64_t i = i0 + lane;
-        const bool sel = i < qhi && qw[2 * i + 1] >= kth;
+        const bool sel = i < qhi && qk[i] >= kth;
         const uint64_t m = __ballot(sel);
         if (sel) emit_one(o, d, pos + mbcnt64(m, 0u), w.cand_idx[d.cand_off + i], w.cand_val[d.cand_off + i]);
         pos += __popcll(m);
@@ -3052,6 +3058,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         g.queue = w.queue;
         g.cand = w.cand_idx;
         g.cval = w.cand_val;
+        g.ckey = w.cand_key;
         DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
             hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o, set_one());

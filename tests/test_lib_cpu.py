@@ -50,10 +50,10 @@ def test_workspace_sizes_scale(L):
     big = L.dgc_select_workspace(10 ** 9, 10 ** 6)
     assert 0 < small < big
     # candidate lists: 6 B per slot, 64 slots per 1024-element segment (0.375 B/elem), the
-    # per-segment counters and offsets (~24 B per segment), plus the resample area: 24 B
-    # per candidate (queue entry 8, index 8, value 4, pair slot 4) for up to
+    # per-segment counters and offsets (~24 B per segment), plus the resample area: 28 B
+    # per candidate (queue entry 8, index 8, value 4, key 4, pair slot 4) for up to
     # min(N, 64k - 1) candidates
-    assert big < (0.375 + 24 / 1024) * 10 ** 9 * 1.05 + 24 * 64 * 10 ** 6
+    assert big < (0.375 + 24 / 1024) * 10 ** 9 * 1.05 + 28 * 64 * 10 ** 6
     assert L.dgc_select_workspace(10 ** 6, 10) < L.dgc_select_workspace(10 ** 6, 1000)
     assert L.dgc_compress_workspace(10 ** 6, 1000, 10309) > L.dgc_select_workspace(10 ** 6, 1000)
     assert L.dgc_decompress_workspace(10 ** 9, 8) > L.dgc_decompress_workspace(10 ** 6, 8)
