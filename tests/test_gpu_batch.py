@@ -261,6 +261,56 @@ def test_batch_index_order_equals_topk_order():
     assert sets > 0
 
 
+def biased_sample_gradient(n, stride, start):
+    """A gradient whose resample set's sampled positions hold its LARGEST keys: 60000
+    magnitudes 3.1 - i * 1e-6 (decreasing with the index) at the first positions the
+    strided sample (start, stride) misses, then 200000 magnitudes 2 + i * 4.5e-6 (the
+    sample's share sets the threshold near their top), N(0, 1e-3) elsewhere."""
+    g = torch.randn(n, generator=torch.Generator().manual_seed(3)) * 1e-3
+    idx = torch.arange(n)
+    free = idx[(idx - start) % stride != 0][:60000]
+    g[free] = 3.1 - torch.arange(60000, dtype=torch.float64).mul(1e-6).float()
+    b0 = int(free[-1]) + 1
+    g[b0: b0 + 200000] = 2.0 + torch.arange(200000, dtype=torch.float64).mul(4.5e-6).float()
+    return g
+
+
+def test_batch_index_order_biased_samples():
+    """K5s bounds its radix passes from 4096 samples taken at fixed candidate positions
+    (rounds 0, 4, 8, 12 in index order) once a set passes 16384 candidates. Here those
+    positions hold the set's largest keys (``biased_sample_gradient``), so the sampled
+    bound sits above the k-th key and the count check must drop it: the set (a resample
+    over ~70k candidates, k = 10000, untied) still equals torch's top-k."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import random
+    from dgc.batch import DGCBatch
+    n = 10_000_000
+    shapes = [("a", (n,)), ("small", (300, 1000))]
+    bs = [DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, device=DEV, seed=11, resample_order=o)
+          for o in ("index", "topk")]
+    stride = bs[0].attrs[0][3]
+    start = random.Random(11).randint(0, stride - 1)   # the batch's first draw: tensor 0's sample start
+    flat = torch.zeros(bs[0].flat_numel)
+    flat[:n] = biased_sample_gradient(n, stride, start)
+    off, m = bs[0].offsets[1], bs[0].numels[1]
+    flat[off: off + m] = torch.randn(m, generator=torch.Generator().manual_seed(4)) * 1e-3
+    outs = []
+    for b in bs:
+        b.grad_flat.copy_(flat.to(DEV))
+        b.compress()
+        outs.append(b.decompress().clone())
+    torch.cuda.synchronize()
+    ia = bs[0].infos()[0]
+    assert ia["branch"] == "resample" and ia["candidates"] > 16384 and ia["tie_rule"] == "set", ia
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    sa, st = bs[0].transmitted()["a"], bs[1].transmitted()["a"]
+    o = np.argsort(st[1].cpu().numpy(), kind="stable")
+    assert np.array_equal(sa[1].cpu().numpy(), st[1].cpu().numpy()[o])
+    assert np.array_equal(bits(sa[0].cpu().numpy()), bits(st[0].cpu().numpy()[o]))
+    assert torch.equal(bs[0].velocity_of("a").view(torch.int32), bs[1].velocity_of("a").view(torch.int32))
+
+
 def designed_big_gradient(n, k, stride, start, seed):
     """A gradient whose resample has more candidates than one workgroup's set path, its
     k-th largest magnitude untied and within an octave above the threshold: k distinct
