@@ -1756,25 +1756,37 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
     const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
     const float* lv = w.lst_val;
     const uint16_t* lo = w.lst_off;
+    // The emit re-reads the entries (from L2) rather than holding them across the scan
+    // and look-back: held, with their offsets, they took the kernel to 145 VGPRs, 3 waves
+    // per SIMD, and 768 of flat-1B's 977 groups resident — the rest started up to 90 us
+    // late (tools/ce_prof.py); re-read it runs at 103 VGPRs, 4 waves, every group at once.
     float4 a[kFirst];
-    uint2 ao[kFirst];   // their offsets too: the emit below then needs no second round trip
 #pragma unroll
     for (int e = 0; e < kFirst; ++e)
-        if ((uint32_t)e < nmax) {
-            a[e] = *reinterpret_cast<const float4*>(lv + lslot(seg0, e, ntile));
-            ao[e] = *reinterpret_cast<const uint2*>(lo + lslot(seg0, e, ntile));
-        }
+        if ((uint32_t)e < nmax) a[e] = *reinterpret_cast<const float4*>(lv + lslot(seg0, e, ntile));
 #pragma unroll
     for (int e = 0; e < kFirst; ++e) {
         const float x[4] = {a[e].x, a[e].y, a[e].z, a[e].w};
 #pragma unroll
         for (int q = 0; q < kCountSegs; ++q) c[q] += (uint32_t)e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
     }
-    for (uint32_t e = kFirst; e < nmax; ++e) {   // longer lists (rare)
-        const float4 b = *reinterpret_cast<const float4*>(lv + lslot(seg0, e, ntile));
-        const float x[4] = {b.x, b.y, b.z, b.w};
+    // longer lists, 8 entries in flight at a time: at 1B a list holds ~7 entries at the
+    // list threshold, so most threads have one of their four lists past 8, and a loop of
+    // one dependent load per entry made this count phase ~37 us of k_count_emit's ~110
+    // (tools/ce_prof.py)
+    for (uint32_t e0 = kFirst; e0 < nmax; e0 += kFirst) {
+        float4 b[kFirst];
 #pragma unroll
-        for (int q = 0; q < kCountSegs; ++q) c[q] += e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
+        for (int e = 0; e < kFirst; ++e)
+            if (e0 + e < nmax) b[e] = *reinterpret_cast<const float4*>(lv + lslot(seg0, e0 + e, ntile));
+#pragma unroll
+        for (int e = 0; e < kFirst; ++e) {
+            if (e0 + e >= nmax) break;
+            const float x[4] = {b[e].x, b[e].y, b[e].z, b[e].w};
+#pragma unroll
+            for (int q = 0; q < kCountSegs; ++q)
+                c[q] += e0 + e < n[q] && n[q] <= (uint32_t)kCap && fabsf(x[q]) >= tc;
+        }
     }
 #pragma unroll
     for (int q = 0; q < kCountSegs; ++q)
@@ -1862,8 +1874,8 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
 #pragma unroll
             for (int e = 0; e < kFirst; ++e)
                 if (e0 + e < nmax) {
-                    ob[e] = e0 == 0 ? ao[e] : *reinterpret_cast<const uint2*>(lo + lslot(seg0, e0 + e, ntile));
-                    vb[e] = e0 == 0 ? a[e] : *reinterpret_cast<const float4*>(lv + lslot(seg0, e0 + e, ntile));
+                    ob[e] = *reinterpret_cast<const uint2*>(lo + lslot(seg0, e0 + e, ntile));
+                    vb[e] = *reinterpret_cast<const float4*>(lv + lslot(seg0, e0 + e, ntile));
                 }
 #pragma unroll
             for (int e = 0; e < kFirst; ++e) {
