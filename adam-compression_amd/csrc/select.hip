@@ -87,7 +87,8 @@ constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks 
 constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
 constexpr float kSpecMarginMax = 0.95f;
 // K5s, the set path of an untied resample (resample_order = 1; see k_resample_set)
-constexpr int kSetReg = 32;                  // one workgroup: keys per thread kept in registers
+constexpr int kSetReg = 16;                  // one workgroup: keys per thread kept in registers (32
+                                             // spilled the radix passes' registers to scratch)
 constexpr int kSetRounds = 256;              // one workgroup up to kSetRounds x 1024 candidates
 constexpr int64_t kSetMax = (int64_t)kSetRounds * 1024;
 // One workgroup up to this many candidates, even for a tensor with a sliced-path slot:
@@ -2534,16 +2535,18 @@ __device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_fl
     // back with every slot's loads independent (a per-round emit waited for the index
     // and value gathers of each round in turn: two dependent round trips per 1024 keys)
     SET_STAMP(4);
-    // (n <= 32K: the keys are all in registers and the LDS rounds' area takes them)
+    // (into the LDS rounds' area past the rounds it holds, when k positions fit there)
     DGC_GLB uint32_t* spos = glb(w.gpos + d.gpos_off);
-    const bool in_lds = rounds <= kSetReg;   // uniform
+    const int64_t lds_used = (int64_t)(rounds > kSetReg ? rounds - kSetReg : 0) * kScanThreads;
+    const bool in_lds = rounds <= kSetReg + kSetLds && lds_used + (int64_t)k <= (int64_t)kSetLds * kScanThreads;
+    uint32_t* lpos = kl + (kSetLds * kScanThreads - k);   // (used only when in_lds)
     for_keys([&](int r, uint32_t x) {   // uniform in r
         const bool sel = tid + r * kScanThreads < n && x >= kth;
         const uint64_t m = __ballot(sel);
         if (sel) {
             const uint32_t q = rbase[r * kWaves + wv] + mbcnt64(m, 0u), i = (uint32_t)(tid + r * kScanThreads);
             if (in_lds)
-                kl[q] = i;
+                lpos[q] = i;
             else
                 spos[q] = i;
         }
@@ -2561,7 +2564,7 @@ __device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_fl
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t q = q0 + u * kScanThreads + tid;
-            const uint32_t i = q < k ? (in_lds ? kl[q] : spos[q]) : 0u;
+            const uint32_t i = q < k ? (in_lds ? lpos[q] : spos[q]) : 0u;
             li[u] = q < k ? cand[i] : 0;
             x[u] = q < k ? cval[i] : 0.f;
         }
