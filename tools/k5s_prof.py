@@ -56,7 +56,21 @@ def main():
             r["end"] = round((s[6] - t0) * 0.01, 2) if s[6] else None
             rows.append(r)
         rows.sort(key=lambda r: -(r["end"] or 0))
-        print(json.dumps({"step": i, "slowest": rows[:6]}), flush=True)
+        # k_nth_select after it (every workgroup stamps its start [7] and end [6]):
+        # first / last workgroup start and last end, from the same origin
+        T = min(64, len(infos))
+        st7 = [p.bt[t][7] for t in range(T) if p.bt[t][7]]
+        en6 = [p.bt[t][6] for t in range(T) if p.bt[t][6]]
+        rel = lambda x: round((x - t0) * 0.01, 2) if t0 and x else None  # noqa: E731
+        nth = dict(first_start=rel(min(st7, default=0)), last_start=rel(max(st7, default=0)),
+                   last_end=rel(max(en6, default=0)), workgroups=len(st7))
+        # the finishing workgroup (an idle one: slots 0-2 = branch read, arrival, finish)
+        fin = [t for t in range(T) if p.bt[t][1]]
+        if fin:
+            f = fin[0]
+            nth["finisher"] = dict(t=f, start=rel(p.bt[f][7]), read=rel(p.bt[f][0]), arrived=rel(p.bt[f][1]),
+                                   finished=rel(p.bt[f][2]), end=rel(p.bt[f][6]))
+        print(json.dumps({"step": i, "nth_select": nth, "slowest": rows[:6]}), flush=True)
 
 
 if __name__ == "__main__":
