@@ -1949,33 +1949,43 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
     }
     __syncthreads();
     for (int t = threadIdx.x; t < w.T; t += blockDim.x) {
+        // every load first, by value (a store through st, info or spec could alias a
+        // later load: interleaved they were one dependent memory round trip each, 6.5 us
+        // for ResNet-50's 54 tensors), then the stores
         SelState* st = w.st + t;
-        st->epoch += 1;
-        const uint32_t k5 = w.nthg[t].status | (st->branch == DGC_BRANCH_RESAMPLE ? f.force : 0u);
+        const SelState s = *st;
+        const int64_t k = w.td[t].k;
+        const bool tail = w.td[t].tail;
+        const uint32_t status = w.nthg[t].status;
+        float* spec = w.spec ? w.spec + kSpecWords * t : nullptr;
+        const float used = spec ? spec[0] : __builtin_huge_valf();
+        const float prev = spec ? spec[1] : __builtin_huge_valf();
+        const uint32_t k5 = status | (s.branch == DGC_BRANCH_RESAMPLE ? f.force : 0u);
         if (k5 & DGC_K5_BROKEN) atomicOr(&broken, k5);
-        const long long cnt = final_count(*st, w.td[t].k);
-        // what the next K1 must zero (first-k branches of a deferring engine only)
-        st->def_mode = (defer && st->branch != DGC_BRANCH_RESAMPLE && !w.td[t].tail && cnt > 0) ? 1 : 0;
-        st->def_t = st->t_cur;
-        st->def_limit = st->limit;
-        st->def_mask_mmt = mask_mmt;
+        const long long cnt = final_count(s, k);
         atomicAdd(&total, (unsigned long long)cnt);
+        st->epoch = s.epoch + 1;
+        // what the next K1 must zero (first-k branches of a deferring engine only)
+        st->def_mode = (defer && s.branch != DGC_BRANCH_RESAMPLE && !tail && cnt > 0) ? 1 : 0;
+        st->def_t = s.t_cur;
+        st->def_limit = s.limit;
+        st->def_mask_mmt = mask_mmt;
         if (info) {
             dgc_select_info& r = info[t];
             r.count = cnt;
-            r.candidates = st->n_cur;
-            r.threshold0 = st->t0;
-            r.threshold = st->t_cur;
-            r.branch = st->branch;
-            r.recounts = st->recounts;
-            r.overflow_segments = st->full_passes ? st->overflow : st->list_spills;
-            r.full_passes = st->full_passes;
-            r.tie_rule = st->tie_rule;
-            r.window_keys = st->win_keys;
+            r.candidates = s.n_cur;
+            r.threshold0 = s.t0;
+            r.threshold = s.t_cur;
+            r.branch = s.branch;
+            r.recounts = s.recounts;
+            r.overflow_segments = s.full_passes ? s.overflow : s.list_spills;
+            r.full_passes = s.full_passes;
+            r.tie_rule = s.tie_rule;
+            r.window_keys = s.win_keys;
             r.k5_status = (int32_t)k5;
-            r.list_threshold = w.spec ? w.spec[kSpecWords * t] : __builtin_huge_valf();   // (updated below)
+            r.list_threshold = used;   // (this call's; spec[0] is updated below)
         }
-        if (w.spec) {
+        if (spec) {
             // spec[0]: next call's list threshold = m x t x growth, growth = 2 - spec[1] / t
             //   (linear extrapolation from the previous final threshold spec[1]) clamped to
             //   [1, 1.5]; spec[1] := t. The ratio t / spec[1] overshoots while the growth
@@ -1990,11 +2000,9 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             //   threshold's candidates), was measured and dropped: on ResNet-50 its longer
             //   lists cost the list counts and the lowering 23 + 14 + 25 us where these take
             //   14 + 5 + 5, and the full passes stayed (same box, 0.372 vs 0.337 ms/step).
-            float* spec = w.spec + kSpecWords * t;
-            const float tc = st->t_cur;
-            const float used = spec[0];
+            const float tc = s.t_cur;
             const bool finite = tc == tc && tc > 0.f && tc < __builtin_huge_valf();
-            const float gr = fminf(fmaxf(2.f - spec[1] / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
+            const float gr = fminf(fmaxf(2.f - prev / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
             float m = margin;
             if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
                 m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
@@ -2900,7 +2908,13 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
         nth_element_wg(glb(w.queue + d.cand_off), st->n_cur, d.k - 1, gl, gr, lq, llp, lrp, lmk,
                        from_global ? w.nthg + t : nullptr);
     }
-    if (f.on && last_block_arrival(w.fin_ticket, gridDim.x)) sel_finish_body(w, f);
+    const bool idle = !(st->branch == DGC_BRANCH_RESAMPLE && (st->rs_nth == 1 || st->rs_nth == 2));
+    if (idle) K5_STAMP(0);   // (profiling build: slots 0-2 are free when the replay did not run)
+    if (f.on && last_block_arrival(w.fin_ticket, gridDim.x)) {
+        if (idle) K5_STAMP(1);
+        sel_finish_body(w, f);
+        if (idle) K5_STAMP(2);
+    }
     K5_STAMP(6);
 }
 
