@@ -46,6 +46,16 @@ def local_rank():
     return int(os.environ.get("LOCAL_RANK", rank()))
 
 
+# A world of one rank returns its input without a collective. Cleared (tests), an
+# initialised one-rank group runs the collective path itself — on a one-GPU box the
+# only way to execute the RCCL branch (tests/test_gpu_rccl.py).
+ONE_RANK_SHORTCUT = True
+
+
+def _shortcut(W):
+    return W == 1 and (ONE_RANK_SHORTCUT or not is_initialized())
+
+
 def _backend_needs_host(t):
     """gloo moves host tensors only; keep GPU tensors on the GPU for nccl (RCCL)."""
     return t.is_cuda and dist.get_backend() != "nccl"
@@ -75,7 +85,7 @@ def allreduce_async_(tensor, name=None, op=Average):
     if op not in (Average, Sum):
         raise NotImplementedError(f"allreduce op {op!r} (Adasum is out of scope)")
     W = size()
-    if W == 1:
+    if _shortcut(W):
         return Handle(output=tensor)
     staged = tensor.cpu() if _backend_needs_host(tensor) else tensor
     work = dist.all_reduce(staged, op=dist.ReduceOp.SUM, async_op=True)
@@ -93,7 +103,7 @@ def allreduce_async_(tensor, name=None, op=Average):
 def allgather_async(tensor, name=None):
     """Variable-length allgather along dim 0 (Horovod semantics)."""
     W = size()
-    if W == 1:
+    if _shortcut(W):
         return Handle(output=tensor)
     dev = tensor.device
     staged = tensor.cpu() if _backend_needs_host(tensor) else tensor
@@ -119,7 +129,7 @@ def allgather_packed_async(payload, out=None):
     W = size()
     if out is None:
         out = torch.empty(W * payload.numel(), dtype=torch.uint8, device=payload.device)
-    if W == 1:
+    if _shortcut(W):
         if out.data_ptr() != payload.data_ptr():
             out.copy_(payload)
         return Handle(output=out)

@@ -1,0 +1,90 @@
+"""The RCCL branch of the collective facade (dgc/comm.py), executed on one MI355X.
+
+A one-GPU box cannot hold two RCCL ranks, so these tests initialise a one-rank `nccl`
+process group (RCCL on ROCm) and clear `comm.ONE_RANK_SHORTCUT`: the collectives then
+run `all_gather_into_tensor` / `all_reduce` on the device tensors themselves (no host
+staging — that is gloo's branch), as at W > 1. Checked: the packed payload allgather,
+the variable-row allgather and the Average allreduce return their inputs, and the
+reference's per-tensor hook path (dgc/horovod/optimizer.py:116-187: compress ->
+packed allgather -> decompress, dense tensors allreduced) over RCCL equals the same
+steps without a collective bit for bit.
+"""
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+import test_gpu_dropin as dropin
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture
+def rccl_one_rank(monkeypatch):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dgc import comm
+    assert not dist.is_initialized()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=DEV)
+    monkeypatch.setattr(comm, "ONE_RANK_SHORTCUT", False)
+    try:
+        assert dist.get_backend() == "nccl" and comm.size() == 1
+        yield comm
+    finally:
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_comm_collectives_over_rccl(rccl_one_rank):
+    comm = rccl_one_rank
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    payload = torch.randint(0, 256, (4099,), dtype=torch.uint8, device=DEV, generator=gen)
+    h = comm.allgather_packed_async(payload)
+    assert h._work is not None   # a collective was issued (the shortcut returns the input)
+    out = comm.synchronize(h)
+    assert out.is_cuda and out.data_ptr() != payload.data_ptr()
+    assert torch.equal(out, payload)
+    rows = torch.randn(37, 3, device=DEV, generator=gen)
+    assert torch.equal(comm.synchronize(comm.allgather_async(rows)), rows)
+    x = torch.randn(1 << 16, device=DEV, generator=gen)
+    want = x.clone()
+    assert torch.equal(comm.synchronize(comm.allreduce_async_(x, op=comm.Average)), want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fp16", [False, True], ids=["wire-dtype-int64", "wire-fp16-int32"])
+def test_per_tensor_path_over_rccl(fp16, rccl_one_rank, monkeypatch):
+    """The hook path with every payload through RCCL equals it with none."""
+    modes = ["fresh", "fresh", "inplace", "fresh"]
+    calls = {"all_gather_into_tensor": 0, "all_reduce": 0}
+
+    def counted(name):
+        fn = getattr(dist, name)
+
+        def wrapper(*a, **kw):
+            calls[name] += 1
+            return fn(*a, **kw)
+        return wrapper
+
+    for name in calls:
+        monkeypatch.setattr(rccl_one_rank.dist, name, counted(name))
+    got = dropin._run(False, fp16, modes, monkeypatch)
+    # every step: a packed allgather per compressed tensor, an allreduce per dense one
+    assert calls["all_gather_into_tensor"] >= len(modes) and calls["all_reduce"] >= len(modes), calls
+    monkeypatch.setattr(rccl_one_rank, "ONE_RANK_SHORTCUT", True)
+    want = dropin._run(False, fp16, modes, monkeypatch)
+    for step, (w, g) in enumerate(zip(want, got)):
+        assert w.keys() == g.keys()
+        for k in w:
+            assert w[k] is not None and g[k] is not None, (step, k)
+            assert torch.equal(dropin._bits(w[k]), dropin._bits(g[k])), (step, k)
