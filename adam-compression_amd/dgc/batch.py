@@ -147,6 +147,8 @@ class DGCBatch:
         nbuf = 2 if self.fill == "sparse" else 1
         self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(nbuf)]
         # W > 1, fp32: the allgather in parts, each scattered as it lands (dgc/exchange.py)
+        # (W = 1 exchanges too when comm.one_rank_collectives(): the RCCL tests' one-rank group)
+        self.exchanging = self.world > 1 or comm.one_rank_collectives()
         self.parts = 1 if self.half else split_parts(self.world, self.capacity, self.exchange_parts)
         self.xchg = None
         self._inflight = None
@@ -156,7 +158,7 @@ class DGCBatch:
             self._gathers = self.xchg.gathers
         else:
             self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=self.device)
-                              for _ in range(nbuf)] if self.world > 1 else self._payloads)
+                              for _ in range(nbuf)] if self.exchanging else self._payloads)
         self._par = 0
         self._last_out = None
         self._last_gathered = None
@@ -284,7 +286,7 @@ class DGCBatch:
     def send(self):
         """Issues the exchange of this step's payload (W > 1): one allgather, or one per
         part (split); ``decompress`` waits for it."""
-        if self.world > 1:
+        if self.exchanging:
             if self.xchg is not None:
                 self._inflight = self.xchg.send(self.payload, self.gathered)
             else:
@@ -320,7 +322,7 @@ class DGCBatch:
         if self.xchg is None:
             for h in handles:
                 h.wait()
-        elif self.world > 1 and not handles:
+        elif self.exchanging and not handles:
             raise RuntimeError("DGCBatch: decompress of a split exchange before send() / exchange()")
         if self.half:   # zero_(), the runs in rank order (each add rounded), the 1/W scale
             _lib.check(L.dgc_decompress_packed16(cur.data_ptr(), self.world, self.rank_stride, self.capacity,

@@ -121,8 +121,10 @@ class DGCBucket:
         self.fill = fill
         nbuf = 2 if fill == "sparse" else 1   # the previous step's gathered indices stay readable
         self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        # (W = 1 exchanges too when comm.one_rank_collectives(): the RCCL tests' one-rank group)
+        self.exchanging = self.world > 1 or comm.one_rank_collectives()
         self._gathers = ([torch.zeros(self.world * self.rank_stride, dtype=torch.uint8, device=dev)
-                          for _ in range(nbuf)] if self.world > 1 else self._payloads)
+                          for _ in range(nbuf)] if self.exchanging else self._payloads)
         # W > 1: the allgather in parts, each scattered as it lands (dgc/exchange.py)
         self.parts = split_parts(self.world, self.k, exchange_parts)
         self.xchg = None
@@ -203,7 +205,7 @@ class DGCBucket:
         """The packed allgather (RCCL over xGMI; gloo stages through the host). Split
         (``parts`` > 1): the parts' collectives are only issued; decompress waits for
         each as it scatters it."""
-        if self.world > 1:
+        if self.exchanging:
             if self.xchg is not None:
                 self._inflight = self.xchg.send(self.payload, self.gathered)
             else:

@@ -56,6 +56,12 @@ def _shortcut(W):
     return W == 1 and (ONE_RANK_SHORTCUT or not is_initialized())
 
 
+def one_rank_collectives():
+    """An initialised one-rank group with the shortcut cleared: the engines exchange
+    through the collectives as at W > 1 (DGCBucket, DGCBatch, the split exchange)."""
+    return is_initialized() and not ONE_RANK_SHORTCUT
+
+
 def _backend_needs_host(t):
     """gloo moves host tensors only; keep GPU tensors on the GPU for nccl (RCCL)."""
     return t.is_cuda and dist.get_backend() != "nccl"

@@ -31,12 +31,13 @@ def split_parts(world, capacity, parts="auto"):
     env = os.environ.get("DGC_EXCHANGE_PARTS")
     if parts == "auto" and env:
         parts = int(env)
+    multi = world > 1 or comm.one_rank_collectives()
     if parts == "auto":
-        if world <= 1 or world * capacity < (1 << 20):
+        if not multi or world * capacity < (1 << 20):
             return 1
         return 2 if world <= 4 else 4
     parts = int(parts)
-    if world <= 1 or parts <= 1:
+    if not multi or parts <= 1:
         return 1
     if parts > 8 or world * parts > 64:
         raise ValueError(f"exchange parts must be 1..8 with world * parts <= 64 (world {world}, parts {parts})")

@@ -158,7 +158,7 @@ class BatchedStep:
             plan["dense_ptrs"] = (ctypes.c_void_p * T)()
             plan["dense_numels"] = (ctypes.c_int64 * T)(*[p.numel() for _, p in dense])
             plan["dense_offs"] = (ctypes.c_int64 * T)(*offs)
-            if comm.size() > 1 and not self.half:
+            if (comm.size() > 1 or comm.one_rank_collectives()) and not self.half:
                 plan["dense_wire"] = torch.empty(end, dtype=torch.float16 if c.fp16_values else torch.float32,
                                                  device=dev)
             if self.half:   # the gathered 16-bit gradients (K1-16's dense branch reads one buffer)
@@ -290,7 +290,7 @@ class BatchedStep:
         _lib.check(L.dgc_gather16(plan["dense_ptrs"], plan["dense_numels"], plan["dense_offs"], len(plan["dense"]),
                                   _lib.ptr(dense_in), st), "dgc_gather16")
         wire = dense_in.to(torch.float16) if self.comp.fp16_values else dense_in
-        if comm.size() > 1:
+        if comm.size() > 1 or comm.one_rank_collectives():
             return comm.allreduce_async_(wire, op=Average)
         if wire is not dense_in:
             dense_in.copy_(wire)   # the fp16 round trip of a bf16 gradient

@@ -88,3 +88,97 @@ def test_per_tensor_path_over_rccl(fp16, rccl_one_rank, monkeypatch):
         for k in w:
             assert w[k] is not None and g[k] is not None, (step, k)
             assert torch.equal(dropin._bits(w[k]), dropin._bits(g[k])), (step, k)
+
+
+def _engine_steps(make, step, steps=5, seed=3):
+    """Outputs of ``steps`` engine steps on seeded gradients (odd steps heavy-tailed:
+    the adaptation loop and the resample run)."""
+    eng = make()
+    gen = torch.Generator(device=DEV).manual_seed(seed)
+    res = []
+    for s in range(steps):
+        res.append(step(eng, s, gen).clone())
+        torch.cuda.synchronize()
+    return eng, res
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("parts", [1, 2], ids=["one-collective", "split-2"])
+@pytest.mark.parametrize("fill", ["inline", "sparse"])
+def test_bucket_over_rccl(fill, parts, rccl_one_rank, monkeypatch):
+    """DGCBucket's exchange through RCCL (one allgather, or the split exchange's two
+    part collectives with the compute stream waiting on each in turn) equals the
+    one-rank step without a collective."""
+    from dgc.bucket import DGCBucket
+    comm = rccl_one_rank
+    N = 3_000_017
+
+    def grad(s, gen):
+        g = torch.randn(N, generator=gen, device=DEV)
+        return g * torch.rand(N, generator=gen, device=DEV).pow(8) * 50 if s % 2 else g
+
+    def run(collective):
+        monkeypatch.setattr(comm, "ONE_RANK_SHORTCUT", not collective)
+        out = torch.zeros(N, device=DEV)
+
+        def step(b, s, gen):
+            b.step(grad(s, gen), out)
+            return out
+        b, res = _engine_steps(lambda: DGCBucket(N, compress_ratio=0.001, momentum=0.9, nesterov=True, device=DEV,
+                                                 world_size=1, seed=42, fill=fill,
+                                                 exchange_parts=parts if collective else 1), step)
+        assert b.exchanging == collective and b.parts == (parts if collective else 1)
+        return res
+
+    got = run(True)
+    want = run(False)
+    for s, (w, g) in enumerate(zip(want, got)):
+        assert torch.equal(w.view(torch.int32), g.view(torch.int32)), s
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("parts", [1, 2], ids=["one-collective", "split-2"])
+@pytest.mark.parametrize("fill", ["inline", "sparse"])
+def test_batch_over_rccl(fill, parts, rccl_one_rank, monkeypatch):
+    """DGCBatch likewise (every tensor's entries in one payload, one exchange)."""
+    from dgc.batch import DGCBatch
+    comm = rccl_one_rank
+    shapes = [("a", (1000, 300)), ("b", (257, 3, 3, 64)), ("c", (70001,)), ("d", (2000, 500))]
+
+    def step(b, s, gen):
+        for n in b.names:
+            g = torch.randn(b.shapes[n], generator=gen, device=DEV) * 1e-3
+            if s % 2:
+                g = g * torch.rand(b.shapes[n], generator=gen, device=DEV).pow(8) * 50
+            b.grad(n).copy_(g)
+        b.compress()
+        b.exchange()
+        return b.decompress()
+
+    def run(collective):
+        monkeypatch.setattr(comm, "ONE_RANK_SHORTCUT", not collective)
+        b, res = _engine_steps(lambda: DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, nesterov=False,
+                                                device=DEV, world_size=1, seed=7, fill=fill,
+                                                exchange_parts=parts if collective else 1), step)
+        assert b.exchanging == collective and b.parts == (parts if collective else 1)
+        return res
+
+    got = run(True)
+    want = run(False)
+    for s, (w, g) in enumerate(zip(want, got)):
+        assert torch.equal(w.view(torch.int32), g.view(torch.int32)), s
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("batch", [True, "sparse"], ids=["batch", "batch-sparse"])
+def test_batched_optimizer_over_rccl(batch, rccl_one_rank, monkeypatch):
+    """DistributedOptimizer(batch=True): the grouped payload allgather and the dense
+    tensors' allreduce through RCCL equal the one-rank step without them."""
+    modes = ["fresh", "fresh", "inplace", "fresh"]
+    got = dropin._run(batch, True, modes, monkeypatch)
+    monkeypatch.setattr(rccl_one_rank, "ONE_RANK_SHORTCUT", True)
+    want = dropin._run(batch, True, modes, monkeypatch)
+    for step, (w, g) in enumerate(zip(want, got)):
+        assert w.keys() == g.keys()
+        for k in w:
+            assert torch.equal(dropin._bits(w[k]), dropin._bits(g[k])), (step, k)
