@@ -25,6 +25,7 @@ import ctypes
 import io
 import json
 import os
+import socket
 import sys
 import time
 
@@ -63,6 +64,9 @@ def parse():
     ap.add_argument("--cpu-numel-1t", type=float, default=5e7, help="CPU-baseline sample (1 thread), flat")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rccl-one-rank", action="store_true",
+                    help="N=1: exchange through a one-rank RCCL group as at N > 1 (the allgather path and its "
+                         "timing executed on a one-GPU box); not the headline configuration")
     ap.add_argument("--phases", action="store_true", help="HIP events around every phase (adds markers)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the dense-fill pass and (W = 1) the drop-in DistributedOptimizer comparison")
@@ -341,12 +345,12 @@ class ModelRun:
         st = self._lib.stream_of(g.device)
         wt = self._lib.VD[self.dense_wire.dtype]
         f32 = self._lib.VD[torch.float32]
-        if self.world == 1:
+        from dgc import comm
+        if self.world == 1 and not comm.one_rank_collectives():
             self._lib.check(L.dgc_compensate_wire(gd.data_ptr(), f32, wt, self.dense_mmt.data_ptr(),
                                                   self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov),
                                                   st), "dgc_compensate_wire")
             return
-        from dgc import comm
         src = (ctypes.c_void_p * 1)(gd.data_ptr())
         self._lib.check(L.dgc_gather_cast(src, self._one[0], self._one[1], 1, self.dense_wire.data_ptr(), wt, st),
                         "dgc_gather_cast")
@@ -563,6 +567,27 @@ def step_bytes(run, world, full_passes):
     return contract, required
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """File-descriptor level: RCCL prints its version banner to stdout when a
+    communicator comes up; the bench's stdout carries the one JSON line only."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def _init_group(dev, **kw):
+    with _stdout_to_stderr():
+        dist.init_process_group("nccl", device_id=dev, **kw)
+        dist.barrier()   # the communicator is up (and has printed) before stdout is back
+
+
 # ---------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -577,11 +602,21 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     backend = None
+    one_rank = args.rccl_one_rank and world == 1
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        _init_group(dev)
         backend = dist.get_backend()
         if dist.get_world_size() != world:
             raise SystemExit(f"bench.py: WORLD_SIZE={world} but the process group has {dist.get_world_size()} ranks")
+    elif one_rank:   # a one-rank RCCL group, the engines exchanging through it (dgc/comm.py)
+        from dgc import comm
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        _init_group(dev, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        comm.ONE_RANK_SHORTCUT = False
+        backend = dist.get_backend()
+    coll = world > 1 or one_rank
     run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev, args.fill)
 
     log(f"{args.workload}: rank {rank}/{world} set up")
@@ -592,7 +627,7 @@ def main():
     # HIP events in the timed steps: K1 (the roofline kernel) always; the allgather when
     # there is one (its bus bandwidth); every phase only with --phases — each event pair
     # costs the GPU a few µs of idle time, ~7 % of a ResNet-50 step with all four phases
-    timed = phases if args.phases else (("compensate", "allgather") if world > 1 else ("compensate",))
+    timed = phases if args.phases else (("compensate", "allgather") if coll else ("compensate",))
     evs = [{p: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for p in timed}
            for _ in range(args.steps)]
     if world > 1:
@@ -625,7 +660,7 @@ def main():
         extras["dense_fill"] = {"ms_per_step": round(dense, 4), "steps": args.steps,
                                 "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
                                         "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
-    xgmi = allgather_probe(run, world) if world > 1 else None
+    xgmi = allgather_probe(run, world) if coll else None
     probe = hbm_probe(*run.probe_buffers())   # after the timed steps: overwrites the state
     ms_step = elapsed * 1e3 / args.steps
     full_passes = info.get("full_passes", 0)
@@ -634,7 +669,7 @@ def main():
     traffic, traffic_src = pmc_traffic(args.workload)
     prof_ms, prof_src = rocprof_k1_ms(args.workload)
     if rank != 0:
-        if world > 1:
+        if coll:
             dist.destroy_process_group()
         return
     k1_ms = ms["compensate"]   # HIP events around K1's launch on the stream it runs on
@@ -650,7 +685,8 @@ def main():
         "unit": "grad elements/s",
         "n_gpus": world,
         "world_size": dist.get_world_size() if world > 1 else 1,
-        "backend": (f"{backend} (RCCL over xGMI)" if backend == "nccl" else backend) if world > 1 else "none (1 rank)",
+        "backend": ((f"{backend} (RCCL over xGMI)" if backend == "nccl" else backend) if world > 1 else
+                    "nccl (RCCL, one rank: --rccl-one-rank)" if one_rank else "none (1 rank)"),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_step,
@@ -680,7 +716,10 @@ def main():
         "compensate_ms_per_step": [round(e["compensate"][0].elapsed_time(e["compensate"][1]), 3) for e in evs],
         "selection": info,
     }
-    if xgmi is not None:
+    if xgmi is not None and world == 1:   # --rccl-one-rank: the collective's own cost, no link traffic
+        res["allgather"] = dict({"payload_bytes_per_rank": run.payload,
+                                 "note": "one rank: the RCCL collectives' cost without link traffic"}, **xgmi)
+    elif xgmi is not None:
         bus = (world - 1) * run.payload / (xgmi["single_ms"] * 1e-3) / 1e9
         res["allgather"] = dict({"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
                                  "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS),
@@ -701,7 +740,7 @@ def main():
         res["cpu_baseline"] = cpu_baseline(run, wl, args.cpu_numel, args.cpu_steps, cores)
         res["cpu_baseline_1thread"] = cpu_baseline(run, wl, args.cpu_numel_1t, 2, 1)
     print(json.dumps(res), flush=True)
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 
