@@ -2481,6 +2481,7 @@ __device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_fl
                 atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
         });
         __syncthreads();
+        if (hi == L) SET_STAMP(7);   // (profiling build: the first pass's histogram done)
         if (tid == 0) sel_bin = -1;
         int bin;
         uint32_t above;

@@ -54,6 +54,7 @@ def main():
             for j, nm in enumerate(names):
                 r[nm] = round((s[j + 1] - s[j]) * 0.01, 2) if s[j + 1] and s[j] else None
             r["end"] = round((s[6] - t0) * 0.01, 2) if s[6] else None
+            r["pass1"] = round((s[7] - s[2]) * 0.01, 2) if s[7] and s[2] else None   # of "radix"
             rows.append(r)
         rows.sort(key=lambda r: -(r["end"] or 0))
         # k_nth_select after it (every workgroup stamps its start [7] and end [6]):
