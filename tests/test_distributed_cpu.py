@@ -51,3 +51,30 @@ def test_comm_collectives_gloo():
         assert gathered == [0.0, 1.0, 10.0, 11.0, 12.0]       # rank order, ragged rows
         assert avg == [1.5, 1.5, 1.5] and sm == [3.0, 3.0]
         assert size == 2 and rk == rank
+
+
+@pytest.mark.timeout(120)
+def test_one_rank_shortcut_switch(monkeypatch):
+    """Without a group a world of one never issues a collective; a one-rank group with
+    comm.ONE_RANK_SHORTCUT cleared does (the RCCL tests' switch, here over gloo)."""
+    import torch
+    import torch.distributed as dist
+    from dgc import comm
+    assert comm.size() == 1 and not comm.one_rank_collectives()
+    monkeypatch.setattr(comm, "ONE_RANK_SHORTCUT", False)
+    assert not comm.one_rank_collectives()   # no group: still the shortcut
+    h = comm.allreduce_async_(torch.ones(3))
+    assert h._work is None
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{H.free_port()}", rank=0, world_size=1)
+    try:
+        assert comm.one_rank_collectives()
+        t = torch.arange(6, dtype=torch.float32).view(3, 2)
+        h = comm.allgather_async(t)
+        assert h._work is not None and torch.equal(comm.synchronize(h), t)
+        x = torch.full((4,), 3.0)
+        h = comm.allreduce_async_(x, op=comm.Average)
+        assert h._work is not None and torch.equal(comm.synchronize(h), torch.full((4,), 3.0))
+        monkeypatch.setattr(comm, "ONE_RANK_SHORTCUT", True)
+        assert not comm.one_rank_collectives() and comm.allreduce_async_(x)._work is None
+    finally:
+        dist.destroy_process_group()
