@@ -215,23 +215,29 @@ __global__ void __launch_bounds__(kBlock) k_gather_cast(MtChunk c, void* __restr
 // what decompress hands it, dgc/compression.py:195-198): the source is the allreduce
 // buffer — fp32, or fp16 widened exactly as `tensor.type(vdtype)` does — or, ROUND16, an
 // fp32 gradient rounded to fp16 and back (a one-rank exchange of an fp16 wire, with no
-// buffer in between). Four elements per thread; the dense tensors are small.
+// buffer in between). div != 1: the source is the allreduce's SUM and the Average's
+// `div_(W)` happens here, in the wire dtype as torch does it (fp32 quotient, rounded to
+// fp16 for an fp16 wire) — no ATen launch. Four elements per thread; the dense tensors
+// are small.
 template <bool NEST, int SRC>   // SRC: 0 fp32, 1 fp16, 2 fp32 rounded through fp16
 __global__ void __launch_bounds__(kBlock)
 k_compensate_wire(const void* __restrict__ src, float* __restrict__ mmt, float* __restrict__ out, int64_t n,
-                  float mom) {
+                  float mom, float div) {
     const int64_t e0 = (int64_t)blockIdx.x * kBlock * 4 + threadIdx.x;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int64_t e = e0 + (int64_t)j * kBlock;
         if (e >= n) break;
         float g;
-        if (SRC == 1)
+        if (SRC == 1) {
             g = f16_to_f32(static_cast<const uint16_t*>(src)[e]);
-        else if (SRC == 2)
+            if (div != 1.f) g = f16_to_f32(f32_to_f16(g / div));
+        } else if (SRC == 2) {
             g = f16_to_f32(f32_to_f16(static_cast<const float*>(src)[e]));
-        else
+        } else {
             g = static_cast<const float*>(src)[e];
+            if (div != 1.f) g = g / div;
+        }
         float m = mmt[e], v = 0.f;
         const float o = comp1<NEST, false>(g, m, v, mom);
         mmt[e] = m;
@@ -330,8 +336,10 @@ int gather_cast(const float* const* srcs, const int64_t* numels, const int64_t* 
 }
 
 int compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float* mmt, float* out, int64_t n,
-                    float mom, bool nesterov, hipStream_t st) {
+                    float mom, bool nesterov, hipStream_t st, int32_t divisor = 1) {
     if (n < 0 || (n > 0 && (!src || !mmt || !out))) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_wire: bad arguments");
+    if (divisor < 1 || (divisor > 1 && round_to != DGC_F32))
+        DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_wire_avg: divisor >= 1, and > 1 only for an exchanged (round_to fp32) source");
     if (n == 0) return DGC_OK;
     int mode;
     if (src_dtype == DGC_F16 && round_to == DGC_F32) mode = 1;
@@ -341,7 +349,8 @@ int compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float*
     const int64_t grid = ceil_div(n, (int64_t)kBlock * 4);
     if (grid > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_wire: n too large");
     const dim3 gd((unsigned)grid), bd(kBlock);
-#define DGC_WIRE(NE, M) hipLaunchKernelGGL((k_compensate_wire<NE, M>), gd, bd, 0, st, src, mmt, out, n, mom)
+    const float div = (float)divisor;
+#define DGC_WIRE(NE, M) hipLaunchKernelGGL((k_compensate_wire<NE, M>), gd, bd, 0, st, src, mmt, out, n, mom, div)
     if (nesterov) {
         if (mode == 0) DGC_WIRE(true, 0); else if (mode == 1) DGC_WIRE(true, 1); else DGC_WIRE(true, 2);
     } else {
@@ -444,6 +453,12 @@ extern "C" int dgc_compensate_wire(const void* src, int32_t src_dtype, int32_t r
                                    int64_t n, float momentum, int32_t nesterov, void* stream) {
     return dgc::compensate_wire(src, src_dtype, round_to, mmt, out, n, momentum, nesterov != 0,
                                 static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_compensate_wire_avg(const void* src, int32_t src_dtype, int32_t world, float* mmt, float* out,
+                                       int64_t n, float momentum, int32_t nesterov, void* stream) {
+    return dgc::compensate_wire(src, src_dtype, DGC_F32, mmt, out, n, momentum, nesterov != 0,
+                                static_cast<hipStream_t>(stream), world);
 }
 
 extern "C" int dgc_sample_strided(const float* vec, int64_t n, int64_t start, int64_t stride,

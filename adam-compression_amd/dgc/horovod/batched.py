@@ -248,7 +248,8 @@ class BatchedStep:
             elif wire is not None:   # compress: tensor.type(float16) (dgc/compression.py:175-177)
                 _lib.check(L.dgc_gather_cast(dptrs, plan["dense_numels"], plan["dense_offs"], len(plan["dense"]),
                                              _lib.ptr(wire), _lib.VD[wire.dtype], st), "dgc_gather_cast")
-                dense_handle = comm.allreduce_async_(wire, op=Average)
+                # Average = the SUM here, its div_(W) folded into dgc_compensate_wire_avg
+                dense_handle = comm.allreduce_async_(wire, op=comm.Sum)
         if b is not None:
             b.decompress()   # into the batch's output, then p.grad (dgc/compression.py:191-194)
             glue.bind_grads(plan["comp_params"], plan["comp_views"])
@@ -266,10 +267,10 @@ class BatchedStep:
                                               _lib.VD[self.dtype], st), "dgc_compensate16")
             elif dense_handle is not None:
                 red = comm.synchronize(dense_handle)
-                _lib.check(L.dgc_compensate_wire(_lib.ptr(red), _lib.VD[red.dtype], _lib.VD[torch.float32],
-                                                 _lib.ptr(mmt), _lib.ptr(out), plan["dense_numel"],
-                                                 float(mem.momentum), int(bool(mem.nesterov)), st),
-                           "dgc_compensate_wire")
+                _lib.check(L.dgc_compensate_wire_avg(_lib.ptr(red), _lib.VD[red.dtype], comm.size(),
+                                                     _lib.ptr(mmt), _lib.ptr(out), plan["dense_numel"],
+                                                     float(mem.momentum), int(bool(mem.nesterov)), st),
+                           "dgc_compensate_wire_avg")
             else:   # one rank: the allreduce is the identity, the fp16 wire a rounding
                 rnd = torch.float16 if self.comp.fp16_values else torch.float32
                 _lib.check(L.dgc_compensate_multi(plan["dense_ptrs"], plan["dense_numels"], plan["dense_offs"],

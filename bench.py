@@ -354,10 +354,12 @@ class ModelRun:
         src = (ctypes.c_void_p * 1)(gd.data_ptr())
         self._lib.check(L.dgc_gather_cast(src, self._one[0], self._one[1], 1, self.dense_wire.data_ptr(), wt, st),
                         "dgc_gather_cast")
-        comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Average))
-        self._lib.check(L.dgc_compensate_wire(self.dense_wire.data_ptr(), wt, f32, self.dense_mmt.data_ptr(),
-                                              self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov), st),
-                        "dgc_compensate_wire")
+        # Average: the SUM, its div_(W) folded into the compensate (no ATen launch)
+        comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Sum))
+        self._lib.check(L.dgc_compensate_wire_avg(self.dense_wire.data_ptr(), wt, comm.size(),
+                                                  self.dense_mmt.data_ptr(),
+                                                  self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov),
+                                                  st), "dgc_compensate_wire_avg")
 
     def probe_buffers(self):
         b = self.b

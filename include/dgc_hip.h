@@ -427,6 +427,12 @@ int dgc_gather_cast(const float* const* srcs, const int64_t* numels, const int64
                     void* dst, int32_t dst_dtype, void* stream);
 int dgc_compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float* mmt, float* out, int64_t n,
                         float momentum, int32_t nesterov, void* stream);
+/* dgc_compensate_wire_avg: the same from the allreduce's SUM over `world` ranks, the
+ *   Average's division folded in (replaces horovod Average's post-division,
+ *   dgc/compression.py:200-212 via hvd.allreduce_async_(op=Average)): g = src / world in
+ *   fp32, rounded to fp16 for an fp16 src, as torch's `div_(world)` on the wire tensor. */
+int dgc_compensate_wire_avg(const void* src, int32_t src_dtype, int32_t world, float* mmt, float* out, int64_t n,
+                            float momentum, int32_t nesterov, void* stream);
 int dgc_compensate_multi(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count,
                          int32_t round_to, float* mmt, float* out, float momentum, int32_t nesterov, void* stream);
 
