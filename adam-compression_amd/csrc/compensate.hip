@@ -231,12 +231,12 @@ k_compensate_wire(const void* __restrict__ src, float* __restrict__ mmt, float* 
         float g;
         if (SRC == 1) {
             g = f16_to_f32(static_cast<const uint16_t*>(src)[e]);
-            if (div != 1.f) g = f16_to_f32(f32_to_f16(g / div));
+            if (div != 1.f) g = f16_to_f32(f32_to_f16(__fdiv_rn(g, div)));
         } else if (SRC == 2) {
             g = f16_to_f32(f32_to_f16(static_cast<const float*>(src)[e]));
         } else {
             g = static_cast<const float*>(src)[e];
-            if (div != 1.f) g = g / div;
+            if (div != 1.f) g = __fdiv_rn(g, div);
         }
         float m = mmt[e], v = 0.f;
         const float o = comp1<NEST, false>(g, m, v, mom);
@@ -361,6 +361,130 @@ int compensate_wire(const void* src, int32_t src_dtype, int32_t round_to, float*
     return DGC_OK;
 }
 
+// ---- the dense Average as the rank-order sum of an allgather ----
+// The reference Average-allreduces every dense tensor (dgc/compression.py:205-206,
+// Horovod allreduce_async_(op=Average)); the oracle restates it as Horovod's result on
+// the rank-order concatenation: acc = x_0; acc += x_1; ...; acc /= W, every op on a
+// tensor of the wire dtype (fp32, or fp16 with fp16_values; bf16 for a bf16 parameter).
+// An RCCL / gloo allreduce sums in ITS order, which decides the last bits at W >= 3 —
+// so the dense values travel by allgather and are summed here, in rank order. ATen's
+// add_ on a 16-bit tensor computes in fp32 and rounds each sum; CPU div_ by the integer
+// W is the fp32 TRUE quotient (on 16-bit tensors identical to its reciprocal form: all
+// 65536 fp16 / bf16 patterns checked for W = 3..12), rounded to the wire dtype. Rank r's
+// n values start at src + r * rank_stride (bytes).
+template <int DT>   // DGC_F32 / DGC_F16 / DGC_BF16
+__device__ __forceinline__ float wire_at(const char* __restrict__ src, int64_t rank_stride, int r, int64_t e) {
+    const char* row = src + (int64_t)r * rank_stride;
+    if (DT == DGC_F32) return reinterpret_cast<const float*>(row)[e];
+    return h16_to_f32<DT>(reinterpret_cast<const uint16_t*>(row)[e]);
+}
+
+template <int DT>
+__device__ __forceinline__ float wire_round(float x) {
+    if (DT == DGC_F32) return x;
+    return round16<DT>(x);
+}
+
+template <int DT>
+__device__ __forceinline__ float rank_average(const char* __restrict__ src, int64_t rank_stride, int world,
+                                              int64_t e, bool average) {
+    float acc = wire_at<DT>(src, rank_stride, 0, e);
+    for (int r = 1; r < world; ++r) acc = wire_round<DT>(__fadd_rn(acc, wire_at<DT>(src, rank_stride, r, e)));
+    if (average) acc = wire_round<DT>(__fdiv_rn(acc, (float)world));
+    return acc;
+}
+
+// dst[e] = the rank-order sum (/ W for Average) in the wire dtype: the per-tensor
+// allreduce (dgc.comm.allreduce_async_). dst may be any rank's row (in place).
+template <int DT>
+__global__ void __launch_bounds__(kBlock)
+k_rank_sum(const char* __restrict__ src, int64_t rank_stride, int world, int64_t n, int average, void* dst) {
+    const int64_t e0 = (int64_t)blockIdx.x * kBlock * 4 + threadIdx.x;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        v[j] = e < n ? rank_average<DT>(src, rank_stride, world, e, average != 0) : 0.f;
+    }
+    // every load above is issued before any store: dst may alias a source row
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        if (e >= n) break;
+        if (DT == DGC_F32) static_cast<float*>(dst)[e] = v[j];
+        else static_cast<uint16_t*>(dst)[e] = f32_to_h16<DT>(v[j]);
+    }
+}
+
+// out = compensate(accumulate=False) of the Average of the gathered dense wire values
+// (decompress's dense branch, dgc/compression.py:195-198: `tensor.type(vdtype)` widens
+// the fp16 wire exactly, then DGCSGDMemory.compensate, dgc/memory.py:64-70).
+template <bool NEST, int DT>
+__global__ void __launch_bounds__(kBlock)
+k_compensate_ranks(const char* __restrict__ src, int64_t rank_stride, int world, float* __restrict__ mmt,
+                   float* __restrict__ out, int64_t n, float mom) {
+    const int64_t e0 = (int64_t)blockIdx.x * kBlock * 4 + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t e = e0 + (int64_t)j * kBlock;
+        if (e >= n) break;
+        const float g = rank_average<DT>(src, rank_stride, world, e, true);
+        float m = mmt[e], v = 0.f;
+        const float o = comp1<NEST, false>(g, m, v, mom);
+        mmt[e] = m;
+        out[e] = o;
+    }
+}
+
+static int check_ranks(const void* src, int32_t dtype, int32_t world, int64_t rank_stride, int64_t n,
+                       const char* who) {
+    if (n < 0 || (n > 0 && !src) || world < 1 || world > 4096)
+        DGC_FAIL(DGC_ERR_INVALID, "%s: bad arguments (n %lld, world %d)", who, (long long)n, (int)world);
+    if (dtype != DGC_F32 && dtype != DGC_F16 && dtype != DGC_BF16) DGC_FAIL(DGC_ERR_DTYPE, "%s: wire dtype", who);
+    const int64_t es = dtype == DGC_F32 ? 4 : 2;
+    if (world > 1 && rank_stride < n * es)
+        DGC_FAIL(DGC_ERR_INVALID, "%s: rank_stride %lld < %lld bytes of values", who, (long long)rank_stride,
+                 (long long)(n * es));
+    if ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)rank_stride) & (uintptr_t)(es - 1))
+        DGC_FAIL(DGC_ERR_INVALID, "%s: source rows must be aligned to the wire dtype", who);
+    if (ceil_div(n, (int64_t)kBlock * 4) > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "%s: n too large", who);
+    return DGC_OK;
+}
+
+int rank_sum(const void* src, int32_t dtype, int32_t world, int64_t rank_stride, int64_t n, int32_t average,
+             void* dst, hipStream_t st) {
+    DGC_TRY(check_ranks(src, dtype, world, rank_stride, n, "dgc_rank_sum"));
+    if (n > 0 && !dst) DGC_FAIL(DGC_ERR_INVALID, "dgc_rank_sum: null destination");
+    if (n == 0) return DGC_OK;
+    const dim3 gd((unsigned)ceil_div(n, (int64_t)kBlock * 4)), bd(kBlock);
+    const char* s = static_cast<const char*>(src);
+    if (dtype == DGC_F32) hipLaunchKernelGGL((k_rank_sum<DGC_F32>), gd, bd, 0, st, s, rank_stride, world, n, average, dst);
+    else if (dtype == DGC_F16) hipLaunchKernelGGL((k_rank_sum<DGC_F16>), gd, bd, 0, st, s, rank_stride, world, n, average, dst);
+    else hipLaunchKernelGGL((k_rank_sum<DGC_BF16>), gd, bd, 0, st, s, rank_stride, world, n, average, dst);
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
+int compensate_ranks(const void* src, int32_t dtype, int32_t world, int64_t rank_stride, float* mmt, float* out,
+                     int64_t n, float mom, bool nesterov, hipStream_t st) {
+    DGC_TRY(check_ranks(src, dtype, world, rank_stride, n, "dgc_compensate_ranks"));
+    if (dtype == DGC_BF16) DGC_FAIL(DGC_ERR_DTYPE, "dgc_compensate_ranks: fp32 parameters take an fp32 or fp16 wire");
+    if (n > 0 && (!mmt || !out)) DGC_FAIL(DGC_ERR_INVALID, "dgc_compensate_ranks: null mmt / out");
+    if (n == 0) return DGC_OK;
+    const dim3 gd((unsigned)ceil_div(n, (int64_t)kBlock * 4)), bd(kBlock);
+    const char* s = static_cast<const char*>(src);
+#define DGC_RANKS(NE, DT) \
+    hipLaunchKernelGGL((k_compensate_ranks<NE, DT>), gd, bd, 0, st, s, rank_stride, world, mmt, out, n, mom)
+    if (nesterov) {
+        if (dtype == DGC_F32) DGC_RANKS(true, DGC_F32); else DGC_RANKS(true, DGC_F16);
+    } else {
+        if (dtype == DGC_F32) DGC_RANKS(false, DGC_F32); else DGC_RANKS(false, DGC_F16);
+    }
+#undef DGC_RANKS
+    DGC_LAUNCHED();
+    return DGC_OK;
+}
+
 int compensate(const float* grad, float* mmt, float* vec, float* out, int64_t n, float momentum,
                bool nesterov, bool accumulate, float* samples, int64_t s_start, int64_t s_stride,
                int64_t s_count, hipStream_t st) {
@@ -459,6 +583,18 @@ extern "C" int dgc_compensate_wire_avg(const void* src, int32_t src_dtype, int32
                                        int64_t n, float momentum, int32_t nesterov, void* stream) {
     return dgc::compensate_wire(src, src_dtype, DGC_F32, mmt, out, n, momentum, nesterov != 0,
                                 static_cast<hipStream_t>(stream), world);
+}
+
+extern "C" int dgc_rank_sum(const void* src, int32_t dtype, int32_t world, int64_t rank_stride, int64_t n,
+                            int32_t average, void* dst, void* stream) {
+    return dgc::rank_sum(src, dtype, world, rank_stride, n, average, dst, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dgc_compensate_ranks(const void* src, int32_t src_dtype, int32_t world, int64_t rank_stride,
+                                    float* mmt, float* out, int64_t n, float momentum, int32_t nesterov,
+                                    void* stream) {
+    return dgc::compensate_ranks(src, src_dtype, world, rank_stride, mmt, out, n, momentum, nesterov != 0,
+                                 static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dgc_sample_strided(const float* vec, int64_t n, int64_t start, int64_t stride,

@@ -2698,7 +2698,6 @@ __global__ void __launch_bounds__(kBlock) k_bigset_hist(SelWS w, BigList bl) {
     __syncthreads();
     const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
     const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
-#pragma unroll 8
     for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[bigset_bin(qk[i], tkey)], 1u);
     __syncthreads();
     for (int i = threadIdx.x; i < kRsBins; i += kBlock)
@@ -2744,7 +2743,6 @@ __global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
     const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
     const int lane = threadIdx.x & 63;
     uint32_t above_cnt = 0;
-#pragma unroll 4
     for (int64_t i0 = lo; i0 < hi; i0 += kBlock) {   // uniform trip count
         const int64_t i = i0 + threadIdx.x;
         const uint32_t key = i < hi ? qk[i] : 0u;
@@ -2854,7 +2852,6 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
     const int64_t q = ceil_div(hi - lo, (int64_t)kW);
     const int64_t qlo = lo + wv * q, qhi = qlo + q < hi ? qlo + q : hi;
     uint32_t c = 0;
-#pragma unroll 8
     for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
         const int64_t i = i0 + lane;
         c += (uint32_t)__popcll(__ballot(i < qhi && qk[i] >= kth));
@@ -2863,7 +2860,6 @@ k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o
     __syncthreads();
     long long pos = b.obase + b.slice_cnt[blockIdx.x];
     for (int i = 0; i < wv; ++i) pos += wc[i];
-#pragma unroll 4
     for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
         const int64_t i = i0 + lane;
         const bool sel = i < qhi && qk[i] >= kth;

@@ -169,6 +169,8 @@ _SIGNATURES = {
     "dgc_compensate_wire_avg": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _F, _I32, _P]),
     "dgc_compensate_multi": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32,
                                             _I32, _P, _P, _F, _I32, _P]),
+    "dgc_rank_sum": (ctypes.c_int, [_P, _I32, _I32, _I64, _I64, _I32, _P, _P]),
+    "dgc_compensate_ranks": (ctypes.c_int, [_P, _I32, _I32, _I64, _P, _P, _I64, _F, _I32, _P]),
     "dgc_batch_select": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, ctypes.POINTER(_I64), _P, _P, _P, _SZ, _I32,
                                          _P]),
     "dgc_mask_packed16": (ctypes.c_int, [_P, _I64, _I32, _I32, _P, _P, _I64, _P]),

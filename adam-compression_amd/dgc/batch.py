@@ -54,7 +54,7 @@ class DGCBatch:
                  sample_ratio=0.01, compress_upper_bound=1.3, compress_lower_bound=0.8, max_adaptation_iters=10,
                  resample=True, fp16_values=False, int32_indices=False, device=None, world_size=None, seed=None,
                  deferred_masking=True, fill="auto", dtype=torch.float32, exchange_parts="auto",
-                 resample_order="index"):
+                 resample_order="index", payload_extra=0):
         if fill not in ("auto", "inline", "sparse"):
             raise ValueError(f"fill must be 'auto', 'inline' or 'sparse', not {fill!r}")
         if dtype not in (torch.float32,) + _lib.HALF:
@@ -71,6 +71,10 @@ class DGCBatch:
         # top-k set in index order (the decompress and the memory update depend on the
         # set only; dgc_select_params.resample_order); "topk": torch.topk's order always
         self.resample_order = resample_order
+        # bytes appended to every rank's payload (after the packed entries): the batched
+        # optimizer's dense wire values ride in the same allgather (``extra_off``; None
+        # when the exchange is split, which carries the sparse entries only)
+        self.payload_extra = int(payload_extra)
         self.device = torch.device(device or "cuda")
         self.names = [n for n, _ in named_shapes]
         self.shapes = {n: tuple(s) for n, s in named_shapes}
@@ -142,14 +146,18 @@ class DGCBatch:
         self.capacity = sum(a[0] for a in self.attrs)
         from .compression import _layout
         self.rank_stride, self.voff, self.ioff = _layout(self.capacity, self.vdtype, self.idtype)
-        # fill="sparse": two payload / gather buffers, so the previous step's gathered
-        # indices stay readable for the re-zero; a new layout forgets them
-        nbuf = 2 if self.fill == "sparse" else 1
-        self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(nbuf)]
         # W > 1, fp32: the allgather in parts, each scattered as it lands (dgc/exchange.py)
         # (W = 1 exchanges too when comm.one_rank_collectives(): the RCCL tests' one-rank group)
         self.exchanging = self.world > 1 or comm.one_rank_collectives()
         self.parts = 1 if self.half else split_parts(self.world, self.capacity, self.exchange_parts)
+        self.extra_off = None
+        if self.payload_extra > 0 and self.parts == 1:
+            self.extra_off = self.rank_stride
+            self.rank_stride = -(-(self.rank_stride + self.payload_extra) // 256) * 256
+        # fill="sparse": two payload / gather buffers, so the previous step's gathered
+        # indices stay readable for the re-zero; a new layout forgets them
+        nbuf = 2 if self.fill == "sparse" else 1
+        self._payloads = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(nbuf)]
         self.xchg = None
         self._inflight = None
         if self.parts > 1:

@@ -10,7 +10,9 @@ behaves as a world of one rank.
 Semantics kept from Horovod:
   * allgather concatenates along dim 0 in rank order, each rank may send a
     different number of rows;
-  * allreduce with ``Average`` is the rank sum divided by the world size, in place.
+  * allreduce with ``Average`` is the rank sum divided by the world size, in place —
+    summed in RANK ORDER (an allgather, then ``dgc_rank_sum``), as the oracle restates
+    Horovod's Average.
 
 The DGC sparse payload itself does NOT go through the generic allgather: each
 rank's (count, values, indices) is packed into one fixed-capacity byte buffer
@@ -86,21 +88,56 @@ class Handle:
         return self._output
 
 
+def _rank_order_sum(rows, W, average):
+    """acc = x_0; acc += x_1 ...; acc /= W on rows of a [W, n] host tensor (torch ops in
+    the rows' dtype: the oracle's restatement of Horovod's Average)."""
+    acc = rows[0].clone()
+    for q in range(1, W):
+        acc.add_(rows[q])
+    if average:
+        acc.div_(W)
+    return acc
+
+
 def allreduce_async_(tensor, name=None, op=Average):
-    """In-place allreduce of ``tensor``; ``synchronize`` returns it (sum, /W for Average)."""
+    """In-place allreduce of ``tensor``; ``synchronize`` returns it (sum, /W for Average).
+
+    The reference Average-allreduces its dense tensors through Horovod
+    (dgc/compression.py:205-206). Its result is restated (tests/golden/make_goldens.py)
+    as the RANK-ORDER sum divided by W, every op in the tensor's dtype; a backend
+    allreduce sums in its own order, which decides the last bits from W = 3 on (fp16
+    wire values above all). So the tensor is allgathered and summed in rank order: on
+    the device by ``dgc_rank_sum`` (RCCL; gloo stages the bytes through the host), with
+    torch ops for a host tensor (the gloo plumbing tests) or a dtype the kernel lacks."""
     if op not in (Average, Sum):
         raise NotImplementedError(f"allreduce op {op!r} (Adasum is out of scope)")
     W = size()
     if _shortcut(W):
         return Handle(output=tensor)
-    staged = tensor.cpu() if _backend_needs_host(tensor) else tensor
-    work = dist.all_reduce(staged, op=dist.ReduceOp.SUM, async_op=True)
+    src = tensor.contiguous().view(-1)
+    n = src.numel()
+    device_sum = tensor.is_cuda and tensor.dtype in (torch.float32, torch.float16, torch.bfloat16)
+    if _backend_needs_host(src) or not tensor.is_cuda:
+        host = src.cpu()
+        gathered = torch.empty(W * n, dtype=src.dtype)
+        work = dist.all_gather_into_tensor(gathered, host, async_op=True)
+    else:
+        gathered = torch.empty(W * n, dtype=src.dtype, device=src.device)
+        work = dist.all_gather_into_tensor(gathered, src, async_op=True)
 
     def finish():
-        if staged is not tensor:
-            tensor.copy_(staged)
-        if op == Average:
-            tensor.div_(W)
+        if device_sum:
+            from . import _lib
+            g = gathered.to(src.device) if not gathered.is_cuda else gathered
+            dst = src if src.data_ptr() == tensor.data_ptr() else torch.empty_like(src)
+            _lib.check(_lib.lib().dgc_rank_sum(_lib.ptr(g), _lib.VD[src.dtype], W, n * src.element_size(), n,
+                                               int(op == Average), _lib.ptr(dst), _lib.stream_of(src.device)),
+                       "dgc_rank_sum")
+            if dst.data_ptr() != tensor.data_ptr():
+                tensor.copy_(dst.view(tensor.shape))
+        else:
+            acc = _rank_order_sum(gathered.view(W, n), W, op == Average)
+            tensor.copy_(acc.view(tensor.shape).to(tensor.device))
         return tensor
 
     return Handle(work, finish)

@@ -13,8 +13,13 @@ so only the last part's share is exposed. The dense result is the single-collect
 decompress's bit for bit (same rank-order sums; tests/test_gpu_split.py).
 
 Used by DGCBucket / DGCBatch (fp32 parameters) at W > 1; ``parts="auto"`` splits a
-step of >= 2^20 gathered entries (2 parts at W <= 4, 4 at W = 8) and leaves smaller ones
-(the model sets' ~0.1M-entry steps: latency-bound collectives) to one allgather.
+step of >= 2^21 gathered entries (2 parts at W <= 4, 4 at W = 8) and leaves smaller ones
+to one allgather: each extra collective costs ~35 us of fixed hand-off
+and hides at most its share of the scatter, which at 2M entries (flat-1B, W = 2: 0.07
+ms) only breaks even and at VGG-16-BN's 1.1M (W = 8) loses.
+
+``DGC_EXCHANGE_PARTS`` overrides ``"auto"``; every rank must issue the same collectives,
+so an override is checked across the ranks when the layout is built (``agree``).
 """
 import ctypes
 import os
@@ -33,15 +38,33 @@ def split_parts(world, capacity, parts="auto"):
         parts = int(env)
     multi = world > 1 or comm.one_rank_collectives()
     if parts == "auto":
-        if not multi or world * capacity < (1 << 20):
+        if not multi or world * capacity < (1 << 21):
             return 1
         return 2 if world <= 4 else 4
     parts = int(parts)
     if not multi or parts <= 1:
-        return 1
-    if parts > 8 or world * parts > 64:
+        parts = 1
+    elif parts > 8 or world * parts > 64:
         raise ValueError(f"exchange parts must be 1..8 with world * parts <= 64 (world {world}, parts {parts})")
+    if env and multi:
+        agree(parts)
     return parts
+
+
+def agree(parts):
+    """Raises unless every rank chose ``parts`` (a per-rank DGC_EXCHANGE_PARTS that
+    differs would issue different collectives and hang or corrupt the exchange). One
+    MAX-allreduce of (parts, -parts) over the process group, at layout time only."""
+    import torch.distributed as dist
+    if not comm.is_initialized():
+        return
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([parts, -parts], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    hi, lo = int(t[0]), -int(t[1])
+    if hi != parts or lo != parts:
+        raise RuntimeError(f"DGC_EXCHANGE_PARTS differs across ranks (parts between {lo} and {hi}); set the "
+                           "same value on every rank")
 
 
 class SplitExchange:

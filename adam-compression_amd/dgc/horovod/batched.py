@@ -15,8 +15,13 @@ those numerics and runs the whole step as
                          p.grad, dgc/compression.py:191-194)
     dense tensors        W = 1: ONE multi-tensor compensate(accumulate=False) straight
                          from the gradients (the fp16 wire's rounding fused); W > 1: ONE
-                         gather (+ fp16 cast) into the allreduce buffer -> ONE allreduce
-                         (Average) -> ONE compensate from the buffer (fp16 widened in it)
+                         gather (+ fp16 cast) into the TAIL of the same packed payload, so
+                         the step's one allgather carries them too -> ONE compensate from
+                         the gathered rows (dgc_compensate_ranks: the Average as the
+                         rank-order sum / W in the wire dtype, the order the reference's
+                         Horovod Average is restated in — an allreduce would sum in the
+                         backend's order). A split exchange, or a step with no compressed
+                         tensor, allgathers the dense values on their own.
 
 with no host synchronisation and no per-parameter launch. The momentums and
 velocities become views of the batch's flat buffers (``memory.momentums[name]`` /
@@ -55,7 +60,7 @@ from ..comm import Average
 from ..compression import DGCCompressor
 from ..memory import DGCSGDMemory
 
-__all__ = ["BatchedStep", "supported"]
+__all__ = ["BatchedStep", "supported", "auto"]
 
 
 def supported(compression):
@@ -64,6 +69,25 @@ def supported(compression):
     mem = getattr(compression, "memory", None)
     return (isinstance(compression, DGCCompressor) and isinstance(mem, DGCSGDMemory)
             and compression.strided_sample and mem.gradient_clipping is None)
+
+
+def auto(compression, named_parameters, op):
+    """``DistributedOptimizer(batch="auto")``, the default: the batched step whenever it
+    computes exactly what the per-tensor hooks would — ``supported``, Average, the
+    compressor's and memory's own compress / decompress / communicate / synchronize /
+    compensate / update (a subclass that overrides one keeps the per-tensor calls it
+    expects), and the trainable parameters on the MI355X sharing one dtype of fp32, bf16
+    or fp16. Anything else runs per tensor, as the reference does."""
+    if op != Average or not supported(compression):
+        return False
+    for base, obj, names in ((DGCCompressor, compression, ("compress", "decompress", "communicate", "synchronize")),
+                             (DGCSGDMemory, compression.memory, ("compensate", "update"))):
+        if any(getattr(type(obj), n) is not getattr(base, n) for n in names):
+            return False
+    params = [p for _, p in named_parameters if p.requires_grad]
+    dts = {p.dtype for p in params}
+    return (bool(params) and all(p.is_cuda for p in params) and len(dts) == 1
+            and dts <= {torch.float32, torch.bfloat16, torch.float16})
 
 
 def _draw():
@@ -110,6 +134,16 @@ class BatchedStep:
         params = dict(self.named)
         dev = self.named[0][1].device
         plan = {"key": key, "batch": None, "comp": [], "dense": [], "dev": dev, "state": [], "dense_state": []}
+        dense = [(n, p) for n, p in self.named if n not in set(comp_names)]
+        offs, end = [], 0
+        for _, p in dense:
+            offs.append(end)
+            end += -(-p.numel() // 4) * 4   # 16-B aligned views
+        # fp32 parameters exchanging (W > 1): the dense wire values ride in the packed
+        # payload's tail, summed in rank order after the ONE allgather (dgc_compensate_ranks)
+        exchanging = comm.size() > 1 or comm.one_rank_collectives()
+        wire_dt = torch.float16 if c.fp16_values else torch.float32
+        dense_bytes = end * torch.empty(0, dtype=wire_dt).element_size() if dense and exchanging and not self.half else 0
         if comp_names:
             shapes = [(n, tuple(params[n].shape)) for n in comp_names]
             b = DGCBatch(shapes, compress_ratio=c.compress_ratio, momentum=mem.momentum, nesterov=mem.nesterov,
@@ -117,7 +151,8 @@ class BatchedStep:
                          compress_upper_bound=c.compress_upper_bound, compress_lower_bound=c.compress_lower_bound,
                          max_adaptation_iters=c.max_adaptation_iters, resample=c.resample,
                          fp16_values=c.fp16_values, int32_indices=c.int32_indices, device=dev,
-                         world_size=comm.size(), deferred_masking=True, fill=self.fill, dtype=self.dtype)
+                         world_size=comm.size(), deferred_masking=True, fill=self.fill, dtype=self.dtype,
+                         payload_extra=dense_bytes)
             for i, n in enumerate(comp_names):
                 numel, _, k, S, ks, stride = c.attributes[n]
                 if (k, S, ks, stride) != tuple(b.attrs[i]):
@@ -137,12 +172,7 @@ class BatchedStep:
             plan["ptrs"] = (ctypes.c_void_p * len(comp_names))()
             plan["sampled"] = {n: c.attributes[n][5] for n in comp_names if c.attributes[n][0] != c.attributes[n][3]}
             plan["order"] = None
-        dense = [(n, p) for n, p in self.named if n not in set(comp_names)]
         if dense:
-            offs, end = [], 0
-            for _, p in dense:
-                offs.append(end)
-                end += -(-p.numel() // 4) * 4   # 16-B aligned views
             out = torch.zeros(end, dtype=self.dtype, device=dev)
             mmt = torch.zeros(end, dtype=self.dtype, device=dev)
             for (n, p), o in zip(dense, offs):
@@ -158,9 +188,14 @@ class BatchedStep:
             plan["dense_ptrs"] = (ctypes.c_void_p * T)()
             plan["dense_numels"] = (ctypes.c_int64 * T)(*[p.numel() for _, p in dense])
             plan["dense_offs"] = (ctypes.c_int64 * T)(*offs)
-            if (comm.size() > 1 or comm.one_rank_collectives()) and not self.half:
-                plan["dense_wire"] = torch.empty(end, dtype=torch.float16 if c.fp16_values else torch.float32,
-                                                 device=dev)
+            if dense_bytes:
+                plan["wire_dtype"] = wire_dt
+                b = plan["batch"]
+                if b is None or b.extra_off is None:
+                    # no compressed tensor (a ratio-1 warmup epoch) or a split exchange: the
+                    # wire values go in an allgather of their own, summed the same way
+                    plan["dense_wire"] = torch.empty(dense_bytes, dtype=torch.uint8, device=dev)
+                    plan["dense_gathered"] = torch.empty(comm.size() * dense_bytes, dtype=torch.uint8, device=dev)
             if self.half:   # the gathered 16-bit gradients (K1-16's dense branch reads one buffer)
                 plan["dense_in"] = torch.zeros(end, dtype=self.dtype, device=dev)
             plan["zeros"] = torch.zeros(max((p.numel() for _, p in dense), default=1), dtype=self.dtype,
@@ -228,7 +263,6 @@ class BatchedStep:
                 ptrs[i] = gflat.data_ptr()
             b.compensate(starts, grad_ptrs=ptrs)
             b.select()
-            b.send()   # the allgather (or its parts), waited for in b.decompress()
         dense_handle = None
         if plan["dense"]:
             dptrs = plan["dense_ptrs"]
@@ -240,17 +274,21 @@ class BatchedStep:
                     g = g.contiguous()
                     plan.setdefault("keep", []).append(g)
                 dptrs[i] = g.data_ptr()
-            wire = plan.get("dense_wire")
             L = _lib.lib()
             st = _lib.stream_of(dev)
             if self.half:
                 dense_handle = self._dense16_exchange(plan, L, st)
-            elif wire is not None:   # compress: tensor.type(float16) (dgc/compression.py:175-177)
+            elif "wire_dtype" in plan:
+                # compress: tensor.type(torch.float16) (dgc/compression.py:175-177), into the
+                # payload's tail (or the dense allgather's own buffer)
+                own = plan.get("dense_wire")
+                dst = own.data_ptr() if own is not None else b.payload.data_ptr() + b.extra_off
                 _lib.check(L.dgc_gather_cast(dptrs, plan["dense_numels"], plan["dense_offs"], len(plan["dense"]),
-                                             _lib.ptr(wire), _lib.VD[wire.dtype], st), "dgc_gather_cast")
-                # Average = the SUM here, its div_(W) folded into dgc_compensate_wire_avg
-                dense_handle = comm.allreduce_async_(wire, op=comm.Sum)
+                                             ctypes.c_void_p(dst), _lib.VD[plan["wire_dtype"]], st), "dgc_gather_cast")
+                if own is not None:
+                    dense_handle = comm.allgather_packed_async(own, out=plan["dense_gathered"])
         if b is not None:
+            b.send()   # the allgather (or its parts), waited for in b.decompress()
             b.decompress()   # into the batch's output, then p.grad (dgc/compression.py:191-194)
             glue.bind_grads(plan["comp_params"], plan["comp_views"])
         if plan["dense"]:
@@ -265,12 +303,17 @@ class BatchedStep:
                 _lib.check(L.dgc_compensate16(_lib.ptr(src), _lib.ptr(mmt), None, _lib.ptr(out), None,
                                               plan["dense_numel"], float(mem.momentum), int(bool(mem.nesterov)), 0,
                                               _lib.VD[self.dtype], st), "dgc_compensate16")
-            elif dense_handle is not None:
-                red = comm.synchronize(dense_handle)
-                _lib.check(L.dgc_compensate_wire_avg(_lib.ptr(red), _lib.VD[red.dtype], comm.size(),
-                                                     _lib.ptr(mmt), _lib.ptr(out), plan["dense_numel"],
-                                                     float(mem.momentum), int(bool(mem.nesterov)), st),
-                           "dgc_compensate_wire_avg")
+            elif "wire_dtype" in plan:
+                # Average = the rank-order sum / W of the gathered wire values, then
+                # compensate(accumulate=False) (dgc/compression.py:195-198, 205-206)
+                if dense_handle is not None:
+                    src, stride = comm.synchronize(dense_handle).data_ptr(), plan["dense_wire"].numel()
+                else:
+                    src, stride = b.gathered.data_ptr() + b.extra_off, b.rank_stride
+                _lib.check(L.dgc_compensate_ranks(ctypes.c_void_p(src), _lib.VD[plan["wire_dtype"]], comm.size(),
+                                                  stride, _lib.ptr(mmt), _lib.ptr(out), plan["dense_numel"],
+                                                  float(mem.momentum), int(bool(mem.nesterov)), st),
+                           "dgc_compensate_ranks")
             else:   # one rank: the allreduce is the identity, the fp16 wire a rounding
                 rnd = torch.float16 if self.comp.fp16_values else torch.float32
                 _lib.check(L.dgc_compensate_multi(plan["dense_ptrs"], plan["dense_numels"], plan["dense_offs"],

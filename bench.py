@@ -295,14 +295,18 @@ class ModelRun:
     (dgc/compression.py:173-177, 195-198)."""
 
     def __init__(self, wl, rank, world, dev, fill="sparse"):
-        from dgc import workloads
+        from dgc import comm, workloads
         from dgc.batch import DGCBatch
         comp, dense = workloads.split(getattr(workloads, wl["model"])())
+        self.n_dense = sum(workloads.numel(s) for _, s in dense)
+        wire_dt = torch.float16 if wl["fp16"] else torch.float32
+        self.exchanging = world > 1 or comm.one_rank_collectives()
+        # W > 1: the dense wire values ride in the tail of the packed payload (one allgather)
+        extra = self.n_dense * torch.empty(0, dtype=wire_dt).element_size() if self.exchanging else 0
         self.b = DGCBatch(comp, compress_ratio=wl["ratio"], momentum=0.9, nesterov=wl["nesterov"],
                           fp16_values=wl["fp16"], int32_indices=wl["int32"], device=dev, world_size=world, seed=42,
-                          fill="inline" if fill in ("inline", "allgather") else "sparse")
+                          fill="inline" if fill in ("inline", "allgather") else "sparse", payload_extra=extra)
         self.n_comp = sum(self.b.numels)
-        self.n_dense = sum(workloads.numel(s) for _, s in dense)
         self.world = world
         gen = torch.Generator(device=dev)
         self.grads = []
@@ -314,7 +318,11 @@ class ModelRun:
             self.grads.append((g, torch.randn(self.n_dense, generator=gen, device=dev) * 1e-3))
         self.dense_mmt = torch.zeros(self.n_dense, device=dev)
         self.dense_out = torch.empty(self.n_dense, device=dev)
-        self.dense_wire = torch.empty(self.n_dense, dtype=torch.float16 if wl["fp16"] else torch.float32, device=dev)
+        self.wire_dt = wire_dt
+        self.dense_wire = self.dense_gathered = None
+        if self.exchanging and self.b.extra_off is None:   # split exchange: the dense values on their own
+            self.dense_wire = torch.empty(extra, dtype=torch.uint8, device=dev)
+            self.dense_gathered = torch.empty(world * extra, dtype=torch.uint8, device=dev)
         self._one = (ctypes.c_int64 * 1)(self.n_dense), (ctypes.c_int64 * 1)(0)
         self.elements = self.n_comp + self.n_dense
         self.k, self.S = self.b.capacity, sum(a[1] for a in self.b.attrs)
@@ -328,8 +336,26 @@ class ModelRun:
         g, gd = self.grads[i % 2]
         ev = ev or {}
         L, b = self._lib.lib(), self.b
+        from dgc import comm
         b.grad_flat = g   # the model's gradients live in the batch's flat buffer (p.grad views)
-        for name, fn in (("compensate", b.compensate), ("select", b.select), ("allgather", b.exchange),
+        st = self._lib.stream_of(g.device)
+        wt = self._lib.VD[self.wire_dt]
+        handle = []
+
+        def select():
+            b.select()
+            if self.exchanging:
+                # dense tensors: the fp16 wire cast (dgc/compression.py:173-177) into the
+                # payload's tail, exchanged by the same allgather
+                src = (ctypes.c_void_p * 1)(gd.data_ptr())
+                own = self.dense_wire
+                dst = own.data_ptr() if own is not None else b.payload.data_ptr() + b.extra_off
+                self._lib.check(L.dgc_gather_cast(src, self._one[0], self._one[1], 1, ctypes.c_void_p(dst), wt, st),
+                                "dgc_gather_cast")
+                if own is not None:
+                    handle.append(comm.allgather_packed_async(own, out=self.dense_gathered))
+
+        for name, fn in (("compensate", b.compensate), ("select", select), ("allgather", b.exchange),
                          ("decompress", b.decompress)):
             pair = ev.get(name)
             if pair:
@@ -337,29 +363,22 @@ class ModelRun:
             fn()
             if pair:
                 pair[1].record()
-        # dense tensors: (fp16 wire cast) -> allreduce Average -> compensate(accumulate=False)
-        # (dgc/compression.py:173-177, 195-198), no ATen kernel: at W = 1 the allreduce is
-        # the identity and the wire cast a rounding, fused into the compensate
-        # (dgc_compensate_wire, round_to fp16); at W > 1 dgc_gather_cast fills the wire
-        # buffer and the compensate widens it
-        st = self._lib.stream_of(g.device)
-        wt = self._lib.VD[self.dense_wire.dtype]
-        f32 = self._lib.VD[torch.float32]
-        from dgc import comm
-        if self.world == 1 and not comm.one_rank_collectives():
-            self._lib.check(L.dgc_compensate_wire(gd.data_ptr(), f32, wt, self.dense_mmt.data_ptr(),
-                                                  self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov),
-                                                  st), "dgc_compensate_wire")
+        # dense tensors: Average -> compensate(accumulate=False) (dgc/compression.py:195-198,
+        # 205-206), no ATen kernel: at W = 1 the Average is the identity and the wire cast a
+        # rounding, fused into the compensate (dgc_compensate_wire, round_to fp16); at W > 1
+        # the rank-order sum / W of the gathered rows, widened (dgc_compensate_ranks)
+        if not self.exchanging:
+            self._lib.check(L.dgc_compensate_wire(gd.data_ptr(), self._lib.VD[torch.float32], wt,
+                                                  self.dense_mmt.data_ptr(), self.dense_out.data_ptr(),
+                                                  self.n_dense, 0.9, int(self.nesterov), st), "dgc_compensate_wire")
             return
-        src = (ctypes.c_void_p * 1)(gd.data_ptr())
-        self._lib.check(L.dgc_gather_cast(src, self._one[0], self._one[1], 1, self.dense_wire.data_ptr(), wt, st),
-                        "dgc_gather_cast")
-        # Average: the SUM, its div_(W) folded into the compensate (no ATen launch)
-        comm.synchronize(comm.allreduce_async_(self.dense_wire, op=comm.Sum))
-        self._lib.check(L.dgc_compensate_wire_avg(self.dense_wire.data_ptr(), wt, comm.size(),
-                                                  self.dense_mmt.data_ptr(),
-                                                  self.dense_out.data_ptr(), self.n_dense, 0.9, int(self.nesterov),
-                                                  st), "dgc_compensate_wire_avg")
+        if handle:
+            src, stride = comm.synchronize(handle[0]).data_ptr(), self.dense_wire.numel()
+        else:
+            src, stride = b.gathered.data_ptr() + b.extra_off, b.rank_stride
+        self._lib.check(L.dgc_compensate_ranks(ctypes.c_void_p(src), wt, comm.size(), stride,
+                                               self.dense_mmt.data_ptr(), self.dense_out.data_ptr(), self.n_dense,
+                                               0.9, int(self.nesterov), st), "dgc_compensate_ranks")
 
     def probe_buffers(self):
         b = self.b
@@ -416,7 +435,9 @@ class DropinRun:
             compression.initialize([(n, params[n]) for n, _ in comp_shapes])
         random.seed(42)
         inner = torch.optim.SGD([p for _, p in self.named], lr=0.0)
-        self.opt = DistributedOptimizer(inner, named_parameters=self.named, compression=compression, batch=batch)
+        kw = {} if batch == "auto" else {"batch": batch}   # "auto": the drop-in default, no argument
+        self.opt = DistributedOptimizer(inner, named_parameters=self.named, compression=compression, **kw)
+        self.batched = self.opt._batched is not None
         # ModelRun's two gradient sets, value for value, as per-parameter tensors; then a
         # distinct copy per step (the per-tensor path decompresses into p.grad in place)
         gen = torch.Generator(device=dev)
@@ -467,21 +488,22 @@ def timed_steps(run, steps, warmup, world):
 
 def dropin_compare(model, rank, world, dev, steps, warmup):
     """The drop-in training step against the engine it wraps, same box, same gradients:
-    DGCBatch alone (ModelRun, both fills), DistributedOptimizer(batch=True / "sparse"),
-    and the reference's per-tensor hook path (few steps: it syncs per tensor)."""
+    DGCBatch alone (ModelRun, both fills), DistributedOptimizer with no batch argument
+    (its default, "auto": the batched step here), batch="sparse", and the reference's
+    per-tensor hook path (batch=False; few steps: it syncs per tensor)."""
     wl = dict(WORKLOADS[model])
     res = {"model": model, "steps": steps, "warmup": warmup}
     for fill in ("inline", "sparse"):
         run = ModelRun(wl, rank, world, dev, fill)
         res[f"dgcbatch_{fill}_ms"] = round(timed_steps(run, steps, warmup, world), 4)
         del run
-    for label, batch, n in (("optimizer_batch_ms", True, steps), ("optimizer_batch_sparse_ms", "sparse", steps),
+    for label, batch, n in (("optimizer_default_ms", "auto", steps), ("optimizer_batch_sparse_ms", "sparse", steps),
                             ("optimizer_per_tensor_ms", False, max(3, steps // 4))):
         run = DropinRun(wl, rank, world, dev, batch, n + warmup)
         res[label] = round(timed_steps(run, n, warmup, world), 4)
         del run
         torch.cuda.empty_cache()
-    res["batch_vs_dgcbatch"] = round(res["optimizer_batch_ms"] / res["dgcbatch_inline_ms"], 3)
+    res["default_vs_dgcbatch"] = round(res["optimizer_default_ms"] / res["dgcbatch_inline_ms"], 3)
     res["batch_sparse_vs_dgcbatch"] = round(res["optimizer_batch_sparse_ms"] / res["dgcbatch_sparse_ms"], 3)
     res["note"] = ("ms per step; dgcbatch = the engine alone (gradients planted in its flat buffer); optimizer = "
                    "dgc.horovod.DistributedOptimizer: fresh p.grad tensors, hooks in backward order, synchronize(), "

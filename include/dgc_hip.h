@@ -435,6 +435,22 @@ int dgc_compensate_wire_avg(const void* src, int32_t src_dtype, int32_t world, f
                             float momentum, int32_t nesterov, void* stream);
 int dgc_compensate_multi(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count,
                          int32_t round_to, float* mmt, float* out, float momentum, int32_t nesterov, void* stream);
+/* The dense Average of an ALLGATHER, summed in rank order (replaces Horovod's
+ * allreduce_async_(op=Average), dgc/compression.py:205-206; the oracle's restatement:
+ * acc = x_0; acc += x_1 ... x_{W-1}; acc /= W, each op on a tensor of the wire dtype —
+ * an allreduce sums in the backend's order, which decides the last bits at W >= 3).
+ * Rank r's n wire values (dtype DGC_F32 / DGC_F16 / DGC_BF16) start at src + r *
+ * rank_stride BYTES. Every add rounds to the wire dtype; the division is the fp32 true
+ * quotient by world (torch's CPU div_), rounded to the wire dtype.
+ * dgc_rank_sum: dst[0..n) = that sum (/ world when average != 0), in the wire dtype; dst
+ *   may be one of the source rows (dgc.comm.allreduce_async_ writes the rank's own tensor).
+ * dgc_compensate_ranks: out = DGCSGDMemory.compensate(Average, accumulate=False), mmt
+ *   updated (dgc/compression.py:195-198 after the exchange; src_dtype DGC_F32 or DGC_F16,
+ *   widened exactly) — the batched step's dense tensors, carried in the packed payload. */
+int dgc_rank_sum(const void* src, int32_t dtype, int32_t world, int64_t rank_stride, int64_t n, int32_t average,
+                 void* dst, void* stream);
+int dgc_compensate_ranks(const void* src, int32_t src_dtype, int32_t world, int64_t rank_stride, float* mmt,
+                         float* out, int64_t n, float momentum, int32_t nesterov, void* stream);
 
 /* ---- K7: DGCSGD.step over `count` parameters of one group (dgc/optim/sgd.py:42-68) ----
  * params[i], grads[i] (and bufs[i], the momentum_buffer, when weight_decay != 0 and

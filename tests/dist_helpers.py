@@ -221,3 +221,60 @@ def comm_worker(rank, world, port, queue):
         queue.put((rank, out))
     finally:
         dist.destroy_process_group()
+
+
+def multi_worker(rank, world, port, golden_dir, label, queue):
+    """tests/golden/optimizer_multi.* case ``label`` at its world size: the reference's
+    DistributedOptimizer + DGCSGD on TinyNet (W = 3 / 4 / 8, fp32 or fp16 wire values,
+    a ratio-1 warmup epoch), run from its data seeds through the product plumbing with the
+    oracle doubles; the dense tensors' Average is dgc.comm's rank-order allgather sum."""
+    import contextlib
+    import io
+    import json
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dgc.horovod import DistributedOptimizer
+        from dgc.optim import DGCSGD
+        cfg = json.load(open(os.path.join(golden_dir, "optimizer_multi.json")))[label]
+        want = np.load(os.path.join(golden_dir, "optimizer_multi.npz"))
+        torch.manual_seed(cfg["model_seed"])
+        model = TinyNet()
+        opt = DGCSGD(model.parameters(), lr=cfg["lr"], momentum=cfg["momentum"], weight_decay=cfg["weight_decay"],
+                     nesterov=cfg["nesterov_sgd"])
+        mem = OracleMemory(momentum=cfg["momentum"])
+        with contextlib.redirect_stdout(io.StringIO()):
+            comp = OracleDGCCompressor(cfg["ratio"], memory=mem, fp16_values=cfg["fp16_values"],
+                                       int32_indices=cfg["int32_indices"], **cfg["warmup"])
+            mem.initialize(model.named_parameters())
+            comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                    backward_passes_per_step=1, op=Average)
+        random.seed(cfg["random_seed"])
+        spe, problems = cfg["steps_per_epoch"], []
+        for ei, e in enumerate(cfg["epochs"]):
+            if e is not None:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    comp.warmup_compress_ratio(e)
+            for t in range(spe):
+                s = ei * spe + t
+                gen = torch.Generator().manual_seed(3000 + 100 * world + 10 * s + rank)
+                x = torch.randn(32, 64, generator=gen)
+                y = torch.randint(0, 10, (32,), generator=gen)
+                torch.nn.functional.cross_entropy(model(x), y).backward()
+                dopt.step()
+                dopt.zero_grad()
+                for n, p in model.named_parameters():
+                    w = want[f"{label}/s{s}/{n}"]
+                    if not np.array_equal(p.detach().numpy().view(np.uint32), w.view(np.uint32)):
+                        problems.append((s, n, float(np.abs(p.detach().numpy() - w).max())))
+        queue.put((rank, problems))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        queue.put((rank, [("error", repr(e), traceback.format_exc())]))
+    finally:
+        dist.destroy_process_group()

@@ -496,6 +496,88 @@ def gen_optimizer_trace(C, M, H, O):
     print(f"optimizer_trace: {len(meta)} (step, rank) call sequences")
 
 
+# The dense Average beyond W = 2: the reference's DistributedOptimizer + DGCSGD on TinyNet
+# at W = 3 / 4 / 8 (fp32 and fp16 wire values): its dense tensors (the biases; every
+# tensor during a ratio-1 warmup epoch) are Average-allreduced (dgc/compression.py:205-206)
+# — restated by the stub as the rank-order sum / W in the wire dtype, where the order
+# decides the last bits. (label, W, fp16_values, int32_indices, epochs, steps_per_epoch,
+# warmup kwargs)
+MULTI_CASES = [
+    ("w3_fp32", 3, False, False, (None,), 3, dict(warmup_epochs=-1)),
+    ("w3_fp16", 3, True, True, (None,), 3, dict(warmup_epochs=-1)),
+    ("w4_fp16", 4, True, False, (None,), 3, dict(warmup_epochs=-1)),
+    ("w8_fp32", 8, False, False, (None,), 3, dict(warmup_epochs=-1)),
+    ("w8_fp16", 8, True, True, (None,), 3, dict(warmup_epochs=-1)),
+    # wm5o (configs/dgc/wm5o.py): ratio 1 for epochs 0-4 (every tensor dense), then 0.01
+    ("w4_fp16_wm5o", 4, True, True, (0, 5), 2, dict(warmup_epochs=5, warmup_coeff=[1, 1, 1, 1, 1])),
+]
+
+
+def gen_optimizer_multi(C, M, H, O):
+    """MULTI_CASES: W ranks emulated in one process (as gen_optimizer); per case the
+    weights after every step (rank 0's; the replicas must be bit-identical, which is
+    checked here) and every rank's compress-call order and gradients (the GPU tests
+    replay them through the product path)."""
+    torch.set_num_threads(1)
+    arrays, meta = {}, {}
+    for label, W, fp16, i32, epochs, spe, wkw in MULTI_CASES:
+        _World.size = W
+        ranks = []
+        for q in range(W):
+            _World.rank = q
+            torch.manual_seed(7)
+            model = TinyNet()
+            opt = O.DGCSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+            mem = M.DGCSGDMemory(momentum=0.9)
+            comp = _quiet(C.DGCCompressor, 0.01, memory=mem, fp16_values=fp16, int32_indices=i32, **wkw)
+            _quiet(mem.initialize, model.named_parameters())
+            _quiet(comp.initialize, [(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+            dopt = H.DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                          backward_passes_per_step=1, op="Average")
+            ranks.append((model, dopt, comp))
+        trace, step_ref = {}, [0]
+        for q, (_, _, comp) in enumerate(ranks):
+            _trace_compress(comp, q, trace, step_ref)
+        random.seed(42)
+        schedule = [(e if t == 0 else None, ei * spe + t) for ei, e in enumerate(epochs) for t in range(spe)]
+        same = True
+        for epoch, s in schedule:
+            if epoch is not None:
+                for q, (_, _, comp) in enumerate(ranks):
+                    _World.rank = q
+                    _quiet(comp.warmup_compress_ratio, epoch)
+            step_ref[0] = s
+            _World.registry.clear()
+            _World.reduced.clear()
+            rstate = random.getstate()
+            for q, (model, dopt, comp) in enumerate(ranks):
+                _World.rank = q
+                random.setstate(rstate)
+                gen = torch.Generator().manual_seed(3000 + 100 * W + 10 * s + q)
+                x = torch.randn(32, 64, generator=gen)
+                y = torch.randint(0, 10, (32,), generator=gen)
+                torch.nn.functional.cross_entropy(model(x), y).backward()
+            for q, (model, dopt, comp) in enumerate(ranks):
+                _World.rank = q
+                dopt.step()
+                dopt.zero_grad()
+            for n, p in ranks[0][0].named_parameters():
+                arrays[f"{label}/s{s}/{n}"] = p.detach().numpy().copy()
+                same &= all(np.array_equal(p.detach().numpy(), dict(m.named_parameters())[n].detach().numpy())
+                            for m, _, _ in ranks[1:])
+        if not same:
+            raise SystemExit(f"optimizer_multi {label}: the reference's replicas diverged")
+        _save_trace(label, trace, arrays, meta)
+        meta[label] = dict(W=W, fp16_values=fp16, int32_indices=i32, epochs=list(epochs), steps_per_epoch=spe,
+                           warmup=wkw, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov_sgd=True,
+                           memory_nesterov=False, ratio=0.01, batch=32, data_seed="3000 + 100*W + 10*step + rank",
+                           model_seed=7, random_seed=42, steps=len(schedule))
+        print(f"optimizer_multi {label}: W={W}, {len(schedule)} steps, replicas bit-identical")
+    np.savez_compressed(os.path.join(HERE, "optimizer_multi.npz"), **arrays)
+    with open(os.path.join(HERE, "optimizer_multi.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
 # 16-bit parameters: the reference's memory + compressor on bf16 / fp16 tensors (every
 # ATen op rounds to the dtype). (name, N, ratio, dtype, kind, scale, nesterov, masking,
 # fp16_values, int32, resample, steps, W)
@@ -579,7 +661,8 @@ def gen_half(C, M, rec):
         json.dump(meta, f, indent=1)
 
 
-GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20", "optimizer_trace", "half")
+GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20", "optimizer_trace", "half",
+              "optimizer_multi")
 
 
 def main(which=GENERATORS):
@@ -599,6 +682,8 @@ def main(which=GENERATORS):
         gen_optimizer_trace(C, M, H, O)
     if "half" in which:
         gen_half(C, M, rec)
+    if "optimizer_multi" in which:
+        gen_optimizer_multi(C, M, H, O)
 
 
 if __name__ == "__main__":

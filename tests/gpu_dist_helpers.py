@@ -105,8 +105,13 @@ def _setup(label, batch, dev, cfg, model_seed=None):
         comp = DGCCompressor(cfg["ratio"], memory=mem, **comp_kw)
         mem.initialize(model.named_parameters())
         comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
-    dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
-                                backward_passes_per_step=1, op=Average, batch=batch)
+    if batch == "default":   # no batch= argument: the drop-in default ("auto") must pick the batched step
+        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                    backward_passes_per_step=1, op=Average)
+        assert dopt._batched is not None, "DistributedOptimizer's default did not take the batched step"
+    else:
+        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                    backward_passes_per_step=1, op=Average, batch=batch)
     calls = []
     orig = comp.compress
 
@@ -478,3 +483,66 @@ def half_batch_worker(rank, world, port, dtype_name, fp16, q):
     q.put((rank, problems))
     import torch.distributed as dist
     dist.destroy_process_group()
+
+
+def multi_replay_worker(rank, world, port, label, batch, queue):
+    """tests/golden/optimizer_multi.* case ``label`` at its own world size W (3, 4 or 8
+    processes on cuda:0 over gloo): the reference's DistributedOptimizer + DGCSGD run on
+    TinyNet, replayed from its recorded per-rank gradients and hook order through the
+    product path — per tensor, or batch=True (dense wire values in the packed payload's
+    tail, ONE allgather per step) — must reach the reference's weights bit for bit after
+    every step. The dense tensors' Average is where W >= 3 can differ: the reference
+    (restated) sums the ranks in rank order in the wire dtype (fp16 for fp16_values)."""
+    import torch.distributed as dist
+    _init(rank, world, port)
+    problems = []
+    try:
+        from dgc.comm import Average
+        from dgc.compression import DGCCompressor
+        from dgc.horovod import DistributedOptimizer
+        from dgc.memory import DGCSGDMemory
+        from dgc.optim import DGCSGD
+        from models import TinyNet
+        meta = json.load(open(os.path.join(GOLDEN, "optimizer_multi.json")))
+        arrays = np.load(os.path.join(GOLDEN, "optimizer_multi.npz"))
+        cfg = meta[label]
+        assert cfg["W"] == world, (cfg["W"], world)
+        dev = torch.device("cuda:0")
+        torch.manual_seed(cfg["model_seed"])
+        model = TinyNet().to(dev)
+        opt = DGCSGD(model.parameters(), lr=cfg["lr"], momentum=cfg["momentum"], weight_decay=cfg["weight_decay"],
+                     nesterov=cfg["nesterov_sgd"])
+        mem = DGCSGDMemory(momentum=cfg["momentum"])
+        with contextlib.redirect_stdout(io.StringIO()):
+            comp = DGCCompressor(cfg["ratio"], memory=mem, fp16_values=cfg["fp16_values"],
+                                 int32_indices=cfg["int32_indices"], **cfg["warmup"])
+            mem.initialize(model.named_parameters())
+            comp.initialize([(n, p) for n, p in model.named_parameters() if p.dim() > 1])
+        dopt = DistributedOptimizer(opt, named_parameters=model.named_parameters(), compression=comp,
+                                    backward_passes_per_step=1, op=Average, batch=batch)
+        params = dict(model.named_parameters())
+        spe = cfg["steps_per_epoch"]
+        schedule = [(e if t == 0 else None, ei * spe + t) for ei, e in enumerate(cfg["epochs"]) for t in range(spe)]
+        random.seed(cfg["random_seed"])
+        for epoch, s in schedule:
+            if epoch is not None:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    comp.warmup_compress_ratio(epoch)
+            key = f"{label}/s{s}/r{rank}"
+            order = meta[key]
+            grads = [arrays[f"{key}/{j}"] for j in range(len(order))]
+            replay_backward(params, order, grads, dev)
+            dopt.step()
+            dopt.zero_grad()
+            torch.cuda.synchronize()
+            for n, p in model.named_parameters():
+                w = arrays[f"{label}/s{s}/{n}"]
+                got = p.detach().cpu().numpy()
+                if not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
+                    problems.append(("weights", s, n, int((got != w).sum()), float(np.abs(got - w).max())))
+        queue.put((rank, problems))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        queue.put((rank, [("error", repr(e), traceback.format_exc())]))
+    finally:
+        dist.destroy_process_group()

@@ -78,3 +78,14 @@ def test_one_rank_shortcut_switch(monkeypatch):
         assert not comm.one_rank_collectives() and comm.allreduce_async_(x)._work is None
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("label,world", [("w3_fp32", 3), ("w4_fp16_wm5o", 4), ("w8_fp16", 8)])
+def test_dense_average_multi_rank_matches_reference(label, world):
+    """W = 3 / 4 / 8 gloo ranks on CPU: the reference's weights (tests/golden/
+    optimizer_multi.*), whose dense tensors' Average is the rank-order sum / W in the wire
+    dtype — dgc.comm.allreduce_async_ as an allgather summed in rank order."""
+    out = run(H.multi_worker, world, GOLDEN, label)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)

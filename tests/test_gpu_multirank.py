@@ -44,7 +44,7 @@ def run(fn, world, *args):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("batch", [False, True], ids=["per-tensor", "batched"])
+@pytest.mark.parametrize("batch", [False, True, "default"], ids=["per-tensor", "batched", "default"])
 @pytest.mark.parametrize("label", ["tinynet", "resnet20"])
 def test_distributed_optimizer_w2_reproduces_reference_weights(label, batch):
     out = run(G.optimizer_replay_worker, 2, label, batch)
@@ -53,7 +53,7 @@ def test_distributed_optimizer_w2_reproduces_reference_weights(label, batch):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("batch", [False, True], ids=["per-tensor", "batched"])
+@pytest.mark.parametrize("batch", [False, True, "default"], ids=["per-tensor", "batched", "default"])
 @pytest.mark.parametrize("label,mode,resume_at", [("resnet20", "fresh", 2), ("resnet20", "fresh", 4),
                                                   ("resnet20", "inplace", 4), ("tinynet", "inplace", 1)])
 def test_checkpoint_resume_w2_reproduces_reference_weights(label, mode, resume_at, batch):
@@ -147,5 +147,23 @@ def test_half_batched_optimizer_w2_equals_per_tensor(dtype, fp16):
     processes on one MI355X over gloo): the per-tensor path's gradients and 16-bit state
     (that path is pinned to the reference's 16-bit fixtures) bit for bit, 4 steps."""
     out = run(G.half_batch_worker, 2, dtype, fp16)
+    for rank, problems in out.items():
+        assert problems == [], (rank, problems)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("batch", [False, True], ids=["per-tensor", "batched"])
+@pytest.mark.parametrize("label", ["w3_fp32", "w3_fp16", "w4_fp16", "w8_fp32", "w8_fp16", "w4_fp16_wm5o"])
+def test_distributed_optimizer_dense_average_reproduces_reference_weights(label, batch):
+    """The dense tensors' Average at W = 3 / 4 / 8 (tests/golden/optimizer_multi.*, the
+    reference's DistributedOptimizer + DGCSGD on TinyNet; fp32 and fp16 wire values; a
+    wm5o run whose first epoch sends every tensor dense): the rank-order sum in the wire
+    dtype, then / W (dgc/compression.py:205-206 as the oracle restates Horovod's
+    Average) — per tensor through dgc.comm's allgather + dgc_rank_sum, batched in the
+    tail of the one packed payload. Weights bit for bit after every step, every rank."""
+    import json
+    import os
+    W = json.load(open(os.path.join(G.GOLDEN, "optimizer_multi.json")))[label]["W"]
+    out = run(G.multi_replay_worker, W, label, batch)
     for rank, problems in out.items():
         assert problems == [], (rank, problems)

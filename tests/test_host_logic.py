@@ -84,3 +84,25 @@ def test_dense_branch_passthrough_and_memory_api():
     quiet(mem2.initialize, [("a", torch.ones(3))])
     mem2.load_state_dict(sd)
     assert mem2.momentums["a"] is sd["momentums"]["a"]
+
+
+def test_distributed_optimizer_default_picks_batched_only_when_equivalent():
+    """DistributedOptimizer's default batch="auto" (dgc.horovod.batched.auto) takes the
+    batched step only where it computes what the per-tensor hooks would: not for host
+    parameters, an overriding subclass, an op other than Average, mixed dtypes or a
+    non-DGC compressor (the gloo CPU tests' oracle doubles keep their per-tensor calls)."""
+    from dgc.comm import Average, Sum
+    from dgc.horovod import batched
+
+    class Sub(DGCCompressor):
+        def compress(self, tensor, name):
+            return super().compress(tensor, name)
+
+    mem = DGCSGDMemory(momentum=0.9)
+    comp = quiet(DGCCompressor, 0.01, memory=mem)
+    cpu = [("w", torch.nn.Parameter(torch.zeros(4, 4)))]
+    assert not batched.auto(comp, cpu, Average)                    # host parameters
+    assert not batched.auto(quiet(Sub, 0.01, memory=mem), cpu, Average)
+    assert not batched.auto(comp, cpu, Sum)
+    assert not batched.auto(quiet(DGCCompressor, 0.01), cpu, Average)   # Memory, not DGCSGDMemory
+    assert not batched.auto(quiet(DGCCompressor, 0.01, memory=mem, strided_sample=False), cpu, Average)
