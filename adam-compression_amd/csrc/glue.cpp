@@ -27,6 +27,16 @@ namespace {
 
 bool is_list(PyObject* o) { return PyList_Check(o); }
 
+// ATen calls below can throw c10::Error (a tensor without storage, ...): the exception
+// becomes a Python RuntimeError instead of crossing the CPython frame (std::terminate)
+#define GLUE_TRY try {
+#define GLUE_CATCH                                                  \
+    }                                                               \
+    catch (const std::exception& e) {                               \
+        PyErr_SetString(PyExc_RuntimeError, e.what());              \
+        return nullptr;                                             \
+    }
+
 PyObject* grad_table(PyObject*, PyObject* args) {
     PyObject* params;
     unsigned long long addr;
@@ -40,6 +50,7 @@ PyObject* grad_table(PyObject*, PyObject* args) {
     PyObject* fallback = PyList_New(0);
     if (!fallback) return nullptr;
     const Py_ssize_t n = PyList_GET_SIZE(params);
+    GLUE_TRY
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject* p = PyList_GET_ITEM(params, i);
         if (!THPVariable_Check(p)) {
@@ -48,8 +59,11 @@ PyObject* grad_table(PyObject*, PyObject* args) {
             return nullptr;
         }
         const at::Tensor& g = THPVariable_Unpack(p).grad();
-        void* ptr = g.defined() ? g.data_ptr() : nullptr;
-        if (!g.defined() || !g.is_contiguous() || (reinterpret_cast<uintptr_t>(ptr) % (uintptr_t)align) != 0) {
+        // a sparse (nn.Embedding(sparse=True)) or otherwise non-strided gradient has no
+        // data pointer: the Python fallback handles it (or raises a Python error)
+        const bool strided = g.defined() && g.layout() == at::kStrided && g.has_storage();
+        void* ptr = strided ? g.data_ptr() : nullptr;
+        if (!strided || !g.is_contiguous() || (reinterpret_cast<uintptr_t>(ptr) % (uintptr_t)align) != 0) {
             PyObject* idx = PyLong_FromSsize_t(i);
             if (!idx || PyList_Append(fallback, idx) != 0) {
                 Py_XDECREF(idx);
@@ -62,6 +76,11 @@ PyObject* grad_table(PyObject*, PyObject* args) {
         }
         table[i] = ptr;
     }
+    } catch (const std::exception& e) {
+        Py_DECREF(fallback);
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+        return nullptr;
+    }
     return fallback;
 }
 
@@ -73,6 +92,7 @@ PyObject* bind_grads(PyObject*, PyObject* args) {
         return nullptr;
     }
     const Py_ssize_t n = PyList_GET_SIZE(params);
+    GLUE_TRY
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject* p = PyList_GET_ITEM(params, i);
         PyObject* v = PyList_GET_ITEM(views, i);
@@ -84,6 +104,7 @@ PyObject* bind_grads(PyObject*, PyObject* args) {
         at::Tensor& grad = const_cast<at::Tensor&>(THPVariable_Unpack(p)).mutable_grad();
         if (!grad.is_same(view)) grad = view;
     }
+    GLUE_CATCH
     Py_RETURN_NONE;
 }
 
@@ -95,6 +116,7 @@ PyObject* release_grads(PyObject*, PyObject* args) {
         return nullptr;
     }
     const Py_ssize_t n = PyList_GET_SIZE(params);
+    GLUE_TRY
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject* p = PyList_GET_ITEM(params, i);
         if (!THPVariable_Check(p)) {
@@ -103,6 +125,7 @@ PyObject* release_grads(PyObject*, PyObject* args) {
         }
         const_cast<at::Tensor&>(THPVariable_Unpack(p)).mutable_grad().reset();
     }
+    GLUE_CATCH
     Py_RETURN_NONE;
 }
 

@@ -186,6 +186,9 @@ _SIGNATURES = {
                                         _F, _P, _P]),
     "dgc_sgd_step": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
                                     ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _P]),
+    "dgc_sgd_step16": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                      ctypes.POINTER(_I64), ctypes.POINTER(_I32), _I32, _F, _F, _F, _F, _I32, _I32,
+                                      _P]),
 }
 
 _lib = None

@@ -101,7 +101,11 @@ class DGCBatch:
         # velocity's exact fp32 image, which the selection reads (dgc_batch_select); the
         # 16-bit state is masked from the payload (dgc_mask_packed16)
         self._vec32 = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev) if self.half else None
+        # the 16-bit decompress's out-of-range flag (a peer's index outside [0, flat_numel));
+        # copied to pinned host memory after every decompress and reset, checked like status
         self._bad16 = torch.zeros(1, dtype=torch.int32, device=dev) if self.half else None
+        self._bad16_host = (torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+                            if self.half else None)
         self.deferred_masking = bool(deferred_masking) and not self.half
         self._pending = False
         self.out_flat = torch.zeros(self.flat_numel, dtype=dtype, device=dev)
@@ -241,6 +245,7 @@ class DGCBatch:
         batched optimizer's p.grad tensors, read in place). Raises first if a previous
         step's resample replay reported DGC_K5_BROKEN (``status``)."""
         self.status.check()
+        self._check_bad16()
         starts = self.draw_starts() if starts is None else starts
         self.starts = starts
         self._par += 1   # a step starts: the other payload / gather buffer
@@ -337,6 +342,8 @@ class DGCBatch:
                                                  _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
                                                  _lib.VD[self.dtype], self.flat_numel, 1.0 / self.world,
                                                  self._bad16.data_ptr(), st), "dgc_decompress_packed16")
+            self._bad16_host.copy_(self._bad16, non_blocking=True)
+            self._bad16.zero_()
             return out
         aliased = out.untyped_storage().data_ptr() == self.grad_flat.untyped_storage().data_ptr()
         reusable = (self.fill == "sparse" and not aliased and self._last_gathered is not None
@@ -370,8 +377,22 @@ class DGCBatch:
         return self.decompress()
 
     # ---------------------------------------------------------------- results
+    def _check_bad16(self, sync=False):
+        """Raises when a 16-bit decompress met an index outside [0, flat_numel) (the fp32
+        engines report it through their status words): the flag of the last decompress the
+        GPU finished (sync=True: of the last one issued)."""
+        if self._bad16_host is None:
+            return
+        if sync:
+            torch.cuda.current_stream(self.device).synchronize()
+        if int(self._bad16_host.numpy()[0]):
+            self._bad16_host.zero_()
+            raise RuntimeError("DGCBatch: a gathered payload held an index outside the flat buffer (foreign or "
+                               "corrupted payload); its entry was dropped from the decompress")
+
     def infos(self):
         self.status.check(sync=True)
+        self._check_bad16(sync=True)
         raw = self.info.cpu().numpy().tobytes()
         out = []
         for t in range(len(self.names)):

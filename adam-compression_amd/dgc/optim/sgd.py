@@ -6,14 +6,17 @@ optimizer keeps momentum only for the weight-decay term: with weight decay wd,
 first step); ``d = d + momentum * buf`` (nesterov) or ``d = buf``; then
 ``p -= lr * (d + grad)``. Without weight decay ``p -= lr * grad``.
 
-On the MI355X every parameter group is ONE fused pass (``dgc_sgd_step``, K7 in
-``csrc/sgd.hip``): read p, grad (+ the momentum buffer), write p (+ buffer), with
-the reference's torch-CPU rounding (``add(alpha)`` is one fused multiply-add), so the
-weights are bit-identical to the reference's. Every other parameter — on the CPU (the
-gloo plumbing tests), or on the GPU but not a contiguous fp32 tensor with a contiguous
-fp32 gradient (fp16/bf16 weights, channels_last convolutions, a non-contiguous
-view) — takes the reference's own torch op sequence, as the reference accepts any of
-them. The optimizer state keeps the reference's layout (``state[p]["momentum_buffer"]``).
+On the MI355X every parameter group is ONE fused pass per dtype (``dgc_sgd_step``,
+K7 in ``csrc/sgd.hip``, for fp32; ``dgc_sgd_step16`` for bf16 / fp16): read p, grad
+(+ the momentum buffer), write p (+ buffer), with the reference's torch-CPU rounding
+(fp32: ``add(alpha)`` is one fused multiply-add; 16-bit: every op rounds to the
+dtype, alpha too, with the CPU kernels' vector body / scalar tail — oracle
+``dgcsgd_step16``, pinned to tests/golden/sgd16.*), so the weights are bit-identical to
+the reference's. Every other parameter — on the CPU (the gloo plumbing tests), or on
+the GPU but not a contiguous fp32 / bf16 / fp16 tensor with a contiguous gradient of
+its dtype (channels_last convolutions, a non-contiguous view) — takes the reference's
+own torch op sequence, as the reference accepts any of them. The optimizer state keeps
+the reference's layout (``state[p]["momentum_buffer"]``).
 """
 import ctypes
 
@@ -41,13 +44,15 @@ class DGCSGD(Optimizer):
         for group in self.param_groups:
             group.setdefault("nesterov", False)
 
+    _DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+
     @staticmethod
     def _fusable(p):
-        """A parameter K7 serves: contiguous fp32 CUDA weight and gradient (and, when it
-        exists, momentum buffer) on one device."""
+        """A parameter K7 serves: contiguous CUDA weight and gradient of one dtype (fp32,
+        bf16 or fp16; and, when it exists, momentum buffer) on one device."""
         g = p.grad
-        return (p.is_cuda and p.dtype == torch.float32 and p.data.is_contiguous() and g.is_cuda
-                and g.dtype == torch.float32 and g.is_contiguous() and g.device == p.device)
+        return (p.is_cuda and p.dtype in DGCSGD._DTYPES and p.data.is_contiguous() and g.is_cuda
+                and g.dtype == p.dtype and g.is_contiguous() and g.device == p.device)
 
     @staticmethod
     def _cpu_param(p, d_p, group, state):
@@ -68,18 +73,21 @@ class DGCSGD(Optimizer):
         p.add_(d.add(d_p), alpha=-group["lr"])
 
     def _fused_group(self, group, params):
-        """One dgc_sgd_step launch (per 48 tensors) over the group's CUDA parameters."""
+        """One dgc_sgd_step(16) launch (per 48 tensors) over the group's CUDA parameters
+        of one device and dtype."""
         from dgc import _lib
         wd, mom = float(group["weight_decay"]), float(group["momentum"])
         use_buf = wd != 0 and mom != 0
         n = len(params)
+        dt = params[0].dtype
         P, G, B = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
         N, F = (ctypes.c_int64 * n)(), (ctypes.c_int32 * n)()
         keep = []
         for i, p in enumerate(params):
             g = p.grad
-            _lib.require_cuda_f32(p.data, "DGCSGD.step")
-            _lib.require_cuda_f32(g, "DGCSGD.step")
+            if _lib.require_cuda_float(p.data, "DGCSGD.step") != dt or g.dtype != dt:
+                raise ValueError("DGCSGD.step: a fused launch takes parameters and gradients of one dtype")
+            _lib.require_cuda_float(g, "DGCSGD.step")
             if g.device != p.device:
                 raise ValueError("DGCSGD.step: parameter and gradient on different devices")
             P[i], G[i], N[i] = p.data.data_ptr(), g.data_ptr(), p.numel()
@@ -89,13 +97,17 @@ class DGCSGD(Optimizer):
                 F[i] = int(buf is None)
                 if buf is None:
                     buf = state["momentum_buffer"] = torch.empty_like(p.data)
-                _lib.require_cuda_f32(buf, "DGCSGD.step")
+                if _lib.require_cuda_float(buf, "DGCSGD.step") != dt:
+                    raise ValueError("DGCSGD.step: momentum buffer of another dtype")
                 B[i] = buf.data_ptr()
             keep.append(g)
         dev = params[0].device
         L = _lib.lib()
-        _lib.check(L.dgc_sgd_step(P, G, B, N, F, n, float(group["lr"]), mom, float(group["dampening"]), wd,
-                                  int(bool(group["nesterov"])), _lib.stream_of(dev)), "dgc_sgd_step")
+        args = (P, G, B, N, F, n, float(group["lr"]), mom, float(group["dampening"]), wd, int(bool(group["nesterov"])))
+        if dt == torch.float32:
+            _lib.check(L.dgc_sgd_step(*args, _lib.stream_of(dev)), "dgc_sgd_step")
+        else:
+            _lib.check(L.dgc_sgd_step16(*args, _lib.VD[dt], _lib.stream_of(dev)), "dgc_sgd_step16")
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -109,8 +121,9 @@ class DGCSGD(Optimizer):
                 if p.grad is None:
                     continue
                 buf = self.state[p].get("momentum_buffer") if p in self.state else None
-                if self._fusable(p) and (buf is None or (buf.dtype == torch.float32 and buf.is_contiguous())):
-                    by_dev.setdefault(p.device, []).append(p)
+                if self._fusable(p) and (buf is None or (buf.dtype == p.dtype and buf.is_contiguous()
+                                                         and buf.device == p.device)):
+                    by_dev.setdefault((p.device, p.dtype), []).append(p)
                 else:
                     self._cpu_param(p, p.grad, group, self.state[p])
             for params in by_dev.values():

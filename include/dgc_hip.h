@@ -460,6 +460,15 @@ int dgc_compensate_ranks(const void* src, int32_t src_dtype, int32_t world, int6
 int dgc_sgd_step(float* const* params, const float* const* grads, float* const* bufs, const int64_t* numels,
                  const int32_t* first, int32_t count, float lr, float momentum, float dampening,
                  float weight_decay, int32_t nesterov, void* stream);
+/* K7-16: the same for bf16 / fp16 parameters (dtype DGC_BF16 / DGC_F16; params, grads,
+ * bufs 16-bit arrays of that dtype): every op rounds to the dtype as the reference's
+ * torch-CPU ops on a 16-bit tensor do — alpha rounded to the dtype; `add(alpha)` rounds
+ * fl32(x + y * alpha) once in the first n - n % 32 elements of a tensor (the CPU
+ * kernels' vector body) and rounds the product first in the last n % 32 (their scalar
+ * tail). */
+int dgc_sgd_step16(void* const* params, const void* const* grads, void* const* bufs, const int64_t* numels,
+                   const int32_t* first, int32_t count, float lr, float momentum, float dampening,
+                   float weight_decay, int32_t nesterov, int32_t dtype, void* stream);
 
 /* ---- 16-bit parameters (bf16 / fp16, dtype = DGC_BF16 / DGC_F16) ----
  * The reference's memory and compressor on a bf16 / fp16 parameter

@@ -661,8 +661,59 @@ def gen_half(C, M, rec):
         json.dump(meta, f, indent=1)
 
 
+# DGCSGD.step on bf16 / fp16 parameters (dgc/optim/sgd.py:42-68 on 16-bit tensors; CPU,
+# one thread): (label, dtype, lr, momentum, dampening, weight_decay, nesterov). The shapes
+# give every length class of the CPU kernels' 32-element vector body and scalar tail.
+SGD16_CASES = [
+    ("bf16_nest_wd", "bfloat16", 0.1, 0.9, 0.0, 1e-4, True),
+    ("bf16_plain_wd_damp", "bfloat16", 0.05, 0.9, 0.1, 5e-4, False),
+    ("bf16_nowd", "bfloat16", 0.1, 0.9, 0.0, 0.0, False),
+    ("fp16_nest_wd", "float16", 0.1, 0.9, 0.0, 1e-4, True),
+    ("fp16_plain_wd_damp", "float16", 0.05, 0.9, 0.1, 5e-4, False),
+    ("fp16_wd_nomom", "float16", 0.1, 0.0, 0.0, 1e-4, False),
+]
+SGD16_SHAPES = [("a", (37,)), ("b", (64, 3, 7, 7)), ("c", (1000,)), ("d", (333, 7)), ("e", (16,)), ("f", (1024, 33))]
+
+
+def sgd16_inputs(gen, dt, steps=3):
+    """The seeded inputs of an SGD16 case (the test regenerates them the same way): the
+    initial parameters, then each step's gradients, drawn in this order."""
+    init = [(torch.randn(s, generator=gen) * 0.5).to(dt) for _, s in SGD16_SHAPES]
+    grads = [[(torch.randn(s, generator=gen) * 0.01).to(dt) for _, s in SGD16_SHAPES] for _ in range(steps)]
+    return init, grads
+
+
+def gen_sgd16(O):
+    """Per case: the parameters after each of 3 DGCSGD steps on 16-bit parameters, and
+    the momentum buffers after the last (16-bit patterns), from the seeded inputs of
+    ``sgd16_inputs`` (torch.Generator(4000 + case) normal draws; the test regenerates them)."""
+    torch.set_num_threads(1)
+    arrays, meta = {}, {}
+    bits = lambda t: t.detach().contiguous().view(torch.int16).numpy().copy()   # noqa: E731
+    for ci, (label, dts, lr, mom, damp, wd, nest) in enumerate(SGD16_CASES):
+        dt = getattr(torch, dts)
+        init, grads = sgd16_inputs(torch.Generator().manual_seed(4000 + ci), dt)
+        params = [torch.nn.Parameter(t) for t in init]
+        opt = O.DGCSGD(params, lr=lr, momentum=mom, dampening=damp, weight_decay=wd, nesterov=nest)
+        for s in range(3):
+            for p, g in zip(params, grads[s]):
+                p.grad = g
+            opt.step()
+            for (n, _), p in zip(SGD16_SHAPES, params):
+                arrays[f"{label}/s{s}/p/{n}"] = bits(p)
+                buf = opt.state[p].get("momentum_buffer")
+                if buf is not None and s == 2:
+                    arrays[f"{label}/buf/{n}"] = bits(buf)
+        meta[label] = dict(dtype=dts, lr=lr, momentum=mom, dampening=damp, weight_decay=wd, nesterov=nest, steps=3,
+                           shapes=SGD16_SHAPES)
+        print(f"sgd16 {label}")
+    np.savez_compressed(os.path.join(HERE, "sgd16.npz"), **arrays)
+    with open(os.path.join(HERE, "sgd16.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
 GENERATORS = ("attributes", "compress", "decompress", "optimizer", "optimizer_resnet20", "optimizer_trace", "half",
-              "optimizer_multi")
+              "optimizer_multi", "sgd16")
 
 
 def main(which=GENERATORS):
@@ -684,6 +735,8 @@ def main(which=GENERATORS):
         gen_half(C, M, rec)
     if "optimizer_multi" in which:
         gen_optimizer_multi(C, M, H, O)
+    if "sgd16" in which:
+        gen_sgd16(O)
 
 
 if __name__ == "__main__":

@@ -444,8 +444,10 @@ def _half_run(batch, dtype, fp16, rank, dev, steps=4):
         comp = DGCCompressor(0.01, memory=DGCSGDMemory(momentum=0.9), fp16_values=fp16, int32_indices=fp16)
         comp.memory.initialize(named)
         comp.initialize([(n, p) for n, p in named if p.dim() > 1])
-    dopt = DistributedOptimizer(torch.optim.SGD([p for _, p in named], lr=0.0), named_parameters=named,
-                                compression=comp, batch=batch)
+    from dgc.optim import DGCSGD
+    # the wrapped optimizer is DGCSGD: its 16-bit step is the fused K7-16 (dgc_sgd_step16)
+    dopt = DistributedOptimizer(DGCSGD([p for _, p in named], lr=0.1, momentum=0.9, weight_decay=1e-4,
+                                       nesterov=True), named_parameters=named, compression=comp, batch=batch)
     random.seed(5)
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     out = []
@@ -457,11 +459,12 @@ def _half_run(batch, dtype, fp16, rank, dev, steps=4):
             p.grad = g.to(dtype)
         for _, hook in reversed(dopt._hook_fns):
             hook()
-        dopt.synchronize()
+        dopt.step()   # synchronize() (compress -> exchange -> decompress) + DGCSGD's fused 16-bit step
         torch.cuda.synchronize()
         st = comp.memory.state_dict()
         out.append({n: p.grad.clone() for n, p in named} | {f"m:{n}": t.clone() for n, t in st["momentums"].items()}
-                   | {f"v:{n}": t.clone() for n, t in st["velocities"].items()})
+                   | {f"v:{n}": t.clone() for n, t in st["velocities"].items()}
+                   | {f"p:{n}": p.detach().clone() for n, p in named})
         dopt.zero_grad()
     return out
 

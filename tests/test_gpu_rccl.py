@@ -2,12 +2,12 @@
 
 A one-GPU box cannot hold two RCCL ranks, so these tests initialise a one-rank `nccl`
 process group (RCCL on ROCm) and clear `comm.ONE_RANK_SHORTCUT`: the collectives then
-run `all_gather_into_tensor` / `all_reduce` on the device tensors themselves (no host
-staging — that is gloo's branch), as at W > 1. Checked: the packed payload allgather,
-the variable-row allgather and the Average allreduce return their inputs, and the
-reference's per-tensor hook path (dgc/horovod/optimizer.py:116-187: compress ->
-packed allgather -> decompress, dense tensors allreduced) over RCCL equals the same
-steps without a collective bit for bit.
+run `all_gather_into_tensor` on the device tensors themselves (no host staging — that
+is gloo's branch), as at W > 1. Checked: the packed payload allgather, the variable-row
+allgather and the Average (an allgather summed in rank order) return their inputs, and
+the reference's per-tensor hook path (dgc/horovod/optimizer.py:116-187: compress ->
+packed allgather -> decompress, dense tensors averaged) over RCCL equals the same steps
+without a collective bit for bit.
 """
 import socket
 
@@ -79,8 +79,10 @@ def test_per_tensor_path_over_rccl(fp16, rccl_one_rank, monkeypatch):
     for name in calls:
         monkeypatch.setattr(rccl_one_rank.dist, name, counted(name))
     got = dropin._run(False, fp16, modes, monkeypatch)
-    # every step: a packed allgather per compressed tensor, an allreduce per dense one
-    assert calls["all_gather_into_tensor"] >= len(modes) and calls["all_reduce"] >= len(modes), calls
+    # every step: a packed allgather per compressed tensor and an allgather per dense one
+    # (the Average summed in rank order by dgc_rank_sum) — no allreduce, whose order is RCCL's
+    dense = sum(1 for _, s in dropin.SHAPES if len(s) <= 1)
+    assert calls["all_gather_into_tensor"] >= len(modes) * (1 + dense) and calls["all_reduce"] == 0, calls
     monkeypatch.setattr(rccl_one_rank, "ONE_RANK_SHORTCUT", True)
     want = dropin._run(False, fp16, modes, monkeypatch)
     for step, (w, g) in enumerate(zip(want, got)):
@@ -170,14 +172,29 @@ def test_batch_over_rccl(fill, parts, rccl_one_rank, monkeypatch):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("fp16", [False, True], ids=["wire-dtype", "wire-fp16"])
 @pytest.mark.parametrize("batch", [True, "sparse"], ids=["batch", "batch-sparse"])
-def test_batched_optimizer_over_rccl(batch, rccl_one_rank, monkeypatch):
-    """DistributedOptimizer(batch=True): the grouped payload allgather and the dense
-    tensors' allreduce through RCCL equal the one-rank step without them."""
+def test_batched_optimizer_over_rccl(batch, fp16, rccl_one_rank, monkeypatch):
+    """DistributedOptimizer(batch=True): ONE RCCL collective per step — the grouped
+    payload allgather, the dense tensors' wire values in its tail — equals the one-rank
+    step without it."""
     modes = ["fresh", "fresh", "inplace", "fresh"]
-    got = dropin._run(batch, True, modes, monkeypatch)
+    calls = {"all_gather_into_tensor": 0, "all_reduce": 0}
+
+    def counted(name):
+        fn = getattr(dist, name)
+
+        def wrapper(*a, **kw):
+            calls[name] += 1
+            return fn(*a, **kw)
+        return wrapper
+
+    for name in calls:
+        monkeypatch.setattr(rccl_one_rank.dist, name, counted(name))
+    got = dropin._run(batch, fp16, modes, monkeypatch)
+    assert calls == {"all_gather_into_tensor": len(modes), "all_reduce": 0}, calls
     monkeypatch.setattr(rccl_one_rank, "ONE_RANK_SHORTCUT", True)
-    want = dropin._run(batch, True, modes, monkeypatch)
+    want = dropin._run(batch, fp16, modes, monkeypatch)
     for step, (w, g) in enumerate(zip(want, got)):
         assert w.keys() == g.keys()
         for k in w:
