@@ -2046,7 +2046,11 @@ __global__ void __launch_bounds__(kBlock) k_emit_queue(const float* __restrict__
 // comparisons, so which boundary ties survive and the order of equal keys come from
 // its exact layout — the replay runs the same operations on the same layout.
 //
-//   entries   (|x| key (31 bits) << 33) | element index (33 bits: N < 2^33)
+//   entries   (|x| key (31 bits) << 33) | element index (33 bits) for N < 2^33; above, the
+//             low 33 bits hold a SLOT in [0, k) and the tensor's cand_idx region maps slot ->
+//             element index: the heap holds k entries at any time, and an entry that
+//             replaces the root takes the root's slot (its key alone is compared, so the
+//             replay is the same)
 //   layout    node i in LDS for i < kHeapTop (levels 0..13), else in the tensor's K5
 //             queue region (>= k entries: cand_cap = min(64k - 1, N) >= k)
 //   fill      the workgroup streams vec in index order, block-scans the candidates
@@ -2257,6 +2261,9 @@ __device__ __forceinline__ void heap_select_wg(const float* __restrict__ vec_fla
     const int64_t k = d.k, n = d.n;
     const bool al = aligned16(vec);
     const HeapNodes h{lds(smem), glb(w.queue + d.cand_off)};
+    // wide (N >= 2^33): node payloads are slots, side[slot] the element index
+    const bool wide = n >= ((int64_t)1 << kHeapKeyShift);
+    DGC_GLB int64_t* side = glb(w.cand_idx + d.cand_off);
     uint64_t* hot = smem + kHeapTop + 1;
     __shared__ uint64_t lds16[16];
     __shared__ uint64_t root_sh;
@@ -2273,7 +2280,10 @@ __device__ __forceinline__ void heap_select_wg(const float* __restrict__ vec_fla
         for (int j = 0; j < 4; ++j) {
             if ((cm >> j) & 1u) {
                 const int64_t g = filled + (int64_t)r++;
-                if (g < k) h.st(g, ((uint64_t)abs_key(x[j]) << kHeapKeyShift) | (uint64_t)(e0 + j));
+                if (g < k) {
+                    h.st(g, ((uint64_t)abs_key(x[j]) << kHeapKeyShift) | (uint64_t)(wide ? g : e0 + j));
+                    if (wide) side[g] = e0 + j;
+                }
             }
         }
         if (filled + (int64_t)total >= k) {
@@ -2319,17 +2329,23 @@ __device__ __forceinline__ void heap_select_wg(const float* __restrict__ vec_fla
         if (!__syncthreads_or(hm != 0)) return true;
         uint64_t htot;
         const uint64_t hb = block_exclusive_scan((uint64_t)__popc(hm), lds16, &htot);
-        const int64_t e0 = c0 + 4 * (int64_t)tid;
         uint64_t q = hb;
+        // hot entries carry the element's offset in this chunk (< kHeapChunk)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if ((hm >> j) & 1u) hot[q++] = ((uint64_t)abs_key(x[j]) << kHeapKeyShift) | (uint64_t)(e0 + j);
+            if ((hm >> j) & 1u) hot[q++] = ((uint64_t)abs_key(x[j]) << kHeapKeyShift) | (uint64_t)(4 * tid + j);
         __syncthreads();
         if (tid < kWave) {   // wave 0: comp(candidate, top) is "strictly greater"
             uint64_t root = root_sh;
             for (uint64_t i = 0; i < htot; ++i) {
-                const uint64_t v = hot[i];
-                if (hkey(v) > hkey(root)) root = heap_replace_root(h, k, v);
+                const uint64_t hv = hot[i];
+                if (hkey(hv) > hkey(root)) {
+                    const int64_t e = c0 + (int64_t)(hv & kHeapIdxMask);
+                    const uint64_t slot = root & kHeapIdxMask;   // the popped root's slot is recycled
+                    if (wide && tid == 0) side[slot] = e;
+                    const uint64_t v = (hv & ~kHeapIdxMask) | (uint64_t)(wide ? (int64_t)slot : e);
+                    root = heap_replace_root(h, k, v);
+                }
             }
             if (tid == 0) root_sh = root;
         }
@@ -2355,7 +2371,8 @@ __device__ __forceinline__ void heap_select_wg(const float* __restrict__ vec_fla
     }
     __syncthreads();
     for (int64_t p = tid; p < k; p += kNthThreads) {
-        const int64_t li = (int64_t)(h.ld(p) & kHeapIdxMask);
+        const int64_t lo = (int64_t)(h.ld(p) & kHeapIdxMask);
+        const int64_t li = wide ? side[lo] : lo;
         emit_one(o, d, obase_s + p, li, vec[li]);
     }
 }
@@ -2886,8 +2903,17 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G,
 
 // The last of the T workgroups to finish (f.on) then runs the finish of the whole call
 // (T arrivals on one ticket; nothing it writes is read by k_emit_queue).
+//
+// A global phase that BROKE (a barrier timed out after the consensus voted GO: its
+// partitions of the queue are not reliable) is recovered here, in the same call: the
+// queue is rebuilt from the gather's candidate keys — entry j = (key_j << 32 | j), as
+// the gather wrote it — and the whole nth_element replayed on this workgroup from
+// [0, n), exact (k5_status DGC_K5_FALLBACK | DGC_K5_RECOVERED). force_broken (parity
+// tests, DGC_K5_FORCE_BROKEN=1): every replayed tensor takes that path, its queue first
+// overwritten with garbage.
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
-                                                            EmitOut o, int from_global, FinishArgs f) {
+                                                            EmitOut o, int from_global, FinishArgs f,
+                                                            int force_broken) {
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
     __shared__ __align__(16) uint64_t smem[kK5SmemBytes / 8];
@@ -2902,8 +2928,26 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
         DGC_LDS uint32_t* llp = reinterpret_cast<DGC_LDS uint32_t*>(lq + kNthLds);
         DGC_LDS uint32_t* lrp = llp + kNthPairLds;
         DGC_LDS uint8_t* lmk = reinterpret_cast<DGC_LDS uint8_t*>(lrp + kNthPairLds);
-        nth_element_wg(glb(w.queue + d.cand_off), st->n_cur, d.k - 1, gl, gr, lq, llp, lrp, lmk,
-                       from_global ? w.nthg + t : nullptr);
+        NthG* g = w.nthg + t;
+        DGC_GLB uint64_t* q = glb(w.queue + d.cand_off);
+        const int64_t nc = st->n_cur;
+        __shared__ int recover;
+        if (threadIdx.x == 0)
+            recover = force_broken ||
+                      (from_global && (__hip_atomic_load(&g->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                                       (uint32_t)DGC_K5_BROKEN));
+        __syncthreads();
+        if (recover) {
+            if (force_broken)
+                for (int64_t j = threadIdx.x; j < nc; j += kNthThreads) q[j] = ~(uint64_t)j;
+            __syncthreads();
+            const DGC_GLB uint32_t* ck = glb(w.cand_key + d.cand_off);
+            for (int64_t j = threadIdx.x; j < nc; j += kNthThreads) q[j] = ((uint64_t)ck[j] << 32) | (uint64_t)j;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                g->status = (g->status & ~(uint32_t)DGC_K5_BROKEN) | (uint32_t)(DGC_K5_FALLBACK | DGC_K5_RECOVERED);
+        }
+        nth_element_wg(q, nc, d.k - 1, gl, gr, lq, llp, lrp, lmk, from_global && !recover ? g : nullptr);
     }
     const bool idle = !(st->branch == DGC_BRANCH_RESAMPLE && (st->rs_nth == 1 || st->rs_nth == 2));
     if (idle) K5_STAMP(0);   // (profiling build: slots 0-2 are free when the replay did not run)
@@ -2921,20 +2965,17 @@ __global__ void k_spec_reset(float* spec, int32_t T) {
 
 // ------------------------------------------------------------------ host driver
 // The resample replays pack what they move into 64-bit entries: K5's queue holds
-// (key << 32 | candidate position), K5b's heap (key31 << 33 | element index). A tensor
-// whose candidates or elements do not fit those widths is refused up front — torch's
-// topk takes any n (dgc/compression.py:124-137), and a truncated position would be a
-// wrong payload, not an error.
+// (key << 32 | candidate position), K5b's heap (key31 << 33 | element index, or a slot
+// of the k heap entries with the index beside it from N = 2^33 on). A tensor whose
+// candidates do not fit K5's width is refused up front — torch's topk takes any n
+// (dgc/compression.py:124-137), and a truncated position would be a wrong payload, not
+// an error. (k < 2^32 follows: the candidate capacity min(64k - 1, n) is >= k.)
 static int check_replay_width(int64_t n, int64_t k, const char* who) {
     if (nth_cand_cap(n, k) > (int64_t)0xFFFFFFFFLL)
         DGC_FAIL(DGC_ERR_OVERFLOW,
                  "%s: the resample replay addresses at most 2^32 - 1 candidates; numel %lld with num_selects %lld "
                  "can have %lld (use resample=False or a smaller tensor)",
                  who, (long long)n, (long long)k, (long long)nth_cand_cap(n, k));
-    if (n >= ((int64_t)1 << kHeapKeyShift))
-        DGC_FAIL(DGC_ERR_OVERFLOW,
-                 "%s: the partial_sort resample replay addresses elements below 2^33; numel %lld "
-                 "(use resample=False or a smaller tensor)", who, (long long)n);
     return DGC_OK;
 }
 
@@ -3071,11 +3112,11 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    // DGC_K5_FORCE_BROKEN=1 (parity tests only): report every resampled tensor as broken,
-    // to exercise the engines' raise without a barrier actually timing out
-    const uint32_t force = std::getenv("DGC_K5_FORCE_BROKEN") ? (uint32_t)DGC_K5_BROKEN : 0u;
+    // DGC_K5_FORCE_BROKEN=1 (parity tests only): every replayed tensor takes the recovery
+    // of a broken global phase (k_nth_select), without a barrier actually timing out
+    const int force = std::getenv("DGC_K5_FORCE_BROKEN") ? 1 : 0;
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
-                         sink, force};
+                         sink, 0u};
     bool finished = false;   // the payload count and records are written
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
@@ -3123,7 +3164,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
         FinishArgs f = fin;
         f.on = 1;   // k_nth_select's last workgroup finishes the call
-        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0, f);
+        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0, f,
+                           force);
         DGC_LAUNCHED();
         finished = true;
         hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);

@@ -57,8 +57,8 @@ enum dgc_status {
     DGC_ERR_DTYPE = 2,        /* unsupported value / index dtype */
     DGC_ERR_OVERFLOW = 3,     /* int32 indices requested for n > 2^31 - 1, or a    */
                               /* resample replay that cannot address the tensor:   */
-                              /* more than 2^32 - 1 candidates (min(64k - 1, n))   */
-                              /* or n >= 2^33 elements (resample = 1 only)         */
+                              /* more than 2^32 - 1 candidates (min(64k - 1, n);   */
+                              /* resample = 1 only)                                */
     DGC_ERR_HIP = 4,          /* a HIP runtime call failed */
     DGC_ERR_WORKSPACE = 5,    /* workspace too small or misaligned */
     DGC_ERR_UNSORTED = 6      /* decompress input has more descending runs than supported */
@@ -149,14 +149,18 @@ typedef struct dgc_select_info {
     int32_t k5_status;        /* resample replay: bit 0 (DGC_K5_FALLBACK) the multi-
                                  workgroup global phase found its workgroups not all
                                  resident and left the whole replay to one workgroup
-                                 (exact, slower); bit 1 (DGC_K5_BROKEN) a barrier of that
-                                 phase timed out after it had started: the selection of
-                                 this tensor is NOT reliable (the engines raise)       */
+                                 (exact, slower); bit 2 (DGC_K5_RECOVERED) a barrier of
+                                 that phase timed out after it had started, so the call
+                                 rebuilt the candidate queue and replayed it on one
+                                 workgroup from scratch (exact, in the same call); bit 1
+                                 (DGC_K5_BROKEN) a replay that could not be recovered:
+                                 the selection of this tensor is NOT reliable (the
+                                 engines raise) — not produced by this library version */
     float list_threshold;     /* the K1 candidate lists' threshold this call used (+inf:
                                  none); diagnostics of the speculative listing       */
 } dgc_select_info;
 
-enum { DGC_K5_FALLBACK = 1, DGC_K5_BROKEN = 2 };
+enum { DGC_K5_FALLBACK = 1, DGC_K5_BROKEN = 2, DGC_K5_RECOVERED = 4 };
 
 const char* dgc_last_error(void);
 const char* dgc_version(void);

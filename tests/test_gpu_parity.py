@@ -378,6 +378,64 @@ def test_resample_partial_sort_path_past_2_32():
     assert int(torch.count_nonzero(vec)) == pos.numel() - k and int(torch.count_nonzero(mmt)) == pos.numel() - k
 
 
+@pytest.mark.timeout(900)
+def test_resample_partial_sort_path_past_2_33():
+    """The partial_sort replay on a tensor of N = 2^33 + 2^28 elements, past the 33-bit
+    element index a heap entry can carry: entries then carry one of k slots, recycled as
+    entries replace the root, and the slot -> element index map beside them. 200k bf16-
+    rounded nonzeros (dense ties), a quarter past 2^33, k = 3,000, every nonzero a
+    candidate (>= 64k): the payload equals torch.topk's over the candidates, in order,
+    and exactly those slots of vec / mmt are zeroed (the reference takes any N:
+    dgc/compression.py:124-137)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    if free < 100 * 2 ** 30:
+        pytest.skip("needs ~100 GiB of free HBM")
+    from dgc import _lib
+    L = _lib.lib()
+    N, k, M = (1 << 33) + (1 << 28), 3000, 200_000
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(4343)
+    lo = torch.randint(0, 1 << 33, (M * 3 // 4 + 1000,), generator=gen, device=DEV).unique()[: M * 3 // 4]
+    hi = torch.randint(1 << 33, N, (M // 4 + 1000,), generator=gen, device=DEV).unique()[: M - lo.numel()]
+    pos = torch.cat([lo, hi]).sort().values
+    vals = torch.randn(pos.numel(), generator=gen, device=DEV).to(torch.bfloat16).float()
+    vals[vals == 0] = 1.0
+    vec = torch.zeros(N, device=DEV)
+    mmt = torch.zeros(N, device=DEV)
+    vec[pos] = vals
+    mmt[pos] = torch.randn(pos.numel(), generator=gen, device=DEV) + 3.0
+    p = _lib.SelectParams()
+    p.numel, p.num_selects, p.num_samples = N, k, N // 100
+    p.upper_count, p.lower_count = O.adapt_bounds(k)
+    p.upper, p.lower, p.max_iters, p.resample, p.masking = 1.3, 0.8, 10, 1, 1
+    p.vdtype, p.idtype, p.update_memory = 0, 0, 1
+    t0 = torch.tensor([float(vals.abs().min())], device=DEV)
+    out_v = torch.empty(k, device=DEV)
+    out_i = torch.empty(k, dtype=torch.int64, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=DEV)
+    wsz = L.dgc_select_workspace(N, k)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    check(L, L.dgc_select(P(vec), P(mmt), P(t0), ctypes.byref(p), P(out_v), P(out_i), P(cnt), P(info), P(ws),
+                          wsz, 0, stream()))
+    torch.cuda.synchronize()
+    inf = _lib.SelectInfo.from_buffer_copy(info.cpu().numpy().tobytes())
+    assert _lib.BRANCHES[inf.branch] == "resample" and inf.tie_rule == 1 and inf.candidates == pos.numel(), inf
+    imp = vals.abs().cpu()
+    want = pos.cpu()[torch.topk(imp, k, 0, largest=True, sorted=False)[1]]
+    assert int(cnt.item()) == k
+    assert torch.equal(out_i.cpu(), want)
+    assert int(want.max()) >= 1 << 33 and np.unique(imp.numpy()[np.isin(pos.cpu().numpy(), want.numpy())]).size < k
+    assert torch.equal(out_v.cpu().view(torch.int32), vals.cpu()[torch.searchsorted(pos.cpu(), want)].view(torch.int32))
+    assert int(torch.count_nonzero(vec[want.to(DEV)])) == 0 and int(torch.count_nonzero(mmt[want.to(DEV)])) == 0
+    assert int(torch.count_nonzero(vec)) == pos.numel() - k and int(torch.count_nonzero(mmt)) == pos.numel() - k
+    del vec, mmt, ws
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("fp16,int32,masking,update", [(True, True, True, True), (False, True, False, True),
                                                         (True, False, True, False)])
 def test_select_wire_and_memory_flags(L, fp16, int32, masking, update):

@@ -100,15 +100,14 @@ def test_batch_desc_validation_without_gpu(L):
 
 
 def test_resample_replay_width_refusals_without_gpu(L):
-    """The resample replays pack candidate positions in 32 bits (K5's queue) and element
-    indices in 33 bits (K5b's heap): a tensor past either width is refused with
-    DGC_ERR_OVERFLOW before anything runs, on every entry point — never a truncated
-    payload. resample=False takes any size."""
+    """The nth_element replay packs candidate positions in 32 bits (K5's queue): a tensor
+    past that width is refused with DGC_ERR_OVERFLOW before anything runs, on every entry
+    point — never a truncated payload. resample=False takes any size, and the
+    partial_sort replay (K5b) any N (slots past 2^33)."""
     from dgc import _lib
     OVERFLOW = 3
     # more than 2^32 - 1 candidates: n >= 2^32, k > 2^26 (a 7B bucket at a warmup ratio)
-    # ... and n >= 2^33 for the partial_sort path
-    for n, k, what in ((2 ** 32 + 4096, 2 ** 26 + 1, b"2^32 - 1 candidates"), (2 ** 33, 1000, b"below 2^33")):
+    for n, k, what in ((2 ** 32 + 4096, 2 ** 26 + 1, b"2^32 - 1 candidates"),):
         p = _lib.SelectParams()
         p.numel, p.num_selects, p.num_samples = n, k, n // 100
         p.max_iters, p.resample = 10, 1
@@ -127,12 +126,14 @@ def test_resample_replay_width_refusals_without_gpu(L):
         assert L.dgc_batch_workspace(ctypes.byref(d)) == 0 and what in L.dgc_last_error()
         d.resample = 0                                     # no replay: no limit of its own
         assert L.dgc_batch_workspace(ctypes.byref(d)) > 0
-    # the largest tensor the replays take passes the width check (and fails on the null vec after it)
-    p = _lib.SelectParams()
-    p.numel, p.num_selects, p.num_samples, p.max_iters, p.resample = 2 ** 33 - 1, 2 ** 26, 2 ** 26, 10, 1
-    out = ctypes.c_void_p(256)
-    rc = L.dgc_select(None, None, None, ctypes.byref(p), out, out, None, None, None, 0, 0, None)
-    assert rc == 1 and b"null vec" in L.dgc_last_error()
+    # past 2^33 elements (K5b's slots) and at the candidate limit the replays take the
+    # tensor: the width check passes (and the call fails on the null vec after it)
+    for n, k in ((2 ** 33 - 1, 2 ** 26), (2 ** 33, 1000), (10 ** 10, 10 ** 6)):
+        p = _lib.SelectParams()
+        p.numel, p.num_selects, p.num_samples, p.max_iters, p.resample = n, k, n // 100, 10, 1
+        out = ctypes.c_void_p(256)
+        rc = L.dgc_select(None, None, None, ctypes.byref(p), out, out, None, None, None, 0, 0, None)
+        assert rc == 1 and b"null vec" in L.dgc_last_error(), (n, k, L.dgc_last_error())
 
 
 def test_host_glue_tables_and_rebinding():
