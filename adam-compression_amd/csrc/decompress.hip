@@ -403,22 +403,58 @@ __device__ void tile_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__
 // grad holds +0.0 on entry (the reference's zero_(), done earlier); only the entries
 // are written. The work scales with the entries, not with n.
 //
-// One run (W = 1): one thread per entry. The first of a repeat sums the repeats in
+// One run (W = 1): four threads per entry. The first of a repeat sums the repeats in
 // order (index_put_ order); a descent or an index outside [0, n) sets the status.
+// An engine payload whose indices ascend (header word 1 = DGC_ORDER_ASCENDING, written
+// by the selection's finish) has each 64-B granule's entries next to each other, so
+// the first entry of a granule writes the WHOLE granule — its entries' sums, +0.0
+// around them (what grad holds there) — one 16-B quarter per thread: full-granule
+// stores instead of 4-B partial writes (1.7x the line rate at scattered lines,
+// tools/scatterbench.hip). Otherwise (the exact replays' topk order, run tables) the
+// first thread of each entry stores its word.
 template <int VD, int ID>
 __global__ void __launch_bounds__(kBlock)
 k_scatter_single(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float scale) {
     const Run run = rs.get_raw(0);   // any order: one run's unique indices need no regrouping
-    const long long j = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const bool gran = rs.payload != nullptr &&
+                      reinterpret_cast<const long long*>(rs.base_of(0))[1] == (long long)DGC_ORDER_ASCENDING;
+    const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long j = t >> 2;
+    const int part = (int)(t & 3);
     if (j >= run.count) return;
     const long long i = load_idx<ID>(run.idx, j);
     const long long ip = j > 0 ? load_idx<ID>(run.idx, j - 1) : -1;
-    if (j > 0 && ip > i) atomicOr(w.status, 2);
+    if (part == 0 && j > 0 && ip > i) atomicOr(w.status, 2);
     if (i < 0 || i >= n) {
-        atomicOr(w.status, 1);
+        if (part == 0) atomicOr(w.status, 1);
         return;
     }
-    if (j > 0 && ip == i) return;   // not the first of a repeat
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(grad), hi = reinterpret_cast<uintptr_t>(grad + n);
+    const uintptr_t g = reinterpret_cast<uintptr_t>(grad + i) & ~(uintptr_t)63;
+    if (gran && g >= lo && g + 64 <= hi) {
+        // the granule's first entry only (a predecessor in the same granule -> not first)
+        if (j > 0 && ip >= 0 && (reinterpret_cast<uintptr_t>(grad + ip) & ~(uintptr_t)63) == g) return;
+        const long long e0 = (long long)((g - lo) >> 2) + 4 * part;   // this thread's 4 elements
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        bool any[4] = {false, false, false, false};
+        for (long long f = j; f < run.count; ++f) {
+            const long long x = f == j ? i : load_idx<ID>(run.idx, f);
+            if (x < 0 || x >= n || (reinterpret_cast<uintptr_t>(grad + x) & ~(uintptr_t)63) != g) break;
+            const long long q = x - e0;
+            if (q >= 0 && q < 4) {
+                const float v = load_val<VD>(run.vals, f);
+                a[q] = any[q] ? __fadd_rn(a[q], v) : __fadd_rn(0.f, v);
+                any[q] = true;
+            }
+        }
+        if (scale != 1.0f)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (any[q]) a[q] = __fmul_rn(a[q], scale);
+        reinterpret_cast<DGC_GLB f4v*>(g)[part] = f4v{a[0], a[1], a[2], a[3]};
+        return;
+    }
+    if (part != 0 || (j > 0 && ip == i)) return;   // one word per distinct index, by its first entry
     float a = __fadd_rn(0.f, load_val<VD>(run.vals, j));
     for (long long f = j + 1; f < run.count && load_idx<ID>(run.idx, f) == i; ++f)
         a = __fadd_rn(a, load_val<VD>(run.vals, f));
@@ -721,7 +757,7 @@ static int run_scatter(const DecWS& w, const RunSrc& rs, float* grad, int64_t n,
     }
     if (runs == 1) {   // a thread per entry
         if (entries > 0) {
-            hipLaunchKernelGGL((k_scatter_single<VD, ID>), dim3((unsigned)ceil_div(entries, (int64_t)kBlock)),
+            hipLaunchKernelGGL((k_scatter_single<VD, ID>), dim3((unsigned)ceil_div(4 * entries, (int64_t)kBlock)),
                                dim3(kBlock), 0, s, w, rs, grad, n, scale);
             DGC_LAUNCHED();
         }

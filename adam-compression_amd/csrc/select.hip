@@ -1934,6 +1934,10 @@ struct FinishArgs {
     // then — so an engine that never synchronises sees it on its next step, for free.
     int32_t* sink;
     uint32_t force;   // DGC_K5_FORCE_BROKEN (tests): status bits added to every resampled tensor
+    // may be null: set to DGC_ORDER_ASCENDING when every emitted index of the call is in
+    // ascending order (no tensor took the exact replay's topk order), else 0 — the
+    // packed payload's header word 1, read by the W = 1 scatter (whole-granule stores)
+    int64_t* order_out;
 };
 
 __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
@@ -1942,10 +1946,11 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
     const float margin = f.margin;
     const int defer = f.defer, mask_mmt = f.mask_mmt;
     __shared__ unsigned long long total;
-    __shared__ uint32_t broken;
+    __shared__ uint32_t broken, topk_order;
     if (threadIdx.x == 0) {
         total = 0;
         broken = 0;
+        topk_order = 0;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < w.T; t += blockDim.x) {
@@ -1962,6 +1967,8 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
         const float prev = spec ? spec[1] : __builtin_huge_valf();
         const uint32_t k5 = status | (s.branch == DGC_BRANCH_RESAMPLE ? f.force : 0u);
         if (k5 & DGC_K5_BROKEN) atomicOr(&broken, k5);
+        // the exact replays (K5, K5b) emit torch.topk's order; every other branch ascends
+        if (s.branch == DGC_BRANCH_RESAMPLE && s.tie_rule == DGC_TIES_EXACT) atomicOr(&topk_order, 1u);
         const long long cnt = final_count(s, k);
         atomicAdd(&total, (unsigned long long)cnt);
         st->epoch = s.epoch + 1;
@@ -2012,6 +2019,7 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
     }
     __syncthreads();
     if (threadIdx.x == 0 && count_out) *count_out = (int64_t)total;
+    if (threadIdx.x == 0 && f.order_out) *f.order_out = topk_order ? 0 : (int64_t)DGC_ORDER_ASCENDING;
     if (threadIdx.x == 0 && broken && f.sink)
         __hip_atomic_store(f.sink, (int32_t)broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3062,7 +3070,7 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
 
 static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L, void* values, void* indices,
                        int64_t* count_out, dgc_select_info* info, const SelWS& w, int keep_lists, int sync_mode,
-                       float margin, int32_t* sink, hipStream_t s) {
+                       float margin, int32_t* sink, int64_t* order_out, hipStream_t s) {
     // keep_lists: a compress call, whose K3 kernels already reset every tensor's state
     // (sel_init_tensor) when they produced its threshold; a pure selection resets here
     if (!keep_lists) {
@@ -3116,7 +3124,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     // of a broken global phase (k_nth_select), without a barrier actually timing out
     const int force = std::getenv("DGC_K5_FORCE_BROKEN") ? 1 : 0;
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
-                         sink, 0u};
+                         sink, 0u, order_out};
     bool finished = false;   // the payload count and records are written
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
@@ -3276,7 +3284,7 @@ int select(float* vec, float* mmt, const float* thr0, const dgc_select_params* p
     hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
     DGC_LAUNCHED();
     return select_core(vec, mmt, cfg_of(*p), L, values, indices, count_out, info, w, 0, sync_mode, 1.f,
-                       p->status_sink, s);
+                       p->status_sink, p->order_out, s);
 }
 
 // ------------------------------------------------------------------ threshold
@@ -3419,7 +3427,7 @@ int compress_finish(float* vec, float* mmt, int64_t s_start, int64_t s_stride, i
     // DGCSGDMemory.update fused into the emit (1), or deferred into the next K1 (2)
     q.update_memory = p->update_memory == 2 ? 2 : 1;
     return select_core(vec, mmt, cfg_of(q), L, values, indices, count_out, info, w, 1, sync_mode, margin,
-                       p->status_sink, s);
+                       p->status_sink, p->order_out, s);
 }
 
 // ------------------------------------------------------------------ batch
@@ -3598,7 +3606,7 @@ int batch_compress_finish(const dgc_batch_desc* b, float* mmt, float* vec, void*
     payload_layout(cap, cfg.vdtype, cfg.idtype, &voff, &ioff);
     char* pl = static_cast<char*>(payload);
     return select_core(vec, mmt, cfg, L, pl + voff, pl + ioff, reinterpret_cast<int64_t*>(pl), info, w, 1,
-                       sync_mode, b->spec_margin, b->status_sink, s);
+                       sync_mode, b->spec_margin, b->status_sink, reinterpret_cast<int64_t*>(pl) + 1, s);
 }
 
 // The strided samples |x[start + q * stride]| of every sampled tensor from a flat fp32
@@ -3656,7 +3664,7 @@ int batch_select(const dgc_batch_desc* b, float* vec32, float* mmt32, const int6
     payload_layout(cap, cfg.vdtype, cfg.idtype, &voff, &ioff);
     char* pl = static_cast<char*>(payload);
     return select_core(vec32, mmt32, cfg, L, pl + voff, pl + ioff, reinterpret_cast<int64_t*>(pl), info, w, 1,
-                       sync_mode, b->spec_margin, b->status_sink, s);
+                       sync_mode, b->spec_margin, b->status_sink, reinterpret_cast<int64_t*>(pl) + 1, s);
 }
 
 int batch_compress(const dgc_batch_desc* b, const float* grad, float* mmt, float* vec, const int64_t* starts,

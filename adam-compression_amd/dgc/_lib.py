@@ -36,7 +36,7 @@ class SelectParams(ctypes.Structure):
                 ("max_iters", ctypes.c_int32), ("resample", ctypes.c_int32), ("masking", ctypes.c_int32),
                 ("vdtype", ctypes.c_int32), ("idtype", ctypes.c_int32), ("update_memory", ctypes.c_int32),
                 ("thr_dtype", ctypes.c_int32), ("resample_order", ctypes.c_int32),
-                ("status_sink", ctypes.c_void_p)]
+                ("status_sink", ctypes.c_void_p), ("order_out", ctypes.c_void_p)]
 
 
 class SelectInfo(ctypes.Structure):

@@ -194,6 +194,7 @@ class DGCBucket:
         """K3 threshold + K4 selection / adaptation / resample / emit + masking, into the payload."""
         L = self._L
         base = self.payload.data_ptr()
+        self.params.order_out = base + 8   # header word 1: the W = 1 scatter's ascending-order flag
         self._pending = self.params.update_memory == 2
         _lib.check(L.dgc_compress_finish(self._vec.data_ptr(), self._mmt.data_ptr(), self.start, self.stride,
                                          self.top_k_samples, ctypes.byref(self.params), self.spec.data_ptr(),

@@ -130,7 +130,18 @@ typedef struct dgc_select_params {
                               /* DGC_K5_BROKEN set) — nothing is written      */
                               /* otherwise — so a DGC_SYNC_DEVICE caller can  */
                               /* check every step without synchronising       */
+    int64_t* order_out;       /* NULL, or a device int64 the call sets to        */
+                              /* DGC_ORDER_ASCENDING when its emitted indices    */
+                              /* ascend (no exact-replay topk order), else 0 —   */
+                              /* an engine points it at its packed payload's     */
+                              /* header word 1, which the W = 1 scatter reads    */
 } dgc_select_params;
+
+/* Packed payload header word 1 of an engine payload whose indices ascend: the W = 1
+ * decompress then writes whole 64-B granules (dgc_batch_compress_finish and
+ * dgc_batch_select set it on their payload; dgc_select / dgc_compress* through
+ * dgc_select_params.order_out). */
+#define DGC_ORDER_ASCENDING 0x444E454353413147LL
 
 /* Device-resident result record written by dgc_select / dgc_compress. */
 typedef struct dgc_select_info {
