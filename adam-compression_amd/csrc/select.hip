@@ -86,10 +86,10 @@ constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgrou
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
 constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
 constexpr float kSpecMarginMax = 0.95f;
-// K5s, the set path of an untied resample (resample_order = 1; see k_resample_set)
-constexpr int kSetReg = 16;                  // one workgroup: keys per thread kept in registers (32
-                                             // spilled the radix passes' registers to scratch)
-constexpr int kSetRounds = 256;              // one workgroup up to kSetRounds x 1024 candidates
+// K5s, the set path of an untied resample (resample_order = 1; see k_resample_set):
+// up to kSetMax candidates over at most 16 workgroups of one launch, 16 rounds of 1024
+// keys each in registers (32 spilled the radix passes' registers to scratch)
+constexpr int kSetRounds = 256;
 constexpr int64_t kSetMax = (int64_t)kSetRounds * 1024;
 // One workgroup up to this many candidates, even for a tensor with a sliced-path slot:
 // routing ResNet-50's 72k-candidate sets over workgroups (DGC_SET_ONE=32768) cut
@@ -169,6 +169,19 @@ struct BigSetWS {
     long long obase;                  // the tensor's first payload slot
 };
 
+// K5s over kSetG co-resident workgroups per tensor (k_resample_set): the residency
+// consensus, the barrier, the key range and the per-pass histograms. arrive / decide /
+// bar_* / broken / mn / mx are reset by sel_init_tensor every call; hist is zero at rest
+// (the workspace is zero-filled at init; the workgroups re-zero what they used).
+constexpr int kSetG = 16;                   // workgroups per tensor
+constexpr int kSetRegC = 16;                // rounds of 1024 candidates per workgroup, in registers
+struct SetG {
+    uint32_t arrive, decide, bar_count, bar_gen, broken;
+    uint32_t mn, mx;
+    uint32_t cnt[kSetG];                    // per workgroup: its candidates >= the k-th key
+    uint32_t hist[3][kRsBins];
+};
+
 // Per-call settings shared by the tensors.
 struct SelCfg {
     float upper, lower;         // fl32(compress_upper_bound), fl32(compress_lower_bound)
@@ -209,6 +222,7 @@ struct SelWS {
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
     BigSetWS* bigset;          // [nbig] K5s over several workgroups
+    SetG* setg;                // [T] K5s over kSetG workgroups of one launch
     uint32_t* fin_ticket;      // k_nth_select's last-workgroup ticket (zeroed by sel_init_tensor)
     int64_t nseg, ngrp;
 };
@@ -380,6 +394,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.gpos = c.take<uint32_t>(L.ngpos);
     w.nthg = c.take<NthG>(L.T);
     w.bigset = c.take<BigSetWS>(L.nbig);
+    w.setg = c.take<SetG>(L.T);
     w.fin_ticket = c.take<uint32_t>(16);
     if (bytes) *bytes = c.bytes();
     return w;
@@ -757,6 +772,10 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         w.nthg[t].arrive = 0;
         w.nthg[t].decide = 0;
         w.nthg[t].status = 0;
+        SetG& sg = w.setg[t];
+        sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = 0;
+        sg.mn = 0xFFFFFFFFu;
+        sg.mx = 0;
         if (t == 0) *w.fin_ticket = 0;
     }
     __syncthreads();   // the caller's threshold (thr[t]) is written
@@ -2396,228 +2415,280 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // 179-194; dgc/memory.py:72-77). When the k-th largest candidate key is not tied
 // across the k boundary (#keys >= kth == k) every top-k is that set, whatever order
 // and tie rule produced it, so it is emitted in index order and the exact replay (K5)
-// skips the tensor (rs_nth = 3). Tied, the replay runs as always.
+// skips the tensor (rs_nth = 3). Tied, the replay runs as always. The k-th largest is
+// found by a radix select over key - min in up to three 11-bit passes (the candidates
+// of one tensor span a few octaves: relative to the minimum their top bits spread over
+// the bins instead of piling into the few bins of their exponents); the emit carries
+// the wire casts and the masking of the K5 emit.
 //
-// One 1024-thread workgroup per tensor over its K5 queue (the candidates in index
-// order, key << 32 | position): the keys in registers (kSetReg per thread, the rest
-// re-read from L2), a radix select of the k-th largest over key - min in up to three
-// 11-bit passes (the candidates of one tensor span a few octaves: relative to the
-// minimum their top bits spread over the bins instead of piling into the few bins of
-// their exponents), then an order-preserving compaction: per 1024-entry round every
-// wave's ballot count goes to LDS, one workgroup scan over the (round, wave) counts
-// gives each its base, and each selected entry is emitted at base + its rank in the
-// ballot — with the wire casts and the masking of the K5 emit.
+// Over kSetG co-resident workgroups of ONE launch (grid kSetG x T): a set of more than
+// kSetRegC x 1024 candidates is cut into kSetG contiguous
+// stretches of rounds, each workgroup's keys in its registers; the key range, the radix
+// passes' histograms and the per-stretch counts go through device atomics with a
+// barrier between the phases (min / max | pass 1 | pass 2 [| pass 3] | counts), and each
+// workgroup emits its stretch's selected entries at the count of the stretches before
+// it plus their order inside it — the index order, as one workgroup emits it. A set of
+// up to kSetRegC x 1024 candidates takes the same code on one workgroup, with no
+// barrier. The G workgroups start with a residency consensus (as K5's global phase):
+// should they not all be resident within kSetArriveTicks, the tensor is left to the
+// exact replay (k_nth_select), exact either way; so is a barrier that times out (not
+// expected after the consensus), and a tie across the k boundary as before.
+// (ResNet-50's 72k-candidate resample: one workgroup walked its keys six times, 24 of
+// 72 rounds from L2 — 59 us of the step.)
+constexpr uint64_t kSetArriveTicks = 200000;   // 2 ms of the 100 MHz wall clock
+constexpr int64_t kSetCoopMin = (int64_t)kSetRegC * kScanThreads;   // above: kSetG workgroups
 
-constexpr int kSetLds = 32;   // rounds of keys kept in LDS after the register rounds (128 KB)
+__device__ __forceinline__ bool setg_consensus(SetG* g, uint32_t G) {
+    __shared__ uint32_t verdict;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t a = __hip_atomic_fetch_add(&g->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a + 1 == G) {
+            atomicCAS(&g->decide, (uint32_t)kNthGUndecided, (uint32_t)kNthGGo);
+        } else {
+            const uint64_t t0 = wall_clock64();
+            while (__hip_atomic_load(&g->decide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kNthGUndecided) {
+                if (wall_clock64() - t0 > kSetArriveTicks) {
+                    atomicCAS(&g->decide, (uint32_t)kNthGUndecided, (uint32_t)kNthGAbort);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        verdict = __hip_atomic_load(&g->decide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return verdict == kNthGGo;
+}
 
-__device__ __forceinline__ void resample_set_wg(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o,
-                                                int64_t one) {
-    const int t = blockIdx.x;
+// Barrier among the G workgroups: everything they exchange is device atomics, read back
+// with agent-scope atomic loads (last_block_arrival's "atomics both sides"), so draining
+// this workgroup's atomics (vmcnt(0)) before the arrival is the only ordering needed.
+__device__ __forceinline__ void setg_barrier(SetG* g, uint32_t G) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t gen = __hip_atomic_load(&g->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t a = __hip_atomic_fetch_add(&g->bar_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a == G - 1) {
+            __hip_atomic_store(&g->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&g->bar_gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            bool passed = false;
+            for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+                if (__hip_atomic_load(&g->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) {
+                    passed = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!passed) __hip_atomic_store(&g->broken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one) {
+    const int t = blockIdx.y;
+    const uint32_t b = blockIdx.x;
     SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const int64_t n64 = st->n_cur;
     // the replay takes it (or, past `one` with a sliced-path slot, k_bigset_*)
-    if (n64 > (d.big >= 0 ? one : kSetMax) || d.k < 1 || n64 <= d.k) return;
+    if (n64 > (d.big >= 0 ? one : kSetMax) || n64 > (int64_t)kSetG * kSetRegC * kScanThreads || d.k < 1 ||
+        n64 <= d.k)
+        return;
+    const uint32_t G = n64 > kSetCoopMin ? (uint32_t)kSetG : 1u;
+    if (b >= G) return;
+    SetG* g = w.setg + t;
+    if (G > 1 && !setg_consensus(g, G)) return;   // not all resident: the replay
     SET_STAMP(0);
     const int n = (int)n64;
     const uint32_t k = (uint32_t)d.k;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int kWaves = kScanThreads / kWave;
-    constexpr int kReg = kSetReg + kSetLds;   // rounds held on chip
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t lds32[16];
     __shared__ uint32_t red[2][kWaves];
-    __shared__ uint32_t prefix, k_rem, sel_above, sel_cnt;
+    __shared__ uint32_t rbase[kSetRegC * kWaves];
+    __shared__ uint32_t sel_above, sel_cnt, s_mn, s_mx, s_base, s_stop;
     __shared__ int sel_bin;
-    __shared__ uint32_t rbase[kSetRounds * kWaves];
     __shared__ long long obase_s;
-    __shared__ uint32_t kl[kSetLds * kScanThreads];   // rounds kSetReg .. kReg - 1
-    // queue entry i = tid + r * 1024 (coalesced high-word loads); its key
-    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
-    auto key_at = [&](int i) -> uint32_t { return i < n ? qk[i] : 0u; };
+    // this workgroup's stretch of rounds; queue entry i = tid + r * 1024 (coalesced)
     const int rounds = (n + kScanThreads - 1) / kScanThreads;
-    uint32_t key[kSetReg];
+    const int per = (rounds + (int)G - 1) / (int)G;
+    const int r0 = (int)b * per, r1 = min(r0 + per, rounds);
+    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
+    uint32_t key[kSetRegC];
 #pragma unroll
-    for (int r = 0; r < kSetReg; ++r) key[r] = key_at(tid + r * kScanThreads);
-    // the LDS rounds: 8 loads in flight per thread
-    for (int r0 = kSetReg; r0 < kReg && r0 < rounds; r0 += 8) {
-        uint32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = r0 + u < rounds ? key_at(tid + (r0 + u) * kScanThreads) : 0u;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) kl[(r0 + u - kSetReg) * kScanThreads + tid] = v[u];
+    for (int r = 0; r < kSetRegC; ++r) {
+        const int i = tid + (r0 + r) * kScanThreads;
+        key[r] = r0 + r < r1 && i < n ? qk[i] : 0u;
     }
-    // every key of this thread with its round (uniform loop bounds): registers, LDS, then
-    // L2 in batches of 8 loads in flight (n > 64K only)
-    auto for_keys = [&](auto fn) {
-#pragma unroll
-        for (int r = 0; r < kSetReg; ++r) fn(r, key[r]);
-        for (int r = kSetReg; r < kReg && r < rounds; ++r) fn(r, kl[(r - kSetReg) * kScanThreads + tid]);
-        for (int r0 = kReg; r0 < rounds; r0 += 8) {
-            uint32_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = r0 + u < rounds ? key_at(tid + (r0 + u) * kScanThreads) : 0u;
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (r0 + u < rounds) fn(r0 + u, v[u]);
-        }
-    };
-    SET_STAMP(1);
+    auto valid = [&](int r) { return r0 + r < r1 && tid + (r0 + r) * kScanThreads < n; };
+    // the key range over every stretch
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
-    for_keys([&](int r, uint32_t x) {
-        if (tid + r * kScanThreads < n) {
-            mn = x < mn ? x : mn;
-            mx = x > mx ? x : mx;
+#pragma unroll
+    for (int r = 0; r < kSetRegC; ++r)
+        if (valid(r)) {
+            mn = key[r] < mn ? key[r] : mn;
+            mx = key[r] > mx ? key[r] : mx;
         }
-    });
     mn = wave_min_u32(mn);
     mx = wave_max(mx);
     if (lane == 0) {
         red[0][wv] = mn;
         red[1][wv] = mx;
     }
-    for (int b = tid; b < kRsBins; b += kScanThreads) h[b] = 0;
+    for (int q = tid; q < kRsBins; q += kScanThreads) h[q] = 0;
+    __syncthreads();
     if (tid == 0) {
-        prefix = 0;
-        k_rem = k;
+        uint32_t a = red[0][0], c = red[1][0];
+#pragma unroll
+        for (int i = 1; i < kWaves; ++i) {
+            a = red[0][i] < a ? red[0][i] : a;
+            c = red[1][i] > c ? red[1][i] : c;
+        }
+        if (G > 1) {
+            if (a != 0xFFFFFFFFu) __hip_atomic_fetch_min(&g->mn, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_max(&g->mx, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            s_mn = a;
+            s_mx = c;
+        }
+    }
+    if (G > 1) {
+        setg_barrier(g, G);
+        if (tid == 0) {
+            s_mn = __hip_atomic_load(&g->mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_mx = __hip_atomic_load(&g->mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __syncthreads();
-    mn = red[0][0];
-    mx = red[1][0];
-#pragma unroll
-    for (int i = 1; i < kWaves; ++i) {
-        mn = red[0][i] < mn ? red[0][i] : mn;
-        mx = red[1][i] > mx ? red[1][i] : mx;
-    }
-    SET_STAMP(2);
-    // passes over the bits of key - mn, 11 at a time from the top
+    mn = s_mn;
+    mx = s_mx;
+    SET_STAMP(1);
+    // passes over the bits of key - mn, 11 at a time from the top (every workgroup picks
+    // the same bin from the same merged histogram)
     const uint32_t span = mx - mn;
     const int L = span ? 32 - __builtin_clz(span) : 0;
-    int hi = L;   // bits above hi: matched by prefix (of key - mn)
-    bool found = L == 0;   // every key equal: the k-th largest is mn
+    int hi = L, pass = 0;
+    uint32_t prefix = 0, k_rem = k;
     uint32_t kth = mn, eq = (uint32_t)n;
-    while (!found) {
+    bool ok = true;
+    while (hi > 0) {
         const int lo = hi > 11 ? hi - 11 : 0;
-        const uint32_t pre = prefix;
-        for_keys([&](int r, uint32_t x) {
-            const uint32_t v = x - mn;
-            if (tid + r * kScanThreads < n && (hi >= 32 || (v >> hi) == pre))
+#pragma unroll
+        for (int r = 0; r < kSetRegC; ++r) {
+            const uint32_t v = key[r] - mn;
+            if (valid(r) && (hi >= 32 || (v >> hi) == prefix))
                 atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
-        });
+        }
         __syncthreads();
-        if (hi == L) SET_STAMP(7);   // (profiling build: the first pass's histogram done)
+        if (G > 1) {
+            uint32_t* gh = g->hist[pass];
+            for (int q = tid; q < kRsBins; q += kScanThreads)
+                if (h[q]) __hip_atomic_fetch_add(&gh[q], h[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            setg_barrier(g, G);
+            for (int q = tid; q < kRsBins; q += kScanThreads)
+                h[q] = __hip_atomic_load(&gh[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+        }
         if (tid == 0) sel_bin = -1;
+        __syncthreads();
         int bin;
         uint32_t above;
-        const bool hit = pick_bin_small<2>(h, k_rem, lds32, &bin, &above);
-        if (hit) {
+        if (pick_bin_small<2>(h, k_rem, lds32, &bin, &above)) {
             sel_bin = bin;
             sel_above = above;
             sel_cnt = h[bin];
         }
         __syncthreads();
-        if (sel_bin < 0) return;   // (cannot happen: k < n keys) — the replay takes it
-        const uint32_t b = (uint32_t)sel_bin, a = sel_above, c = sel_cnt;
+        const int sb = sel_bin;
+        const uint32_t a = sel_above, c = sel_cnt;
         __syncthreads();   // every thread has read sel_*
-        if (tid == 0) {
-            prefix = (pre << (hi - lo)) | b;
-            k_rem -= a;
-        }
         for (int q = tid; q < kRsBins; q += kScanThreads) h[q] = 0;
-        __syncthreads();
+        ++pass;
+        if (sb < 0) {   // (cannot happen: k < n keys) — the replay takes it
+            ok = false;
+            break;
+        }
+        prefix = (prefix << (hi - lo)) | (uint32_t)sb;
+        k_rem -= a;
         hi = lo;
         if (lo == 0) {
-            found = true;
             kth = mn + prefix;
             eq = c;
         }
     }
     // tied across the boundary (more keys == kth than the k - #(> kth) still needed):
     // only torch's exact order of operations knows which ones — the replay
-    SET_STAMP(3);
-    if (eq != k_rem) return;
-    // order-preserving compaction: (round, wave) counts, one scan, ranks from ballots
-    for_keys([&](int r, uint32_t x) {   // uniform in r
-        const uint32_t c = (uint32_t)__popcll(__ballot(tid + r * kScanThreads < n && x >= kth));
+    if (eq != k_rem) ok = false;
+    SET_STAMP(2);
+    // order-preserving compaction: (round, wave) ballot counts, one workgroup scan, the
+    // stretches before this one (their counts through the last barrier)
+    uint32_t mine = 0;
+#pragma unroll
+    for (int r = 0; r < kSetRegC; ++r) {
+        const uint32_t c = ok ? (uint32_t)__popcll(__ballot(valid(r) && key[r] >= kth)) : 0u;
         if (lane == 0) rbase[r * kWaves + wv] = c;
-    });
-    if (wv == 0) {
-        const long long b = out_base(w, t);
-        if (lane == 0) obase_s = b;
+        mine += c;
     }
     __syncthreads();
     {
-        constexpr int kPerT = kSetRounds * kWaves / kScanThreads;   // 4 (round, wave) counts per thread
-        uint32_t c[kPerT], sum = 0;
-#pragma unroll
-        for (int j = 0; j < kPerT; ++j) {
-            c[j] = kPerT * tid + j < rounds * kWaves ? rbase[kPerT * tid + j] : 0u;
-            sum += c[j];
-        }
+        const uint32_t c = tid < kSetRegC * kWaves ? rbase[tid] : 0u;
         uint32_t total;
-        uint32_t run = block_exclusive_scan32(sum, lds32, &total);
-#pragma unroll
-        for (int j = 0; j < kPerT; ++j) {
-            if (kPerT * tid + j < rounds * kWaves) rbase[kPerT * tid + j] = run;
-            run += c[j];
+        const uint32_t run = block_exclusive_scan32(c, lds32, &total);
+        if (tid < kSetRegC * kWaves) rbase[tid] = run;
+        if (tid == 0) {
+            s_base = 0;
+            s_stop = ok ? 0u : 1u;
+            if (G > 1) __hip_atomic_store(&g->cnt[b], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    __syncthreads();
-    // the selected queue positions in output order into the tensor's pair-slot region
-    // (free on this path): plain stores, no load waits on them; then the emit reads them
-    // back with every slot's loads independent (a per-round emit waited for the index
-    // and value gathers of each round in turn: two dependent round trips per 1024 keys)
-    SET_STAMP(4);
-    // (into the LDS rounds' area past the rounds it holds, when k positions fit there)
-    DGC_GLB uint32_t* spos = glb(w.gpos + d.gpos_off);
-    const int64_t lds_used = (int64_t)(rounds > kSetReg ? rounds - kSetReg : 0) * kScanThreads;
-    const bool in_lds = rounds <= kSetReg + kSetLds && lds_used + (int64_t)k <= (int64_t)kSetLds * kScanThreads;
-    uint32_t* lpos = kl + (kSetLds * kScanThreads - k);   // (used only when in_lds)
-    for_keys([&](int r, uint32_t x) {   // uniform in r
-        const bool sel = tid + r * kScanThreads < n && x >= kth;
-        const uint64_t m = __ballot(sel);
-        if (sel) {
-            const uint32_t q = rbase[r * kWaves + wv] + mbcnt64(m, 0u), i = (uint32_t)(tid + r * kScanThreads);
-            if (in_lds)
-                lpos[q] = i;
-            else
-                spos[q] = i;
+    (void)mine;
+    if (G > 1) {
+        setg_barrier(g, G);
+        if (tid == 0) {
+            uint32_t base = 0;
+            for (uint32_t i = 0; i < b; ++i)
+                base += __hip_atomic_load(&g->cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_base = base;
+            if (__hip_atomic_load(&g->broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) s_stop = 1;
         }
-    });
-    if (!in_lds) __threadfence_block();
+        // every workgroup has read the histograms: re-zero this one's share of those used
+        for (int p = 0; p < pass; ++p)
+            for (int q = (int)b * (kRsBins / kSetG) + tid; q < ((int)b + 1) * (kRsBins / kSetG); q += kScanThreads)
+                g->hist[p][q] = 0;
+    }
+    if (wv == 0) {
+        const long long ob = out_base(w, t);
+        if (lane == 0) obase_s = ob;
+    }
     __syncthreads();
-    SET_STAMP(5);
-    const long long ob = obase_s;
-    // the index and the value of a slot are independent loads (the gather kept the value)
+    if (s_stop) return;   // uniform: a tie or a broken barrier — the replay takes the tensor
+    SET_STAMP(3);
+    const long long ob = obase_s + (long long)s_base;
     const int64_t* cand = w.cand_idx + d.cand_off;
     const float* cval = w.cand_val + d.cand_off;
-    for (uint32_t q0 = 0; q0 < k; q0 += 4 * kScanThreads) {
-        int64_t li[4];
-        float x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t q = q0 + u * kScanThreads + tid;
-            const uint32_t i = q < k ? (in_lds ? lpos[q] : spos[q]) : 0u;
-            li[u] = q < k ? cand[i] : 0;
-            x[u] = q < k ? cval[i] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t q = q0 + u * kScanThreads + tid;
-            if (q < k) emit_one(o, d, ob + q, li[u], x[u]);
+    for (int r = 0; r < kSetRegC; ++r) {
+        const bool sel = valid(r) && key[r] >= kth;
+        const uint64_t m = __ballot(sel);
+        if (sel) {
+            const int i = tid + (r0 + r) * kScanThreads;
+            emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(m, 0u), cand[i], cval[i]);
         }
     }
-    if (tid == 0) {
+    if (b == 0 && tid == 0) {
         st->rs_nth = 3;   // K5's replay and emit skip the tensor
         st->tie_rule = DGC_TIES_SET;
     }
-    SET_STAMP(6);
-}
-
-__global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one) {
-    resample_set_wg(vec_flat, w, o, one);
+    SET_STAMP(4);
 }
 
 // ---------------------------------------------------------------- K5s over several workgroups
@@ -3136,7 +3207,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         g.ckey = w.cand_key;
         DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
-            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o, set_one());
+            hipLaunchKernelGGL(k_resample_set, dim3(kSetG, (unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o,
+                               set_one());
             DGC_LAUNCHED();
             if (L.nbig > 0) {   // candidate counts above one workgroup's: sliced over workgroups
                 BigList bl{};
@@ -3510,6 +3582,7 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
     SelWS w = carve_select(ws, L);
     DGC_HIP(hipMemsetAsync(w.st, 0, sizeof(SelState) * L.T, s));
     if (L.nbig) DGC_HIP(hipMemsetAsync(w.bigset, 0, sizeof(BigSetWS) * L.nbig, s));   // zero at rest
+    DGC_HIP(hipMemsetAsync(w.setg, 0, sizeof(SetG) * L.T, s));                         // zero at rest
     DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
     for (int which = 0; which < BT_COUNT; ++which)
         DGC_HIP(hipMemcpyAsync(w.bt[which], bt[which].data(), sizeof(int32_t) * (L.T + 1), hipMemcpyHostToDevice, s));
