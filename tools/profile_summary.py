@@ -81,23 +81,36 @@ def main():
                     prev = e
                 f.write(f"step span {(int(tr[i1]['Start_Timestamp']) - int(tr[i0]['Start_Timestamp'])) / 1e6:.3f} ms\n")
     if pmc and os.path.isdir(pmc):
+        # per kernel and counter, the values in dispatch order; the first `warm` launches
+        # of each kernel are dropped as kstats drops them (the warmup steps: first touch
+        # of the buffers, full passes before the lists exist), so the bytes per launch and
+        # the timed duration per launch describe the same launches
         agg = collections.defaultdict(lambda: collections.defaultdict(list))
         for fn in glob.glob(f"{pmc}/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(fn)):
-                agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                key = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+                agg[r["Kernel_Name"]][r["Counter_Name"]].append((key, float(r["Counter_Value"])))
         res = {}
         for k, cs in agg.items():
             if "dgc::" not in k:
                 continue
-            avg = {c: sum(v) / len(v) for c, v in cs.items()}
+            timed = {c: [v for _, v in sorted(vals)][warm:] or [v for _, v in sorted(vals)] for c, vals in cs.items()}
+            avg = {c: sum(v) / len(v) for c, v in timed.items()}
             f_kb, w_kb = avg.get("FETCH_SIZE"), avg.get("WRITE_SIZE")
             fb = f_kb * 1024 if f_kb is not None else 0
             wb = w_kb * 1024 if w_kb is not None else 0
             stream = any(s in k for s in STREAMING)
-            res[k[:120]] = {"launches": max(len(v) for v in cs.values()), "FETCH_SIZE_KB_avg": f_kb,
+            hb = (2 * fb + wb) if stream else None
+            t_ms = ks.get(k[:120], {}).get("timed_avg_ms")
+            res[k[:120]] = {"launches": max(len(v) for v in cs.values()),
+                            "timed_launches": max(len(v) for v in timed.values()), "FETCH_SIZE_KB_avg": f_kb,
                             "WRITE_SIZE_KB_avg": w_kb, "calibrated": stream,
-                            "hbm_bytes_per_launch": (2 * fb + wb) if stream else None,
-                            "hbm_bytes_per_launch_range": None if stream else [fb + wb, 2 * fb + wb]}
+                            "hbm_bytes_per_launch": hb,
+                            "hbm_bytes_per_launch_range": None if stream else [fb + wb, 2 * fb + wb],
+                            # the implied rate over the same (timed) launches; above the 8 TB/s
+                            # peak it says the bytes or the time are not the same launches'
+                            "implied_GBs": (round((hb if hb is not None else fb + wb) / (t_ms * 1e6), 1)
+                                            if t_ms else None)}
         with open(f"{out}/pmc_{wl}.json", "w") as f:
             json.dump({"command": command, "kernels": res}, f, indent=1)
     if bench:
