@@ -642,14 +642,26 @@ static int mask_flush(float* vec, float* mmt, const Layout& L, const SelWS& w, h
 // float4 index = 256*seg + 64*u + lane (u = 0..3), each instruction 1 KB contiguous;
 // non-temporal loads and stores. seg_lcnt = exact count at t_list; a segment that
 // holds an unpadded scalar tail is marked spilled (re-read when needed).
-template <bool NEST>
+// ONE (a one-tensor call): the tensor's tables ride in the arguments (ot) — block 0
+// writes them into the workspace for the kernels after K1, which replaces a k_put_one
+// launch before every K1 (and its wait) — and the sample start in sc.
+template <bool NEST, bool ONE>
 __global__ void __launch_bounds__(kBlock)
 k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat, float* __restrict__ vec_flat,
-                  float mom, SelWS w, StartChunk sc, int wt) {
-    const int t = task(w, BT_K1, blockIdx.x);
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+                  float mom, SelWS w, StartChunk sc, int wt, OneTable ot) {
+    const int t = ONE ? 0 : task(w, BT_K1, blockIdx.x);
+    const TDesc d = ONE ? ot.d : w.td[t];   // by value: stores below cannot alias it
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_K1][t]) * kSegPerBlock4 + wave;   // local segment
+    const int64_t b0 = ONE ? 0 : w.bt[BT_K1][t];   // the tensor's first block
+    const int64_t ls = ((int64_t)blockIdx.x - b0) * kSegPerBlock4 + wave;   // local segment
+    if (ONE && blockIdx.x == 0 && threadIdx.x == 0) {
+        w.td[0] = ot.d;
+        for (int which = 0; which < BT_COUNT; ++which) {
+            w.bt[which][0] = ot.bt[which][0];
+            w.bt[which][1] = ot.bt[which][1];
+        }
+        w.small[0] = 0;
+    }
     // sample starts (and gradient pointers) of the first sc.count tensors ride in the arguments
     const bool arg_start = t < sc.count;
     const float* gsrc = !sc.ptrs ? g_flat + d.off : (arg_start ? sc.grad[t] : w.gptr[t]);
@@ -659,11 +671,11 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     const int64_t n4 = d.nv4, n = d.n;
     const float tl = w.spec ? w.spec[kSpecWords * t] : __builtin_huge_valf();
     SelState* st = w.st + t;
-    if (blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) st->t_list = tl;
+    if (blockIdx.x == b0 && threadIdx.x == 0) st->t_list = tl;
     const bool sample = d.samp_off >= 0;
     const int64_t start = !sample ? 0 : (arg_start ? sc.start[t] : w.starts[t]);
     const int64_t scount = !sample ? 0 : (arg_start ? ceil_div(d.n - start, d.stride) : w.scnt[t]);
-    if (arg_start && blockIdx.x == w.bt[BT_K1][t] && threadIdx.x == 0) {
+    if (arg_start && blockIdx.x == b0 && threadIdx.x == 0) {
         w.starts[t] = sc.start[t];
         w.scnt[t] = sample ? scount : d.n;
     }
@@ -3440,14 +3452,14 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
     SelWS w;
     OneTable ot{};
     DGC_TRY(one_ws(p, s_start, s_stride, 1, spec, ws, ws_bytes, L, w, ot));
-    hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
-    DGC_LAUNCHED();
     const int64_t n = p->numel;
     const bool sampled = n != p->num_samples;
     const int64_t cnt = sampled ? ceil_div(n - s_start, s_stride) : 0;
     const bool list_path = aligned16(grad) && aligned16(mmt) && aligned16(vec) &&
                            (!sampled || (s_stride >= 4 && s_stride < (1LL << 30)));
     if (!list_path) {
+        hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
+        DGC_LAUNCHED();
         DGC_TRY(mask_flush(vec, mmt, L, w, s));   // a deferring finish left its masking to K1
         DGC_TRY(compensate(grad, mmt, vec, nullptr, n, momentum, nesterov, true, sampled ? w.samples : nullptr,
                            s_start, s_stride, cnt, s));
@@ -3457,13 +3469,18 @@ int compress_begin(const float* grad, float* mmt, float* vec, float momentum, bo
     }
     if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_compress: n too large");
     if (L.grid[BT_K1] > 0) {
-        const StartChunk none{};   // k_put_one wrote the start
+        StartChunk one{};   // the start (and the tables, ot) in the arguments: no k_put_one
+        one.count = 1;
+        one.start[0] = ot.start;
         if (nesterov)
-            hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
-                               vec, momentum, w, none, (int)write_through(n));
+            hipLaunchKernelGGL((k_compensate_list<true, true>), dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s,
+                               grad, mmt, vec, momentum, w, one, (int)write_through(n), ot);
         else
-            hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad,
-                               mmt, vec, momentum, w, none, (int)write_through(n));
+            hipLaunchKernelGGL((k_compensate_list<false, true>), dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s,
+                               grad, mmt, vec, momentum, w, one, (int)write_through(n), ot);
+        DGC_LAUNCHED();
+    } else {
+        hipLaunchKernelGGL(k_put_one, dim3(1), dim3(64), 0, s, w, ot);
         DGC_LAUNCHED();
     }
     if (n & 3) {   // scalar tail (< 4 elements) incl. its samples; its segment is marked spilled
@@ -3654,11 +3671,11 @@ int batch_compress_begin(const dgc_batch_desc* b, const float* grad, const float
     }
     if (L.grid[BT_K1] > 0x7FFFFFFFLL) DGC_FAIL(DGC_ERR_INVALID, "dgc_batch_compress: too many segments");
     if (b->nesterov)
-        hipLaunchKernelGGL(k_compensate_list<true>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt, vec,
-                           b->momentum, w, arg, (int)write_through(L.nseg * kSeg));
+        hipLaunchKernelGGL((k_compensate_list<true, false>), dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad,
+                           mmt, vec, b->momentum, w, arg, (int)write_through(L.nseg * kSeg), OneTable{});
     else
-        hipLaunchKernelGGL(k_compensate_list<false>, dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad, mmt,
-                           vec, b->momentum, w, arg, (int)write_through(L.nseg * kSeg));
+        hipLaunchKernelGGL((k_compensate_list<false, false>), dim3((unsigned)L.grid[BT_K1]), dim3(kBlock), 0, s, grad,
+                           mmt, vec, b->momentum, w, arg, (int)write_through(L.nseg * kSeg), OneTable{});
     DGC_LAUNCHED();
     return DGC_OK;
 }
