@@ -403,6 +403,108 @@ __device__ __forceinline__ void rs_small_wg(const float* __restrict__ x, int64_t
     __syncthreads();
 }
 
+// The k-th largest |x| of a K1 sample WINDOW (select.hip: every sample with key >= the
+// window threshold, ks..kWinMax of them) in ONE 1024-thread workgroup, PER keys per
+// thread in registers. The window's keys all sit within a few octaves above its
+// threshold — the few bins of their exponents, where a fixed-digit pass 0 serialises
+// ~n LDS atomics on a handful of addresses (76 us at 83k keys) and the maxima floor of
+// rs_small_wg does not apply (k above the thread count) — so the digits are taken from
+// key - min instead, 12 bits at a time from the top of the span (4096 bins: two passes
+// for a span below 2^24 key units), as the resample set path does. NaN anywhere: NaN.
+constexpr int kWinPer = 64;
+constexpr int kWinMax = kWinPer * kScanThreads;   // 65536 keys
+__device__ __forceinline__ void rs_window_wg(const float* __restrict__ x, int64_t n, uint64_t k64, float* out) {
+    constexpr int kBins = 4096;
+    __shared__ uint32_t h[kBins];
+    __shared__ uint32_t lds32[16];
+    __shared__ uint32_t red[3][kScanThreads / kWave];
+    __shared__ uint32_t sel_above;
+    __shared__ int sel_bin;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nn = (int)n;   // <= kWinMax
+    const uint32_t k = (uint32_t)k64;
+    // element 4 * (tid + j4 * 1024) + e -> key[4 * j4 + e] (16-B loads; the window is 16-B aligned)
+    uint32_t key[kWinPer];
+#pragma unroll
+    for (int j4 = 0; j4 < kWinPer / 4; ++j4) {
+        const int i = 4 * (tid + j4 * kScanThreads);
+        if (i + 3 < nn) {
+            const float4 f = reinterpret_cast<const float4*>(x)[i / 4];
+            key[4 * j4] = abs_key(f.x);
+            key[4 * j4 + 1] = abs_key(f.y);
+            key[4 * j4 + 2] = abs_key(f.z);
+            key[4 * j4 + 3] = abs_key(f.w);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) key[4 * j4 + e] = i + e < nn ? abs_key(x[i + e]) : 0u;
+        }
+    }
+    auto in = [&](int j) { return 4 * (tid + (j / 4) * kScanThreads) + (j & 3) < nn; };
+    uint32_t mn = 0xFFFFFFFFu, mx = 0, nan = 0;
+#pragma unroll
+    for (int j = 0; j < kWinPer; ++j)
+        if (in(j)) {
+            nan |= key[j] > 0x7F800000u ? 1u : 0u;
+            mn = key[j] < mn ? key[j] : mn;
+            mx = key[j] > mx ? key[j] : mx;
+        }
+    mn = wave_min_u32(mn);
+    mx = wave_max(mx);
+    nan = wave_max(nan);
+    if (lane == 0) {
+        red[0][wv] = mn;
+        red[1][wv] = mx;
+        red[2][wv] = nan;
+    }
+    for (int b = tid; b < kBins; b += kScanThreads) h[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kScanThreads / kWave; ++i) {
+        mn = red[0][i] < mn ? red[0][i] : mn;
+        mx = red[1][i] > mx ? red[1][i] : mx;
+        nan |= red[2][i];
+    }
+    if (nan || k == 0 || k > (uint32_t)nn) {   // uniform
+        if (tid == 0) *out = __uint_as_float(0x7FC00000u);
+        __syncthreads();
+        return;
+    }
+    const uint32_t span = mx - mn;
+    int hi = span ? 32 - __builtin_clz(span) : 0;
+    uint32_t prefix = 0, k_rem = k;
+    while (hi > 0) {
+        const int lo = hi > 12 ? hi - 12 : 0;
+#pragma unroll
+        for (int j = 0; j < kWinPer; ++j) {
+            const uint32_t v = key[j] - mn;
+            if (in(j) && (hi >= 32 || (v >> hi) == prefix)) atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
+        }
+        if (tid == 0) sel_bin = -1;
+        __syncthreads();
+        int bin;
+        uint32_t above;
+        if (pick_bin_small<4>(h, k_rem, lds32, &bin, &above)) {
+            sel_bin = bin;
+            sel_above = above;
+        }
+        __syncthreads();
+        const int sb = sel_bin;
+        const uint32_t a = sel_above;
+        __syncthreads();   // every thread has read sel_*
+        for (int b = tid; b < kBins; b += kScanThreads) h[b] = 0;
+        if (sb < 0) {   // (cannot happen: k <= n)
+            if (tid == 0) *out = __uint_as_float(0x7FC00000u);
+            __syncthreads();
+            return;
+        }
+        prefix = (prefix << (hi - lo)) | (uint32_t)sb;
+        k_rem -= a;
+        hi = lo;
+    }
+    if (tid == 0) *out = __uint_as_float(mn + prefix);
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(kScanThreads)
 k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
     rs_small_wg(x, n, k, out);

@@ -680,9 +680,12 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
         w.scnt[t] = sample ? scount : d.n;
     }
     float* sout = sample ? w.samples + d.samp_off : nullptr;
-    // the sample window list: every sample with key >= key(t_list) (inf and NaN too)
+    // the sample window list: every sample with key >= the window threshold spec[2] (a
+    // prediction of this call's sampled threshold, just below it; the list threshold
+    // before the first prediction), inf and NaN too
     float* win = w.samples + d.win_off;
-    const uint32_t win_key = abs_key(tl);
+    const float tw = w.spec ? w.spec[kSpecWords * t + 2] : __builtin_huge_valf();
+    const uint32_t win_key = abs_key(tw < __builtin_huge_valf() ? tw : tl);
     const bool windowed = sample && d.win_cap > 0;
     uint32_t* win_cnt = &st->win_cnt[st->epoch & 1];
     // waves past the tensor's last segment load nothing and list nothing, but stay for
@@ -1039,13 +1042,13 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const 
     if ((int32_t)blockIdx.x >= nsmall) {
         const SelState* st = w.st + t;
         const uint32_t cnt = st->win_cnt[st->epoch & 1];
-        const bool take = cnt >= ks && cnt <= (uint64_t)d.win_cap && cnt <= (uint32_t)kSmallN;
+        const bool take = cnt >= ks && cnt <= (uint64_t)d.win_cap && cnt <= (uint32_t)kWinMax;
         if (threadIdx.x == 0) {
             w.rs[t].small_done = take ? 1u : 0u;
             w.rs[t].win_n = take ? cnt : 0u;   // the record's window_keys (sel_init_tensor)
         }
         if (!take) return;   // uniform
-        rs_small_wg(w.samples + d.win_off, cnt, ks, w.thr + t);
+        rs_window_wg(w.samples + d.win_off, cnt, ks, w.thr + t);
         sel_init_tensor(w, t, 1);
         return;
     }
@@ -2046,6 +2049,21 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
                 m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
             spec[0] = finite ? tc * m * gr : __builtin_huge_valf();
             spec[1] = finite ? tc : __builtin_huge_valf();
+            // spec[2]: next call's sample-window threshold = mw x t0 x growth0, growth0 =
+            //   2 - spec[3] / t0 clamped to [1, 1.5] (the sampled threshold's own linear
+            //   extrapolation), spec[3] := t0. The window must hold >= ks samples and, for
+            //   the one-workgroup select (rs_window_wg), <= kWinMax: mw = 0.97 after a window
+            //   of that size, 0.985 after a larger one, 0.9 after one that missed (fewer than
+            //   ks samples above it: this call's threshold came from the passes over every
+            //   sample). The list threshold's margin (~0.95) put 8 ks samples in the window
+            //   at 1B, past one workgroup's registers.
+            const float t0 = s.t0;
+            const bool f0 = t0 == t0 && t0 > 0.f && t0 < __builtin_huge_valf();
+            const float g0 = fminf(fmaxf(2.f - spec[3] / t0, 1.f), 1.5f);
+            const uint32_t wc = s.win_cnt[s.epoch & 1];   // this call's window, taken or not
+            const float mw = wc > (uint32_t)kWinMax ? 0.985f : (s.win_keys > 0 ? 0.97f : 0.9f);
+            spec[2] = f0 ? t0 * mw * g0 : __builtin_huge_valf();
+            spec[3] = f0 ? t0 : __builtin_huge_valf();
         }
     }
     __syncthreads();
