@@ -11,6 +11,8 @@ replayed tensor down that path (its queue first overwritten with garbage): DGCBu
 DGCBatch and DistributedOptimizer(batch=True) must produce exactly the healthy run's
 outputs and state, in the same step, with no raise.
 """
+import random
+
 import pytest
 import torch
 
@@ -124,6 +126,7 @@ def test_batched_optimizer_recovers_broken_replay(monkeypatch):
         else:
             monkeypatch.delenv("DGC_K5_FORCE_BROKEN", raising=False)
         torch.manual_seed(0)
+        random.seed(0)   # the sample starts: the reference's Python-global random.randint draws
         model = torch.nn.Linear(2000, 1000).to(DEV)
         comp = DGCCompressor(0.01, memory=DGCSGDMemory(momentum=0.9))
         comp.memory.initialize(model.named_parameters())
