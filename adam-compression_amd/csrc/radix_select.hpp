@@ -505,6 +505,102 @@ __device__ __forceinline__ void rs_window_wg(const float* __restrict__ x, int64_
     __syncthreads();
 }
 
+// K1 also histograms the window as it appends to it (select.hip k_compensate_list): one
+// agent atomic per windowed sample (~3 ks of the S samples) into kWinBins bins of
+// 2^kWinShift key units above the window key — bins 0 .. kWinBins - 3 span a factor
+// of ~1.4 in |x| —, the keys past that range in bin kWinBins - 2 and NaN in the last.
+constexpr int kWinBins = 4096;
+constexpr int kWinShift = 10;
+constexpr int kWinBinCap = 4096;   // keys of the k-th key's bin gathered on chip
+__device__ __forceinline__ uint32_t win_bin(uint32_t key, uint32_t wk) {
+    if (key > 0x7F800000u) return kWinBins - 1;   // NaN
+    const uint32_t b = (key - wk) >> kWinShift;   // key >= wk: a windowed sample
+    return b < (uint32_t)(kWinBins - 2) ? b : (uint32_t)(kWinBins - 2);
+}
+
+// The k-th largest key of a COMPLETE window (all cnt of its keys in x) from K1's
+// histogram gh, in one workgroup, re-zeroing gh for the next call: the bin of the k-th
+// key from a scan of the 4096 counts (no pass over the keys), then that bin's keys —
+// one read of the window, ~100 of them at 1B — in one exact 1024-bin pass over their
+// low kWinShift bits. Returns false, *out untouched, when the k-th key lies past the
+// binned range or its bin holds more than kWinBinCap keys (rs_window_wg or the passes
+// then take the window); NaN in the window: NaN, as rs_window_wg.
+__device__ __forceinline__ bool rs_window_hist_wg(const float* __restrict__ x, uint32_t cnt,
+                                                  uint32_t* __restrict__ gh, uint32_t wk, uint32_t k,
+                                                  float* out) {
+    __shared__ uint32_t h[kWinBins];
+    __shared__ uint32_t buf[kWinBinCap];
+    __shared__ uint32_t lds32[16];
+    __shared__ uint32_t sel_above, nbuf;
+    __shared__ int sel_bin;
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int q = tid; q < kWinBins; q += kScanThreads) {
+        h[q] = gh[q];
+        gh[q] = 0;
+    }
+    if (tid == 0) {
+        sel_bin = -1;
+        nbuf = 0;
+    }
+    __syncthreads();
+    if (h[kWinBins - 1]) {   // uniform: a NaN sample
+        if (tid == 0) *out = __uint_as_float(0x7FC00000u);
+        __syncthreads();
+        return true;
+    }
+    int bin;
+    uint32_t above;
+    if (pick_bin_small<kWinBins / kScanThreads>(h, k, lds32, &bin, &above)) {
+        sel_bin = bin;
+        sel_above = above;
+    }
+    __syncthreads();
+    const int b = sel_bin;
+    const uint32_t a = sel_above;
+    if (b < 0 || b >= kWinBins - 2 || h[b] > (uint32_t)kWinBinCap) return false;   // uniform
+    const uint32_t want = h[b];
+    const uint32_t lo = wk + ((uint32_t)b << kWinShift);
+    // the bin's keys (their low bits) into LDS: one wave-aggregated append per 64 keys
+    for (int64_t i0 = 4 * (int64_t)tid; i0 < (int64_t)cnt; i0 += 4 * kScanThreads) {
+        float v[4];
+        if (i0 + 3 < (int64_t)cnt) {
+            const float4 f = *reinterpret_cast<const float4*>(x + i0);   // the window is 16-B aligned
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = i0 + e < (int64_t)cnt ? x[i0 + e] : -1.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t d = __float_as_uint(v[e]) - lo;   // v < 0 (padding): huge
+            const bool in = v[e] >= 0.f && d < (1u << kWinShift);
+            const uint64_t m = __ballot(in);
+            if (!m) continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&nbuf, (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+            if (in && pos < (uint32_t)kWinBinCap) buf[pos] = d;
+        }
+    }
+    __syncthreads();
+    const uint32_t nb = nbuf;
+    if (nb != want) return false;   // (cannot happen for a complete window) uniform
+    for (int q = tid; q < (1 << kWinShift); q += kScanThreads) h[q] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < nb; i += kScanThreads) atomicAdd(&h[buf[i]], 1u);
+    if (tid == 0) sel_bin = -1;
+    __syncthreads();
+    static_assert((1 << kWinShift) == kScanThreads, "one sub-bin per thread");
+    if (pick_bin_small<1>(h, k - a, lds32, &bin, &above)) sel_bin = bin;
+    __syncthreads();
+    const int sb = sel_bin;
+    if (tid == 0 && sb >= 0) *out = __uint_as_float(lo + (uint32_t)sb);
+    __syncthreads();
+    return sb >= 0;
+}
+
 __global__ void __launch_bounds__(kScanThreads)
 k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
     rs_small_wg(x, n, k, out);

@@ -85,7 +85,11 @@ constexpr int kSpillDiv = 32;                   // lists dropped when > nseg/32 
 constexpr int kQueuePerBlock = kBlock;          // K5 emit: outputs per workgroup
 constexpr int kCapBlocks = 2048;                // grid-stride launches: blocks per whole bucket (one tensor)
 constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of several tensors
-constexpr float kSpecMarginMax = 0.95f;
+// The adaptive list margin's ceiling (k_sel_finish, spec[4]): kSpecCeil0 at first, up by
+// kSpecCeilUp after every hit to kSpecMarginMax, down by kSpecCeilDown after a miss.
+constexpr float kSpecCeil0 = 0.95f;
+constexpr float kSpecMarginMax = 0.985f;
+constexpr float kSpecCeilUp = 0.005f, kSpecCeilDown = 0.05f;
 // K5s, the set path of an untied resample (resample_order = 1; see k_resample_set):
 // up to kSetMax candidates over at most 16 workgroups of one launch, 16 rounds of 1024
 // keys each in registers (32 spilled the radix passes' registers to scratch)
@@ -100,8 +104,8 @@ constexpr int kBigSlice = 8192;              // above: slices of this many candi
 constexpr int kBigSlices = 1024;             //   up to this many slices (8M candidates)
 constexpr int kBigMax = 64;                  //   for up to this many tensors of a call
 constexpr int kBigBuf = 65536;               //   keys of the k-th key's coarse bin gathered
-constexpr int kBigShift = 12;                //   coarse bins of 4096 key units above t_cur         // the adaptive list margin's ceiling (k_sel_finish)
-constexpr int kSpecWords = 4;                   // per-tensor speculation state (dgc_compress_begin: spec)
+constexpr int kBigShift = 12;                //   coarse bins of 4096 key units above t_cur
+constexpr int kSpecWords = 8;                   // per-tensor speculation state (dgc_compress_begin: spec)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
@@ -116,6 +120,7 @@ struct TDesc {
     int64_t upper_count, lower_count;  // floor(k * upper), ceil(lower * k)
     int64_t samp_off;       // offset of its samples in the flat sample buffer; -1: none / N == S
     int64_t win_off, win_cap;          // its K1 sample window list in the sample buffer (cap 0: none)
+    int64_t whist_off;                 // K1's histogram of that window (kWinBins u32, zero at rest)
     int64_t cand_off, cand_cap;        // K5 queue region: min(N, 64k - 1) candidates
     int64_t gpos_off;       // K5 pair slots: 2 x (cand_cap / 2 + 1)
     int64_t idx_base;       // added to the emitted indices (its flat offset in a batch, 0 alone)
@@ -141,6 +146,7 @@ struct SelState {
     int32_t def_mode, def_mask_mmt;
     float def_t;
     int32_t win_keys;      // keys K3 read from the K1 sample window list (0: the samples)
+    uint32_t win_key;      // the window's key (K1's block 0): its histogram's bin 0
     long long def_limit;
     uint32_t tickets[4];
     uint32_t tk8[9];       // sharded arrival of the count passes (last_block_arrival8)
@@ -319,6 +325,8 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.win_cap = (d.samp_off >= 0 && d.S + 1 > kSmallN) ? std::min<int64_t>(d.S + 1, (d.S + 1) / 16 + 4096) : 0;
         d.win_off = samp;
         samp += (int64_t)align_up((size_t)d.win_cap, 64);
+        d.whist_off = samp;
+        if (d.win_cap > 0) samp += kWinBins;
         d.cand_off = cand;
         d.cand_cap = nth_cand_cap(d.n, d.k);
         cand += d.cand_cap;
@@ -688,6 +696,8 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
     const uint32_t win_key = abs_key(tw < __builtin_huge_valf() ? tw : tl);
     const bool windowed = sample && d.win_cap > 0;
     uint32_t* win_cnt = &st->win_cnt[st->epoch & 1];
+    uint32_t* whist = reinterpret_cast<uint32_t*>(w.samples + d.whist_off);
+    if (windowed && blockIdx.x == b0 && threadIdx.x == 0) st->win_key = win_key;
     // waves past the tensor's last segment load nothing and list nothing, but stay for
     // the block barrier of the spill count
     int64_t q0 = 0, r0 = 0;
@@ -749,6 +759,7 @@ k_compensate_list(const float* __restrict__ g_flat, float* __restrict__ mmt_flat
             base = __shfl(base, leader);
             const uint32_t pos = base + (uint32_t)__popcll(hb & ((1ull << lane) - 1));
             if (hit && pos < (uint64_t)d.win_cap) win[pos] = hv;
+            if (hit) atomicAdd(&whist[win_bin(__float_as_uint(hv), win_key)], 1u);   // (no return value)
         }
         list_append(ge_mask(x, valid, tl), x, u * 256, c, lo, lv, seg, ntile);
         mk = max(mk, tile_max_key(x, valid));
@@ -1035,20 +1046,33 @@ __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w, int64_t ks
 // the ks-th largest of its window (SampleKeys); for VGG-16-BN's big tensors ~3 ks keys,
 // where the passes were four launches. A window that does not qualify is left to them.
 __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const float* vec_flat, int64_t ks1,
-                                                                 int32_t nsmall) {
+                                                                 int32_t nsmall, int32_t use_hist) {
     const int t = w.small[blockIdx.x];
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const uint64_t ks = (uint64_t)ks_of(d, t, ks1);
     if ((int32_t)blockIdx.x >= nsmall) {
         const SelState* st = w.st + t;
         const uint32_t cnt = st->win_cnt[st->epoch & 1];
-        const bool take = cnt >= ks && cnt <= (uint64_t)d.win_cap && cnt <= (uint32_t)kWinMax;
+        const bool complete = cnt >= ks && cnt <= (uint64_t)d.win_cap;
+        uint32_t* gh = reinterpret_cast<uint32_t*>(w.samples + d.whist_off);
+        bool take = false;
+        if (complete) {   // K1's histogram of the window first (it re-zeroes it), then its keys
+            if (use_hist)
+                take = rs_window_hist_wg(w.samples + d.win_off, cnt, gh, st->win_key, (uint32_t)ks, w.thr + t);
+            else
+                for (int q = threadIdx.x; q < kWinBins; q += kScanThreads) gh[q] = 0;
+            if (!take && cnt <= (uint32_t)kWinMax) {
+                rs_window_wg(w.samples + d.win_off, cnt, ks, w.thr + t);
+                take = true;
+            }
+        } else {
+            for (int q = threadIdx.x; q < kWinBins; q += kScanThreads) gh[q] = 0;   // zero at rest
+        }
         if (threadIdx.x == 0) {
             w.rs[t].small_done = take ? 1u : 0u;
             w.rs[t].win_n = take ? cnt : 0u;   // the record's window_keys (sel_init_tensor)
         }
         if (!take) return;   // uniform
-        rs_window_wg(w.samples + d.win_off, cnt, ks, w.thr + t);
         sel_init_tensor(w, t, 1);
         return;
     }
@@ -1972,9 +1996,10 @@ struct FinishArgs {
     // ascending order (no tensor took the exact replay's topk order), else 0 — the
     // packed payload's header word 1, read by the W = 1 scatter (whole-granule stores)
     int64_t* order_out;
+    float margin_max;   // the adaptive list margin's ceiling (kSpecMarginMax; DGC_SPEC_MARGIN_MAX for A/B runs)
 };
 
-__device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
+__device__ __forceinline__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
     int64_t* count_out = f.count_out;
     dgc_select_info* info = f.info;
     const float margin = f.margin;
@@ -1991,8 +2016,27 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
         // every load first, by value (a store through st, info or spec could alias a
         // later load: interleaved they were one dependent memory round trip each, 6.5 us
         // for ResNet-50's 54 tensors), then the stores
+        // (the fields it uses, one by one: a copy of the whole state indexed by the epoch
+        // gave the finish a 1.2 KB/lane scratch frame — k_nth_select 13 -> 22 us at 1B)
         SelState* st = w.st + t;
-        const SelState s = *st;
+        struct {
+            float t0, t_cur;
+            int32_t branch, recounts, overflow, full_passes, list_spills, epoch, tie_rule, win_keys;
+            long long n_cur, limit;
+        } s;
+        s.t0 = st->t0;
+        s.t_cur = st->t_cur;
+        s.branch = st->branch;
+        s.recounts = st->recounts;
+        s.overflow = st->overflow;
+        s.full_passes = st->full_passes;
+        s.list_spills = st->list_spills;
+        s.epoch = st->epoch;
+        s.tie_rule = st->tie_rule;
+        s.win_keys = st->win_keys;
+        s.n_cur = st->n_cur;
+        s.limit = st->limit;
+        const uint32_t wc = st->win_cnt[s.epoch & 1];   // this call's window, taken or not
         const int64_t k = w.td[t].k;
         const bool tail = w.td[t].tail;
         const uint32_t status = w.nthg[t].status;
@@ -2003,7 +2047,7 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
         if (k5 & DGC_K5_BROKEN) atomicOr(&broken, k5);
         // the exact replays (K5, K5b) emit torch.topk's order; every other branch ascends
         if (s.branch == DGC_BRANCH_RESAMPLE && s.tie_rule == DGC_TIES_EXACT) atomicOr(&topk_order, 1u);
-        const long long cnt = final_count(s, k);
+        const long long cnt = s.branch == DGC_BRANCH_RESAMPLE ? (long long)k : s.limit;   // final_count
         atomicAdd(&total, (unsigned long long)cnt);
         st->epoch = s.epoch + 1;
         // what the next K1 must zero (first-k branches of a deferring engine only)
@@ -2033,10 +2077,11 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             //   decelerates (the accumulating velocity's threshold grows ~linearly). The
             //   margin m adapts: after a call whose threshold landed at or above its list
             //   threshold (a hit), m = 1.05 x that call's list/final ratio, within [margin,
-            //   kSpecMarginMax] — the lists shrink towards the selection while the threshold
-            //   moves predictably (at 1B on the bench's dynamics 4 % of the elements at 0.8
-            //   vs 0.7 % at 0.95); a miss (the threshold fell below it: a full select pass
-            //   ran) resets m to margin. A prediction from the SAMPLED threshold series, with
+            //   spec[4]] — the lists shrink towards the selection while the threshold moves
+            //   predictably (at 1B on the bench's dynamics 4 % of the elements at 0.8 vs
+            //   0.7 % at 0.95; ceiling 0.985: flat-1B's step 0.204 -> 0.179 ms past K1, same
+            //   box); a miss (the threshold fell below it: a full select pass ran) resets m
+            //   to margin and lowers the ceiling spec[4]. A prediction from the SAMPLED threshold series, with
             //   the lower of the last two final/sampled ratios (lists that hold a lowered
             //   threshold's candidates), was measured and dropped: on ResNet-50 its longer
             //   lists cost the list counts and the lowering 23 + 14 + 25 us where these take
@@ -2044,9 +2089,18 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             const float tc = s.t_cur;
             const bool finite = tc == tc && tc > 0.f && tc < __builtin_huge_valf();
             const float gr = fminf(fmaxf(2.f - prev / tc, 1.f), 1.5f);   // first call: 2 - inf -> 1
+            // the ceiling learns how closely t follows its prediction: it climbs while the
+            // lists hold t (a hit) and steps down after a miss — a threshold that jitters
+            // keeps its lists wider, a steady one (the bench's) narrows them to ~1.5 %
+            const float c0 = spec[4] < __builtin_huge_valf() ? spec[4] : fmaxf(margin, kSpecCeil0);
+            const bool tried = used < __builtin_huge_valf() && tc > 0.f;
+            const bool hit = tried && tc >= used;
+            const float mcap = !tried ? c0
+                                : hit ? fminf(c0 + kSpecCeilUp, fmaxf(margin, f.margin_max))
+                                      : fmaxf(c0 - kSpecCeilDown, margin);
             float m = margin;
-            if (used < __builtin_huge_valf() && tc >= used && tc > 0.f)
-                m = fminf(fmaxf(1.05f * (used / tc), margin), fmaxf(margin, kSpecMarginMax));
+            if (hit) m = fminf(fmaxf(1.05f * (used / tc), margin), mcap);
+            spec[4] = mcap;
             spec[0] = finite ? tc * m * gr : __builtin_huge_valf();
             spec[1] = finite ? tc : __builtin_huge_valf();
             // spec[2]: next call's sample-window threshold = mw x t0 x growth0, growth0 =
@@ -2060,7 +2114,6 @@ __device__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
             const float t0 = s.t0;
             const bool f0 = t0 == t0 && t0 > 0.f && t0 < __builtin_huge_valf();
             const float g0 = fminf(fmaxf(2.f - spec[3] / t0, 1.f), 1.5f);
-            const uint32_t wc = s.win_cnt[s.epoch & 1];   // this call's window, taken or not
             const float mw = wc > (uint32_t)kWinMax ? 0.985f : (s.win_keys > 0 ? 0.97f : 0.9f);
             spec[2] = f0 ? t0 * mw * g0 : __builtin_huge_valf();
             spec[3] = f0 ? t0 : __builtin_huge_valf();
@@ -3224,8 +3277,12 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     // DGC_K5_FORCE_BROKEN=1 (parity tests only): every replayed tensor takes the recovery
     // of a broken global phase (k_nth_select), without a barrier actually timing out
     const int force = std::getenv("DGC_K5_FORCE_BROKEN") ? 1 : 0;
+    static const float margin_max = [] {
+        const char* e = std::getenv("DGC_SPEC_MARGIN_MAX");
+        return e ? std::strtof(e, nullptr) : kSpecMarginMax;
+    }();
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
-                         sink, 0u, order_out};
+                         sink, 0u, order_out, margin_max};
     bool finished = false;   // the payload count and records are written
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
@@ -3413,8 +3470,10 @@ int kth_largest(const float* x, int64_t n, int64_t k, float* out, void* ws, size
 // three multi-block passes.
 static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStream_t s, int64_t ks1 = 0) {
     if (L.nsmall + L.nwins) {
+        // DGC_NO_WIN_HIST=1 (A/B runs): the window's keys only, not K1's histogram of them
+        static const int use_hist = std::getenv("DGC_NO_WIN_HIST") ? 0 : 1;
         hipLaunchKernelGGL(k_rs_small_multi, dim3((unsigned)(L.nsmall + L.nwins)), dim3(kScanThreads), 0, s, w, vec,
-                           ks1, L.nsmall);
+                           ks1, L.nsmall, use_hist);
         DGC_LAUNCHED();
     }
     if (L.grid[BT_SAMP] > 0) {
@@ -3618,6 +3677,7 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
     DGC_HIP(hipMemsetAsync(w.st, 0, sizeof(SelState) * L.T, s));
     if (L.nbig) DGC_HIP(hipMemsetAsync(w.bigset, 0, sizeof(BigSetWS) * L.nbig, s));   // zero at rest
     DGC_HIP(hipMemsetAsync(w.setg, 0, sizeof(SetG) * L.T, s));                         // zero at rest
+    DGC_HIP(hipMemsetAsync(w.samples, 0, sizeof(float) * L.nsamp, s));   // the window histograms: zero at rest
     DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
     for (int which = 0; which < BT_COUNT; ++which)
         DGC_HIP(hipMemcpyAsync(w.bt[which], bt[which].data(), sizeof(int32_t) * (L.T + 1), hipMemcpyHostToDevice, s));

@@ -111,7 +111,7 @@ class DGCBucket:
         # zero-filled: per-tensor state (deferred masking, spill and window counts) lives in it
         self.ws = torch.zeros(L.dgc_compress_workspace(N, self.k, self.num_samples), dtype=torch.uint8,
                               device=dev)
-        self.spec = torch.full((4,), float("inf"), dtype=torch.float32, device=dev)
+        self.spec = torch.full((8,), float("inf"), dtype=torch.float32, device=dev)
         self.info = torch.zeros(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
         self.rank_stride, self.voff, self.ioff = _layout(self.k, self.vdtype, self.idtype)
         if fill not in ("auto", "inline", "allgather", "sparse"):

@@ -298,7 +298,7 @@ class DGCCompressor:
                 ws = self._ws.get(dev, wsz, name)
                 spec = self._spec.get(name)
                 if spec is None or spec.device != dev:
-                    spec = self._spec[name] = torch.full((4,), float("inf"), dtype=torch.float32, device=dev)
+                    spec = self._spec[name] = torch.full((8,), float("inf"), dtype=torch.float32, device=dev)
                 info = torch.empty(_lib.INFO_BYTES, dtype=torch.uint8, device=dev)
                 base = payload.data_ptr()
                 voff, ioff = lay[4], lay[5]

@@ -216,16 +216,20 @@ int dgc_select(float* vec, float* mmt, const float* thr0, const dgc_select_param
 
 /* ---- fused compress: compensate + sample + threshold + select ----
  * Speculative listing: K1 also lists every element with |vec_new| >= spec_threshold[0]
- * into the selection workspace. spec_threshold is a device float[4], in/out, per
- * tensor (NULL = off); initialise all four to +inf. When the sampled threshold comes out
+ * into the selection workspace. spec_threshold is a device float[8], in/out, per
+ * tensor (NULL = off); initialise all eight to +inf. When the sampled threshold comes out
  * >= spec[0] and few segment lists overflowed, every count and selection is served
  * from the lists and the separate re-read of vec is skipped; otherwise one full pass
  * runs. Results are identical either way (spec only chooses the work).
  * On return spec[1] = the final threshold t and spec[0] = m x t x growth, growth =
  * 2 - (previous t) / t (linear extrapolation) clamped to [1, 1.5]; m = spec_margin (0.8
  * is a good one) after a call whose t fell below its list threshold, else 1.05 x (list
- * threshold / t) of that call, within [spec_margin, 0.95]: the lists shrink while t
- * moves predictably. spec[2..3] are reserved.
+ * threshold / t) of that call, within [spec_margin, spec[4]]: the lists shrink while t
+ * moves predictably. spec[4], the ceiling, starts at 0.95 and moves within
+ * [spec_margin, 0.985]: +0.005 after every call whose t held at or above its list
+ * threshold, -0.05 after one that fell below it. spec[2..3] predict the sampled
+ * threshold for K1's sample window (spec[2] = the window threshold, spec[3] = the last
+ * sampled threshold); spec[5..7] are reserved.
  * dgc_compress = dgc_compress_begin (K1) + dgc_compress_finish (K3, K4), which share
  * one workspace and must see the same sample_start/stride/params. The workspace
  * carries per-tensor state from call to call (a deferred masking, the K1 list-spill
