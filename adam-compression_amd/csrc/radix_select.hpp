@@ -560,30 +560,40 @@ __device__ __forceinline__ bool rs_window_hist_wg(const float* __restrict__ x, u
     if (b < 0 || b >= kWinBins - 2 || h[b] > (uint32_t)kWinBinCap) return false;   // uniform
     const uint32_t want = h[b];
     const uint32_t lo = wk + ((uint32_t)b << kWinShift);
-    // the bin's keys (their low bits) into LDS: one wave-aggregated append per 64 keys
-    for (int64_t i0 = 4 * (int64_t)tid; i0 < (int64_t)cnt; i0 += 4 * kScanThreads) {
-        float v[4];
-        if (i0 + 3 < (int64_t)cnt) {
-            const float4 f = *reinterpret_cast<const float4*>(x + i0);   // the window is 16-B aligned
-            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-        } else {
+    // the bin's keys (their low bits) into LDS: one wave-aggregated append per 64 keys;
+    // kWinBatch 16-B loads per thread in flight before any is used (one at a time, the
+    // walk over 36k keys was ~9 dependent round trips: K3 16 us at 1B)
+    constexpr int kWinBatch = 8;
+    const int64_t n4 = cnt / 4;
+    const float4* x4 = reinterpret_cast<const float4*>(x);   // the window is 16-B aligned
+    auto take = [&](float v) {
+        const uint32_t d = __float_as_uint(v) - lo;   // v < 0 (padding): huge
+        const bool in = v >= 0.f && d < (1u << kWinShift);
+        const uint64_t m = __ballot(in);
+        if (!m) return;
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&nbuf, (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        if (in && pos < (uint32_t)kWinBinCap) buf[pos] = d;
+    };
+    for (int64_t jb = 0; jb < n4; jb += kWinBatch * kScanThreads) {   // (the same trip count everywhere)
+        float4 f[kWinBatch];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = i0 + e < (int64_t)cnt ? x[i0 + e] : -1.f;
+        for (int u = 0; u < kWinBatch; ++u) {
+            const int64_t j = jb + tid + (int64_t)u * kScanThreads;
+            f[u] = j < n4 ? x4[j] : make_float4(-1.f, -1.f, -1.f, -1.f);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t d = __float_as_uint(v[e]) - lo;   // v < 0 (padding): huge
-            const bool in = v[e] >= 0.f && d < (1u << kWinShift);
-            const uint64_t m = __ballot(in);
-            if (!m) continue;
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&nbuf, (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
-            const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-            if (in && pos < (uint32_t)kWinBinCap) buf[pos] = d;
+        for (int u = 0; u < kWinBatch; ++u) {
+            take(f[u].x);
+            take(f[u].y);
+            take(f[u].z);
+            take(f[u].w);
         }
     }
+    if (tid < (int)(cnt & 3u)) take(x[4 * n4 + tid]);   // (wave 0 only: its ballot is its own)
     __syncthreads();
     const uint32_t nb = nbuf;
     if (nb != want) return false;   // (cannot happen for a complete window) uniform

@@ -254,6 +254,7 @@ struct Layout {
     int64_t max_cand = 0;       // the largest K5 candidate capacity of a tensor
     int32_t nsmall = 0;
     int32_t nwins = 0;          // tensors with a K1 sample window (their ids follow the small ones)
+    int32_t nplain = 0;         // multi-block threshold tasks without a window (k_rs_reset_samples)
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool tail_any = false;      // some tensor is compensated partly outside K1 (unpadded tail)
     int64_t grid[BT_COUNT] = {};
@@ -347,6 +348,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         seg_end = std::max(seg_end, d.seg0 + d.nseg);
         const int64_t scnt = sampled ? d.S + 1 : d.n;
         if (scnt <= kSmallN) small.push_back(t);
+        else if (!(d.win_cap > 0 && !d.tail)) ++L.nplain;
     }
     L.nseg = seg_end;
     L.ngrp = grp;
@@ -1027,15 +1029,8 @@ __global__ void __launch_bounds__(kBlock) k_rs_reset_samples(SelWS w, int64_t ks
     const int t = blockIdx.x;
     if (w.bt[BT_SAMP][t + 1] == w.bt[BT_SAMP][t]) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    if (d.win_cap > 0 && !d.tail && w.rs[t].small_done) return;   // k_rs_small_multi selected its window
-    const int64_t ks = ks_of(d, t, ks1);
-    RSState* rs = w.rs + t;
-    rs_reset(rs, (uint64_t)ks);
-    if (threadIdx.x == 0 && d.samp_off >= 0 && d.win_cap > 0 && !d.tail) {
-        const SelState* st = w.st + t;
-        const uint32_t cnt = st->win_cnt[st->epoch & 1];
-        if (cnt >= (uint64_t)ks && cnt <= (uint64_t)d.win_cap) rs->win_n = cnt;
-    }
+    if (d.win_cap > 0 && !d.tail) return;   // windowed: k_rs_small_multi reset it (or selected its window)
+    rs_reset(w.rs + t, (uint64_t)ks_of(d, t, ks1));
 }
 
 // One workgroup per small tensor: all three passes from LDS, then the tensor's
@@ -1068,11 +1063,19 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const 
         } else {
             for (int q = threadIdx.x; q < kWinBins; q += kScanThreads) gh[q] = 0;   // zero at rest
         }
-        if (threadIdx.x == 0) {
-            w.rs[t].small_done = take ? 1u : 0u;
-            w.rs[t].win_n = take ? cnt : 0u;   // the record's window_keys (sel_init_tensor)
+        if (!take) {   // the multi-block passes take the task: its reset (their k, and the
+            // window's keys instead of the samples when the window is complete)
+            rs_reset(w.rs + t, ks);
+            if (threadIdx.x == 0) {
+                w.rs[t].small_done = 0u;
+                w.rs[t].win_n = complete ? cnt : 0u;
+            }
+            return;
         }
-        if (!take) return;   // uniform
+        if (threadIdx.x == 0) {
+            w.rs[t].small_done = 1u;
+            w.rs[t].win_n = cnt;   // the record's window_keys (sel_init_tensor)
+        }
         sel_init_tensor(w, t, 1);
         return;
     }
@@ -3477,8 +3480,10 @@ static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStre
         DGC_LAUNCHED();
     }
     if (L.grid[BT_SAMP] > 0) {
-        hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w, ks1);
-        DGC_LAUNCHED();
+        if (L.nplain) {   // (a windowed task's reset is k_rs_small_multi's)
+            hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w, ks1);
+            DGC_LAUNCHED();
+        }
         DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
     }
     return DGC_OK;
