@@ -181,10 +181,10 @@ __device__ __forceinline__ void rs_reset(RSState* st, uint64_t k) {
 __global__ void k_rs_init(RSState* st, uint64_t k) { rs_reset(st, k); }
 
 template <class Src>
-__global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
-    const int t = src.task(blockIdx.x);
+__device__ __forceinline__ void rs_hist_body(const Src& src, int pass, int bx) {
+    const int t = src.task(bx);
     if (!src.active(t)) return;   // uniform per workgroup
-    if ((int)blockIdx.x - src.first_block(t) >= src.blocks(t)) return;   // not a participant of the task
+    if (bx - src.first_block(t) >= src.blocks(t)) return;   // not a participant of the task
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t nan_cnt;
     __shared__ uint64_t lds16[16];
@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
     const uint32_t pmask = rs_pmask(pass), dmask = rs_dmask(pass);
     const int shift = rs_shift(pass);
     const int b0 = src.first_block(t), nb = src.blocks(t);
-    src.visit(t, (int64_t)blockIdx.x - b0, nb, [&](uint32_t key) {
+    src.visit(t, (int64_t)bx - b0, nb, [&](uint32_t key) {
         if ((key & pmask) == prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
         if (pass == 0 && key > 0x7F800000u) atomicAdd(&nan_cnt, 1u);
     });
@@ -614,6 +614,53 @@ __device__ __forceinline__ bool rs_window_hist_wg(const float* __restrict__ x, u
 __global__ void __launch_bounds__(kScanThreads)
 k_rs_small(const float* __restrict__ x, int64_t n, uint64_t k, float* out) {
     rs_small_wg(x, n, k, out);
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
+    rs_hist_body(src, pass, (int)blockIdx.x);
+}
+
+// The three passes in ONE launch (a source with chain words, src.chain(): 8 words, zero
+// at rest): when no task is active — every window was selected in one workgroup, the
+// steady state — every workgroup returns at once (three gated launches were ~15 us of a
+// flat-1B step). Otherwise the passes run in order over virtual blocks claimed from an
+// atomic counter, a workgroup waiting for a pass's completion count (one agent-scope
+// release per workgroup and pass, an acquire before the next); only running workgroups
+// claim blocks, so nothing assumes the grid co-resident. The last workgroup out
+// re-zeroes the words.
+template <class Src>
+__global__ void __launch_bounds__(kBlock) k_rs_passes(Src src, int grid, int ntasks) {
+    __shared__ uint32_t s_u;
+    bool mine_any = false;   // a task with blocks that the one-workgroup selections left to the passes
+    for (int t = threadIdx.x; t < ntasks; t += blockDim.x) mine_any |= src.blocks(t) > 0 && src.active(t);
+    if (!__syncthreads_or(mine_any)) return;   // uniform; no task turns active during the call
+    uint32_t* cc = src.chain();   // [0..2] claims, [3..5] completions, [6] workgroups out
+    for (int pass = 0; pass < 3; ++pass) {
+        uint32_t mine = 0;
+        for (;;) {
+            __syncthreads();
+            if (threadIdx.x == 0) s_u = atomicAdd(&cc[pass], 1u);
+            __syncthreads();
+            const uint32_t vb = s_u;
+            if (vb >= (uint32_t)grid) break;   // uniform
+            rs_hist_body(src, pass, (int)vb);
+            ++mine;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (mine) __hip_atomic_fetch_add(&cc[3 + pass], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (__hip_atomic_load(&cc[3 + pass], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)grid)
+                __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&cc[6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
+        for (int i = 0; i < 7; ++i) __hip_atomic_store(&cc[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The three histogram passes over any task source; every active task's state must

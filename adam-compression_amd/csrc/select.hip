@@ -90,21 +90,17 @@ constexpr int kCapBlocksBatch = 16384;          // ... per whole batch of severa
 constexpr float kSpecCeil0 = 0.95f;
 constexpr float kSpecMarginMax = 0.985f;
 constexpr float kSpecCeilUp = 0.005f, kSpecCeilDown = 0.05f;
-// K5s, the set path of an untied resample (resample_order = 1; see k_resample_set):
-// up to kSetMax candidates over at most 16 workgroups of one launch, 16 rounds of 1024
-// keys each in registers (32 spilled the radix passes' registers to scratch)
-constexpr int kSetRounds = 256;
-constexpr int64_t kSetMax = (int64_t)kSetRounds * 1024;
-// One workgroup up to this many candidates, even for a tensor with a sliced-path slot:
-// routing ResNet-50's 72k-candidate sets over workgroups (DGC_SET_ONE=32768) cut
-// k_resample_set 63 -> 20 us but cost 61 us in the four k_bigset_* launches (same box,
-// step 0.286 -> 0.309 ms)
-constexpr int64_t kSetOne = kSetMax;
-constexpr int kBigSlice = 8192;              // above: slices of this many candidates per workgroup
-constexpr int kBigSlices = 1024;             //   up to this many slices (8M candidates)
-constexpr int kBigMax = 64;                  //   for up to this many tensors of a call
-constexpr int kBigBuf = 65536;               //   keys of the k-th key's coarse bin gathered
-constexpr int kBigShift = 12;                //   coarse bins of 4096 key units above t_cur
+// K5s, the set path of an untied resample (resample_order = 1; see k_resample_set): one
+// launch, kSetG workgroups per tensor, kSetRegC rounds of 1024 keys per workgroup in
+// registers (32 spilled the radix passes' registers to scratch) — kSetMax candidates;
+// a tensor whose capacity exceeds that (VGG-16-BN's fc6: 6.5M) gets up to kSetGBig
+// workgroups (for up to kBigMax such tensors per call), kSetRoundsMax rounds each.
+constexpr int kSetG = 16;
+constexpr int kSetGBig = 128;
+constexpr int kSetRegC = 16;
+constexpr int kSetRoundsMax = 64;
+constexpr int64_t kSetMax = (int64_t)kSetG * kSetRegC * 1024;
+constexpr int kBigMax = 64;
 constexpr int kSpecWords = 8;                   // per-tensor speculation state (dgc_compress_begin: spec)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
 
@@ -128,7 +124,7 @@ struct TDesc {
     double inv_stride;
     float inv_stride_f;
     int32_t tail;           // the elements [4*nv4, n) are compensated outside K1 (unpadded)
-    int32_t big;            // its K5s multi-workgroup set state (BigSetWS index), -1: none
+    int32_t big;            // its K5s extra workgroups (SetMap index), -1: none
 };
 
 struct SelState {
@@ -163,28 +159,14 @@ struct SelState {
     unsigned long long lower_cnt[kMaxLower + 1];   // counts at t_1..t_m (multi-threshold pass)
 };
 
-// K5s over several workgroups (k_bigset_*): one per tensor with d.big >= 0. Zero at
-// rest where noted (the workspace is zero-filled at init).
-struct BigSetWS {
-    uint32_t hist[kRsBins];           // coarse histogram (zero at rest: k_bigset_select re-zeroes it)
-    uint32_t slice_cnt[kBigSlices];   // per slice: keys above the k-th key's coarse bin, then its payload base
-    uint32_t bufn;                    // keys gathered from that bin (reset by k_bigset_hist)
-    int32_t ok;                       // the set path runs (1) or leaves the tensor to the replay (0)
-    uint32_t b0, a0;                  // the coarse bin and the keys above it
-    uint32_t kth;                     // the k-th largest key
-    long long obase;                  // the tensor's first payload slot
-};
-
-// K5s over kSetG co-resident workgroups per tensor (k_resample_set): the residency
-// consensus, the barrier, the key range and the per-pass histograms. arrive / decide /
-// bar_* / broken / mn / mx are reset by sel_init_tensor every call; hist is zero at rest
-// (the workspace is zero-filled at init; the workgroups re-zero what they used).
-constexpr int kSetG = 16;                   // workgroups per tensor
-constexpr int kSetRegC = 16;                // rounds of 1024 candidates per workgroup, in registers
+// K5s over co-resident workgroups per tensor (k_resample_set): the residency consensus,
+// the barrier, the key range and the per-pass histograms. arrive / decide / bar_* /
+// broken / mn / mx are reset by sel_init_tensor every call; hist is zero at rest (the
+// workspace is zero-filled at init; the workgroups re-zero what they used).
 struct SetG {
     uint32_t arrive, decide, bar_count, bar_gen, broken;
     uint32_t mn, mx;
-    uint32_t cnt[kSetG];                    // per workgroup: its candidates >= the k-th key
+    uint32_t cnt[kSetGBig];                 // per workgroup: its candidates >= the k-th key
     uint32_t hist[3][kRsBins];
 };
 
@@ -227,9 +209,9 @@ struct SelWS {
     uint32_t* cand_key;        // K5: their |x| keys, dense (the set paths read 4 B per candidate, not 8)
     uint32_t* gpos;            // K5: pair slots of the global-memory partition passes
     NthG* nthg;                // [T] K5: the multi-workgroup global phase's state
-    BigSetWS* bigset;          // [nbig] K5s over several workgroups
     SetG* setg;                // [T] K5s over kSetG workgroups of one launch
     uint32_t* fin_ticket;      // k_nth_select's last-workgroup ticket (zeroed by sel_init_tensor)
+    uint32_t* chain;           // k_chain_one's claim / completion / gate words (zeroed by sel_init_tensor)
     int64_t nseg, ngrp;
 };
 
@@ -258,8 +240,9 @@ struct Layout {
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool tail_any = false;      // some tensor is compensated partly outside K1 (unpadded tail)
     int64_t grid[BT_COUNT] = {};
-    int32_t nbig = 0;           // tensors whose candidates may exceed one workgroup's set path
+    int32_t nbig = 0;           // tensors whose candidates may exceed kSetMax (K5s extra workgroups)
     int32_t big[kBigMax] = {};
+    int32_t big_first[kBigMax + 1] = {};   // their extra workgroups (SetMap)
 };
 
 // Capped grids serve the launches that are most likely gated no-ops (the list count
@@ -286,13 +269,6 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, in
         }
     }
     return 0;
-}
-
-// Candidates above which a resample set goes over several workgroups (k_bigset_*) when
-// its tensor has a slot: DGC_SET_ONE=n (A/B runs; results are identical either way).
-static int64_t set_one() {
-    static const int64_t v = std::getenv("DGC_SET_ONE") ? std::atoll(std::getenv("DGC_SET_ONE")) : kSetOne;
-    return v;
 }
 
 static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, std::vector<TDesc>& td,
@@ -335,9 +311,12 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.gpos_off = gpos;
         gpos += 2 * (d.cand_cap / 2 + 1);
         d.big = -1;
-        if (d.cand_cap > set_one() && d.cand_cap <= (int64_t)kBigSlices * kBigSlice && L.nbig < kBigMax) {
+        if (d.cand_cap > kSetMax && L.nbig < kBigMax) {   // K5s workgroups to hold its stretches in registers
+            const int64_t want = ceil_div(d.cand_cap, (int64_t)kSetRegC * 1024);
             d.big = L.nbig;
-            L.big[L.nbig++] = t;
+            L.big[L.nbig] = t;
+            L.big_first[L.nbig + 1] = L.big_first[L.nbig] + (int32_t)(std::min<int64_t>(want, kSetGBig) - kSetG);
+            ++L.nbig;
         }
         d.idx_base = T > 1 ? d.off : 0;
         d.nv4 = padded ? ceil_div(d.n, (int64_t)4) : d.n / 4;
@@ -403,9 +382,9 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.cand_key = c.take<uint32_t>(L.ncand);
     w.gpos = c.take<uint32_t>(L.ngpos);
     w.nthg = c.take<NthG>(L.T);
-    w.bigset = c.take<BigSetWS>(L.nbig);
     w.setg = c.take<SetG>(L.T);
     w.fin_ticket = c.take<uint32_t>(16);
+    w.chain = c.take<uint32_t>(32);
     if (bytes) *bytes = c.bytes();
     return w;
 }
@@ -804,7 +783,10 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = 0;
         sg.mn = 0xFFFFFFFFu;
         sg.mx = 0;
-        if (t == 0) *w.fin_ticket = 0;
+        if (t == 0) {
+            *w.fin_ticket = 0;
+            for (int i = 0; i < 24; ++i) w.chain[i] = 0;   // k_chain_one's (24..31: k_rs_passes', zero at rest)
+        }
     }
     __syncthreads();   // the caller's threshold (thr[t]) is written
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
@@ -999,6 +981,7 @@ struct SampleKeys {
     }
     __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
     __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
+    __device__ __forceinline__ uint32_t* chain() const { return w.chain + 24; }   // k_rs_passes
     // the final pass's last workgroup: the threshold is known, reset the selection state
     __device__ __forceinline__ void done(int t) const { sel_init_tensor(w, t, 1); }
     template <class F>
@@ -1092,9 +1075,9 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const 
 // Spilled segments are re-read by the block's waves. One atomic per block into its group;
 // the tensor's last workgroup then takes the adaptation step (decide_tensor).
 static_assert(kBlock * kCountSegs == kGroupSegs, "k_count_lists: one group per workgroup");
-__global__ void __launch_bounds__(kBlock)
-k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
-    const int t = task(w, BT_CNT, blockIdx.x);
+__device__ __forceinline__ void count_lists_body(const float* __restrict__ vec_flat, const SelWS& w, const SelCfg& p,
+                                                 int64_t bx) {
+    const int t = task(w, BT_CNT, (int)bx);
     const SelState* st = w.st + t;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
     const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
@@ -1109,7 +1092,7 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         bsum = 0;
     }
     __syncthreads();
-    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_CNT][t]) * kBlock * kCountSegs;
+    const int64_t lseg0 = (bx - w.bt[BT_CNT][t]) * kBlock * kCountSegs;
     uint32_t lc[kCountSegs];
     const uint32_t tkey = abs_key(tc);
 #pragma unroll
@@ -1170,9 +1153,14 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     __syncthreads();
     if (threadIdx.x == 0 && bsum) atomicAdd(&w.grp_cnt[d.grp0 + lseg0 / kGroupSegs], (unsigned long long)bsum);
     // the tensor's last workgroup takes the adaptation step (no k_decide launch)
-    if (last_block_arrival8(w.st[t].tk8, (uint32_t)((int64_t)blockIdx.x - w.bt[BT_CNT][t]),
+    if (last_block_arrival8(w.st[t].tk8, (uint32_t)(bx - w.bt[BT_CNT][t]),
                             (uint32_t)(w.bt[BT_CNT][t + 1] - w.bt[BT_CNT][t])))
         decide_tensor(w, p, t);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
+    count_lists_body(vec_flat, w, p, blockIdx.x);
 }
 
 // t_cur < t_list: full select pass at t_cur — one wave per kSuper segments (16
@@ -1181,9 +1169,9 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
 // launch that is most likely a gated no-op). The tensor's last workgroup then takes the
 // adaptation step (decide_tensor).
 template <bool ALIGNED>
-__global__ void __launch_bounds__(kBlock)
-k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) {
-    const int t = task(w, which, blockIdx.x);
+__device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_flat, const SelWS& w, int which,
+                                                 const SelCfg& p, int64_t bx) {
+    const int t = task(w, which, (int)bx);
     const SelState* st = w.st + t;
     if (!st->active || st->t_cur >= st->t_list) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -1196,7 +1184,7 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
     __shared__ uint32_t wovf[kSegPerBlock4];
     const int64_t nsuper = ceil_div(d.nseg, (int64_t)kSuper);
     const int64_t nb = w.bt[which][t + 1] - w.bt[which][t];
-    for (int64_t bi = (int64_t)blockIdx.x - w.bt[which][t]; bi * kSegPerBlock4 < nsuper; bi += nb) {
+    for (int64_t bi = bx - w.bt[which][t]; bi * kSegPerBlock4 < nsuper; bi += nb) {
         const int64_t sup = bi * kSegPerBlock4 + wave;
         uint32_t ctot = 0, novf = 0;
         if (sup < nsuper) {
@@ -1244,8 +1232,14 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
         __syncthreads();
     }
     // the tensor's last workgroup takes the adaptation step (no k_decide launch)
-    if (last_block_arrival8(w.st[t].tk8, (uint32_t)((int64_t)blockIdx.x - w.bt[which][t]), (uint32_t)nb))
+    if (last_block_arrival8(w.st[t].tk8, (uint32_t)(bx - w.bt[which][t]), (uint32_t)nb))
         decide_tensor(w, p, t);
+}
+
+template <bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)
+k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) {
+    select_pass_body<ALIGNED>(vec_flat, w, which, p, blockIdx.x);
 }
 
 // Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
@@ -1253,9 +1247,9 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
 // workgroup of the tensor picks j* = the first j whose count reaches lower*k (else
 // max_iters) and arms the count pass + decide at t_{j*}.
 template <bool ALIGNED>
-__global__ void __launch_bounds__(kBlock)
-k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
-    const int t = task(w, BT_CAP4, blockIdx.x);
+__device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_flat, const SelWS& w,
+                                                  const SelCfg& p, int64_t bx) {
+    const int t = task(w, BT_CAP4, (int)bx);
     SelState* st = w.st + t;
     if (!st->lower_pending) return;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -1271,7 +1265,7 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     for (int j = 0; j <= kMaxLower; ++j) c[j] = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nb = w.bt[BT_CAP4][t + 1] - w.bt[BT_CAP4][t];
-    for (int64_t ls = ((int64_t)blockIdx.x - w.bt[BT_CAP4][t]) * kSegPerBlock4 + wave; ls < d.nseg;
+    for (int64_t ls = (bx - w.bt[BT_CAP4][t]) * kSegPerBlock4 + wave; ls < d.nseg;
          ls += nb * kSegPerBlock4) {
         for (int tile = 0; tile < kSegTiles; ++tile) {
             float x[4];
@@ -1318,6 +1312,12 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     }
 }
 
+template <bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)
+k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
+    lower_counts_body<ALIGNED>(vec_flat, w, p, blockIdx.x);
+}
+
 // The "lower" recounts served by the K1 candidate lists: the counts at the first
 // kLowerLists thresholds t_j that are >= t_list, from the complete lists (a spilled
 // segment is re-read by a wave). When one of them reaches lower*k, the first such j
@@ -1326,9 +1326,9 @@ k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
 // segment, like k_count_lists.
 constexpr int kLowerLists = 4;
 
-__global__ void __launch_bounds__(kBlock)
-k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
-    const int t = task(w, BT_SEG, blockIdx.x);
+__device__ __forceinline__ void lower_lists_body(const float* __restrict__ vec_flat, const SelWS& w, const SelCfg& p,
+                                                 int64_t bx) {
+    const int t = task(w, BT_SEG, (int)bx);
     SelState* st = w.st + t;
     if (!st->lower_pending) return;
     float th[kLowerLists + 1];
@@ -1349,7 +1349,7 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     if (threadIdx.x == 0) nspill = 0;
     if (threadIdx.x <= kLowerLists) bsum[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t lseg0 = ((int64_t)blockIdx.x - w.bt[BT_SEG][t]) * kBlock;
+    const int64_t lseg0 = (bx - w.bt[BT_SEG][t]) * kBlock;
     const int64_t ls = lseg0 + threadIdx.x;
     uint32_t c[kLowerLists + 1];
 #pragma unroll
@@ -1421,6 +1421,11 @@ k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
         }
         }
     }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_lower_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
+    lower_lists_body(vec_flat, w, p, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ emit
@@ -1525,9 +1530,9 @@ constexpr int kEmitShort = 16;                  // lists up to this long: a thre
 constexpr uint32_t kEmitSkip = 0xFFFFFFFFu;
 static_assert(kCap == kWave, "wave-per-list emission needs kCap == wavefront width");
 
-__global__ void __launch_bounds__(kEmitSegs)
-k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
-    const int t = task(w, BT_GRP, blockIdx.x);
+__device__ __forceinline__ void emit_body(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& oa,
+                                          int64_t bx) {
+    const int t = task(w, BT_GRP, (int)bx);
     const SelState* st = w.st + t;
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
     if (st->spec_emitted) return;                                        // k_count_emit did
@@ -1541,7 +1546,7 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
     const bool defer_here = o.defer && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
-    const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
+    const int64_t lb = bx - w.bt[BT_GRP][t];
     const int64_t lg = lb / kEmitSplit;                      // group within the tensor
     const int sub = (int)(lb % kEmitSplit);                  // its quarter
     const int64_t g = d.grp0 + lg;
@@ -1650,6 +1655,84 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
         const int j = jw + __builtin_ctzll(spilled);
         spilled &= spilled - 1;
         emit_reread_firstk(vec, d, lseg0 + j, ga + off_a[j], limit, obase, tc, o, !defer_here);
+    }
+}
+
+__global__ void __launch_bounds__(kEmitSegs)
+k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
+    emit_body(vec_flat, w, oa, blockIdx.x);
+}
+
+// One-tensor DGC_SYNC_DEVICE selections with the lowering shortcut (the flat bucket):
+// every pass after the first count — the full select pass, the lowering from the lists
+// and over vec, the count at the lowered threshold (lists, or a full pass), and the
+// emit / K5 gather — in ONE launch instead of six. In the steady state the first count
+// already wrote the first-k payload (k_count_emit, spec_emitted) and every workgroup
+// returns at once: the six gated no-op launches cost ~30 us of a flat-1B step (same box,
+// measured by leaving them out). Otherwise the phases run in order over virtual blocks
+// that workgroups claim from an atomic counter; each phase's gate is decided once, by
+// the first workgroup to reach it, from the state the phases before left; a workgroup
+// waits for a phase's completion count (one agent-scope release per workgroup and phase,
+// an acquire before going on) before the next phase. Only running workgroups claim
+// blocks, so nothing assumes the grid co-resident.
+constexpr int kChainPhases = 6;
+enum { CH_CLAIM = 0, CH_DONE = kChainPhases, CH_GATE = 2 * kChainPhases };
+static_assert(3 * kChainPhases <= 32, "SelWS::chain words");
+static_assert(kEmitSegs == kBlock, "k_chain_one runs the emit with kBlock threads");
+
+template <bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)   // (2 waves per SIMD: 16 loads in flight per wave keep a full pass HBM-bound)
+k_chain_one(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut e) {
+    const SelState* st = w.st;
+    uint32_t* cc = w.chain;
+    __shared__ uint32_t s_u;
+    if (threadIdx.x == 0) s_u = (st->done && st->spec_emitted) ? 1u : 0u;
+    __syncthreads();
+    if (s_u) return;   // uniform: the payload stands
+    for (int ph = 0; ph < kChainPhases; ++ph) {
+        __syncthreads();   // (s_u is reused)
+        if (threadIdx.x == 0) {
+            uint32_t gate = __hip_atomic_load(&cc[CH_GATE + ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (gate == 0) {
+                bool run = true;   // the emit / gather: its body gates itself
+                if (ph == 0 || ph == 4) run = st->active && !(st->t_cur >= st->t_list);
+                else if (ph == 1 || ph == 2) run = st->lower_pending != 0;
+                else if (ph == 3) run = st->active && st->t_cur >= st->t_list;
+                const uint32_t want = run ? 2u : 1u;
+                const uint32_t prev = atomicCAS(&cc[CH_GATE + ph], 0u, want);
+                gate = prev == 0u ? want : prev;
+            }
+            s_u = gate;
+        }
+        __syncthreads();
+        if (s_u != 2u) continue;   // uniform
+        const int which = (ph == 0 || ph == 4) ? BT_CAP16 : ph == 1 ? BT_SEG : ph == 2 ? BT_CAP4
+                          : ph == 3 ? BT_CNT : BT_GRP;
+        const uint32_t nvb = (uint32_t)w.bt[which][1];
+        uint32_t mine = 0;
+        for (;;) {
+            __syncthreads();
+            if (threadIdx.x == 0) s_u = atomicAdd(&cc[CH_CLAIM + ph], 1u);
+            __syncthreads();
+            const uint32_t vb = s_u;
+            if (vb >= nvb) break;   // uniform
+            if (ph == 0 || ph == 4) select_pass_body<ALIGNED>(vec_flat, w, BT_CAP16, p, vb);
+            else if (ph == 1) lower_lists_body(vec_flat, w, p, vb);
+            else if (ph == 2) lower_counts_body<ALIGNED>(vec_flat, w, p, vb);
+            else if (ph == 3) count_lists_body(vec_flat, w, p, vb);
+            else emit_body(vec_flat, w, e, vb);
+            ++mine;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's stores are in L2
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (mine) __hip_atomic_fetch_add(&cc[CH_DONE + ph], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (__hip_atomic_load(&cc[CH_DONE + ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nvb)
+                __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        __syncthreads();
     }
 }
 
@@ -2507,8 +2590,10 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // the bins instead of piling into the few bins of their exponents); the emit carries
 // the wire casts and the masking of the K5 emit.
 //
-// Over kSetG co-resident workgroups of ONE launch (grid kSetG x T): a set of more than
-// kSetRegC x 1024 candidates is cut into kSetG contiguous
+// Over G co-resident workgroups of ONE launch (kSetG per tensor; up to kSetGBig for a
+// tensor whose capacity exceeds kSetMax — VGG-16-BN's fc6, where four sliced launches
+// k_bigset_* ran as no-ops every step before): a set of more than kSetRegC x 1024
+// candidates is cut into G contiguous
 // stretches of rounds, each workgroup's keys in its registers; the key range, the radix
 // passes' histograms and the per-stretch counts go through device atomics with a
 // barrier between the phases (min / max | pass 1 | pass 2 [| pass 3] | counts), and each
@@ -2576,20 +2661,47 @@ __device__ __forceinline__ void setg_barrier(SetG* g, uint32_t G) {
     __syncthreads();
 }
 
+// The grid: kSetG workgroups per tensor, then kSetGBig - kSetG more for each tensor whose
+// candidate capacity exceeds kSetMax (SetMap; up to kBigMax of them, the rest of such
+// a tensor's sets above kSetMax go to the replay).
+struct SetMap {
+    int32_t n;                    // tensors with extra workgroups
+    int32_t t[kBigMax];           // their ids
+    int32_t first[kBigMax + 1];   // their extra workgroups' first block after kSetG x T
+};
+
 __global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one) {
-    const int t = blockIdx.y;
-    const uint32_t b = blockIdx.x;
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m) {
+    int t;
+    uint32_t b;
+    const uint32_t bx = blockIdx.x, base_blocks = (uint32_t)(kSetG * w.T);
+    if (bx < base_blocks) {
+        t = (int)(bx / kSetG);
+        b = bx % kSetG;
+    } else {
+        const uint32_t e = bx - base_blocks;
+        int j = 0;
+        while (j + 1 < m.n && (uint32_t)m.first[j + 1] <= e) ++j;
+        t = m.t[j];
+        b = kSetG + (e - (uint32_t)m.first[j]);
+    }
     SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const uint32_t Gt = d.big >= 0 ? (uint32_t)(kSetG + m.first[d.big + 1] - m.first[d.big]) : (uint32_t)kSetG;
     const int64_t n64 = st->n_cur;
-    // the replay takes it (or, past `one` with a sliced-path slot, k_bigset_*)
-    if (n64 > (d.big >= 0 ? one : kSetMax) || n64 > (int64_t)kSetG * kSetRegC * kScanThreads || d.k < 1 ||
-        n64 <= d.k)
-        return;
-    const uint32_t G = n64 > kSetCoopMin ? (uint32_t)kSetG : 1u;
-    if (b >= G) return;
+    if (d.k < 1 || n64 <= d.k) return;
+    // this set's workgroups: one up to kSetCoopMin candidates, else kSetG, and for a big
+    // tensor as many as keep its stretches in registers (up to Gt); each stretch's rounds
+    // past the registers are read from L2 on every walk, up to kSetRoundsMax per stretch
+    const int rounds = (int)((n64 + kScanThreads - 1) / kScanThreads);
+    uint32_t G = 1;
+    if (n64 > kSetCoopMin) {
+        const uint32_t want = (uint32_t)((rounds + kSetRegC - 1) / kSetRegC);
+        G = want > (uint32_t)kSetG ? (want < Gt ? want : Gt) : (uint32_t)kSetG;
+    }
+    const int per = (rounds + (int)G - 1) / (int)G;
+    if (per > kSetRoundsMax || b >= G) return;   // (past kSetRoundsMax: the replay)
     SetG* g = w.setg + t;
     if (G > 1 && !setg_consensus(g, G)) return;   // not all resident: the replay
     SET_STAMP(0);
@@ -2600,30 +2712,34 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t lds32[16];
     __shared__ uint32_t red[2][kWaves];
-    __shared__ uint32_t rbase[kSetRegC * kWaves];
+    __shared__ uint32_t rbase[kSetRoundsMax * kWaves];
     __shared__ uint32_t sel_above, sel_cnt, s_mn, s_mx, s_base, s_stop;
     __shared__ int sel_bin;
     __shared__ long long obase_s;
     // this workgroup's stretch of rounds; queue entry i = tid + r * 1024 (coalesced)
-    const int rounds = (n + kScanThreads - 1) / kScanThreads;
-    const int per = (rounds + (int)G - 1) / (int)G;
     const int r0 = (int)b * per, r1 = min(r0 + per, rounds);
     const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
+    auto valid = [&](int r) { return r0 + r < r1 && tid + (r0 + r) * kScanThreads < n; };
     uint32_t key[kSetRegC];
 #pragma unroll
-    for (int r = 0; r < kSetRegC; ++r) {
-        const int i = tid + (r0 + r) * kScanThreads;
-        key[r] = r0 + r < r1 && i < n ? qk[i] : 0u;
-    }
-    auto valid = [&](int r) { return r0 + r < r1 && tid + (r0 + r) * kScanThreads < n; };
+    for (int r = 0; r < kSetRegC; ++r) key[r] = valid(r) ? qk[tid + (r0 + r) * kScanThreads] : 0u;
+    // every round of the stretch: the registers, then (a big set only) the rest from L2
+    auto walk = [&](auto&& f) {
+#pragma unroll
+        for (int r = 0; r < kSetRegC; ++r) f(r, key[r], valid(r));
+        for (int r = kSetRegC; r < per; ++r) {
+            const bool v = valid(r);
+            f(r, v ? qk[tid + (r0 + r) * kScanThreads] : 0u, v);
+        }
+    };
     // the key range over every stretch
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
-#pragma unroll
-    for (int r = 0; r < kSetRegC; ++r)
-        if (valid(r)) {
-            mn = key[r] < mn ? key[r] : mn;
-            mx = key[r] > mx ? key[r] : mx;
+    walk([&](int, uint32_t kk, bool v) {
+        if (v) {
+            mn = kk < mn ? kk : mn;
+            mx = kk > mx ? kk : mx;
         }
+    });
     mn = wave_min_u32(mn);
     mx = wave_max(mx);
     if (lane == 0) {
@@ -2668,12 +2784,10 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     bool ok = true;
     while (hi > 0) {
         const int lo = hi > 11 ? hi - 11 : 0;
-#pragma unroll
-        for (int r = 0; r < kSetRegC; ++r) {
-            const uint32_t v = key[r] - mn;
-            if (valid(r) && (hi >= 32 || (v >> hi) == prefix))
-                atomicAdd(&h[(v >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
-        }
+        walk([&](int, uint32_t kk, bool v) {
+            const uint32_t x = kk - mn;
+            if (v && (hi >= 32 || (x >> hi) == prefix)) atomicAdd(&h[(x >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
+        });
         __syncthreads();
         if (G > 1) {
             uint32_t* gh = g->hist[pass];
@@ -2717,26 +2831,23 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     SET_STAMP(2);
     // order-preserving compaction: (round, wave) ballot counts, one workgroup scan, the
     // stretches before this one (their counts through the last barrier)
-    uint32_t mine = 0;
-#pragma unroll
-    for (int r = 0; r < kSetRegC; ++r) {
-        const uint32_t c = ok ? (uint32_t)__popcll(__ballot(valid(r) && key[r] >= kth)) : 0u;
+    walk([&](int r, uint32_t kk, bool v) {
+        const uint32_t c = ok ? (uint32_t)__popcll(__ballot(v && kk >= kth)) : 0u;
         if (lane == 0) rbase[r * kWaves + wv] = c;
-        mine += c;
-    }
+    });
     __syncthreads();
     {
-        const uint32_t c = tid < kSetRegC * kWaves ? rbase[tid] : 0u;
+        const uint32_t c = tid < per * kWaves ? rbase[tid] : 0u;
         uint32_t total;
         const uint32_t run = block_exclusive_scan32(c, lds32, &total);
-        if (tid < kSetRegC * kWaves) rbase[tid] = run;
+        if (tid < per * kWaves) rbase[tid] = run;
         if (tid == 0) {
             s_base = 0;
             s_stop = ok ? 0u : 1u;
             if (G > 1) __hip_atomic_store(&g->cnt[b], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    (void)mine;
+    static_assert(kSetRoundsMax * kWaves <= kScanThreads, "one compaction count per thread");
     if (G > 1) {
         setg_barrier(g, G);
         if (tid == 0) {
@@ -2747,9 +2858,10 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
             if (__hip_atomic_load(&g->broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) s_stop = 1;
         }
         // every workgroup has read the histograms: re-zero this one's share of those used
+        const int share = (kRsBins + (int)G - 1) / (int)G;
+        const int qlo = (int)b * share, qhi = min(qlo + share, kRsBins);
         for (int p = 0; p < pass; ++p)
-            for (int q = (int)b * (kRsBins / kSetG) + tid; q < ((int)b + 1) * (kRsBins / kSetG); q += kScanThreads)
-                g->hist[p][q] = 0;
+            for (int q = qlo + tid; q < qhi; q += kScanThreads) g->hist[p][q] = 0;
     }
     if (wv == 0) {
         const long long ob = out_base(w, t);
@@ -2761,15 +2873,14 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     const long long ob = obase_s + (long long)s_base;
     const int64_t* cand = w.cand_idx + d.cand_off;
     const float* cval = w.cand_val + d.cand_off;
-#pragma unroll
-    for (int r = 0; r < kSetRegC; ++r) {
-        const bool sel = valid(r) && key[r] >= kth;
-        const uint64_t m = __ballot(sel);
+    walk([&](int r, uint32_t kk, bool v) {
+        const bool sel = v && kk >= kth;
+        const uint64_t mm = __ballot(sel);
         if (sel) {
             const int i = tid + (r0 + r) * kScanThreads;
-            emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(m, 0u), cand[i], cval[i]);
+            emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(mm, 0u), cand[i], cval[i]);
         }
-    }
+    });
     if (b == 0 && tid == 0) {
         st->rs_nth = 3;   // K5's replay and emit skip the tensor
         st->tie_rule = DGC_TIES_SET;
@@ -2777,279 +2888,6 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     SET_STAMP(4);
 }
 
-// ---------------------------------------------------------------- K5s over several workgroups
-// The set path for candidate counts above one workgroup's kSetMax (VGG-16-BN's fc6:
-// up to 64k = 6.5M candidates), in slices of kBigSlice candidates, one workgroup each:
-//   k_bigset_hist    coarse histogram of key - key(t_cur) in 4096-unit bins (the
-//                    candidates are >= t_cur; 2048 bins = the octave above it, the last
-//                    one open-ended), LDS then agent atomics into hist
-//   k_bigset_gather  every workgroup picks the coarse bin b0 of the k-th largest from the
-//                    histogram; counts its slice's keys above b0 and gathers the keys in
-//                    b0 (key, position) into the tensor's K5 pair-slot region
-//   k_bigset_select  one workgroup per tensor: hist re-zeroed for the next call; the exact
-//                    k-th key among the gathered ones (one 4096-bin pass: b0 spans 4096
-//                    key values), the tie check, the slices' payload bases
-//   k_bigset_emit    each slice emits its keys >= the k-th in index order
-// b0 the open-ended bin, more than kBigBuf keys in b0, or a tie across the boundary:
-// the tensor is left to the exact replay (ok = 0), as in k_resample_set.
-struct BigList {
-    int32_t n;
-    int64_t one;   // the one-workgroup path's limit for these tensors (set_one)
-    int32_t t[kBigMax];
-};
-
-template <int NT>
-__device__ __forceinline__ uint32_t block_exscan_n(uint32_t v, uint32_t* lds, uint32_t* total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t incl = wave_incl_scan<DppAdd>(v);
-    if (lane == 63) lds[wid] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < NT / 64; ++i) {
-        const uint32_t x = lds[i];
-        wbase += i < wid ? x : 0u;
-        tot += x;
-    }
-    __syncthreads();
-    *total = tot;
-    return wbase + incl - v;
-}
-
-// pick_bin_small for NT threads of PER bins each (bins = PER x NT, counts in LDS)
-template <int PER, int NT>
-__device__ __forceinline__ bool pick_bin_n(const uint32_t* h, uint32_t k, uint32_t* lds, int* bin, uint32_t* above) {
-    constexpr int bins = PER * NT;
-    const int t = threadIdx.x;
-    uint32_t c[PER], sum = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        c[j] = h[bins - 1 - (PER * t + j)];
-        sum += c[j];
-    }
-    uint32_t total;
-    uint32_t run = block_exscan_n<NT>(sum, lds, &total);
-    bool hit = false;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        if (!hit && run < k && k <= run + c[j]) {
-            hit = true;
-            *bin = bins - 1 - (PER * t + j);
-            *above = run;
-        }
-        run += c[j];
-    }
-    return hit;
-}
-
-// The tensor of launch row j if its resample takes the multi-workgroup set path now.
-__device__ __forceinline__ int bigset_task(const SelWS& w, const BigList& bl, int j, int64_t& cnt) {
-    if (j >= bl.n) return -1;
-    const int t = bl.t[j];
-    const SelState* st = w.st + t;
-    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return -1;
-    cnt = st->n_cur;
-    if (cnt <= bl.one || cnt > (int64_t)kBigSlices * kBigSlice || cnt <= w.td[t].k) return -1;
-    return t;
-}
-
-// (key, position) pairs of the k-th key's coarse bin, in the tensor's pair-slot region
-// (2 x (cand_cap / 2 + 1) words)
-__device__ __forceinline__ uint32_t bigset_buf_cap(const TDesc& d) {
-    const int64_t c = d.cand_cap / 2 + 1;
-    return (uint32_t)(c < kBigBuf ? c : kBigBuf);
-}
-
-__device__ __forceinline__ uint32_t bigset_bin(uint32_t key, uint32_t tkey) {
-    const uint32_t v = (key - tkey) >> kBigShift;
-    return v < (uint32_t)kRsBins - 1 ? v : (uint32_t)kRsBins - 1;
-}
-
-__global__ void __launch_bounds__(kBlock) k_bigset_hist(SelWS w, BigList bl) {
-    int64_t cnt;
-    const int t = bigset_task(w, bl, blockIdx.y, cnt);
-    if (t < 0) return;   // uniform per workgroup
-    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
-    if ((int64_t)blockIdx.x >= nsl) return;
-    const TDesc d = w.td[t];
-    const SelState* st = w.st + t;
-    BigSetWS& b = w.bigset[d.big];
-    const uint32_t tkey = abs_key(st->t_cur);
-    __shared__ uint32_t h[kRsBins];
-    for (int i = threadIdx.x; i < kRsBins; i += kBlock) h[i] = 0;
-    __syncthreads();
-    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
-    const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[bigset_bin(qk[i], tkey)], 1u);
-    __syncthreads();
-    for (int i = threadIdx.x; i < kRsBins; i += kBlock)
-        if (h[i]) atomicAdd(&b.hist[i], h[i]);
-    if (blockIdx.x == 0 && threadIdx.x == 0) b.bufn = 0;
-}
-
-__global__ void __launch_bounds__(kBlock) k_bigset_gather(SelWS w, BigList bl) {
-    int64_t cnt;
-    const int t = bigset_task(w, bl, blockIdx.y, cnt);
-    if (t < 0) return;
-    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
-    if ((int64_t)blockIdx.x >= nsl) return;
-    const TDesc d = w.td[t];
-    const SelState* st = w.st + t;
-    BigSetWS& b = w.bigset[d.big];
-    const uint32_t tkey = abs_key(st->t_cur);
-    __shared__ uint32_t h[kRsBins];
-    __shared__ uint32_t lds[kBlock / kWave];
-    __shared__ int sel;
-    __shared__ uint32_t sel_above;
-    for (int i = threadIdx.x; i < kRsBins; i += kBlock) h[i] = b.hist[i];
-    if (threadIdx.x == 0) sel = -1;
-    __syncthreads();
-    int bin;
-    uint32_t above;
-    if (pick_bin_n<kRsBins / kBlock, kBlock>(h, (uint32_t)d.k, lds, &bin, &above)) {
-        sel = bin;
-        sel_above = above;
-    }
-    __syncthreads();
-    const int b0 = sel;
-    const uint32_t bcap = bigset_buf_cap(d);
-    const bool ok = b0 >= 0 && b0 < kRsBins - 1 && h[b0] <= bcap;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        b.ok = ok ? 1 : 0;
-        b.b0 = (uint32_t)b0;
-        b.a0 = sel_above;
-    }
-    if (!ok) return;   // uniform
-    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
-    DGC_GLB uint32_t* buf = glb(w.gpos + d.gpos_off);   // (key, position) pairs; the replay's pair slots
-    const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
-    const int lane = threadIdx.x & 63;
-    uint32_t above_cnt = 0;
-    for (int64_t i0 = lo; i0 < hi; i0 += kBlock) {   // uniform trip count
-        const int64_t i = i0 + threadIdx.x;
-        const uint32_t key = i < hi ? qk[i] : 0u;
-        const uint32_t bb = bigset_bin(key, tkey);
-        above_cnt += i < hi && bb > (uint32_t)b0;
-        const bool in = i < hi && bb == (uint32_t)b0;
-        const uint64_t m = __ballot(in);
-        if (m) {
-            uint32_t slot = 0;
-            if (lane == 0) slot = atomicAdd(&b.bufn, (uint32_t)__popcll(m));
-            slot = __shfl(slot, 0) + mbcnt64(m, 0u);
-            if (in && slot < bcap) {
-                buf[2 * slot] = key;
-                buf[2 * slot + 1] = (uint32_t)i;
-            }
-        }
-    }
-    uint32_t tot;
-    block_exscan_n<kBlock>(above_cnt, lds, &tot);
-    if (threadIdx.x == 0) b.slice_cnt[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_bigset_select(SelWS w, BigList bl) {
-    int64_t cnt;
-    const int t = bigset_task(w, bl, blockIdx.x, cnt);
-    if (t < 0) return;
-    const TDesc d = w.td[t];
-    SelState* st = w.st + t;
-    BigSetWS& b = w.bigset[d.big];
-    for (int i = threadIdx.x; i < kRsBins; i += kScanThreads) b.hist[i] = 0;   // read by k_bigset_gather
-    if (!b.ok) return;
-    constexpr int kBins = 4096;   // the coarse bin's 4096 key values, one pass
-    __shared__ uint32_t h[kBins];
-    __shared__ uint32_t sc[kBigSlices];
-    __shared__ uint32_t lds32[16];
-    __shared__ int sel;
-    __shared__ uint32_t sel_above, sel_cnt;
-    __shared__ long long ob_s;
-    const int tid = threadIdx.x;
-    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
-    const uint32_t n0 = b.bufn, a0 = b.a0;
-    const uint32_t k = (uint32_t)d.k;
-    const uint32_t base_key = abs_key(st->t_cur) + (b.b0 << kBigShift);
-    const DGC_GLB uint32_t* buf = glb(w.gpos + d.gpos_off);
-    for (int i = tid; i < kBins; i += kScanThreads) h[i] = 0;
-    for (int i = tid; i < kBigSlices; i += kScanThreads) sc[i] = 0;
-    if (tid == 0) sel = -1;
-    __syncthreads();
-    const bool fits = n0 <= bigset_buf_cap(d) && a0 < k && k - a0 <= n0;
-    if (fits)
-        for (uint32_t i = tid; i < n0; i += kScanThreads) atomicAdd(&h[buf[2 * i] - base_key], 1u);
-    __syncthreads();
-    int bin;
-    uint32_t above;
-    if (fits && pick_bin_small<kBins / kScanThreads>(h, k - a0, lds32, &bin, &above)) {
-        sel = bin;
-        sel_above = above;
-        sel_cnt = h[bin];
-    }
-    __syncthreads();
-    // tied across the boundary (or nothing found): the exact replay
-    if (sel < 0 || sel_cnt != k - a0 - sel_above) {
-        if (tid == 0) b.ok = 0;
-        return;
-    }
-    const uint32_t kth = base_key + (uint32_t)sel;
-    // each slice's selected keys: those above b0 plus its gathered keys >= kth
-    for (uint32_t i = tid; i < n0; i += kScanThreads)
-        if (buf[2 * i] >= kth) atomicAdd(&sc[buf[2 * i + 1] / kBigSlice], 1u);
-    if (tid < kWave) {
-        const long long o = out_base(w, t);
-        if (tid == 0) ob_s = o;
-    }
-    __syncthreads();
-    uint32_t mine = tid < nsl ? sc[tid] + b.slice_cnt[tid] : 0u;   // nsl <= kBigSlices <= kScanThreads
-    uint32_t total;
-    const uint32_t base = block_exclusive_scan32(mine, lds32, &total);
-    if (tid < nsl) b.slice_cnt[tid] = base;
-    if (tid == 0) {
-        b.kth = kth;
-        b.obase = ob_s;
-        st->rs_nth = 3;   // K5's replay and emit skip the tensor; k_bigset_emit writes it
-        st->tie_rule = DGC_TIES_SET;
-    }
-}
-
-__global__ void __launch_bounds__(kBlock)
-k_bigset_emit(const float* __restrict__ vec_flat, SelWS w, BigList bl, EmitOut o) {
-    const int j = blockIdx.y;
-    if (j >= bl.n) return;
-    const int t = bl.t[j];
-    const SelState* st = w.st + t;
-    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 3) return;
-    const TDesc d = w.td[t];
-    const BigSetWS& b = w.bigset[d.big];
-    const int64_t cnt = st->n_cur;
-    if (!b.ok || cnt <= bl.one) return;   // the one-workgroup path emitted it
-    const int64_t nsl = ceil_div(cnt, (int64_t)kBigSlice);
-    if ((int64_t)blockIdx.x >= nsl) return;
-    const uint32_t kth = b.kth;
-    const DGC_GLB uint32_t* qk = glb(w.cand_key + d.cand_off);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr int kW = kBlock / kWave;
-    __shared__ uint32_t wc[kW];
-    // each wave a contiguous quarter of the slice, 64 keys per round
-    const int64_t lo = (int64_t)blockIdx.x * kBigSlice, hi = lo + kBigSlice < cnt ? lo + kBigSlice : cnt;
-    const int64_t q = ceil_div(hi - lo, (int64_t)kW);
-    const int64_t qlo = lo + wv * q, qhi = qlo + q < hi ? qlo + q : hi;
-    uint32_t c = 0;
-    for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
-        const int64_t i = i0 + lane;
-        c += (uint32_t)__popcll(__ballot(i < qhi && qk[i] >= kth));
-    }
-    if (lane == 0) wc[wv] = c;
-    __syncthreads();
-    long long pos = b.obase + b.slice_cnt[blockIdx.x];
-    for (int i = 0; i < wv; ++i) pos += wc[i];
-    for (int64_t i0 = qlo; i0 < qhi; i0 += kWave) {
-        const int64_t i = i0 + lane;
-        const bool sel = i < qhi && qk[i] >= kth;
-        const uint64_t m = __ballot(sel);
-        if (sel) emit_one(o, d, pos + mbcnt64(m, 0u), w.cand_idx[d.cand_off + i], w.cand_val[d.cand_off + i]);
-        pos += __popcll(m);
-    }
-}
 
 // K5's global-memory phase by G workgroups per tensor (grid G x T, a plain launch sized
 // so all of them fit at once; a residency consensus decides whether they run it, see
@@ -3287,37 +3125,28 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
                          sink, 0u, order_out, margin_max};
     bool finished = false;   // the payload count and records are written
+    // one tensor, device decisions, the lowering shortcut: the passes after the first
+    // count and the gather in one launch (k_chain_one); DGC_NO_CHAIN=1 (A/B runs) launches
+    // them one by one
+    static const bool no_chain = std::getenv("DGC_NO_CHAIN") != nullptr;
+    const bool chained = L.T == 1 && keep_lists && sync_mode == DGC_SYNC_DEVICE && lower_fast && !no_chain;
+    EmitOut g = o;   // the K5 gather (+ every other tensor's payload)
+    g.queue = w.queue;
+    g.cand = w.cand_idx;
+    g.cval = w.cand_val;
+    g.ckey = w.cand_key;
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
-        EmitOut g = o;
-        g.queue = w.queue;
-        g.cand = w.cand_idx;
-        g.cval = w.cand_val;
-        g.ckey = w.cand_key;
-        DGC_TRY(launch_emit(L, vec, w, g, s));
+        if (!chained) DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
-            hipLaunchKernelGGL(k_resample_set, dim3(kSetG, (unsigned)L.T), dim3(kScanThreads), 0, s, vec, w, o,
-                               set_one());
+            SetMap m{};
+            m.n = L.nbig;
+            for (int j = 0; j < L.nbig; ++j) m.t[j] = L.big[j];
+            for (int j = 0; j <= L.nbig; ++j) m.first[j] = L.big_first[j];
+            const unsigned grid = (unsigned)(kSetG * L.T + L.big_first[L.nbig]);
+            hipLaunchKernelGGL(k_resample_set, dim3(grid), dim3(kScanThreads), 0, s, vec, w, o, m);
             DGC_LAUNCHED();
-            if (L.nbig > 0) {   // candidate counts above one workgroup's: sliced over workgroups
-                BigList bl{};
-                bl.n = L.nbig;
-                bl.one = set_one();
-                int64_t maxcap = 0;
-                for (int j = 0; j < L.nbig; ++j) bl.t[j] = L.big[j];
-                maxcap = L.max_cand;
-                const dim3 g((unsigned)std::min<int64_t>(ceil_div(maxcap, (int64_t)kBigSlice), kBigSlices),
-                             (unsigned)L.nbig);
-                hipLaunchKernelGGL(k_bigset_hist, g, dim3(kBlock), 0, s, w, bl);
-                DGC_LAUNCHED();
-                hipLaunchKernelGGL(k_bigset_gather, g, dim3(kBlock), 0, s, w, bl);
-                DGC_LAUNCHED();
-                hipLaunchKernelGGL(k_bigset_select, dim3((unsigned)L.nbig), dim3(kScanThreads), 0, s, w, bl);
-                DGC_LAUNCHED();
-                hipLaunchKernelGGL(k_bigset_emit, g, dim3(kBlock), 0, s, vec, w, bl, o);
-                DGC_LAUNCHED();
-            }
         }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
         if (G > 1) {
@@ -3342,7 +3171,16 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    DGC_TRY(keep_lists ? pass(3, true, fuse) : pass(2, false));
+    DGC_TRY(keep_lists ? pass(chained ? 1 : 3, true, fuse) : pass(2, false));
+    if (chained) {
+        const unsigned grid = (unsigned)std::min<int64_t>(
+            kCapBlocks, std::max({L.grid[BT_CAP16], L.grid[BT_SEG], L.grid[BT_CAP4], L.grid[BT_CNT], L.grid[BT_GRP]}));
+        if (al)
+            hipLaunchKernelGGL(k_chain_one<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p, g);
+        else
+            hipLaunchKernelGGL(k_chain_one<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, p, g);
+        DGC_LAUNCHED();
+    }
     bool emitted = false;   // the payload of every non-K5 tensor is written
     if (sync_mode == DGC_SYNC_HOST) {
         // read the decisions back and launch only what they need
@@ -3377,7 +3215,9 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
     } else if (L.adapt_any) {
         // every kernel below early-exits on a device flag when it is not needed
-        if (lower_fast) {
+        if (chained) {
+            // (k_chain_one ran them)
+        } else if (lower_fast) {
             DGC_TRY(lower());
             DGC_TRY(pass(3, true));
         } else {
@@ -3484,7 +3324,16 @@ static int thresholds(const SelWS& w, const Layout& L, const float* vec, hipStre
             hipLaunchKernelGGL(k_rs_reset_samples, dim3((unsigned)L.T), dim3(kBlock), 0, s, w, ks1);
             DGC_LAUNCHED();
         }
-        DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
+        // DGC_NO_RS_CHAIN=1 (A/B runs): the three passes as three launches
+        static const bool no_chain = std::getenv("DGC_NO_RS_CHAIN") != nullptr;
+        if (no_chain) {
+            DGC_TRY(radix_select_passes(SampleKeys{w, vec}, (int)L.grid[BT_SAMP], s));
+        } else {
+            const int grid = (int)L.grid[BT_SAMP];
+            hipLaunchKernelGGL(k_rs_passes<SampleKeys>, dim3((unsigned)std::min(grid, 1024)), dim3(kBlock), 0, s,
+                               SampleKeys{w, vec}, grid, (int)L.T);
+            DGC_LAUNCHED();
+        }
     }
     return DGC_OK;
 }
@@ -3680,8 +3529,8 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
         DGC_FAIL(DGC_ERR_WORKSPACE, "dgc_batch_init: workspace needs %zu bytes, 256-B aligned", need);
     SelWS w = carve_select(ws, L);
     DGC_HIP(hipMemsetAsync(w.st, 0, sizeof(SelState) * L.T, s));
-    if (L.nbig) DGC_HIP(hipMemsetAsync(w.bigset, 0, sizeof(BigSetWS) * L.nbig, s));   // zero at rest
     DGC_HIP(hipMemsetAsync(w.setg, 0, sizeof(SetG) * L.T, s));                         // zero at rest
+    DGC_HIP(hipMemsetAsync(w.chain, 0, 32 * sizeof(uint32_t), s));                     // zero at rest
     DGC_HIP(hipMemsetAsync(w.samples, 0, sizeof(float) * L.nsamp, s));   // the window histograms: zero at rest
     DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
     for (int which = 0; which < BT_COUNT; ++which)

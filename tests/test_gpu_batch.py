@@ -334,11 +334,11 @@ def designed_big_gradient(n, k, stride, start, seed):
 
 @pytest.mark.timeout(600)
 def test_batch_index_order_big_resample():
-    """The multi-workgroup set path (k_bigset_*: more candidates than one workgroup's
-    262144) against the exact replay: a 20M-element tensor (k = 20000, up to 64k = 1.28M
-    candidates) whose first gradient (``designed_big_gradient``) resamples over ~520k
-    candidates, then random steps — the same sets, outputs and state as
-    resample_order="topk"."""
+    """The set path past kSetMax = 262144 candidates (a tensor whose capacity exceeds it
+    gets up to 128 co-resident workgroups in k_resample_set) against the exact replay: a
+    20M-element tensor (k = 20000, up to 64k = 1.28M candidates) whose first gradient
+    (``designed_big_gradient``) resamples over ~520k candidates (32 workgroups), then
+    random steps — the same sets, outputs and state as resample_order="topk"."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import random
