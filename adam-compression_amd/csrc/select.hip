@@ -2670,38 +2670,13 @@ struct SetMap {
     int32_t first[kBigMax + 1];   // their extra workgroups' first block after kSetG x T
 };
 
-__global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m) {
-    int t;
-    uint32_t b;
-    const uint32_t bx = blockIdx.x, base_blocks = (uint32_t)(kSetG * w.T);
-    if (bx < base_blocks) {
-        t = (int)(bx / kSetG);
-        b = bx % kSetG;
-    } else {
-        const uint32_t e = bx - base_blocks;
-        int j = 0;
-        while (j + 1 < m.n && (uint32_t)m.first[j + 1] <= e) ++j;
-        t = m.t[j];
-        b = kSetG + (e - (uint32_t)m.first[j]);
-    }
-    SelState* st = w.st + t;
-    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
-    const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    const uint32_t Gt = d.big >= 0 ? (uint32_t)(kSetG + m.first[d.big + 1] - m.first[d.big]) : (uint32_t)kSetG;
+// (OVF: a stretch longer than the registers hold — a set above ~2M candidates; the
+// common case compiles without the L2 rounds)
+template <bool OVF>
+__device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& o,
+                                                  int t, uint32_t b, uint32_t G, int per, int rounds,
+                                                  SelState* st, const TDesc& d) {
     const int64_t n64 = st->n_cur;
-    if (d.k < 1 || n64 <= d.k) return;
-    // this set's workgroups: one up to kSetCoopMin candidates, else kSetG, and for a big
-    // tensor as many as keep its stretches in registers (up to Gt); each stretch's rounds
-    // past the registers are read from L2 on every walk, up to kSetRoundsMax per stretch
-    const int rounds = (int)((n64 + kScanThreads - 1) / kScanThreads);
-    uint32_t G = 1;
-    if (n64 > kSetCoopMin) {
-        const uint32_t want = (uint32_t)((rounds + kSetRegC - 1) / kSetRegC);
-        G = want > (uint32_t)kSetG ? (want < Gt ? want : Gt) : (uint32_t)kSetG;
-    }
-    const int per = (rounds + (int)G - 1) / (int)G;
-    if (per > kSetRoundsMax || b >= G) return;   // (past kSetRoundsMax: the replay)
     SetG* g = w.setg + t;
     if (G > 1 && !setg_consensus(g, G)) return;   // not all resident: the replay
     SET_STAMP(0);
@@ -2712,7 +2687,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m)
     __shared__ uint32_t h[kRsBins];
     __shared__ uint32_t lds32[16];
     __shared__ uint32_t red[2][kWaves];
-    __shared__ uint32_t rbase[kSetRoundsMax * kWaves];
+    __shared__ uint32_t rbase[(OVF ? kSetRoundsMax : kSetRegC) * kWaves];
     __shared__ uint32_t sel_above, sel_cnt, s_mn, s_mx, s_base, s_stop;
     __shared__ int sel_bin;
     __shared__ long long obase_s;
@@ -2727,10 +2702,11 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m)
     auto walk = [&](auto&& f) {
 #pragma unroll
         for (int r = 0; r < kSetRegC; ++r) f(r, key[r], valid(r));
-        for (int r = kSetRegC; r < per; ++r) {
-            const bool v = valid(r);
-            f(r, v ? qk[tid + (r0 + r) * kScanThreads] : 0u, v);
-        }
+        if (OVF)
+            for (int r = kSetRegC; r < per; ++r) {
+                const bool v = valid(r);
+                f(r, v ? qk[tid + (r0 + r) * kScanThreads] : 0u, v);
+            }
     };
     // the key range over every stretch
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
@@ -2886,6 +2862,44 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m)
         st->tie_rule = DGC_TIES_SET;
     }
     SET_STAMP(4);
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m) {
+    int t;
+    uint32_t b;
+    const uint32_t bx = blockIdx.x, base_blocks = (uint32_t)(kSetG * w.T);
+    if (bx < base_blocks) {
+        t = (int)(bx / kSetG);
+        b = bx % kSetG;
+    } else {
+        const uint32_t e = bx - base_blocks;
+        int j = 0;
+        while (j + 1 < m.n && (uint32_t)m.first[j + 1] <= e) ++j;
+        t = m.t[j];
+        b = kSetG + (e - (uint32_t)m.first[j]);
+    }
+    SelState* st = w.st + t;
+    if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
+    const TDesc d = w.td[t];   // by value: stores below cannot alias it
+    const uint32_t Gt = d.big >= 0 ? (uint32_t)(kSetG + m.first[d.big + 1] - m.first[d.big]) : (uint32_t)kSetG;
+    const int64_t n64 = st->n_cur;
+    if (d.k < 1 || n64 <= d.k) return;
+    // this set's workgroups: one up to kSetCoopMin candidates, else kSetG, and for a big
+    // tensor as many as keep its stretches in registers (up to Gt); each stretch's rounds
+    // past the registers are read from L2 on every walk, up to kSetRoundsMax per stretch
+    const int rounds = (int)((n64 + kScanThreads - 1) / kScanThreads);
+    uint32_t G = 1;
+    if (n64 > kSetCoopMin) {
+        const uint32_t want = (uint32_t)((rounds + kSetRegC - 1) / kSetRegC);
+        G = want > (uint32_t)kSetG ? (want < Gt ? want : Gt) : (uint32_t)kSetG;
+    }
+    const int per = (rounds + (int)G - 1) / (int)G;
+    if (per > kSetRoundsMax || b >= G) return;   // (past kSetRoundsMax: the replay)
+    if (per > kSetRegC)
+        resample_set_body<true>(vec_flat, w, o, t, b, G, per, rounds, st, d);
+    else
+        resample_set_body<false>(vec_flat, w, o, t, b, G, per, rounds, st, d);
 }
 
 

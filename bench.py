@@ -656,12 +656,27 @@ def main():
            for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
+    # the collectives the timed steps issue (counted on the host: each is one Python call)
+    counts = {"all_gather_into_tensor": 0, "all_reduce": 0}
+    saved = {name: getattr(dist, name) for name in counts}
+    if coll:
+        def counted(name):
+            fn = saved[name]
+
+            def wrapper(*a, **kw):
+                counts[name] += 1
+                return fn(*a, **kw)
+            return wrapper
+        for name in counts:
+            setattr(dist, name, counted(name))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         run.step(i, evs[i])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    for name, fn in saved.items():
+        setattr(dist, name, fn)
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -740,6 +755,8 @@ def main():
         "compensate_ms_per_step": [round(e["compensate"][0].elapsed_time(e["compensate"][1]), 3) for e in evs],
         "selection": info,
     }
+    if coll:
+        res["collectives_per_step"] = {name: c / args.steps for name, c in counts.items()}
     if xgmi is not None and world == 1:   # --rccl-one-rank: the collective's own cost, no link traffic
         res["allgather"] = dict({"payload_bytes_per_rank": run.payload,
                                  "note": "one rank: the RCCL collectives' cost without link traffic"}, **xgmi)
