@@ -460,4 +460,61 @@ __device__ __forceinline__ bool last_block_arrival8(uint32_t* tk, uint32_t lb, u
     return is_last;
 }
 
+// ---------------------------------------------------------------- chained launches
+// The end of one phase of a chained launch (k_chain_one, k_rs_passes), by the whole
+// workgroup. Its stores are drained into its XCD's L2 and its completed virtual blocks
+// added to its XCD's count (done[8]: one word per XCD, so a count > 0 also says the XCD
+// holds writes of the phase). Once all nvb blocks are done, ONE workgroup per such XCD
+// writes that XCD's L2 back (agent release; `xrel[x]` elects it, `rel` counts them) —
+// not every workgroup: each release writes back the whole XCD L2, ~1.7-6.5 us
+// (MI355X_MICROARCH.md §inter-workgroup visibility), and a phase of 2048 workgroups paid
+// it 2048 times. Then every workgroup acquires (its CU's L1) and goes on. Words zero at
+// the start of the call. (The s_waitcnt after the release: the ROCm 7.2 hazard that can
+// drop it; after the acquire: its invalidate completes asynchronously.)
+struct ChainPhase {
+    uint32_t done[8];
+    uint32_t rel;
+    uint32_t xrel[8];
+    uint32_t pad[15];
+};
+static_assert(sizeof(ChainPhase) == 128, "one 128-B line per phase");
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x & 7u;
+}
+
+__device__ __forceinline__ void chain_phase_end(ChainPhase* cp, uint32_t mine, uint32_t nvb) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t x = xcc_id();
+        if (mine) __hip_atomic_fetch_add(&cp->done[x], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t m = 0;
+        for (;;) {
+            uint32_t tot = 0;
+            m = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t c = __hip_atomic_load(&cp->done[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tot += c;
+                m |= (c ? 1u : 0u) << i;
+            }
+            if (tot >= nvb) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (((m >> x) & 1u) && atomicCAS(&cp->xrel[x], 0u, 1u) == 0u) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&cp->rel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        while (__hip_atomic_load(&cp->rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)__popc(m))
+            __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 }  // namespace dgc

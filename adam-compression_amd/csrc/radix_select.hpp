@@ -621,21 +621,22 @@ __global__ void __launch_bounds__(kBlock) k_rs_hist(Src src, int pass) {
     rs_hist_body(src, pass, (int)blockIdx.x);
 }
 
-// The three passes in ONE launch (a source with chain words, src.chain(): 8 words, zero
-// at rest): when no task is active — every window was selected in one workgroup, the
+// The three passes in ONE launch (a source with chain words, src.chain(): 128 words,
+// zero at rest): when no task is active — every window was selected in one workgroup, the
 // steady state — every workgroup returns at once (three gated launches were ~15 us of a
 // flat-1B step). Otherwise the passes run in order over virtual blocks claimed from an
-// atomic counter, a workgroup waiting for a pass's completion count (one agent-scope
-// release per workgroup and pass, an acquire before the next); only running workgroups
-// claim blocks, so nothing assumes the grid co-resident. The last workgroup out
-// re-zeroes the words.
+// atomic counter, a workgroup waiting for a pass's completion count (chain_phase_end:
+// one L2 write-back per XCD and pass, an acquire per workgroup); only running
+// workgroups claim blocks, so nothing assumes the grid co-resident. The last workgroup
+// out re-zeroes the words.
 template <class Src>
 __global__ void __launch_bounds__(kBlock) k_rs_passes(Src src, int grid, int ntasks) {
     __shared__ uint32_t s_u;
     bool mine_any = false;   // a task with blocks that the one-workgroup selections left to the passes
     for (int t = threadIdx.x; t < ntasks; t += blockDim.x) mine_any |= src.blocks(t) > 0 && src.active(t);
     if (!__syncthreads_or(mine_any)) return;   // uniform; no task turns active during the call
-    uint32_t* cc = src.chain();   // [0..2] claims, [3..5] completions, [6] workgroups out
+    uint32_t* cc = src.chain();   // [0..2] claims, [3] workgroups out; a ChainPhase per pass from word 32
+#pragma unroll 1   // (unrolled, the three passes' bodies took 156 VGPRs: 3 waves per SIMD against 7)
     for (int pass = 0; pass < 3; ++pass) {
         uint32_t mine = 0;
         for (;;) {
@@ -647,20 +648,11 @@ __global__ void __launch_bounds__(kBlock) k_rs_passes(Src src, int grid, int nta
             rs_hist_body(src, pass, (int)vb);
             ++mine;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            if (mine) __hip_atomic_fetch_add(&cc[3 + pass], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (__hip_atomic_load(&cc[3 + pass], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)grid)
-                __builtin_amdgcn_s_sleep(2);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        __syncthreads();
+        chain_phase_end(reinterpret_cast<ChainPhase*>(cc + 32) + pass, mine, (uint32_t)grid);
     }
     if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(&cc[6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
-        for (int i = 0; i < 7; ++i) __hip_atomic_store(&cc[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&cc[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
+        for (int i = 0; i < 32 + 3 * 32; ++i) __hip_atomic_store(&cc[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The three histogram passes over any task source; every active task's state must

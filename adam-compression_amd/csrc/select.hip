@@ -102,6 +102,8 @@ constexpr int kSetRoundsMax = 64;
 constexpr int64_t kSetMax = (int64_t)kSetG * kSetRegC * 1024;
 constexpr int kBigMax = 64;
 constexpr int kSpecWords = 8;                   // per-tensor speculation state (dgc_compress_begin: spec)
+constexpr int kChainOneWords = 256;             // SelWS::chain: k_chain_one's words (zeroed every call) ...
+constexpr int kChainWords = kChainOneWords + 128;   // ... then k_rs_passes' (zero at rest)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
@@ -384,7 +386,7 @@ static SelWS carve_select(void* base, const Layout& L, size_t* bytes = nullptr) 
     w.nthg = c.take<NthG>(L.T);
     w.setg = c.take<SetG>(L.T);
     w.fin_ticket = c.take<uint32_t>(16);
-    w.chain = c.take<uint32_t>(32);
+    w.chain = c.take<uint32_t>(kChainWords);
     if (bytes) *bytes = c.bytes();
     return w;
 }
@@ -783,11 +785,10 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = 0;
         sg.mn = 0xFFFFFFFFu;
         sg.mx = 0;
-        if (t == 0) {
-            *w.fin_ticket = 0;
-            for (int i = 0; i < 24; ++i) w.chain[i] = 0;   // k_chain_one's (24..31: k_rs_passes', zero at rest)
-        }
+        if (t == 0) *w.fin_ticket = 0;
     }
+    if (t == 0)   // k_chain_one's words (k_rs_passes', past kChainOneWords, are zero at rest)
+        for (int i = threadIdx.x; i < kChainOneWords; i += blockDim.x) w.chain[i] = 0;
     __syncthreads();   // the caller's threshold (thr[t]) is written
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
@@ -802,7 +803,9 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         if (v) atomicAdd(&spills, v);
         st->spill[e ^ 1][threadIdx.x] = 0;   // slot of the next call's K1
     }
-    if (threadIdx.x == 0) st->win_cnt[e ^ 1] = 0;
+    if (threadIdx.x == 0) {
+        st->win_cnt[e ^ 1] = 0;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         const float t0 = w.thr[t];
@@ -981,7 +984,7 @@ struct SampleKeys {
     }
     __device__ __forceinline__ RSState* state(int t) const { return w.rs + t; }
     __device__ __forceinline__ float* out(int t) const { return w.thr + t; }
-    __device__ __forceinline__ uint32_t* chain() const { return w.chain + 24; }   // k_rs_passes
+    __device__ __forceinline__ uint32_t* chain() const { return w.chain + kChainOneWords; }   // k_rs_passes
     // the final pass's last workgroup: the threshold is known, reset the selection state
     __device__ __forceinline__ void done(int t) const { sel_init_tensor(w, t, 1); }
     template <class F>
@@ -1664,41 +1667,42 @@ k_emit(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
 }
 
 // One-tensor DGC_SYNC_DEVICE selections with the lowering shortcut (the flat bucket):
-// every pass after the first count — the full select pass, the lowering from the lists
-// and over vec, the count at the lowered threshold (lists, or a full pass), and the
-// emit / K5 gather — in ONE launch instead of six. In the steady state the first count
-// already wrote the first-k payload (k_count_emit, spec_emitted) and every workgroup
-// returns at once: the six gated no-op launches cost ~30 us of a flat-1B step (same box,
-// measured by leaving them out). Otherwise the phases run in order over virtual blocks
-// that workgroups claim from an atomic counter; each phase's gate is decided once, by
-// the first workgroup to reach it, from the state the phases before left; a workgroup
-// waits for a phase's completion count (one agent-scope release per workgroup and phase,
-// an acquire before going on) before the next phase. Only running workgroups claim
-// blocks, so nothing assumes the grid co-resident.
-constexpr int kChainPhases = 6;
-enum { CH_CLAIM = 0, CH_DONE = kChainPhases, CH_GATE = 2 * kChainPhases };
-static_assert(3 * kChainPhases <= 32, "SelWS::chain words");
-static_assert(kEmitSegs == kBlock, "k_chain_one runs the emit with kBlock threads");
+// the lowering from the lists, the lowering over vec and the count at the lowered
+// threshold from the lists — three launches that are gated no-ops in the steady state —
+// in ONE launch. The two full select passes and the emit stay launches of their own:
+// chained, their HBM-bound bodies ran at the combined kernel's 2 waves per SIMD
+// (177 VGPRs) and a step whose lists missed took 0.43 ms longer (flat-1B, same box). When
+// every tensor is decided (the steady state: the first count's decide) every workgroup
+// returns at once. Otherwise the phases run in order
+// over virtual blocks that workgroups claim from an atomic counter; each phase's gate is
+// decided once, by the first workgroup to reach it, from the state the phases before
+// left; a workgroup waits for a phase's completion count (chain_phase_end: one L2
+// write-back per XCD that wrote, an acquire per workgroup) before the next phase. Only
+// running workgroups claim blocks, so nothing assumes the grid co-resident.
+constexpr int kChainPhases = 3;
+enum { CH_CLAIM = 0, CH_GATE = kChainPhases };   // words of the first line; then a ChainPhase each
+static_assert(32 + kChainPhases * 32 <= kChainOneWords, "SelWS::chain words");
 
 template <bool ALIGNED>
-__global__ void __launch_bounds__(kBlock)   // (2 waves per SIMD: 16 loads in flight per wave keep a full pass HBM-bound)
-k_chain_one(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut e) {
-    const SelState* st = w.st;
+__global__ void __launch_bounds__(kBlock)
+k_chain_one(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     uint32_t* cc = w.chain;
     __shared__ uint32_t s_u;
-    if (threadIdx.x == 0) s_u = (st->done && st->spec_emitted) ? 1u : 0u;
-    __syncthreads();
-    if (s_u) return;   // uniform: the payload stands
+    bool open = false;   // a tensor still adapting (every phase below gates on that)
+    for (int t = threadIdx.x; !open && t < w.T; t += blockDim.x) open = !w.st[t].done;
+    if (!__syncthreads_or(open)) return;   // uniform: the steady state
     for (int ph = 0; ph < kChainPhases; ++ph) {
-        __syncthreads();   // (s_u is reused)
+        // does any tensor need the phase
+        bool any = false;
+        for (int t = threadIdx.x; !any && t < w.T; t += blockDim.x) {
+            const SelState& u = w.st[t];
+            any = ph < 2 ? u.lower_pending != 0 : (u.active && u.t_cur >= u.t_list);
+        }
+        any = __syncthreads_or(any);   // (also: s_u is free again)
         if (threadIdx.x == 0) {
             uint32_t gate = __hip_atomic_load(&cc[CH_GATE + ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (gate == 0) {
-                bool run = true;   // the emit / gather: its body gates itself
-                if (ph == 0 || ph == 4) run = st->active && !(st->t_cur >= st->t_list);
-                else if (ph == 1 || ph == 2) run = st->lower_pending != 0;
-                else if (ph == 3) run = st->active && st->t_cur >= st->t_list;
-                const uint32_t want = run ? 2u : 1u;
+                const uint32_t want = any ? 2u : 1u;
                 const uint32_t prev = atomicCAS(&cc[CH_GATE + ph], 0u, want);
                 gate = prev == 0u ? want : prev;
             }
@@ -1706,9 +1710,8 @@ k_chain_one(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut e) {
         }
         __syncthreads();
         if (s_u != 2u) continue;   // uniform
-        const int which = (ph == 0 || ph == 4) ? BT_CAP16 : ph == 1 ? BT_SEG : ph == 2 ? BT_CAP4
-                          : ph == 3 ? BT_CNT : BT_GRP;
-        const uint32_t nvb = (uint32_t)w.bt[which][1];
+        const int which = ph == 0 ? BT_SEG : ph == 1 ? BT_CAP4 : BT_CNT;
+        const uint32_t nvb = (uint32_t)w.bt[which][w.T];
         uint32_t mine = 0;
         for (;;) {
             __syncthreads();
@@ -1716,23 +1719,12 @@ k_chain_one(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut e) {
             __syncthreads();
             const uint32_t vb = s_u;
             if (vb >= nvb) break;   // uniform
-            if (ph == 0 || ph == 4) select_pass_body<ALIGNED>(vec_flat, w, BT_CAP16, p, vb);
-            else if (ph == 1) lower_lists_body(vec_flat, w, p, vb);
-            else if (ph == 2) lower_counts_body<ALIGNED>(vec_flat, w, p, vb);
-            else if (ph == 3) count_lists_body(vec_flat, w, p, vb);
-            else emit_body(vec_flat, w, e, vb);
+            if (ph == 0) lower_lists_body(vec_flat, w, p, vb);
+            else if (ph == 1) lower_counts_body<ALIGNED>(vec_flat, w, p, vb);
+            else count_lists_body(vec_flat, w, p, vb);
             ++mine;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's stores are in L2
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            if (mine) __hip_atomic_fetch_add(&cc[CH_DONE + ph], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (__hip_atomic_load(&cc[CH_DONE + ph], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nvb)
-                __builtin_amdgcn_s_sleep(2);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        __syncthreads();
+        chain_phase_end(reinterpret_cast<ChainPhase*>(cc + 32) + ph, mine, nvb);
     }
 }
 
@@ -3139,11 +3131,13 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
                          sink, 0u, order_out, margin_max};
     bool finished = false;   // the payload count and records are written
-    // one tensor, device decisions, the lowering shortcut: the passes after the first
-    // count and the gather in one launch (k_chain_one); DGC_NO_CHAIN=1 (A/B runs) launches
-    // them one by one
+    // one tensor, device decisions, the lowering shortcut: the lowering and the count at
+    // the lowered threshold in one launch (k_chain_one); DGC_NO_CHAIN=1 (A/B runs)
+    // launches them one by one
     static const bool no_chain = std::getenv("DGC_NO_CHAIN") != nullptr;
-    const bool chained = L.T == 1 && keep_lists && sync_mode == DGC_SYNC_DEVICE && lower_fast && !no_chain;
+    static const bool chain_batch = std::getenv("DGC_CHAIN_BATCH") != nullptr;   // (A/B: the batches too)
+    const bool chained = (L.T == 1 || chain_batch) && keep_lists && sync_mode == DGC_SYNC_DEVICE && lower_fast &&
+                         !no_chain;
     EmitOut g = o;   // the K5 gather (+ every other tensor's payload)
     g.queue = w.queue;
     g.cand = w.cand_idx;
@@ -3152,7 +3146,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
-        if (!chained) DGC_TRY(launch_emit(L, vec, w, g, s));
+        DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
             SetMap m{};
             m.n = L.nbig;
@@ -3185,16 +3179,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_LAUNCHED();
         return DGC_OK;
     };
-    DGC_TRY(keep_lists ? pass(chained ? 1 : 3, true, fuse) : pass(2, false));
-    if (chained) {
-        const unsigned grid = (unsigned)std::min<int64_t>(
-            kCapBlocks, std::max({L.grid[BT_CAP16], L.grid[BT_SEG], L.grid[BT_CAP4], L.grid[BT_CNT], L.grid[BT_GRP]}));
-        if (al)
-            hipLaunchKernelGGL(k_chain_one<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p, g);
-        else
-            hipLaunchKernelGGL(k_chain_one<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, p, g);
-        DGC_LAUNCHED();
-    }
+    DGC_TRY(keep_lists ? pass(3, true, fuse) : pass(2, false));
     bool emitted = false;   // the payload of every non-K5 tensor is written
     if (sync_mode == DGC_SYNC_HOST) {
         // read the decisions back and launch only what they need
@@ -3229,8 +3214,15 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
     } else if (L.adapt_any) {
         // every kernel below early-exits on a device flag when it is not needed
-        if (chained) {
-            // (k_chain_one ran them)
+        if (chained) {   // lower() and pass(3)'s count in one launch, then its full pass
+            const unsigned grid = (unsigned)std::min<int64_t>(
+                kCapBlocks, std::max({L.grid[BT_SEG], L.grid[BT_CAP4], L.grid[BT_CNT]}));
+            if (al)
+                hipLaunchKernelGGL(k_chain_one<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
+            else
+                hipLaunchKernelGGL(k_chain_one<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
+            DGC_LAUNCHED();
+            DGC_TRY(pass(2, true));
         } else if (lower_fast) {
             DGC_TRY(lower());
             DGC_TRY(pass(3, true));
@@ -3544,7 +3536,7 @@ int batch_init(const dgc_batch_desc* b, void* ws, size_t ws_bytes, hipStream_t s
     SelWS w = carve_select(ws, L);
     DGC_HIP(hipMemsetAsync(w.st, 0, sizeof(SelState) * L.T, s));
     DGC_HIP(hipMemsetAsync(w.setg, 0, sizeof(SetG) * L.T, s));                         // zero at rest
-    DGC_HIP(hipMemsetAsync(w.chain, 0, 32 * sizeof(uint32_t), s));                     // zero at rest
+    DGC_HIP(hipMemsetAsync(w.chain, 0, kChainWords * sizeof(uint32_t), s));            // zero at rest
     DGC_HIP(hipMemsetAsync(w.samples, 0, sizeof(float) * L.nsamp, s));   // the window histograms: zero at rest
     DGC_HIP(hipMemcpyAsync(w.td, td.data(), sizeof(TDesc) * L.T, hipMemcpyHostToDevice, s));
     for (int which = 0; which < BT_COUNT; ++which)
