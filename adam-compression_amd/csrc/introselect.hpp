@@ -80,8 +80,9 @@ __shared__ unsigned int k5_lsteps[4];
          if (blockIdx.x < 64) g_k5prof.bt[blockIdx.x][i] = t_; } } while (0)
 #define K5_STEP(i) \
     do { if (threadIdx.x == 0) k5_lsteps[i] += 1; } while (0)
+// (in resample_set_body: the set's first workgroup, slot = tensor)
 #define SET_STAMP(i) \
-    do { if (threadIdx.x == 0 && blockIdx.x < 64) g_k5prof.set[blockIdx.x][i] = wall_clock64(); } while (0)
+    do { if (threadIdx.x == 0 && b == 0 && t < 64) g_k5prof.set[t][i] = wall_clock64(); } while (0)
 #define K5_SUB_BEGIN() unsigned long long k5_t0 = wall_clock64()
 #define K5_SUB(i, global) \
     do { if ((global) && threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); \

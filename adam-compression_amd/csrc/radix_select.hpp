@@ -492,6 +492,7 @@ __device__ __forceinline__ void rs_window_wg(const float* __restrict__ x, int64_
         const uint32_t a = sel_above;
         __syncthreads();   // every thread has read sel_*
         for (int b = tid; b < kBins; b += kScanThreads) h[b] = 0;
+        __syncthreads();   // zeroed before the next pass's adds (a wave ahead lost counts to a late zero)
         if (sb < 0) {   // (cannot happen: k <= n)
             if (tid == 0) *out = __uint_as_float(0x7FC00000u);
             __syncthreads();

@@ -91,16 +91,19 @@ constexpr float kSpecCeil0 = 0.95f;
 constexpr float kSpecMarginMax = 0.985f;
 constexpr float kSpecCeilUp = 0.005f, kSpecCeilDown = 0.05f;
 // K5s, the set path of an untied resample (resample_order = 1; see k_resample_set): one
-// launch, kSetG workgroups per tensor, kSetRegC rounds of 1024 keys per workgroup in
-// registers (32 spilled the radix passes' registers to scratch) — kSetMax candidates;
-// a tensor whose capacity exceeds that (VGG-16-BN's fc6: 6.5M) gets up to kSetGBig
-// workgroups (for up to kBigMax such tensors per call), kSetRoundsMax rounds each.
+// launch, workgroups per tensor by its candidate capacity (BT_SET) — one up to
+// kSetCoopMin, kSetG up to kSetG x kSetCoopMin, up to kSetGBig beyond (VGG-16-BN's fc6) —
+// kSetRegC rounds of 1024 keys per workgroup in registers (32 spilled the radix
+// passes' registers to scratch), up to kSetRoundsMax rounds from L2 beyond.
 constexpr int kSetG = 16;
 constexpr int kSetGBig = 128;
 constexpr int kSetRegC = 16;
 constexpr int kSetRoundsMax = 64;
-constexpr int64_t kSetMax = (int64_t)kSetG * kSetRegC * 1024;
-constexpr int kBigMax = 64;
+constexpr int64_t kSetCoopMin = (int64_t)kSetRegC * 1024;   // (kScanThreads keys per round)
+// its radix select: two passes over key - key(t_cur), bits [kSetLo0, kSetSpan) clamped
+// (the top bin takes every key past the span) then [0, kSetLo0)
+constexpr int kSetSpan = 25, kSetLo0 = 13;
+constexpr int kSetBins0 = 1 << (kSetSpan - kSetLo0), kSetBins1 = 1 << kSetLo0;   // 4096, 8192
 constexpr int kSpecWords = 8;                   // per-tensor speculation state (dgc_compress_begin: spec)
 constexpr int kChainOneWords = 256;             // SelWS::chain: k_chain_one's words (zeroed every call) ...
 constexpr int kChainWords = kChainOneWords + 128;   // ... then k_rs_passes' (zero at rest)
@@ -126,7 +129,6 @@ struct TDesc {
     double inv_stride;
     float inv_stride_f;
     int32_t tail;           // the elements [4*nv4, n) are compensated outside K1 (unpadded)
-    int32_t big;            // its K5s extra workgroups (SetMap index), -1: none
 };
 
 struct SelState {
@@ -169,7 +171,7 @@ struct SetG {
     uint32_t arrive, decide, bar_count, bar_gen, broken;
     uint32_t mn, mx;
     uint32_t cnt[kSetGBig];                 // per workgroup: its candidates >= the k-th key
-    uint32_t hist[3][kRsBins];
+    uint32_t hist0[kSetBins0], hist1[kSetBins1];   // the radix passes' merged histograms
 };
 
 // Per-call settings shared by the tensors.
@@ -182,7 +184,7 @@ struct SelCfg {
 };
 
 // Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
-enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_CNT, BT_COUNT };
+enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_CNT, BT_SET, BT_COUNT };
 
 struct SelWS {
     int32_t T;
@@ -242,9 +244,6 @@ struct Layout {
     bool adapt_any = false;     // some tensor has N > S (the adaptation loop can run)
     bool tail_any = false;      // some tensor is compensated partly outside K1 (unpadded tail)
     int64_t grid[BT_COUNT] = {};
-    int32_t nbig = 0;           // tensors whose candidates may exceed kSetMax (K5s extra workgroups)
-    int32_t big[kBigMax] = {};
-    int32_t big_first[kBigMax + 1] = {};   // their extra workgroups (SetMap)
 };
 
 // Capped grids serve the launches that are most likely gated no-ops (the list count
@@ -264,6 +263,10 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, in
         case BT_CNT: return ceil_div(d.nseg, (int64_t)kBlock * kCountSegs);
         case BT_GRP: return ceil_div(d.nseg, (int64_t)(kGroupSegs / kEmitSplit));
         case BT_QUEUE: return ceil_div(d.k, (int64_t)kQueuePerBlock);
+        case BT_SET:   // K5s: a resample set holds count(t_cur) <= cand_cap > k candidates
+            if (d.k < 1 || d.cand_cap <= d.k) return 0;
+            if (d.cand_cap <= kSetCoopMin) return 1;
+            return std::min<int64_t>(kSetGBig, std::max<int64_t>(kSetG, ceil_div(d.cand_cap, kSetCoopMin)));
         case BT_SAMP: {
             const int64_t cnt = d.samp_off < 0 ? d.n : d.S + 1;
             if (cnt <= kSmallN) return 0;   // one-workgroup threshold (k_rs_small_multi)
@@ -312,14 +315,6 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         L.max_cand = std::max(L.max_cand, d.cand_cap);
         d.gpos_off = gpos;
         gpos += 2 * (d.cand_cap / 2 + 1);
-        d.big = -1;
-        if (d.cand_cap > kSetMax && L.nbig < kBigMax) {   // K5s workgroups to hold its stretches in registers
-            const int64_t want = ceil_div(d.cand_cap, (int64_t)kSetRegC * 1024);
-            d.big = L.nbig;
-            L.big[L.nbig] = t;
-            L.big_first[L.nbig + 1] = L.big_first[L.nbig] + (int32_t)(std::min<int64_t>(want, kSetGBig) - kSetG);
-            ++L.nbig;
-        }
         d.idx_base = T > 1 ? d.off : 0;
         d.nv4 = padded ? ceil_div(d.n, (int64_t)4) : d.n / 4;
         d.tail = (!padded && (d.n & 3)) ? 1 : 0;
@@ -2577,18 +2572,18 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // across the k boundary (#keys >= kth == k) every top-k is that set, whatever order
 // and tie rule produced it, so it is emitted in index order and the exact replay (K5)
 // skips the tensor (rs_nth = 3). Tied, the replay runs as always. The k-th largest is
-// found by a radix select over key - min in up to three 11-bit passes (the candidates
-// of one tensor span a few octaves: relative to the minimum their top bits spread over
-// the bins instead of piling into the few bins of their exponents); the emit carries
-// the wire casts and the masking of the K5 emit.
+// found by a radix select over key - key(t_cur) (every candidate is >= t_cur) in three
+// 11-bit passes over the open range up to 0x7FFFFFFF; the emit carries the wire casts
+// and the masking of the K5 emit.
 //
-// Over G co-resident workgroups of ONE launch (kSetG per tensor; up to kSetGBig for a
-// tensor whose capacity exceeds kSetMax — VGG-16-BN's fc6, where four sliced launches
-// k_bigset_* ran as no-ops every step before): a set of more than kSetRegC x 1024
-// candidates is cut into G contiguous
-// stretches of rounds, each workgroup's keys in its registers; the key range, the radix
-// passes' histograms and the per-stretch counts go through device atomics with a
-// barrier between the phases (min / max | pass 1 | pass 2 [| pass 3] | counts), and each
+// Over G co-resident workgroups of ONE launch (the tensor's BT_SET workgroups: kSetG,
+// up to kSetGBig for a capacity past kSetG x kSetCoopMin — VGG-16-BN's fc6, where four
+// sliced launches k_bigset_* ran as no-ops every step before; one for a capacity up to
+// kSetCoopMin, and none for a tensor that cannot resample — a fixed 16 per tensor took
+// ~10 us to dispatch): a set of more than kSetCoopMin candidates is cut into G contiguous
+// stretches of rounds, each workgroup's keys in its registers; the radix passes'
+// histograms and the per-stretch counts go through device atomics with a barrier
+// between the phases (pass 1 | pass 2 | pass 3 | counts), and each
 // workgroup emits its stretch's selected entries at the count of the stretches before
 // it plus their order inside it — the index order, as one workgroup emits it. A set of
 // up to kSetRegC x 1024 candidates takes the same code on one workgroup, with no
@@ -2599,7 +2594,7 @@ static_assert(kK5SmemBytes <= 160 * 1024 - 1024, "K5 / K5b LDS");
 // (ResNet-50's 72k-candidate resample: one workgroup walked its keys six times, 24 of
 // 72 rounds from L2 — 59 us of the step.)
 constexpr uint64_t kSetArriveTicks = 200000;   // 2 ms of the 100 MHz wall clock
-constexpr int64_t kSetCoopMin = (int64_t)kSetRegC * kScanThreads;   // above: kSetG workgroups
+static_assert(kSetCoopMin == (int64_t)kSetRegC * kScanThreads, "K5s: one workgroup holds kSetCoopMin keys");
 
 __device__ __forceinline__ bool setg_consensus(SetG* g, uint32_t G) {
     __shared__ uint32_t verdict;
@@ -2653,15 +2648,6 @@ __device__ __forceinline__ void setg_barrier(SetG* g, uint32_t G) {
     __syncthreads();
 }
 
-// The grid: kSetG workgroups per tensor, then kSetGBig - kSetG more for each tensor whose
-// candidate capacity exceeds kSetMax (SetMap; up to kBigMax of them, the rest of such
-// a tensor's sets above kSetMax go to the replay).
-struct SetMap {
-    int32_t n;                    // tensors with extra workgroups
-    int32_t t[kBigMax];           // their ids
-    int32_t first[kBigMax + 1];   // their extra workgroups' first block after kSetG x T
-};
-
 // (OVF: a stretch longer than the registers hold — a set above ~2M candidates; the
 // common case compiles without the L2 rounds)
 template <bool OVF>
@@ -2676,11 +2662,10 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
     const uint32_t k = (uint32_t)d.k;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int kWaves = kScanThreads / kWave;
-    __shared__ uint32_t h[kRsBins];
+    __shared__ uint32_t h[kSetBins1];
     __shared__ uint32_t lds32[16];
-    __shared__ uint32_t red[2][kWaves];
     __shared__ uint32_t rbase[(OVF ? kSetRoundsMax : kSetRegC) * kWaves];
-    __shared__ uint32_t sel_above, sel_cnt, s_mn, s_mx, s_base, s_stop;
+    __shared__ uint32_t sel_above, sel_cnt, s_base, s_stop;
     __shared__ int sel_bin;
     __shared__ long long obase_s;
     // this workgroup's stretch of rounds; queue entry i = tid + r * 1024 (coalesced)
@@ -2700,69 +2685,39 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
                 f(r, v ? qk[tid + (r0 + r) * kScanThreads] : 0u, v);
             }
     };
-    // the key range over every stretch
-    uint32_t mn = 0xFFFFFFFFu, mx = 0;
-    walk([&](int, uint32_t kk, bool v) {
-        if (v) {
-            mn = kk < mn ? kk : mn;
-            mx = kk > mx ? kk : mx;
-        }
-    });
-    mn = wave_min_u32(mn);
-    mx = wave_max(mx);
-    if (lane == 0) {
-        red[0][wv] = mn;
-        red[1][wv] = mx;
-    }
-    for (int q = tid; q < kRsBins; q += kScanThreads) h[q] = 0;
+    // the key range: every candidate has |x| >= t_cur (the gather's test), so key(t_cur)
+    // bounds it from below, and the two passes cover kSetSpan bits above it (4 octaves):
+    // the first pass's top bin also takes every key past that span, and should the k-th
+    // largest fall there the replay takes the tensor (exact either way). Two passes of
+    // 4096 and 8192 bins, not three of 2048: each pass of a cooperative set is a merge
+    // and a barrier (~5 us over 16 workgroups). A min/max phase over the keys cost a
+    // barrier too (2.2 us in one workgroup, 5.5 us over 16); an open range up to
+    // 0x7FFFFFFF piled the first pass into a few bins (LDS atomics on the same words:
+    // +8 us in one workgroup, tools/k5s_prof.py).
+    const uint32_t mn = abs_key(st->t_cur);
+    for (int q = tid; q < kSetBins1; q += kScanThreads) h[q] = 0;
     __syncthreads();
-    if (tid == 0) {
-        uint32_t a = red[0][0], c = red[1][0];
-#pragma unroll
-        for (int i = 1; i < kWaves; ++i) {
-            a = red[0][i] < a ? red[0][i] : a;
-            c = red[1][i] > c ? red[1][i] : c;
-        }
-        if (G > 1) {
-            if (a != 0xFFFFFFFFu) __hip_atomic_fetch_min(&g->mn, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_max(&g->mx, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            s_mn = a;
-            s_mx = c;
-        }
-    }
-    if (G > 1) {
-        setg_barrier(g, G);
-        if (tid == 0) {
-            s_mn = __hip_atomic_load(&g->mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_mx = __hip_atomic_load(&g->mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    mn = s_mn;
-    mx = s_mx;
     SET_STAMP(1);
-    // passes over the bits of key - mn, 11 at a time from the top (every workgroup picks
-    // the same bin from the same merged histogram)
-    const uint32_t span = mx - mn;
-    const int L = span ? 32 - __builtin_clz(span) : 0;
-    int hi = L, pass = 0;
+    static_assert(kSetBins0 == 4 * kScanThreads && kSetBins1 == 8 * kScanThreads, "pick_bin_small<4 | 8>");
+    int passes = 0;   // (whose merged histograms this workgroup re-zeroes its share of)
     uint32_t prefix = 0, k_rem = k;
     uint32_t kth = mn, eq = (uint32_t)n;
     bool ok = true;
-    while (hi > 0) {
-        const int lo = hi > 11 ? hi - 11 : 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t nb = pass == 0 ? (uint32_t)kSetBins0 : (uint32_t)kSetBins1;
         walk([&](int, uint32_t kk, bool v) {
             const uint32_t x = kk - mn;
-            if (v && (hi >= 32 || (x >> hi) == prefix)) atomicAdd(&h[(x >> lo) & ((1u << (hi - lo)) - 1u)], 1u);
+            if (!v) return;
+            if (pass == 0) atomicAdd(&h[min(x >> kSetLo0, nb - 1u)], 1u);
+            else if ((x >> kSetLo0) == prefix) atomicAdd(&h[x & (nb - 1u)], 1u);
         });
         __syncthreads();
-        if (G > 1) {
-            uint32_t* gh = g->hist[pass];
-            for (int q = tid; q < kRsBins; q += kScanThreads)
+        if (G > 1) {   // every workgroup picks the same bin from the same merged histogram
+            uint32_t* gh = pass == 0 ? g->hist0 : g->hist1;
+            for (int q = tid; q < (int)nb; q += kScanThreads)
                 if (h[q]) __hip_atomic_fetch_add(&gh[q], h[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             setg_barrier(g, G);
-            for (int q = tid; q < kRsBins; q += kScanThreads)
+            for (int q = tid; q < (int)nb; q += kScanThreads)
                 h[q] = __hip_atomic_load(&gh[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
         }
@@ -2770,7 +2725,9 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
         __syncthreads();
         int bin;
         uint32_t above;
-        if (pick_bin_small<2>(h, k_rem, lds32, &bin, &above)) {
+        const bool hit = pass == 0 ? pick_bin_small<4>(h, k_rem, lds32, &bin, &above)
+                                   : pick_bin_small<8>(h, k_rem, lds32, &bin, &above);
+        if (hit) {
             sel_bin = bin;
             sel_above = above;
             sel_cnt = h[bin];
@@ -2779,20 +2736,22 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
         const int sb = sel_bin;
         const uint32_t a = sel_above, c = sel_cnt;
         __syncthreads();   // every thread has read sel_*
-        for (int q = tid; q < kRsBins; q += kScanThreads) h[q] = 0;
-        ++pass;
-        if (sb < 0) {   // (cannot happen: k < n keys) — the replay takes it
-            ok = false;
+        for (int q = tid; q < (int)nb; q += kScanThreads) h[q] = 0;
+        __syncthreads();   // zeroed before the next pass's adds (a wave ahead lost counts to a late zero)
+        passes = pass + 1;
+        if (sb < 0 || (pass == 0 && sb == kSetBins0 - 1)) {   // (sb < 0 cannot happen: k < n keys)
+            ok = false;   // the k-th largest is 4 octaves or more above t_cur: the replay takes it
             break;
         }
-        prefix = (prefix << (hi - lo)) | (uint32_t)sb;
         k_rem -= a;
-        hi = lo;
-        if (lo == 0) {
-            kth = mn + prefix;
+        if (pass == 0) {
+            prefix = (uint32_t)sb;
+        } else {
+            kth = mn + ((prefix << kSetLo0) | (uint32_t)sb);
             eq = c;
         }
     }
+    __syncthreads();
     // tied across the boundary (more keys == kth than the k - #(> kth) still needed):
     // only torch's exact order of operations knows which ones — the replay
     if (eq != k_rem) ok = false;
@@ -2826,10 +2785,12 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
             if (__hip_atomic_load(&g->broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) s_stop = 1;
         }
         // every workgroup has read the histograms: re-zero this one's share of those used
-        const int share = (kRsBins + (int)G - 1) / (int)G;
-        const int qlo = (int)b * share, qhi = min(qlo + share, kRsBins);
-        for (int p = 0; p < pass; ++p)
-            for (int q = qlo + tid; q < qhi; q += kScanThreads) g->hist[p][q] = 0;
+        for (int p = 0; p < passes; ++p) {
+            const int nb = p == 0 ? kSetBins0 : kSetBins1, share = (nb + (int)G - 1) / (int)G;
+            uint32_t* gh = p == 0 ? g->hist0 : g->hist1;
+            const int qlo = (int)b * share, qhi = min(qlo + share, nb);
+            for (int q = qlo + tid; q < qhi; q += kScanThreads) gh[q] = 0;
+        }
     }
     if (wv == 0) {
         const long long ob = out_base(w, t);
@@ -2841,14 +2802,37 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
     const long long ob = obase_s + (long long)s_base;
     const int64_t* cand = w.cand_idx + d.cand_off;
     const float* cval = w.cand_val + d.cand_off;
-    walk([&](int r, uint32_t kk, bool v) {
-        const bool sel = v && kk >= kth;
-        const uint64_t mm = __ballot(sel);
-        if (sel) {
+    // the register rounds 8 at a time, every selected candidate's index and value loaded
+    // before the first store (the stores may alias the loads, so a round-by-round walk
+    // waited out a load round trip per round: 12 us for 16k candidates in one workgroup)
+    constexpr int kEmitRounds = 8;
+    static_assert(kSetRegC % kEmitRounds == 0, "emit batches");
+#pragma unroll
+    for (int r0b = 0; r0b < kSetRegC; r0b += kEmitRounds) {
+        int64_t ci[kEmitRounds];
+        float cv[kEmitRounds];
+        bool sl[kEmitRounds];
+#pragma unroll
+        for (int j = 0; j < kEmitRounds; ++j) {
+            const int r = r0b + j;
+            sl[j] = valid(r) && key[r] >= kth;
             const int i = tid + (r0 + r) * kScanThreads;
-            emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(mm, 0u), cand[i], cval[i]);
+            ci[j] = sl[j] ? cand[i] : 0;
+            cv[j] = sl[j] ? cval[i] : 0.f;
         }
-    });
+#pragma unroll
+        for (int j = 0; j < kEmitRounds; ++j) {
+            const uint64_t mm = __ballot(sl[j]);
+            if (sl[j]) emit_one(o, d, ob + rbase[(r0b + j) * kWaves + wv] + mbcnt64(mm, 0u), ci[j], cv[j]);
+        }
+    }
+    if (OVF)
+        for (int r = kSetRegC; r < per; ++r) {
+            const int i = tid + (r0 + r) * kScanThreads;
+            const bool sel = valid(r) && qk[i] >= kth;
+            const uint64_t mm = __ballot(sel);
+            if (sel) emit_one(o, d, ob + rbase[r * kWaves + wv] + mbcnt64(mm, 0u), cand[i], cval[i]);
+        }
     if (b == 0 && tid == 0) {
         st->rs_nth = 3;   // K5's replay and emit skip the tensor
         st->tie_rule = DGC_TIES_SET;
@@ -2857,24 +2841,13 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
 }
 
 __global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m) {
-    int t;
-    uint32_t b;
-    const uint32_t bx = blockIdx.x, base_blocks = (uint32_t)(kSetG * w.T);
-    if (bx < base_blocks) {
-        t = (int)(bx / kSetG);
-        b = bx % kSetG;
-    } else {
-        const uint32_t e = bx - base_blocks;
-        int j = 0;
-        while (j + 1 < m.n && (uint32_t)m.first[j + 1] <= e) ++j;
-        t = m.t[j];
-        b = kSetG + (e - (uint32_t)m.first[j]);
-    }
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+    const int t = task(w, BT_SET, (int)blockIdx.x);
+    const uint32_t b = blockIdx.x - (uint32_t)w.bt[BT_SET][t];
     SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
-    const uint32_t Gt = d.big >= 0 ? (uint32_t)(kSetG + m.first[d.big + 1] - m.first[d.big]) : (uint32_t)kSetG;
+    const uint32_t Gt = (uint32_t)(w.bt[BT_SET][t + 1] - w.bt[BT_SET][t]);   // this tensor's workgroups
     const int64_t n64 = st->n_cur;
     if (d.k < 1 || n64 <= d.k) return;
     // this set's workgroups: one up to kSetCoopMin candidates, else kSetG, and for a big
@@ -2882,9 +2855,10 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, SetMap m)
     // past the registers are read from L2 on every walk, up to kSetRoundsMax per stretch
     const int rounds = (int)((n64 + kScanThreads - 1) / kScanThreads);
     uint32_t G = 1;
-    if (n64 > kSetCoopMin) {
+    if (n64 > kSetCoopMin) {   // (then Gt >= kSetG: n64 <= cand_cap)
         const uint32_t want = (uint32_t)((rounds + kSetRegC - 1) / kSetRegC);
         G = want > (uint32_t)kSetG ? (want < Gt ? want : Gt) : (uint32_t)kSetG;
+        G = G < Gt ? G : Gt;
     }
     const int per = (rounds + (int)G - 1) / (int)G;
     if (per > kSetRoundsMax || b >= G) return;   // (past kSetRoundsMax: the replay)
@@ -3147,13 +3121,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
         DGC_TRY(launch_emit(L, vec, w, g, s));
-        if (p.set_order) {   // K5s: an untied resample set in index order (the rest: the replay)
-            SetMap m{};
-            m.n = L.nbig;
-            for (int j = 0; j < L.nbig; ++j) m.t[j] = L.big[j];
-            for (int j = 0; j <= L.nbig; ++j) m.first[j] = L.big_first[j];
-            const unsigned grid = (unsigned)(kSetG * L.T + L.big_first[L.nbig]);
-            hipLaunchKernelGGL(k_resample_set, dim3(grid), dim3(kScanThreads), 0, s, vec, w, o, m);
+        if (p.set_order && L.grid[BT_SET] > 0) {   // K5s: an untied resample set in index order (the rest: the replay)
+            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.grid[BT_SET]), dim3(kScanThreads), 0, s, vec, w, o);
             DGC_LAUNCHED();
         }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);

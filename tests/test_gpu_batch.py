@@ -311,19 +311,20 @@ def test_batch_index_order_biased_samples():
     assert torch.equal(bs[0].velocity_of("a").view(torch.int32), bs[1].velocity_of("a").view(torch.int32))
 
 
-def designed_big_gradient(n, k, stride, start, seed):
+def designed_big_gradient(n, k, stride, start, seed, top=1.2):
     """A gradient whose resample has more candidates than one workgroup's set path, its
-    k-th largest magnitude untied and within an octave above the threshold: k distinct
-    magnitudes 1.2 + i * 2e-7 at positions the strided sample (start, stride) misses, a
-    plateau of 500k magnitudes exactly 1.0, N(0, 1e-3) elsewhere, random signs. The
-    samples see only the plateau, so the threshold is 1.0 and its count (~520k) passes
-    1.3k: resample over ~520k candidates, whose top k are the distinct ones."""
+    k-th largest magnitude untied and `top` / 1 above the threshold (within an octave by
+    default): k distinct magnitudes top + i * 2e-7 at positions the strided sample
+    (start, stride) misses, a plateau of 500k magnitudes exactly 1.0, N(0, 1e-3)
+    elsewhere, random signs. The samples see only the plateau, so the threshold is 1.0
+    and its count (~520k) passes 1.3k: resample over ~520k candidates, whose top k are
+    the distinct ones."""
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, generator=g) * 1e-3
     off = (start + stride // 2) % stride                      # a residue the samples never hit
     slots = torch.arange(off, n, stride)
     big = slots[torch.randperm(slots.numel(), generator=g)[:k]]
-    x[big] = 1.2 + torch.arange(k, dtype=torch.float64).mul(2e-7).float()
+    x[big] = (top + torch.arange(k, dtype=torch.float64).mul(2e-7)).float()
     rest = torch.ones(n, dtype=torch.bool)
     rest[big] = False
     cand = rest.nonzero().view(-1)
@@ -334,8 +335,8 @@ def designed_big_gradient(n, k, stride, start, seed):
 
 @pytest.mark.timeout(600)
 def test_batch_index_order_big_resample():
-    """The set path past kSetMax = 262144 candidates (a tensor whose capacity exceeds it
-    gets up to 128 co-resident workgroups in k_resample_set) against the exact replay: a
+    """The set path past 16 x 16384 = 262144 candidates (a tensor whose capacity exceeds
+    it gets up to 128 co-resident workgroups in k_resample_set) against the exact replay: a
     20M-element tensor (k = 20000, up to 64k = 1.28M candidates) whose first gradient
     (``designed_big_gradient``) resamples over ~520k candidates (32 workgroups), then
     random steps — the same sets, outputs and state as resample_order="topk"."""
@@ -382,3 +383,40 @@ def test_batch_index_order_big_resample():
         assert torch.equal(bs[0].velocity_of(name).view(torch.int32), bs[1].velocity_of(name).view(torch.int32))
         assert torch.equal(bs[0].momentum_of(name).view(torch.int32), bs[1].momentum_of(name).view(torch.int32))
     assert big_sets > 0
+
+
+@pytest.mark.timeout(600)
+def test_batch_index_order_wide_span_resample():
+    """A resample whose k-th largest is more than four octaves above the threshold (the
+    designed gradient with its k distinct magnitudes at 40, the plateau at 1.0): past
+    the set path's 25-bit key span above key(t_cur), so the exact replay takes the
+    tensor — the payload, velocity and momentum of resample_order="index" equal
+    resample_order="topk"'s bit for bit, in topk's order."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import random
+    from dgc.batch import DGCBatch
+    shapes = [("big", (20_000_000,)), ("small", (300, 1000))]
+    bs = [DGCBatch(shapes, compress_ratio=0.001, momentum=0.9, device=DEV, seed=5, resample_order=o)
+          for o in ("index", "topk")]
+    k, _, _, stride = bs[0].attrs[0]
+    start = random.Random(5).randint(0, stride - 1)
+    g = torch.randn(bs[0].flat_numel, generator=torch.Generator(device=DEV).manual_seed(78), device=DEV) * 1e-3
+    g[bs[0].offsets[0]: bs[0].offsets[0] + bs[0].numels[0]] = \
+        designed_big_gradient(bs[0].numels[0], k, stride, start, 100, top=40.0).to(DEV)
+    outs = []
+    for b in bs:
+        b.grad_flat.copy_(g)
+        b.compress()
+        outs.append(b.decompress().clone())
+    torch.cuda.synchronize()
+    ia, it = bs[0].infos(), bs[1].infos()
+    assert ia[0]["branch"] == "resample" and ia[0]["candidates"] > 262144, ia[0]
+    assert ia[0]["tie_rule"] != "set" and ia[0]["tie_rule"] == it[0]["tie_rule"], (ia[0], it[0])
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    sa, st = bs[0].transmitted()["big"], bs[1].transmitted()["big"]
+    assert torch.equal(sa[1], st[1])
+    assert np.array_equal(bits(sa[0].cpu().numpy()), bits(st[0].cpu().numpy()))
+    for name in bs[0].names:
+        assert torch.equal(bs[0].velocity_of(name).view(torch.int32), bs[1].velocity_of(name).view(torch.int32))
+        assert torch.equal(bs[0].momentum_of(name).view(torch.int32), bs[1].momentum_of(name).view(torch.int32))

@@ -1,7 +1,7 @@
-"""Where a model set's K5s time goes (k_resample_set, one workgroup per resampled
-tensor), in the bench's steady state: the profiling build's per-workgroup stamps —
-start, keys loaded, min/max, radix select, compaction counts + scan, positions
-written, emit end — for the last step.
+"""Where a model set's K5s time goes (k_resample_set), in the bench's steady state:
+the profiling build's stamps of each set's first workgroup — past the residency
+consensus, min/max merged, radix select, compaction counts merged, emit end — for
+the last steps.
 
   make -C adam-compression_amd/csrc k5prof
   python tools/k5s_prof.py [resnet50|vgg16_bn] [steps]
@@ -34,7 +34,9 @@ def main():
     L.dgc_k5_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
     run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, torch.device("cuda:0"))
     b = run.b
-    names = ("load", "minmax", "radix", "count", "positions", "emit")
+    # resample_set_body's stamps (the set's first workgroup): 0 past the residency
+    # consensus, 1 min/max merged, 2 radix select done, 3 compaction counts merged, 4 emit end
+    names = ("minmax", "radix", "compact", "emit")
     for i in range(steps):
         torch.cuda.synchronize()
         _lib.check(L.dgc_k5_prof(None, 1))
@@ -53,8 +55,7 @@ def main():
                      start=round((s[0] - t0) * 0.01, 2))
             for j, nm in enumerate(names):
                 r[nm] = round((s[j + 1] - s[j]) * 0.01, 2) if s[j + 1] and s[j] else None
-            r["end"] = round((s[6] - t0) * 0.01, 2) if s[6] else None
-            r["pass1"] = round((s[7] - s[2]) * 0.01, 2) if s[7] and s[2] else None   # of "radix"
+            r["end"] = round((s[4] - t0) * 0.01, 2) if s[4] else None
             rows.append(r)
         rows.sort(key=lambda r: -(r["end"] or 0))
         # k_nth_select after it (every workgroup stamps its start [7] and end [6]):
