@@ -782,8 +782,11 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         sg.mx = 0;
         if (t == 0) *w.fin_ticket = 0;
     }
-    if (t == 0)   // k_chain_one's words (k_rs_passes', past kChainOneWords, are zero at rest)
-        for (int i = threadIdx.x; i < kChainOneWords; i += blockDim.x) w.chain[i] = 0;
+    // k_chain_one's words (k_rs_passes', past kChainOneWords, are zero at rest); one store
+    // per thread (every caller runs >= kBlock threads): a strided loop here gave
+    // k_rs_small_multi a 320 B/lane scratch frame and doubled its time (15 -> 29 us)
+    static_assert(kChainOneWords <= kBlock, "sel_init_tensor: one chain word per thread");
+    if (t == 0 && threadIdx.x < kChainOneWords) w.chain[threadIdx.x] = 0;
     __syncthreads();   // the caller's threshold (thr[t]) is written
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
