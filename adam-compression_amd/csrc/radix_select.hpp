@@ -28,8 +28,16 @@ namespace dgc {
 
 constexpr int kRsBins = 2048;
 
-#ifndef RS_STAMP
-#define RS_STAMP(i) do { } while (0)   // tools/rsbench.hip: phase timestamps
+#ifdef DGC_K5_PROF
+// tools/k3_prof.py (profiling build, make k5prof): per-workgroup wall-clock stamps of the
+// one-workgroup thresholds (k_rs_small_multi, workgroup = task < 64) — 0 start, 1 keys
+// loaded + pass-0 floor, 2 floor picked, 3..8 each pass's histogram / pick, 9 threshold
+// written, 10 selection state reset, 11 kernel end
+__device__ unsigned long long g_rs_prof[64][12];
+#define RS_STAMP(i) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 64) g_rs_prof[blockIdx.x][i] = wall_clock64(); } while (0)
+#else
+#define RS_STAMP(i) do { } while (0)
 #endif
 constexpr int kSmallN = 32768;
 constexpr int kScanThreads = 1024;
@@ -290,6 +298,41 @@ __device__ __forceinline__ bool pick_bin_small(const uint32_t* h, uint32_t k, ui
     return hit;
 }
 
+// Keys of x[0, nn) (nn >= 4, x 16-B aligned) into registers, PER per thread: element
+// 4 * (tid + j4 * kScanThreads) + e -> key[4 * j4 + e], 0 past nn. Every 16-B load is
+// issued, in bounds (a float4 past the whole ones re-reads the last whole one), before
+// any is used: a load under an if / else per float4 made the compiler wait out each one
+// before the next (8 round trips, ~8 us of K3 at 32k samples); the partial float4
+// (nn & 3 elements) is read after, by the thread that owns it.
+template <int PER>
+__device__ __forceinline__ void load_keys4(const float* __restrict__ x, int nn, uint32_t (&key)[PER]) {
+    const int tid = threadIdx.x;
+    const int nf4 = nn >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    float4 f[PER / 4];
+#pragma unroll
+    for (int j4 = 0; j4 < PER / 4; ++j4) {
+        const int q = tid + j4 * kScanThreads;
+        f[j4] = x4[q < nf4 ? q : nf4 - 1];
+    }
+#pragma unroll
+    for (int j4 = 0; j4 < PER / 4; ++j4) {
+        const bool in = tid + j4 * kScanThreads < nf4;
+        key[4 * j4] = in ? abs_key(f[j4].x) : 0u;
+        key[4 * j4 + 1] = in ? abs_key(f[j4].y) : 0u;
+        key[4 * j4 + 2] = in ? abs_key(f[j4].z) : 0u;
+        key[4 * j4 + 3] = in ? abs_key(f[j4].w) : 0u;
+    }
+    if ((nn & 3) && nf4 % kScanThreads == tid) {
+#pragma unroll
+        for (int j4 = 0; j4 < PER / 4; ++j4)
+            if (j4 == nf4 / kScanThreads)
+#pragma unroll
+                for (int e = 0; e < 3; ++e)
+                    if (e < (nn & 3)) key[4 * j4 + e] = abs_key(x[4 * nf4 + e]);
+    }
+}
+
 // All three passes of one key set of <= kSmallN keys in ONE 1024-thread workgroup
 // (k_rs_small, k_rs_small_multi): x[0..n) -> *out = k-th largest |x| (NaN if any |x|
 // is NaN). Every key load in flight at once (kSmallN / kScanThreads per
@@ -321,23 +364,8 @@ __device__ __forceinline__ void rs_small_wg(const float* __restrict__ x, int64_t
     // are masked by `in` below
     uint32_t key[kPer];
     uint32_t mx = 0, my_nan = 0;
-    if (aligned16(x)) {
-        // kPer / 4 16-B loads per thread (a quarter of the load instructions): element
-        // i = 4 * (tid + j4 * kScanThreads) + e lands in key[4 * j4 + e]
-#pragma unroll
-        for (int j4 = 0; j4 < kPer / 4; ++j4) {
-            const int i = 4 * (tid + j4 * kScanThreads);
-            if (i + 3 < nn) {
-                const float4 f = reinterpret_cast<const float4*>(x)[i / 4];
-                key[4 * j4] = abs_key(f.x);
-                key[4 * j4 + 1] = abs_key(f.y);
-                key[4 * j4 + 2] = abs_key(f.z);
-                key[4 * j4 + 3] = abs_key(f.w);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) key[4 * j4 + e] = i + e < nn ? abs_key(x[i + e]) : 0u;
-            }
-        }
+    if (aligned16(x) && nn >= 4) {
+        load_keys4<kPer>(x, nn, key);
     } else {
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
@@ -347,7 +375,7 @@ __device__ __forceinline__ void rs_small_wg(const float* __restrict__ x, int64_t
     }
     // element index of key[j] (the two layouts above)
     auto elem = [&](int j) -> int {
-        return aligned16(x) ? 4 * (tid + (j / 4) * kScanThreads) + (j & 3) : tid + j * kScanThreads;
+        return aligned16(x) && nn >= 4 ? 4 * (tid + (j / 4) * kScanThreads) + (j & 3) : tid + j * kScanThreads;
     };
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -401,6 +429,7 @@ __device__ __forceinline__ void rs_small_wg(const float* __restrict__ x, int64_t
     }
     if (tid == 0) *out = (nan_cnt || sel_bin < 0) ? __uint_as_float(0x7FC00000u) : __uint_as_float(prefix);
     __syncthreads();
+    RS_STAMP(9);
 }
 
 // The k-th largest |x| of a K1 sample WINDOW (select.hip: every sample with key >= the
@@ -425,19 +454,11 @@ __device__ __forceinline__ void rs_window_wg(const float* __restrict__ x, int64_
     const uint32_t k = (uint32_t)k64;
     // element 4 * (tid + j4 * 1024) + e -> key[4 * j4 + e] (16-B loads; the window is 16-B aligned)
     uint32_t key[kWinPer];
+    if (nn >= 4) {
+        load_keys4<kWinPer>(x, nn, key);
+    } else {
 #pragma unroll
-    for (int j4 = 0; j4 < kWinPer / 4; ++j4) {
-        const int i = 4 * (tid + j4 * kScanThreads);
-        if (i + 3 < nn) {
-            const float4 f = reinterpret_cast<const float4*>(x)[i / 4];
-            key[4 * j4] = abs_key(f.x);
-            key[4 * j4 + 1] = abs_key(f.y);
-            key[4 * j4 + 2] = abs_key(f.z);
-            key[4 * j4 + 3] = abs_key(f.w);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) key[4 * j4 + e] = i + e < nn ? abs_key(x[i + e]) : 0u;
-        }
+        for (int j = 0; j < kWinPer; ++j) key[j] = (j & ~3) == 0 && tid == 0 && j < nn ? abs_key(x[j]) : 0u;
     }
     auto in = [&](int j) { return 4 * (tid + (j / 4) * kScanThreads) + (j & 3) < nn; };
     uint32_t mn = 0xFFFFFFFFu, mx = 0, nan = 0;

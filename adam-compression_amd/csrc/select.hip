@@ -1066,6 +1066,7 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const 
     const float* x = d.samp_off < 0 ? vec_flat + d.off : w.samples + d.samp_off;
     rs_small_wg(x, w.scnt[t], ks, w.thr + t);
     sel_init_tensor(w, t, 1);
+    RS_STAMP(10);
 }
 
 // ------------------------------------------------------------------ count passes
@@ -3798,6 +3799,11 @@ extern "C" int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt
 #ifdef DGC_K5_PROF
 extern "C" int dgc_ce_prof(void* out) {
     DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_ce_prof), sizeof(dgc::g_ce_prof)));
+    return DGC_OK;
+}
+
+extern "C" int dgc_rs_prof(void* out) {   // tools/k3_prof.py
+    DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_rs_prof), sizeof(dgc::g_rs_prof)));
     return DGC_OK;
 }
 
