@@ -787,17 +787,30 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
     // k_rs_small_multi a 320 B/lane scratch frame and doubled its time (15 -> 29 us)
     static_assert(kChainOneWords <= kBlock, "sel_init_tensor: one chain word per thread");
     if (t == 0 && threadIdx.x < kChainOneWords) w.chain[threadIdx.x] = 0;
+    __shared__ uint32_t spills;
+    if (threadIdx.x == 0) spills = 0;
     __syncthreads();   // the caller's threshold (thr[t]) is written
+    // every load of the reset in flight at once — the epoch, both spill slots, the
+    // threshold, the window count: as three dependent round trips they were ~3 us of K3
+    const int ep = st->epoch;
+    uint32_t sp0 = 0, sp1 = 0;
+    if (threadIdx.x < kSpillShards) {
+        sp0 = st->spill[0][threadIdx.x];
+        sp1 = st->spill[1][threadIdx.x];
+    }
+    float t0 = 0.f;
+    uint32_t win_n = 0;
+    if (threadIdx.x == 0) {
+        t0 = w.thr[t];
+        win_n = w.rs[t].win_n;
+    }
     for (int64_t i = threadIdx.x; i < d.ngrp; i += blockDim.x) {
         w.grp_cnt[d.grp0 + i] = 0;
         w.grp_lb[d.grp0 + i] = 0;
     }
-    __shared__ uint32_t spills;
-    if (threadIdx.x == 0) spills = 0;
-    __syncthreads();
-    const int e = st->epoch & 1;
+    const int e = ep & 1;
     if (threadIdx.x < kSpillShards) {
-        const uint32_t v = st->spill[e][threadIdx.x];
+        const uint32_t v = e ? sp1 : sp0;
         if (v) atomicAdd(&spills, v);
         st->spill[e ^ 1][threadIdx.x] = 0;   // slot of the next call's K1
     }
@@ -806,8 +819,7 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float t0 = w.thr[t];
-        st->win_keys = (d.win_cap > 0 && !d.tail) ? (int32_t)w.rs[t].win_n : 0;
+        st->win_keys = (d.win_cap > 0 && !d.tail) ? (int32_t)win_n : 0;
         st->t0 = t0;
         st->t_cur = t0;
         st->list_spills = keep_lists ? (int32_t)spills : 0;
