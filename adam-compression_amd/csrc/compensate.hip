@@ -115,7 +115,7 @@ k_mask(float* __restrict__ mmt, float* __restrict__ vec, const I* __restrict__ i
         int64_t i = (int64_t)idx[q];
         if (i < 0) i += n;             // torch index_fill_ wraps negative indices
         if (i < 0 || i >= n) {
-            atomicOr(bad, 1);
+            raise_flag(bad);
             continue;
         }
         if (mmt) mmt[i] = 0.f;

@@ -21,6 +21,10 @@
 // zero_() * (1/W).
 #include "dgc_common.hpp"
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 namespace dgc {
 
 constexpr int kChunk = 4096;
@@ -36,7 +40,10 @@ struct Run {
 struct DecWS {
     Run* runs;
     int32_t* nruns;
-    int32_t* status;      // bit 0: index out of range
+    int32_t* status;      // bit 0: index out of range, bit 1: a run out of order, bit 2: a header count
+                          // outside [0, capacity] (that run is clamped)
+    int32_t* sink;        // null, or the host-mapped words [index, count] bound to this workspace
+                          // (dgc_decompress_bind_sink): the error bits also land there
     int32_t* ndesc;       // detected descents
     int32_t* ovf_cnt;     // sparse scatter: super-chunks queued for the workgroup path
     int32_t* ovf_list;
@@ -53,9 +60,12 @@ struct DecWS {
     int64_t sort_cap;
 };
 
+int32_t* bound_sink(const void* ws);
+
 static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, int64_t sort_cap = 0, size_t* bytes = nullptr) {
     Carver c(base);
     DecWS w{};
+    w.sink = base ? bound_sink(base) : nullptr;
     w.nchunks = ceil_div(n, kChunk);
     w.runs = c.take<Run>(kMaxRuns);
     w.nruns = c.take<int32_t>(4);
@@ -72,6 +82,18 @@ static DecWS carve_dec(void* base, int64_t n, int32_t max_runs, int64_t sort_cap
     w.sort_buf = c.take<char>(sort_cap ? (size_t)max_runs * sort_cap * 12 : 0);
     if (bytes) *bytes = c.bytes();
     return w;
+}
+
+// An index outside [0, n) (dropped from the sum; the reference's index_put_ raises), or
+// a gathered header count outside [0, capacity] (the run is clamped): the status word
+// for dgc_decompress_status, and the bound sink for an engine's per-step check.
+__device__ __forceinline__ void flag_index(const DecWS& w) {
+    atomicOr(w.status, 1);
+    raise_flag(w.sink);
+}
+__device__ __forceinline__ void flag_count(const DecWS& w) {
+    atomicOr(w.status, 4);
+    raise_flag(w.sink ? w.sink + 1 : nullptr);
 }
 
 template <int VD>
@@ -110,6 +132,11 @@ struct RunSrc {
     __device__ __forceinline__ const char* base_of(int q) const {
         const int r = q / parts, p = q - r * parts;
         return payload + (int64_t)p * pstride + (int64_t)r * stride;
+    }
+    // the header's count as gathered (packed mode, a part that has landed), unclamped
+    __device__ __forceinline__ long long raw_count(int q) const {
+        if (!payload || (parts > 1 && q % parts >= ready)) return 0;
+        return *reinterpret_cast<const long long*>(base_of(q));
     }
     __device__ __forceinline__ Run get_raw(int q) const {
         if (!payload) return table[q];
@@ -206,6 +233,10 @@ k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap, int ystep, int yoff) {
     const Run run = rs.get_raw(r);
     long long* bnd = w.bnd + (int64_t)r * stride;
     const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const long long c = rs.raw_count(r);
+        if (c < 0 || c > rs.capacity) flag_count(w);
+    }
     for (int64_t e0 = (int64_t)blockIdx.x * kBlock; e0 <= run.count; e0 += (int64_t)gridDim.x * kBlock) {
         const int64_t e = e0 + threadIdx.x;
         long long lo = 0, hi = 0;
@@ -214,7 +245,7 @@ k_bounds(DecWS w, RunSrc rs, int64_t n, int64_t cap, int ystep, int yoff) {
             const long long ic = e < run.count ? load_idx<ID>(run.idx, e) : 0;
             lo = e > 0 ? chunk_rank(ip, n, w.nchunks) : 0;
             hi = e < run.count ? chunk_rank(ic, n, w.nchunks) : stride;
-            if (e < run.count && (ic < 0 || ic >= n)) atomicOr(w.status, 1);
+            if (e < run.count && (ic < 0 || ic >= n)) flag_index(w);
             if (e > 0 && e < run.count && ic < ip) {
                 atomicOr(w.status, 2);
                 if (w.sort_cap) atomicOr(&w.unsorted[r], 1);
@@ -268,7 +299,7 @@ __global__ void __launch_bounds__(kRegroupThreads) k_regroup(DecWS w, RunSrc rs,
     for (long long e = tid; e < run.count; e += kRegroupThreads) {
         const long long i = load_idx<ID>(run.idx, e);
         if (i < 0 || i >= n) {
-            atomicOr(w.status, 1);
+            flag_index(w);
             continue;
         }
         atomicAdd((unsigned long long*)&bnd[(i >> 12) + 1], 1ull);
@@ -343,7 +374,7 @@ __device__ void tile_chunk(const DecWS& w, const RunSrc& rs, float* __restrict__
             cnt = b1 - b0;
             // idx < 0 or >= n; a split phase's runs that have not landed (count 0) have no
             // bounds yet (their slots hold an earlier call's)
-            if (c == 0 && run.count > 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) atomicOr(w.status, 1);
+            if (c == 0 && run.count > 0 && (bnd[0] > 0 || bnd[w.nchunks] < run.count)) flag_index(w);
         }
         const long long incl = (long long)wave_incl_scan64((uint64_t)cnt);   // the whole wave 0 is here
         if (tid < nr) roff[tid] = (int)(incl - cnt);
@@ -421,12 +452,16 @@ k_scatter_single(DecWS w, RunSrc rs, float* __restrict__ grad, int64_t n, float 
     const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
     const long long j = t >> 2;
     const int part = (int)(t & 3);
+    if (t == 0) {
+        const long long c = rs.raw_count(0);
+        if (c < 0 || c > rs.capacity) flag_count(w);
+    }
     if (j >= run.count) return;
     const long long i = load_idx<ID>(run.idx, j);
     const long long ip = j > 0 ? load_idx<ID>(run.idx, j - 1) : -1;
     if (part == 0 && j > 0 && ip > i) atomicOr(w.status, 2);
     if (i < 0 || i >= n) {
-        if (part == 0) atomicOr(w.status, 1);
+        if (part == 0) flag_index(w);
         return;
     }
     const uintptr_t lo = reinterpret_cast<uintptr_t>(grad), hi = reinterpret_cast<uintptr_t>(grad + n);
@@ -1115,6 +1150,36 @@ int fill_zero(float* x, int64_t n, hipStream_t s, const ZeroWords& z) {
 }
 
 }  // namespace dgc
+
+// ---------------------------------------------------------------- sink bindings
+// workspace -> host-mapped error words (dgc_decompress_bind_sink); looked up on the host
+// when a call carves its workspace, so the kernels get the pointer as an argument.
+namespace dgc {
+namespace {
+std::mutex g_sink_mu;
+std::vector<std::pair<const void*, int32_t*>> g_sinks;
+}  // namespace
+
+int32_t* bound_sink(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_sink_mu);
+    for (const auto& b : g_sinks)
+        if (b.first == ws) return b.second;
+    return nullptr;
+}
+}  // namespace dgc
+
+extern "C" int dgc_decompress_bind_sink(const void* ws, int32_t* sink) {
+    if (!ws) DGC_FAIL(DGC_ERR_INVALID, "dgc_decompress_bind_sink: null workspace");
+    std::lock_guard<std::mutex> lk(dgc::g_sink_mu);
+    auto& v = dgc::g_sinks;
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].first == ws) {
+            v.erase(v.begin() + (long)i);
+            break;
+        }
+    if (sink) v.emplace_back(ws, sink);
+    return DGC_OK;
+}
 
 extern "C" size_t dgc_decompress_packed_workspace(int64_t n, int32_t world, int64_t capacity) {
     size_t b = 0;

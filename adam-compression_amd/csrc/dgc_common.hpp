@@ -409,6 +409,15 @@ __device__ __forceinline__ float comp1(float g, float& m, float& v, float mom) {
     }
     return m;
 }
+// ---------------------------------------------------------------- error flags
+// A flag the host polls without synchronising (an engine's pinned status sink) or a
+// device int32: every writer stores the same constant — idempotent, so no
+// read-modify-write has to cross PCIe — at system scope, so the store reaches host
+// memory and not only this XCD's L2. Written only on an error path.
+__device__ __forceinline__ void raise_flag(int32_t* f, int32_t v = 1) {
+    if (f) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------- last arrival
 // True in every thread of the workgroup that arrives last at `ticket` among
 // `nblocks`. The data handed to the last workgroup is ONLY device-scope atomics

@@ -74,7 +74,7 @@ k_mask16(uint16_t* __restrict__ mmt, uint16_t* __restrict__ vec, const I* __rest
         int64_t i = (int64_t)idx[q];
         if (i < 0) i += n;   // index_fill_ wraps negative indices
         if (i < 0 || i >= n) {
-            atomicOr(bad, 1);
+            raise_flag(bad);
             continue;
         }
         if (mmt) mmt[i] = 0;   // +0 in both dtypes
@@ -96,7 +96,7 @@ k_scatter16(const void* __restrict__ values, const I* __restrict__ idx, int64_t 
         int64_t i = (int64_t)idx[q];
         if (i < 0) i += n;   // index_put_ wraps negative indices
         if (i < 0 || i >= n) {
-            atomicOr(bad, 1);
+            raise_flag(bad);
             continue;
         }
         float v;
@@ -123,7 +123,7 @@ k_segsum16(const void* __restrict__ values, const I* __restrict__ idx, int64_t t
         if (q > 0 && (int64_t)idx[q - 1] == i0) continue;   // not the first of its run
         int64_t i = i0 < 0 ? i0 + n : i0;
         if (i < 0 || i >= n) {
-            atomicOr(bad, 1);
+            raise_flag(bad);
             continue;
         }
         float acc = 0.f;   // grad.zero_()
@@ -169,15 +169,19 @@ k_mask_packed16(const char* __restrict__ payload, int64_t ioff, uint16_t* __rest
 // run's count read on the device).
 template <int DT, int VD, typename I>
 __global__ void __launch_bounds__(kBlock)
-k_scatter_packed16(const char* __restrict__ run, int64_t voff, int64_t ioff, uint16_t* __restrict__ out, int64_t n,
-                   int32_t* bad) {
-    const int64_t count = *reinterpret_cast<const int64_t*>(run);
+k_scatter_packed16(const char* __restrict__ run, int64_t capacity, int64_t voff, int64_t ioff,
+                   uint16_t* __restrict__ out, int64_t n, int32_t* bad) {
+    int64_t count = *reinterpret_cast<const int64_t*>(run);
+    if (count < 0 || count > capacity) {   // a corrupted header: flag it (2), scatter none of it
+        if (blockIdx.x == 0 && threadIdx.x == 0) raise_flag(bad, 2);
+        count = 0;
+    }
     const I* idx = reinterpret_cast<const I*>(run + ioff);
     const void* values = run + voff;
     for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < count; q += (int64_t)gridDim.x * kBlock) {
         const int64_t i = (int64_t)idx[q];
         if (i < 0 || i >= n) {
-            atomicOr(bad, 1);
+            raise_flag(bad);
             continue;
         }
         float v;
@@ -407,11 +411,11 @@ static int scatter_packed16_t(const char* p, int32_t world, int64_t stride, int6
     for (int32_t r = 0; r < world; ++r) {   // rank order: one launch per run
         const char* run = p + (int64_t)r * stride;
         if (vd == DGC_F32)
-            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_F32, I>), dim3(grid), dim3(kBlock), 0, s, run, voff, ioff, out, n, bad);
+            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_F32, I>), dim3(grid), dim3(kBlock), 0, s, run, capacity, voff, ioff, out, n, bad);
         else if (vd == DGC_F16)
-            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_F16, I>), dim3(grid), dim3(kBlock), 0, s, run, voff, ioff, out, n, bad);
+            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_F16, I>), dim3(grid), dim3(kBlock), 0, s, run, capacity, voff, ioff, out, n, bad);
         else
-            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_BF16, I>), dim3(grid), dim3(kBlock), 0, s, run, voff, ioff, out, n, bad);
+            hipLaunchKernelGGL((k_scatter_packed16<DT, DGC_BF16, I>), dim3(grid), dim3(kBlock), 0, s, run, capacity, voff, ioff, out, n, bad);
         DGC_LAUNCHED();
     }
     return DGC_OK;

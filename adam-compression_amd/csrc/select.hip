@@ -770,6 +770,7 @@ __global__ void k_no_lists(SelWS w) {
 __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     SelState* st = w.st + t;
+    __shared__ uint32_t setg_broken;
     if (threadIdx.x == 0) {   // K5's multi-workgroup barrier and consensus start from zero
         w.nthg[t].bar_count = 0;
         w.nthg[t].bar_gen = 0;
@@ -777,6 +778,7 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         w.nthg[t].decide = 0;
         w.nthg[t].status = 0;
         SetG& sg = w.setg[t];
+        setg_broken = sg.broken;
         sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = 0;
         sg.mn = 0xFFFFFFFFu;
         sg.mx = 0;
@@ -790,6 +792,14 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
     __shared__ uint32_t spills;
     if (threadIdx.x == 0) spills = 0;
     __syncthreads();   // the caller's threshold (thr[t]) is written
+    if (setg_broken) {
+        // a barrier of this tensor's last K5s timed out: its workgroups may have run
+        // different numbers of passes, leaving merged-histogram bins they did not re-zero
+        // (or re-zeroed before a late add) — restore "zero at rest" for the whole table
+        SetG& sg = w.setg[t];
+        for (int q = threadIdx.x; q < kSetBins0; q += blockDim.x) sg.hist0[q] = 0;
+        for (int q = threadIdx.x; q < kSetBins1; q += blockDim.x) sg.hist1[q] = 0;
+    }
     // every load of the reset in flight at once — the epoch, both spill slots, the
     // threshold, the window count: as three dependent round trips they were ~3 us of K3
     const int ep = st->epoch;

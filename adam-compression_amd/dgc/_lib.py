@@ -68,33 +68,86 @@ def info_dict(i, what):
 INFO_BYTES = ctypes.sizeof(SelectInfo)
 
 
+# every sink's pinned words stay allocated for the life of the process: the library
+# holds their addresses (dgc_select_params.status_sink, dgc_decompress_bind_sink)
+_SINK_WORDS = []
+
+
+def _unbind(ws_ptr):
+    if _lib is not None:
+        _lib.dgc_decompress_bind_sink(ctypes.c_void_p(ws_ptr), None)
+
+
 class StatusSink:
-    """The engines' per-step check of the resample replay (DGC_K5_BROKEN) without a host
-    synchronisation: a pinned host int32 whose address goes to the library as
-    ``status_sink``; a finish whose replay broke stores its k5_status there (nothing is
-    written otherwise). ``check()`` reads the host word — free — and raises once it is set,
-    i.e. at the first step the host issues after the GPU finished the broken call (a host
-    that runs ahead of the GPU sees it that many steps later; ``check(sync=True)``
-    waits for the stream first)."""
+    """The engines' per-step error check without a host synchronisation: four pinned
+    host int32 words the kernels write only when something is wrong —
+
+      [0] the selection's finish: its k5_status when a resample replay broke
+          (DGC_K5_BROKEN; ``status_sink``)
+      [1] decompress: an index outside the output (1: dropped; the reference's
+          ``index_put_`` raises, dgc/compression.py:191); the 16-bit decompress also
+          stores 2 here for a bad header count
+      [2] decompress: a gathered header count outside [0, capacity] (a corrupted
+          payload, the reference's "allgathered data are random data" README.md:132)
+      [3] DGCSGDMemory.update: an index outside [-n, n) (the reference's
+          ``index_fill_`` raises, dgc/memory.py:76-77)
+
+    ``bind(ws)`` routes a decompress workspace's error bits into words [1, 2]
+    (``dgc_decompress_bind_sink``); ``index_flag`` is word [3]'s address, passed as a
+    kernel's ``bad_flag``. ``check()`` reads the words — free — and raises once one is
+    set, i.e. at the first step the host issues after the GPU finished the bad call (a
+    host that runs ahead of the GPU sees it that many steps later; ``check(sync=True)``
+    waits for the stream first). A reported decompress / masking error is cleared, so a
+    caller that catches it can go on."""
 
     def __init__(self, what, device):
         self.what = what
         self.device = device
-        self.word = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
-        self._view = self.word.numpy()   # the same host word, read without a tensor op
+        self.word = torch.zeros(4, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+        _SINK_WORDS.append(self.word)
+        self._view = self.word.numpy()   # the same host words, read without a tensor op
 
     @property
     def address(self):
         return self.word.data_ptr()
 
+    @property
+    def decompress_words(self):
+        return self.word.data_ptr() + 4
+
+    @property
+    def index_flag(self):
+        return self.word.data_ptr() + 12
+
+    def bind(self, ws):
+        """Routes the decompress workspace tensor ``ws``'s error bits here (unbound when
+        ``ws`` is freed)."""
+        import weakref
+        check(lib().dgc_decompress_bind_sink(ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(self.decompress_words)),
+              "dgc_decompress_bind_sink")
+        weakref.finalize(ws, _unbind, ws.data_ptr())
+        return ws
+
     def check(self, sync=False):
         if sync:
             torch.cuda.current_stream(self.device).synchronize()
-        v = int(self._view[0])
-        if v & K5_BROKEN:
+        v = self._view
+        k5 = int(v[0])
+        if k5 & K5_BROKEN:
             raise RuntimeError(f"{self.what}: the resample replay's multi-workgroup phase timed out at a barrier after "
-                               f"it started (k5_status {v}; workgroups not co-resident?); the selection of that step "
+                               f"it started (k5_status {k5}; workgroups not co-resident?); the selection of that step "
                                "is not reliable")
+        if v[1] or v[2] or v[3]:
+            why = []
+            if v[1] & 1:
+                why.append("a decompressed index was outside the gradient (its entry was dropped)")
+            if v[2] or v[1] & 2:
+                why.append("a gathered payload header held a count outside [0, capacity] (the run was clamped)")
+            if v[3]:
+                why.append("DGCSGDMemory.update got an index outside the state (not masked)")
+            v[1:] = 0
+            raise RuntimeError(f"{self.what}: " + "; ".join(why) + " — a foreign or corrupted payload (the reference's "
+                               "index_put_ / index_fill_ raise IndexError here)")
 
 
 class BatchDesc(ctypes.Structure):
@@ -155,6 +208,7 @@ _SIGNATURES = {
     "dgc_clear_split": (ctypes.c_int, [_P, _I32, _I32, _I64, _I32, _I32, _P, _I64, _P, _SZ, _P]),
     "dgc_fill_zero": (ctypes.c_int, [_P, _I64, _P]),
     "dgc_decompress_status": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
+    "dgc_decompress_bind_sink": (ctypes.c_int, [_P, _P]),
     "dgc_batch_workspace": (_SZ, [ctypes.POINTER(BatchDesc)]),
     "dgc_batch_init": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _SZ, _P]),
     "dgc_batch_compress": (ctypes.c_int, [ctypes.POINTER(BatchDesc), _P, _P, _P, ctypes.POINTER(_I64), _P, _P, _P,

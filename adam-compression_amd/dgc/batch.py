@@ -101,17 +101,14 @@ class DGCBatch:
         # velocity's exact fp32 image, which the selection reads (dgc_batch_select); the
         # 16-bit state is masked from the payload (dgc_mask_packed16)
         self._vec32 = torch.zeros(self.flat_numel, dtype=torch.float32, device=dev) if self.half else None
-        # the 16-bit decompress's out-of-range flag (a peer's index outside [0, flat_numel));
-        # copied to pinned host memory after every decompress and reset, checked like status
-        self._bad16 = torch.zeros(1, dtype=torch.int32, device=dev) if self.half else None
-        self._bad16_host = (torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
-                            if self.half else None)
         self.deferred_masking = bool(deferred_masking) and not self.half
         self._pending = False
         self.out_flat = torch.zeros(self.flat_numel, dtype=dtype, device=dev)
         self._L = _lib.lib()
         self.info = torch.zeros(len(self.names) * _lib.INFO_BYTES, dtype=torch.uint8, device=dev)
-        self.status = _lib.StatusSink("DGCBatch", dev)   # DGC_K5_BROKEN, checked every step
+        # DGC_K5_BROKEN and the decompress's bad index / gathered count (a peer's payload
+        # corrupted in transit), written by the kernels into pinned words, checked every step
+        self.status = _lib.StatusSink("DGCBatch", dev)
         self.set_ratio(compress_ratio)
 
     # ---------------------------------------------------------------- layout
@@ -176,6 +173,7 @@ class DGCBatch:
         self._last_gathered = None
         self.dec_ws = (torch.empty(L.dgc_decompress_packed_workspace(self.flat_numel, self.world, self.capacity),
                                    dtype=torch.uint8, device=self.device) if self.xchg is None else None)
+        self.status.bind(self.dec_ws if self.xchg is None else self.xchg.ws)
 
     @property
     def payload(self):
@@ -243,9 +241,9 @@ class DGCBatch:
         or — ``grad_ptrs``, a ctypes array of T device pointers, each to the tensor's
         numel contiguous fp32 elements, 16-B aligned — from wherever they are (the
         batched optimizer's p.grad tensors, read in place). Raises first if a previous
-        step's resample replay reported DGC_K5_BROKEN (``status``)."""
+        step's resample replay reported DGC_K5_BROKEN, or its decompress met an index
+        or a gathered count out of range (``status``)."""
         self.status.check()
-        self._check_bad16()
         starts = self.draw_starts() if starts is None else starts
         self.starts = starts
         self._par += 1   # a step starts: the other payload / gather buffer
@@ -341,9 +339,8 @@ class DGCBatch:
             _lib.check(L.dgc_decompress_packed16(cur.data_ptr(), self.world, self.rank_stride, self.capacity,
                                                  _lib.VD[self.vdtype], _lib.ID[self.idtype], out.data_ptr(),
                                                  _lib.VD[self.dtype], self.flat_numel, 1.0 / self.world,
-                                                 self._bad16.data_ptr(), st), "dgc_decompress_packed16")
-            self._bad16_host.copy_(self._bad16, non_blocking=True)
-            self._bad16.zero_()
+                                                 ctypes.c_void_p(self.status.decompress_words), st),
+                       "dgc_decompress_packed16")
             return out
         aliased = out.untyped_storage().data_ptr() == self.grad_flat.untyped_storage().data_ptr()
         reusable = (self.fill == "sparse" and not aliased and self._last_gathered is not None
@@ -377,22 +374,8 @@ class DGCBatch:
         return self.decompress()
 
     # ---------------------------------------------------------------- results
-    def _check_bad16(self, sync=False):
-        """Raises when a 16-bit decompress met an index outside [0, flat_numel) (the fp32
-        engines report it through their status words): the flag of the last decompress the
-        GPU finished (sync=True: of the last one issued)."""
-        if self._bad16_host is None:
-            return
-        if sync:
-            torch.cuda.current_stream(self.device).synchronize()
-        if int(self._bad16_host.numpy()[0]):
-            self._bad16_host.zero_()
-            raise RuntimeError("DGCBatch: a gathered payload held an index outside the flat buffer (foreign or "
-                               "corrupted payload); its entry was dropped from the decompress")
-
     def infos(self):
         self.status.check(sync=True)
-        self._check_bad16(sync=True)
         raw = self.info.cpu().numpy().tobytes()
         out = []
         for t in range(len(self.names)):

@@ -137,6 +137,8 @@ class DGCBucket:
         self._last_gathered = None
         self.dec_ws = (torch.empty(L.dgc_decompress_packed_workspace(N, self.world, self.k), dtype=torch.uint8,
                                    device=dev) if self.xchg is None else None)
+        # a bad index or gathered count in the decompress lands in ``status`` (raised next step)
+        self.status.bind(self.dec_ws if self.xchg is None else self.xchg.ws)
         self.scale = 1.0 / self.world
         self._L = L
         if fill in ("allgather", "sparse"):
@@ -178,7 +180,8 @@ class DGCBucket:
     # ---------------------------------------------------------------- phases
     def compensate(self, grad):
         """K1: compensate + fused strided sample + speculative candidate lists. Raises
-        first if a previous step's resample replay reported DGC_K5_BROKEN (``status``)."""
+        first if a previous step's resample replay reported DGC_K5_BROKEN, or its
+        decompress met an index or a gathered count out of range (``status``)."""
         self.status.check()
         L = self._L
         self._par += 1   # a step starts: the other payload / gather buffer
@@ -288,6 +291,7 @@ class DGCBucket:
         ``events`` maps a phase name to a (start, end) pair of torch.cuda.Event recorded
         around it on the current stream."""
         ev = events or {}
+        self.status.check()   # before anything of this step is issued
         # an output that shares storage with the gradient (the reference's in-place
         # layout) is rewritten with each new gradient: always the dense fill there
         aliased = out.untyped_storage().data_ptr() == grad.untyped_storage().data_ptr()

@@ -12,13 +12,17 @@ Semantics kept from Horovod:
     different number of rows;
   * allreduce with ``Average`` is the rank sum divided by the world size, in place —
     summed in RANK ORDER (an allgather, then ``dgc_rank_sum``), as the oracle restates
-    Horovod's Average.
+    Horovod's Average, for tensors up to ``RANK_ORDER_MAX`` elements (every dense DGC
+    tensor: biases and BatchNorm vectors); a larger one (``Compression.none``, a ratio-1
+    warmup epoch) is a backend allreduce, whose summation order is the backend's.
 
 The DGC sparse payload itself does NOT go through the generic allgather: each
 rank's (count, values, indices) is packed into one fixed-capacity byte buffer
 (``dgc_payload_layout``) and exchanged with a single ``all_gather_into_tensor``
 (see ``allgather_packed_async``), so no size exchange is needed.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -88,6 +92,13 @@ class Handle:
         return self._output
 
 
+# Dense tensors up to this many elements are averaged in rank order through an allgather
+# (W x the tensor's bytes in flight); larger ones take the backend's allreduce (a ring
+# moves ~2x the bytes whatever W is). The dense tensors of the DGC configs are <= 4096
+# elements each; DGC_RANK_ORDER_MAX overrides the cap (0: always the backend allreduce).
+RANK_ORDER_MAX = int(os.environ.get("DGC_RANK_ORDER_MAX", str(1 << 20)))
+
+
 def _rank_order_sum(rows, W, average):
     """acc = x_0; acc += x_1 ...; acc /= W on rows of a [W, n] host tensor (torch ops in
     the rows' dtype: the oracle's restatement of Horovod's Average)."""
@@ -116,6 +127,8 @@ def allreduce_async_(tensor, name=None, op=Average):
         return Handle(output=tensor)
     src = tensor.contiguous().view(-1)
     n = src.numel()
+    if n > RANK_ORDER_MAX:
+        return _backend_allreduce(tensor, src, W, op == Average)
     device_sum = tensor.is_cuda and tensor.dtype in (torch.float32, torch.float16, torch.bfloat16)
     if _backend_needs_host(src) or not tensor.is_cuda:
         host = src.cpu()
@@ -138,6 +151,24 @@ def allreduce_async_(tensor, name=None, op=Average):
         else:
             acc = _rank_order_sum(gathered.view(W, n), W, op == Average)
             tensor.copy_(acc.view(tensor.shape).to(tensor.device))
+        return tensor
+
+    return Handle(work, finish)
+
+
+def _backend_allreduce(tensor, src, W, average):
+    """A large dense tensor: the backend's SUM allreduce (RCCL's ring over xGMI on the
+    device; gloo on a host copy), then ``div_(W)`` for Average — the reference's Horovod
+    allreduce, in the backend's summation order (bit-equal to the rank-order restatement
+    at W = 2, where fp addition commutes; parity unpinned from W = 3 on)."""
+    buf = src.cpu() if _backend_needs_host(src) else src   # gloo moves host tensors
+    work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True)
+
+    def finish():
+        if average:
+            buf.div_(W)
+        if buf.data_ptr() != tensor.data_ptr():
+            tensor.copy_(buf.view(tensor.shape))
         return tensor
 
     return Handle(work, finish)

@@ -102,7 +102,8 @@ class DGCCompressor:
         self._ws = _lib.Workspace()
         self._params = {}
         self._payloads = {}
-        self._bad16 = {}       # device -> int32 flag: out-of-range indices (dgc_decompress16)
+        self._status = {}      # device -> StatusSink: bad indices / gathered counts in the decompress
+        self._bound_ws = {}    # device -> the decompress workspace bound to that sink
         self._spec = {}        # name -> device float: speculative list threshold (dgc_compress)
         self.layout_epoch = 0  # bumped by initialize(): the batched step re-derives its layout
 
@@ -162,6 +163,31 @@ class DGCCompressor:
                 print(f"update compress ratio: {ratio}")
             self.compress_ratio = ratio
             self.initialize(self.attributes.items())
+
+    # ------------------------------------------------------------------ errors
+    def _sink(self, device):
+        """This compressor's StatusSink on ``device``: the decompress kernels store an
+        out-of-range index or a gathered count outside [0, capacity] there (the
+        reference's index_put_ raises, dgc/compression.py:191)."""
+        sink = self._status.get(device)
+        if sink is None:
+            sink = self._status[device] = _lib.StatusSink("DGCCompressor", device)
+        return sink
+
+    def _dec_ws(self, device, nbytes):
+        ws = self._ws.get(device, nbytes, "decompress")
+        if self._bound_ws.get(device) is not ws:
+            self._sink(device).bind(ws)
+            self._bound_ws[device] = ws
+        return ws
+
+    def check(self, sync=False):
+        """Raises if a decompress issued earlier met a bad index or gathered count (read
+        from pinned host words: free; ``sync=True`` waits for the stream first). Runs at
+        every compress / decompress / synchronize, so an error surfaces one call later
+        than the reference's, which raises inside its index_put_."""
+        for sink in self._status.values():
+            sink.check(sync)
 
     # ------------------------------------------------------------------ kernels
     def _select_params(self, name, masking, update_memory, dtype=torch.float32):
@@ -268,6 +294,7 @@ class DGCCompressor:
 
     def compress(self, tensor, name):
         """dgc/compression.py:155-177."""
+        self.check()
         if self.compress_ratio < 1.0 and name in self.attributes:
             numel, shape, k, S, ks, stride = self.attributes[name]
             mem = self.memory
@@ -340,7 +367,10 @@ class DGCCompressor:
                               "DGCCompressor")
 
     def decompress(self, tensor, ctx):
-        """dgc/compression.py:179-198."""
+        """dgc/compression.py:179-198. An index outside the gradient (or a gathered
+        count outside the payload's capacity) is reported through this compressor's
+        StatusSink and raised at the next call (``check``)."""
+        self.check()
         name, numel, shape, vdtype, idtype, grad = ctx
         if self.compress_ratio < 1.0 and name in self.attributes:
             assert isinstance(tensor, (list, tuple))
@@ -354,7 +384,7 @@ class DGCCompressor:
             if isinstance(tensor, _Gathered) and tensor.packed is not None:
                 p = tensor
                 wsz = L.dgc_decompress_packed_workspace(numel, p.world, p.capacity)
-                ws = self._ws.get(dev, wsz, "decompress")
+                ws = self._dec_ws(dev, wsz)
                 vd = _lib.VD[p.vdtype]
                 idd = _lib.ID[p.idtype]
                 _lib.check(L.dgc_decompress_packed(_lib.ptr(p.packed), p.world, p.rank_stride, p.capacity, vd,
@@ -368,6 +398,8 @@ class DGCCompressor:
                 values = values.to(torch.float32)
             if indices.dtype not in _lib.ID:
                 indices = indices.to(torch.int64)
+            # index_put_ wraps a negative index (>= -numel); the kernels take [0, numel)
+            indices = torch.where(indices < 0, indices + numel, indices)
             offs = getattr(tensor, "run_offsets", None)
             import ctypes
             if offs is not None:
@@ -377,7 +409,7 @@ class DGCCompressor:
             else:
                 arr, nruns = None, 0
                 wsz = L.dgc_decompress_workspace(numel, 64)
-            ws = self._ws.get(dev, wsz, "decompress")
+            ws = self._dec_ws(dev, wsz)
             status = L.dgc_decompress(_lib.ptr(values), _lib.VD[values.dtype], _lib.ptr(indices),
                                       _lib.ID[indices.dtype], values.numel(), arr, nruns, _lib.ptr(grad), numel,
                                       scale, _lib.ptr(ws), wsz, stream)
@@ -419,12 +451,10 @@ class DGCCompressor:
             nruns = len(offs) - 1
         arr = (ctypes.c_int64 * len(offs))(*[int(o) for o in offs])
         dev = grad.device
-        bad = self._bad16.get(dev)
-        if bad is None:
-            bad = self._bad16[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+        bad = ctypes.c_void_p(self._sink(dev).decompress_words)   # 1: an index outside the gradient
         _lib.check(_lib.lib().dgc_decompress16(_lib.ptr(values), _lib.VD[values.dtype], _lib.ptr(indices),
                                                _lib.ID[indices.dtype], arr, nruns, _lib.ptr(grad),
-                                               _lib.VD[grad.dtype], numel, scale, _lib.ptr(bad),
+                                               _lib.VD[grad.dtype], numel, scale, bad,
                                                _lib.stream_of(dev)), "dgc_decompress16")
         return grad.view(shape)
 
@@ -456,13 +486,20 @@ class DGCCompressor:
         return payload, lay
 
     def synchronize(self, handle):
-        """dgc/compression.py:208-212."""
+        """dgc/compression.py:208-212. A gathered header whose count is outside [0,
+        capacity] (a payload corrupted in transit, README.md:132) raises here."""
+        self.check()
         if isinstance(handle, _PackedHandle):
             gathered = handle.handle.wait()
             W = gathered.numel() // handle.stride
             rows = gathered.view(W, handle.stride)
             head = rows[:, :16].contiguous().view(torch.int64).view(W, 2).tolist()
             counts = [c for c, _ in head]
+            bad = [r for r, c in enumerate(counts) if not 0 <= c <= handle.capacity]
+            if bad:
+                raise RuntimeError(f"DGCCompressor.synchronize: {handle.name}: the payload gathered from rank(s) {bad} "
+                                   f"holds count(s) {[counts[r] for r in bad]} outside [0, {handle.capacity}] "
+                                   "(corrupted in transit?)")
             vb = torch.empty(0, dtype=handle.vdtype).element_size()
             ib = torch.empty(0, dtype=handle.idtype).element_size()
             vals = [rows[r, handle.voff: handle.voff + c * vb].view(handle.vdtype) for r, c in enumerate(counts)]

@@ -165,12 +165,14 @@ class _DistributedOptimizer(torch.optim.Optimizer):
 
     def synchronize(self):
         if self._batched is not None:
-            if self._requires_update:
-                # one grouped compress -> allgather -> decompress (+ one dense allreduce)
-                self._batched.step(self._order)
-            self._reset_cells()
-            self._order.clear()
-            self._handles.clear()
+            try:
+                if self._requires_update:
+                    # one grouped compress -> allgather -> decompress (+ one dense allreduce)
+                    self._batched.step(self._order)
+            finally:   # a step that raised (a corrupted payload reported) leaves the hooks re-armed
+                self._reset_cells()
+                self._order.clear()
+                self._handles.clear()
             self._synchronized = True
             return
         for p in self._requires_update - set(self._handles.keys()):

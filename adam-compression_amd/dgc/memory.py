@@ -14,6 +14,8 @@ keyed by name, so ``state_dict`` / ``load_state_dict`` and checkpoints are uncha
 bf16 / fp16 parameters run ``dgc_compensate16`` / ``dgc_mask_indices16``: every op of
 the reference rounds to the dtype, as ATen does on a 16-bit tensor.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -56,7 +58,7 @@ class DGCSGDMemory(Memory):
         self.nesterov = nesterov
         self.momentums = {}
         self.velocities = {}
-        self._bad = {}
+        self._status = {}   # device -> StatusSink: update() with an index outside the state
         # callables run before the state is read or replaced: a batched step
         # (dgc/horovod/batched.py) applies a deferred momentum masking there
         self._before_read = []
@@ -64,6 +66,15 @@ class DGCSGDMemory(Memory):
     def _sync(self):
         for fn in self._before_read:
             fn()
+        self.check()
+
+    def check(self, sync=False):
+        """Raises if an ``update`` issued earlier got an index outside [-n, n) (the
+        reference's index_fill_ raises there, dgc/memory.py:76-77): the kernel stores a
+        flag in pinned host memory, read here for free at every call (``sync=True``
+        waits for the stream first)."""
+        for sink in self._status.values():
+            sink.check(sync)
 
     def initialize(self, named_parameters):
         """zeros_like per parameter (dgc/memory.py:43-48)."""
@@ -154,14 +165,14 @@ class DGCSGDMemory(Memory):
         if idx.dtype not in _lib.ID:
             idx = idx.to(torch.int64)
         idx = idx.contiguous()
-        bad = self._bad.get(vec.device)
-        if bad is None:
-            bad = self._bad[vec.device] = torch.zeros(1, dtype=torch.int32, device=vec.device)
+        sink = self._status.get(vec.device)
+        if sink is None:
+            sink = self._status[vec.device] = _lib.StatusSink("DGCSGDMemory.update", vec.device)
         L = _lib.lib()
         fn = L.dgc_mask_indices16 if dt in _lib.HALF else L.dgc_mask_indices
         _lib.check(fn(_lib.ptr(mmt) if self.momentum_masking else None, _lib.ptr(vec),
                       vec.numel(), _lib.ptr(idx), _lib.ID[idx.dtype], idx.numel(),
-                      _lib.ptr(bad), _lib.stream_of(vec.device)), "dgc_mask_indices")
+                      ctypes.c_void_p(sink.index_flag), _lib.stream_of(vec.device)), "dgc_mask_indices")
 
     def state_dict(self):
         self._sync()

@@ -42,10 +42,14 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_COPY_GBS = 6290.0            # measured float4 copy ceiling (same guide)
 XGMI_LINK_GBS = 153.0            # per link, per direction
 
+# Synthetic gradients: a fresh N(0, 1) gradient per rank and step, seed
+# 0xD6C + 1000 * rank + step (torch.randn on the device, generated before the timed
+# region), the sample starts from random.Random(42) — except flat-7B-bf16, whose 28 GB
+# buffers allow two (steps alternate between seeds 0xD6C + 1000 * rank + {0, 1}).
 WORKLOADS = {
     "flat-1B": dict(kind="flat", numel=10 ** 9, ratio=1e-3, grad="normal", nesterov=True,
                     config="BASELINE configs[3]: synthetic 1B-element flat gradient bucket"),
-    "flat-7B-bf16": dict(kind="flat", numel=7 * 10 ** 9, ratio=1e-4, grad="bf16", nesterov=True,
+    "flat-7B-bf16": dict(kind="flat", numel=7 * 10 ** 9, ratio=1e-4, grad="bf16", nesterov=True, buffers=2,
                          config="BASELINE configs[4]: synthetic 7B-element bf16-origin gradient"),
     "resnet50": dict(kind="model", model="resnet50", ratio=1e-3, fp16=False, int32=False, nesterov=False,
                      config="BASELINE configs[1]: ResNet-50 ImageNet gradient set"),
@@ -60,7 +64,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="flat-1B", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-numel", type=float, default=3e8, help="CPU-baseline sample (all cores), flat")
+    ap.add_argument("--cpu-numel", type=float, default=1e9,
+                    help="CPU baseline (all cores), flat: elements per step (default: the whole 1B bucket)")
     ap.add_argument("--cpu-numel-1t", type=float, default=5e7, help="CPU-baseline sample (1 thread), flat")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
@@ -108,11 +113,12 @@ def cpu_model():
 
 def cpu_baseline(run, wl, numel, steps, threads):
     """The reference op sequence restated on torch CPU (oracle/torch_cpu.py, pinned to
-    the reference's golden fixtures), timed on this host over a bounded sample of the
-    workload (rank 0, N=1 only) with the GPU run's OWN inputs (BASELINE.md "Inputs"):
-    the two alternating gradient buffers copied back from HBM (model sets: every
-    compressed tensor; flat buckets: the first ``numel`` elements of each buffer) and
-    the sample starts drawn from ``random.Random(42)`` in the GPU engines' order."""
+    the reference's golden fixtures), timed on this host (rank 0, N=1 only) with the GPU
+    run's OWN inputs: the gradients of its first ``steps + 1`` steps copied back from
+    HBM before the timing (model sets: every compressed tensor; flat buckets: the first
+    ``numel`` elements — all of flat-1B's by default), the same sample starts
+    (``random.Random(42)`` in the GPU engines' order), one warm-up step, then ``steps``
+    timed steps."""
     from oracle import torch_cpu
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
@@ -121,48 +127,41 @@ def cpu_baseline(run, wl, numel, steps, threads):
     try:
         if wl["kind"] == "model":
             b = run.b
-            grads = [g.cpu() for g, _ in run.grads]
+            host = [run.grad_of(i)[0].cpu() for i in range(steps + 1)]
             tensors = []
-            for i, (off, n) in enumerate(zip(b.offsets, b.numels)):
+            for off, n in zip(b.offsets, b.numels):
                 attrs = torch_cpu.attributes(n, wl["ratio"])
-                tensors.append((attrs, [g[off: off + n] for g in grads], torch.zeros(n), torch.zeros(n),
+                tensors.append((attrs, [g[off: off + n] for g in host], torch.zeros(n), torch.zeros(n),
                                 torch.empty(n)))
             N = sum(t[0][0] for t in tensors)
-            state = {"i": 0}
 
-            def step():
-                i = state["i"]
-                state["i"] += 1
+            def step(i):
                 for attrs, gs, m, v, out in tensors:   # DGCBatch.draw_starts' order
                     start = rng.randint(0, attrs[4] - 1) if attrs[0] != attrs[2] else 0
-                    torch_cpu.cpu_step(gs[i % 2], m, v, out, attrs, start, nesterov=wl["nesterov"])
-            what = (f"all {len(tensors)} compressed tensors ({N} elements) of {wl['model']}, the GPU run's "
-                    f"two gradient sets")
+                    torch_cpu.cpu_step(gs[i], m, v, out, attrs, start, nesterov=wl["nesterov"])
+            what = f"all {len(tensors)} compressed tensors ({N} elements) of {wl['model']}"
         else:
             N = int(min(numel, run.N))
             attrs = torch_cpu.attributes(N, wl["ratio"])
-            gs = [g[:N].cpu() for g in run.grads]
+            host = [run.grad_of(i)[:N].cpu() for i in range(steps + 1)]
             m, v, out = torch.zeros(N), torch.zeros(N), torch.empty(N)
-            state = {"i": 0}
 
-            def step():
-                i = state["i"]
-                state["i"] += 1
-                torch_cpu.cpu_step(gs[i % 2], m, v, out, attrs, rng.randint(0, attrs[4] - 1),
-                                   nesterov=wl["nesterov"])
-            what = (f"the first {N} elements of the GPU run's two {wl['numel']}-element gradient buffers "
-                    f"(same ratio, sample stride {attrs[4]})")
-        step()   # warm-up
+            def step(i):
+                torch_cpu.cpu_step(host[i], m, v, out, attrs, rng.randint(0, attrs[4] - 1), nesterov=wl["nesterov"])
+            what = (f"the whole {N}-element bucket" if N == run.N else
+                    f"the first {N} elements of the {run.N}-element bucket (same ratio, sample stride {attrs[4]})")
+        step(0)   # warm-up
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
+        for i in range(steps):
+            step(i + 1)
         dt = (time.perf_counter() - t0) / steps
     finally:
         torch.set_num_threads(prev)
     return {"value": N / dt, "unit": "grad elements/s", "cores": threads, "kind": "port",
-            "sample": f"{what} x {steps} steps after 1 warm-up step, sample starts from random.Random(42) "
-                      f"(compensate+sparsify+update+decompress, W=1, torch {torch.__version__} CPU ops as the "
-                      f"reference issues them): {dt * 1e3:.1f} ms/step on {threads} thread(s); {cpu_model()}"}
+            "sample": f"{what}, the GPU run's gradients of steps 1..{steps} after step 0 as warm-up, sample "
+                      f"starts from random.Random(42) (compensate+sparsify+update+decompress, W=1, torch "
+                      f"{torch.__version__} CPU ops as the reference issues them): {dt * 1e3:.1f} ms/step on "
+                      f"{threads} thread(s); {cpu_model()}"}
 
 
 # ---------------------------------------------------------------------------- profiles
@@ -245,34 +244,56 @@ def spawn(envs):
 
 
 # ---------------------------------------------------------------------------- workloads
-class FlatRun:
-    """One flat bucket per rank through dgc.bucket.DGCBucket."""
+def gradient_seed(rank, step):
+    """the synthetic gradient of ``rank`` at ``step``."""
+    return 0xD6C + 1000 * rank + step
 
-    def __init__(self, wl, rank, world, dev, fill):
+
+def fill_gradient(g, seed, bf16=False, chunk=1 << 30):
+    """g = N(0, 1) from one generator seeded ``seed``, in 2^30-element chunks (bf16-rounded
+    for the bf16-origin workload: dense ties)."""
+    gen = torch.Generator(device=g.device)
+    gen.manual_seed(seed)
+    for c0 in range(0, g.numel(), chunk):
+        c1 = min(g.numel(), c0 + chunk)
+        x = torch.randn(c1 - c0, generator=gen, device=g.device)
+        g[c0:c1] = x.to(torch.bfloat16).float() if bf16 else x
+        del x
+    return g
+
+
+def buffers_that_fit(nsteps, nbytes, dev, reserve):
+    """How many per-step gradient buffers of ``nbytes`` fit in the free HBM beside
+    ``reserve`` bytes still to be allocated (at least 2; steps cycle through them)."""
+    free, _ = torch.cuda.mem_get_info(dev)
+    return max(2, min(nsteps, int((free - reserve) // nbytes)))
+
+
+class FlatRun:
+    """One flat bucket per rank through dgc.bucket.DGCBucket; one gradient per step
+    (``nsteps`` buffers, generated before timing), or the workload's fixed ``buffers``."""
+
+    def __init__(self, wl, rank, world, dev, fill, nsteps=2):
         from dgc.bucket import DGCBucket
         N = wl["numel"]
         self.N = N
         self.b = DGCBucket(N, compress_ratio=wl["ratio"], momentum=0.9, nesterov=wl["nesterov"], device=dev,
                            world_size=world, fill=fill)
-        gen = torch.Generator(device=dev)
-        self.grads = []
-        for s in range(2):   # two alternating gradients per rank, generated before timing
-            gen.manual_seed(0xD6C + 1000 * rank + s)
-            g = torch.empty(N, device=dev)
-            for c0 in range(0, N, 1 << 30):
-                c1 = min(N, c0 + (1 << 30))
-                x = torch.randn(c1 - c0, generator=gen, device=dev)
-                g[c0:c1] = x.to(torch.bfloat16).float() if wl["grad"] == "bf16" else x
-                del x
-            self.grads.append(g)
         self.out = torch.empty(N, device=dev)
+        want = wl.get("buffers", nsteps)
+        self.nbuf = buffers_that_fit(want, 4 * N, dev, reserve=8 << 30) if "buffers" not in wl else want
+        self.grads = [fill_gradient(torch.empty(N, device=dev), gradient_seed(rank, s), wl["grad"] == "bf16")
+                      for s in range(self.nbuf)]
         self.elements = N
         self.k, self.S = self.b.k, self.b.num_samples
         self.payload = self.b.rank_stride
         self.vbytes, self.ibytes = 4, 8
 
+    def grad_of(self, i):
+        return self.grads[i % self.nbuf]
+
     def step(self, i, ev=None):
-        self.b.step(self.grads[i % 2], self.out, ev)
+        self.b.step(self.grad_of(i), self.out, ev)
 
     def k1_bytes(self):
         return 20 * self.N + 4 * self.b.cnt    # read g, mmt, vec; write mmt, vec; write the samples
@@ -289,12 +310,23 @@ class FlatRun:
                 "fill": b.fill, "exchange_parts": b.parts}
 
 
+def model_gradients(b, n_dense, seed, dev):
+    """A model set's gradients of one step: (flat compressed gradients in ``b``'s layout,
+    dense gradients), N(0, 1) x 1e-3 tensor after tensor from one generator."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    g = torch.zeros(b.flat_numel, device=dev)
+    for off, n in zip(b.offsets, b.numels):
+        g[off: off + n] = torch.randn(n, generator=gen, device=dev) * 1e-3
+    return g, torch.randn(n_dense, generator=gen, device=dev) * 1e-3
+
+
 class ModelRun:
     """A model's gradient set per rank: the compressed tensors through one DGCBatch
     step, the dense (dim <= 1) tensors as one flat allreduce + compensate(accumulate=False)
     (dgc/compression.py:173-177, 195-198)."""
 
-    def __init__(self, wl, rank, world, dev, fill="sparse"):
+    def __init__(self, wl, rank, world, dev, fill="sparse", nsteps=2):
         from dgc import comm, workloads
         from dgc.batch import DGCBatch
         comp, dense = workloads.split(getattr(workloads, wl["model"])())
@@ -308,14 +340,10 @@ class ModelRun:
                           fill="inline" if fill in ("inline", "allgather") else "sparse", payload_extra=extra)
         self.n_comp = sum(self.b.numels)
         self.world = world
-        gen = torch.Generator(device=dev)
-        self.grads = []
-        for s in range(2):
-            gen.manual_seed(0xD6C + 1000 * rank + s)
-            g = torch.zeros(self.b.flat_numel, device=dev)
-            for off, n in zip(self.b.offsets, self.b.numels):
-                g[off: off + n] = torch.randn(n, generator=gen, device=dev) * 1e-3
-            self.grads.append((g, torch.randn(self.n_dense, generator=gen, device=dev) * 1e-3))
+        # one gradient set per step (x1e-3): every compressed tensor in the batch's flat
+        # layout, then the dense tensors, from one generator seeded gradient_seed(rank, step)
+        self.nbuf = buffers_that_fit(nsteps, 4 * (self.b.flat_numel + self.n_dense), dev, reserve=2 << 30)
+        self.grads = [model_gradients(self.b, self.n_dense, gradient_seed(rank, s), dev) for s in range(self.nbuf)]
         self.dense_mmt = torch.zeros(self.n_dense, device=dev)
         self.dense_out = torch.empty(self.n_dense, device=dev)
         self.wire_dt = wire_dt
@@ -332,8 +360,11 @@ class ModelRun:
         from dgc import _lib
         self._lib = _lib
 
+    def grad_of(self, i):
+        return self.grads[i % self.nbuf]
+
     def step(self, i, ev=None):
-        g, gd = self.grads[i % 2]
+        g, gd = self.grad_of(i)
         ev = ev or {}
         L, b = self._lib.lib(), self.b
         from dgc import comm
@@ -438,12 +469,12 @@ class DropinRun:
         kw = {} if batch == "auto" else {"batch": batch}   # "auto": the drop-in default, no argument
         self.opt = DistributedOptimizer(inner, named_parameters=self.named, compression=compression, **kw)
         self.batched = self.opt._batched is not None
-        # ModelRun's two gradient sets, value for value, as per-parameter tensors; then a
-        # distinct copy per step (the per-tensor path decompresses into p.grad in place)
+        # ModelRun's per-step gradient sets, value for value, as per-parameter tensors (the
+        # per-tensor path decompresses into p.grad in place: a distinct set per step)
         gen = torch.Generator(device=dev)
-        base = []
-        for s_ in range(2):
-            gen.manual_seed(0xD6C + 1000 * rank + s_)
+        self.sets = []
+        for s_ in range(steps):
+            gen.manual_seed(gradient_seed(rank, s_))
             g = {n: torch.randn(workloads.numel(sh), generator=gen, device=dev).mul_(1e-3).view(sh)
                  for n, sh in comp_shapes}
             nd = sum(workloads.numel(sh) for _, sh in dense_shapes)
@@ -452,8 +483,7 @@ class DropinRun:
             for n, sh in dense_shapes:
                 g[n] = d[o: o + workloads.numel(sh)].clone().view(sh)
                 o += workloads.numel(sh)
-            base.append([g[n] for n, _ in self.named])
-        self.sets = [[t.clone() for t in base[i % 2]] for i in range(steps)]
+            self.sets.append([g[n] for n, _ in self.named])
         self.elements = sum(p.numel() for _, p in self.named)
         self.hooks = list(reversed(self.opt._hook_fns))
 
@@ -466,9 +496,22 @@ class DropinRun:
         self.opt.zero_grad()
 
 
+def data_note(wl, run, nsteps):
+    per = ("a fresh gradient per rank and step, seed 0xD6C + 1000*rank + step (SURVEY.md §8d), generated in "
+           "HBM before the timed region")
+    if "buffers" in wl:
+        per = (f"{wl['buffers']} gradient buffers per rank (seeds 0xD6C + 1000*rank + {{0, 1}}), steps alternate "
+               f"between them: a buffer per step would need {nsteps} x {4 * run.N / 1e9:.0f} GB of HBM")
+    elif run.nbuf < nsteps:
+        per += f" ({run.nbuf} buffers fit in HBM: steps cycle through them)"
+    kind = {"normal": "N(0,1)", "bf16": "N(0,1) rounded to bf16 (held in fp32)"}.get(wl.get("grad"), "N(0,1) x1e-3")
+    return (f"synthetic: torch.randn {kind} gradients, {per}; sample starts from random.Random(42); "
+            "momentum/velocity state evolves across steps from zero")
+
+
 def timed_steps(run, steps, warmup, world):
     """ms per step of ``run.step`` over ``steps`` steps after ``warmup`` (barrier +
-    synchronize on both sides, max over ranks)."""
+    synchronize on both sides, max over ranks); step i takes gradient set i."""
     for i in range(warmup):
         run.step(i)
     torch.cuda.synchronize()
@@ -494,7 +537,7 @@ def dropin_compare(model, rank, world, dev, steps, warmup):
     wl = dict(WORKLOADS[model])
     res = {"model": model, "steps": steps, "warmup": warmup}
     for fill in ("inline", "sparse"):
-        run = ModelRun(wl, rank, world, dev, fill)
+        run = ModelRun(wl, rank, world, dev, fill, steps + warmup)
         res[f"dgcbatch_{fill}_ms"] = round(timed_steps(run, steps, warmup, world), 4)
         del run
     for label, batch, n in (("optimizer_default_ms", "auto", steps), ("optimizer_batch_sparse_ms", "sparse", steps),
@@ -641,7 +684,9 @@ def main():
         comm.ONE_RANK_SHORTCUT = False
         backend = dist.get_backend()
     coll = world > 1 or one_rank
-    run = FlatRun(wl, rank, world, dev, args.fill) if wl["kind"] == "flat" else ModelRun(wl, rank, world, dev, args.fill)
+    nsteps = args.warmup + args.steps
+    run = (FlatRun(wl, rank, world, dev, args.fill, nsteps) if wl["kind"] == "flat" else
+           ModelRun(wl, rank, world, dev, args.fill, nsteps))
 
     log(f"{args.workload}: rank {rank}/{world} set up")
     phases = ("compensate", "select", "allgather", "decompress")
@@ -672,7 +717,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        run.step(i, evs[i])
+        run.step(args.warmup + i, evs[i])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     for name, fn in saved.items():
@@ -695,7 +740,7 @@ def main():
             dense = timed_steps(run, args.steps, 2, world)
             run.b.fill = "sparse"
         else:
-            dense = timed_steps(ModelRun(wl, rank, world, dev, "inline"), args.steps, args.warmup, world)
+            dense = timed_steps(ModelRun(wl, rank, world, dev, "inline", nsteps), args.steps, args.warmup, world)
         extras["dense_fill"] = {"ms_per_step": round(dense, 4), "steps": args.steps,
                                 "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
                                         "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
@@ -735,9 +780,7 @@ def main():
         "vs_baseline_note": "null: BASELINE.md holds no published number for this metric (the reference publishes "
                             "none); the CPU restatement of the reference timed on this host is cpu_baseline",
         "dtype": "f32",
-        "data": "synthetic: torch.randn N(0,1) gradients (bf16-rounded for flat-7B-bf16; x1e-3 for the model "
-                "sets), 2 alternating buffers per rank (seed 0xD6C + 1000*rank + buffer); momentum/velocity "
-                "state evolves across steps",
+        "data": data_note(wl, run, nsteps),
         "config": dict({"workload": f"{args.workload} ({wl['config']})", "compress_ratio": wl["ratio"],
                         "nesterov": wl["nesterov"], "momentum": 0.9, "momentum_masking": True, "wire": wire,
                         "parallelism": f"dp{world}"}, **run.config()),

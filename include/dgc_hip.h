@@ -188,7 +188,10 @@ int dgc_compensate(const float* grad, float* mmt, float* vec, float* out, int64_
 
 /* DGCSGDMemory.update (dgc/memory.py:72-77) as a standalone scatter: vec[i] = 0 and,
  * when mmt != NULL (momentum_masking), mmt[i] = 0 for i in indices[0..count).
- * Negative indices wrap like torch; out-of-range ones set *bad_flag (device int). */
+ * Negative indices wrap like torch (index_fill_); an index outside [-n, n) — where the
+ * reference's index_fill_ raises (dgc/memory.py:76-77) — is skipped and sets *bad_flag:
+ * a device int32 or a host-mapped (pinned) one the caller polls without synchronising;
+ * the library stores 1 there (never clears it). */
 int dgc_mask_indices(float* mmt, float* vec, int64_t n, const void* indices, int32_t idtype,
                      int64_t count, int32_t* bad_flag, void* stream);
 
@@ -418,11 +421,23 @@ int dgc_clear_split(const void* prev_gathered, int32_t world, int32_t parts, int
                     int32_t idtype, float* grad, int64_t n, void* ws, size_t ws_bytes, void* stream);
 
 /* Status word written by the decompress kernels: bit 0 = an index was out of
- * range [0, n) and was ignored; bit 1 = a run was not non-decreasing. Packed runs
+ * range [0, n) and was ignored (the reference's index_put_ raises,
+ * dgc/compression.py:191); bit 1 = a run was not non-decreasing; bit 2 = a packed
+ * header's count was outside [0, capacity] (the run was clamped to it). Packed runs
  * are then regrouped and summed exactly (indices unique within a run); a run given by
  * run_offsets to dgc_decompress is not regrouped (its stray entries were ignored).
  * Reads 4 bytes from the workspace (synchronous). */
 int dgc_decompress_status(const void* ws, int32_t* status, void* stream);
+/* Binds a decompress workspace to two host-mapped (pinned) int32 words [index, count]:
+ * every later decompress / scatter call on `ws` (dgc_decompress, dgc_decompress_packed,
+ * _over, dgc_scatter_packed, _cleared, dgc_scatter_split) that meets status bit 0 also
+ * stores 1 into sink[0], bit 2 into sink[1], from the kernel that finds it — so a
+ * DGC_SYNC_DEVICE caller (the engines) raises at its next step, as the reference raises
+ * at its index_put_, with no host synchronisation (nothing is written while the data are
+ * healthy). The library never clears the words. sink = NULL unbinds; rebinding `ws`
+ * replaces its binding. The binding is keyed by the workspace address: unbind before
+ * the workspace is freed. */
+int dgc_decompress_bind_sink(const void* ws, int32_t* sink);
 
 /* Measurement only (bench.py): K1's memory shape — d = a + c, e = b + c over n
  * floats (n/4 float4; 16-B aligned buffers), three non-temporal 16-B reads and two
@@ -525,6 +540,10 @@ int dgc_mask_packed16(const void* payload, int64_t capacity, int32_t vdtype, int
 int dgc_decompress_packed16(const void* payload, int32_t world, int64_t rank_stride, int64_t capacity,
                             int32_t vdtype, int32_t idtype, void* grad, int32_t dtype, int64_t n, float scale,
                             int32_t* bad_flag, void* stream);
+/* bad_flag of dgc_mask_indices16 / dgc_decompress16 / dgc_decompress_packed16: a device
+ * or host-mapped int32 that receives 1 when an index is outside [-n, n) (negative ones
+ * wrap as in index_put_ / index_fill_; the packed form takes none below 0) and 2 when a
+ * packed header's count is outside [0, capacity] (that run is skipped); never cleared. */
 int dgc_gather16(const void* const* srcs, const int64_t* numels, const int64_t* offsets, int32_t count, void* dst,
                  void* stream);
 

@@ -218,6 +218,23 @@ def comm_worker(rank, world, port, queue):
         b = torch.full((2,), float(rank + 1))
         out.append(comm.synchronize(comm.allreduce_async_(b, name="b", op=comm.Sum)).tolist())
         out.append((comm.size(), comm.rank()))
+        # above RANK_ORDER_MAX: the backend's allreduce (no allgather of W copies)
+        calls = {"all_reduce": 0, "all_gather_into_tensor": 0}
+        real = {k: getattr(dist, k) for k in calls}
+
+        def counted(k):
+            def f(*a, **kw):
+                calls[k] += 1
+                return real[k](*a, **kw)
+            return f
+        for k in calls:
+            setattr(dist, k, counted(k))
+        big = torch.arange(comm.RANK_ORDER_MAX + 5, dtype=torch.float32) * (rank + 1)
+        got = comm.synchronize(comm.allreduce_async_(big, name="big", op=comm.Average))
+        for k in calls:
+            setattr(dist, k, real[k])
+        want = torch.arange(comm.RANK_ORDER_MAX + 5, dtype=torch.float32) * sum(range(1, world + 1)) / world
+        out.append((got is big, torch.equal(got, want), dict(calls)))
         queue.put((rank, out))
     finally:
         dist.destroy_process_group()

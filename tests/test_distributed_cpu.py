@@ -47,10 +47,12 @@ def test_resnet20_config0_matches_reference():
 @pytest.mark.timeout(300)
 def test_comm_collectives_gloo():
     out = run(H.comm_worker, 2)
-    for rank, (gathered, avg, sm, (size, rk)) in out.items():
+    for rank, (gathered, avg, sm, (size, rk), big) in out.items():
         assert gathered == [0.0, 1.0, 10.0, 11.0, 12.0]       # rank order, ragged rows
         assert avg == [1.5, 1.5, 1.5] and sm == [3.0, 3.0]
         assert size == 2 and rk == rank
+        # a tensor above comm.RANK_ORDER_MAX: one in-place backend allreduce, / W
+        assert big == (True, True, {"all_reduce": 1, "all_gather_into_tensor": 0}), big
 
 
 @pytest.mark.timeout(120)

@@ -1,6 +1,6 @@
 """Parity at the bench's own size: the 1e9-element flat bucket (BASELINE configs[3])
-stepped through dgc.bucket.DGCBucket exactly as bench.py steps it (the same two
-alternating seeded gradients, ratio 0.001, nesterov), compared with the numpy oracle
+stepped through dgc.bucket.DGCBucket exactly as bench.py steps it (the same fresh
+gradient per step, seed 0xD6C + step, ratio 0.001, nesterov), compared with the numpy oracle
 after EVERY step: the transmitted indices (in order) and values, momentum and
 velocity, and the decompressed dense gradient, all bit for bit. The steady state the
 bench times — K1's speculative candidate lists serving the selection, spilled lists,
@@ -41,17 +41,13 @@ def test_flat_1b_bucket_steps_match_oracle():
     b = DGCBucket(N, compress_ratio=1e-3, momentum=0.9, nesterov=True, device=DEV, seed=42, fill="sparse")
     attrs = O.attributes(N, 1e-3)
     rng = random.Random(42)
-    gen = torch.Generator(device=DEV)
-    grads = []
-    for s in range(2):   # bench.py's FlatRun: seeds 0xD6C + 1000*rank + buffer, rank 0
-        gen.manual_seed(0xD6C + s)
-        grads.append(torch.randn(N, generator=gen, device=DEV))
+    g = torch.empty(N, device=DEV)
     out = torch.empty(N, device=DEV)
     m_o = np.zeros(N, np.float32)
     v_o = np.zeros(N, np.float32)
     seen = []
     for s in range(steps):
-        g = grads[s % 2]
+        _bench_gradient(g, N, 0xD6C + s, bf16=False)   # bench.py's FlatRun, rank 0, step s
         start = rng.randint(0, attrs[4] - 1)
         b.step(g, out)
         torch.cuda.synchronize()

@@ -1,7 +1,7 @@
 """Parity at the steady state the bench times, for the two model-set workloads
 (BASELINE configs[1] ResNet-50, configs[2] VGG-16-BN): ``bench.py``'s own ``ModelRun``
-— the same ``DGCBatch`` settings, the same two alternating x1e-3 ``randn`` gradient
-sets (seeds 0xD6C + buffer), the same sample starts (``random.Random(42)``, one draw
+— the same ``DGCBatch`` settings, the same x1e-3 ``randn`` gradient set per step (seed
+0xD6C + step), the same sample starts (``random.Random(42)``, one draw
 per sampled tensor per step), the same persistent output with the sparse re-zero —
 stepped 25 times and compared with the oracle after EVERY step, tensor by tensor:
 
@@ -52,20 +52,22 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
         pytest.skip("no GPU")
     bench = _bench()
     wl = bench.WORKLOADS[workload]
-    run = bench.ModelRun(wl, 0, 1, DEV, "sparse")
+    steps = 25
+    run = bench.ModelRun(wl, 0, 1, DEV, "sparse", nsteps=steps)
+    assert run.nbuf == steps
     b = run.b
     assert b.fill == "sparse"
     fp16, int32, nest, ratio = wl["fp16"], wl["int32"], wl["nesterov"], wl["ratio"]
-    host = [[g[off: off + n].cpu().numpy() for off, n in zip(b.offsets, b.numels)] for g, _ in run.grads]
-    dense_host = [gd.cpu().numpy() for _, gd in run.grads]
     attrs = [O.attributes(n, ratio) for n in b.numels]
     state = [(np.zeros(n, np.float32), np.zeros(n, np.float32)) for n in b.numels]
     dense_m = np.zeros(run.n_dense, np.float32)
     ref_rng = random.Random(42)
     exact = as_set = full_pass_steps = resample_max = 0
     branches = {}
-    steps = 25
     for s in range(steps):
+        g, gd = run.grad_of(s)
+        host = [g[off: off + n].cpu().numpy() for off, n in zip(b.offsets, b.numels)]
+        dense_host = gd.cpu().numpy()
         run.step(s)
         torch.cuda.synchronize()
         sent = b.transmitted()
@@ -80,7 +82,7 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
             key = f"{workload}/step{s}/{name}"
             assert start == b.starts[t], key
             m_o, v_o = state[t]
-            O.compensate(host[s % 2][t], m_o, v_o, 0.9, nest)
+            O.compensate(host[t], m_o, v_o, 0.9, nest)
             ov, oi, oinfo = O.sparsify(v_o, a, start)
             info = infos[t]
             assert info["branch"] == oinfo["branch"], (key, info)
@@ -111,7 +113,7 @@ def test_model_set_bench_steady_state_matches_oracle(workload):
                 resample_max = max(resample_max, info["candidates"])
                 assert info["tie_rule"] in ("exact", "set"), (key, info)
         # dense tensors: wire cast -> (W = 1 allreduce) -> compensate(accumulate=False)
-        src = dense_host[s % 2].astype(np.float16).astype(np.float32) if fp16 else dense_host[s % 2]
+        src = dense_host.astype(np.float16).astype(np.float32) if fp16 else dense_host
         want = O.compensate(src, dense_m, None, 0.9, nest, accumulate=False)
         assert np.array_equal(bits(run.dense_out.cpu().numpy()), bits(want)), (workload, s)
         print(f"{workload} step {s}: branches so far {branches}, resamples exact {exact} / set {as_set} "

@@ -23,7 +23,7 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     full = len(sys.argv) > 3 and sys.argv[3] == "all"   # every tensor, not only the notable ones
     dev = torch.device("cuda:0")
-    run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, dev)
+    run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, dev, "sparse", steps)   # a gradient set per step
     b = run.b
     for i in range(steps):
         run.step(i)
