@@ -2648,7 +2648,7 @@ __device__ __forceinline__ bool setg_consensus(SetG* g, uint32_t G) {
 // Barrier among the G workgroups: everything they exchange is device atomics, read back
 // with agent-scope atomic loads (last_block_arrival's "atomics both sides"), so draining
 // this workgroup's atomics (vmcnt(0)) before the arrival is the only ordering needed.
-__device__ __forceinline__ void setg_barrier(SetG* g, uint32_t G) {
+__device__ __forceinline__ void setg_barrier(SetG* g, uint32_t G, uint32_t* status) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2667,7 +2667,10 @@ __device__ __forceinline__ void setg_barrier(SetG* g, uint32_t G) {
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (!passed) __hip_atomic_store(&g->broken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!passed) {   // the replay takes the tensor (exact); recorded for the caller
+                __hip_atomic_store(&g->broken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicOr(status, (uint32_t)DGC_K5_SET_BROKEN);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -2682,7 +2685,10 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
                                                   SelState* st, const TDesc& d) {
     const int64_t n64 = st->n_cur;
     SetG* g = w.setg + t;
-    if (G > 1 && !setg_consensus(g, G)) return;   // not all resident: the replay
+    if (G > 1 && !setg_consensus(g, G)) {   // not all resident: the replay (recorded for the caller)
+        if (b == 0 && threadIdx.x == 0) atomicOr(&w.nthg[t].status, (uint32_t)DGC_K5_SET_FALLBACK);
+        return;
+    }
     SET_STAMP(0);
     const int n = (int)n64;
     const uint32_t k = (uint32_t)d.k;
@@ -2742,7 +2748,7 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
             uint32_t* gh = pass == 0 ? g->hist0 : g->hist1;
             for (int q = tid; q < (int)nb; q += kScanThreads)
                 if (h[q]) __hip_atomic_fetch_add(&gh[q], h[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            setg_barrier(g, G);
+            setg_barrier(g, G, &w.nthg[t].status);
             for (int q = tid; q < (int)nb; q += kScanThreads)
                 h[q] = __hip_atomic_load(&gh[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
@@ -2802,7 +2808,7 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
     }
     static_assert(kSetRoundsMax * kWaves <= kScanThreads, "one compaction count per thread");
     if (G > 1) {
-        setg_barrier(g, G);
+        setg_barrier(g, G, &w.nthg[t].status);
         if (tid == 0) {
             uint32_t base = 0;
             for (uint32_t i = 0; i < b; ++i)

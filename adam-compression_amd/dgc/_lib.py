@@ -48,7 +48,7 @@ class SelectInfo(ctypes.Structure):
                 ("k5_status", ctypes.c_int32), ("list_threshold", ctypes.c_float)]
 
 
-K5_FALLBACK, K5_BROKEN, K5_RECOVERED = 1, 2, 4
+K5_FALLBACK, K5_BROKEN, K5_RECOVERED, K5_SET_FALLBACK, K5_SET_BROKEN = 1, 2, 4, 8, 16
 
 
 def info_dict(i, what):
@@ -62,7 +62,8 @@ def info_dict(i, what):
                 overflow_segments=i.overflow_segments, full_passes=i.full_passes,
                 tie_rule=TIE_RULES.get(i.tie_rule, i.tie_rule), window_keys=i.window_keys,
                 list_threshold=i.list_threshold,
-                k5_fallback=bool(i.k5_status & K5_FALLBACK), k5_recovered=bool(i.k5_status & K5_RECOVERED))
+                k5_fallback=bool(i.k5_status & K5_FALLBACK), k5_recovered=bool(i.k5_status & K5_RECOVERED),
+                k5s_fallback=bool(i.k5_status & K5_SET_FALLBACK), k5s_broken=bool(i.k5_status & K5_SET_BROKEN))
 
 
 INFO_BYTES = ctypes.sizeof(SelectInfo)

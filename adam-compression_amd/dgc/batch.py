@@ -296,12 +296,13 @@ class DGCBatch:
 
     def send(self):
         """Issues the exchange of this step's payload (W > 1): one allgather, or one per
-        part (split); ``decompress`` waits for it."""
+        part (split); ``decompress`` waits for it. Nothing is issued in between, so a
+        single allgather goes out on the current stream (``comm.COLLECTIVE_ISSUE``)."""
         if self.exchanging:
             if self.xchg is not None:
                 self._inflight = self.xchg.send(self.payload, self.gathered)
             else:
-                self._inflight = [comm.allgather_packed_async(self.payload, out=self.gathered)]
+                self._inflight = [comm.allgather_packed_async(self.payload, out=self.gathered, wait=True)]
 
     def exchange(self):
         """The exchange; a single allgather is also waited for here, a split one part by

@@ -213,7 +213,7 @@ class DGCBucket:
             if self.xchg is not None:
                 self._inflight = self.xchg.send(self.payload, self.gathered)
             else:
-                comm.allgather_packed_async(self.payload, out=self.gathered).wait()
+                comm.allgather_packed_async(self.payload, out=self.gathered, wait=True).wait()
 
     def _decompress_split(self, out, dense, cleared=False):
         """The split exchange's decompress: the zero_() (the dense fill, or the sparse

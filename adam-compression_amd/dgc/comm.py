@@ -198,8 +198,20 @@ def allgather_async(tensor, name=None):
     return Handle(work, finish)
 
 
-def allgather_packed_async(payload, out=None):
-    """Fixed-size byte allgather of one packed DGC payload per rank -> [W * P] bytes."""
+# How a collective whose result the caller waits for at once is issued under RCCL:
+# "current" (default) with async_op=False — torch then runs it on the caller's current
+# stream, ordered like a kernel launch; "async" with async_op=True and wait() — on
+# torch's collective stream, joined to the current stream by events, which costs a
+# stream hand-off per collective (~35 us at one rank). DGC_COLLECTIVE_ISSUE
+# selects; bench.py --rccl-one-rank times both.
+COLLECTIVE_ISSUE = os.environ.get("DGC_COLLECTIVE_ISSUE", "current")
+
+
+def allgather_packed_async(payload, out=None, wait=False):
+    """Fixed-size byte allgather of one packed DGC payload per rank -> [W * P] bytes.
+    ``wait=True``: the caller needs the result before its next launch (a single
+    collective per step) — under RCCL it is issued on the current stream
+    (``COLLECTIVE_ISSUE`` "current"), so the returned handle is already complete."""
     W = size()
     if out is None:
         out = torch.empty(W * payload.numel(), dtype=torch.uint8, device=payload.device)
@@ -212,6 +224,9 @@ def allgather_packed_async(payload, out=None):
         host_out = torch.empty(out.numel(), dtype=torch.uint8)
         work = dist.all_gather_into_tensor(host_out, host_in, async_op=True)
         return Handle(work, lambda: out.copy_(host_out))
+    if wait and COLLECTIVE_ISSUE == "current":
+        dist.all_gather_into_tensor(out, payload, async_op=False)
+        return Handle(output=out)
     work = dist.all_gather_into_tensor(out, payload, async_op=True)
     return Handle(work, lambda: out)
 

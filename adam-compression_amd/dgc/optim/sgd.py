@@ -12,7 +12,12 @@ K7 in ``csrc/sgd.hip``, for fp32; ``dgc_sgd_step16`` for bf16 / fp16): read p, g
 (fp32: ``add(alpha)`` is one fused multiply-add; 16-bit: every op rounds to the
 dtype, alpha too, with the CPU kernels' vector body / scalar tail — oracle
 ``dgcsgd_step16``, pinned to tests/golden/sgd16.*), so the weights are bit-identical to
-the reference's. Every other parameter — on the CPU (the gloo plumbing tests), or on
+the reference's. For 16-bit parameters "the reference's" means what the fixtures pin: a
+ONE-thread CPU run on the AVX2 kernels (32-element vector body; tests/golden/
+make_goldens.py sets torch.set_num_threads(1)). A multi-threaded CPU run gives every
+parallel chunk of a tensor over 32768 elements its own scalar tail, the AVX512 kernels
+a 64-element body, and a CUDA run one rounding with an fp32 alpha — parity with those
+is unpinned. Every other parameter — on the CPU (the gloo plumbing tests), or on
 the GPU but not a contiguous fp32 / bf16 / fp16 tensor with a contiguous gradient of
 its dtype (channels_last convolutions, a non-contiguous view) — takes the reference's
 own torch op sequence, as the reference accepts any of them. The optimizer state keeps

@@ -304,6 +304,9 @@ class FlatRun:
     def info(self):
         return self.b.last_info()
 
+    def records(self):
+        return [self.b.last_info()]
+
     def config(self):
         b = self.b
         return {"numel": self.N, "num_selects": b.k, "num_samples": b.num_samples, "sample_stride": b.stride,
@@ -418,6 +421,9 @@ class ModelRun:
     def k1_bytes(self):
         # every compressed tensor: read g, mmt, vec; write mmt, vec; plus the samples written
         return 20 * self.n_comp + 4 * sum(a[1] + 1 for a in self.b.attrs if a[1] != 0)
+
+    def records(self):
+        return self.b.infos()
 
     def info(self):
         infos = self.b.infos()
@@ -555,28 +561,36 @@ def dropin_compare(model, rank, world, dev, steps, warmup):
     return res
 
 
+CEILING_BYTES = 256 << 20   # per rank: the large-message allgather that bounds what RCCL can give here
+
+
 def allgather_probe(run, world, reps=5):
-    """The step's exchange alone, after the timed steps: one RCCL allgather of the packed
-    payload (its bus bandwidth), and — split exchange — the parts' collectives issued
-    and waited for together (dgc/exchange.py)."""
+    """The step's exchange alone, after the timed steps, with HIP events on the compute
+    stream around issue + completion: one RCCL allgather of the packed payload issued
+    both ways (``comm.COLLECTIVE_ISSUE``: on the current stream, async_op=False; on
+    torch's collective stream, async_op=True + wait), the split exchange's parts when
+    there are any, and a same-run ceiling — ``all_gather_into_tensor`` of 256 MB per rank
+    (its bus bandwidth is the most RCCL moves over these links in this run)."""
     from dgc import comm
     b = run.b
     pay = b.payload
-    out = torch.empty(world * pay.numel(), dtype=torch.uint8, device=pay.device)
+    dev = pay.device
+    out = torch.empty(world * pay.numel(), dtype=torch.uint8, device=dev)
 
-    def timed(fn):
+    def timed(fn, n=reps):
         fn()
         dist.barrier()
         torch.cuda.synchronize()
         a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        for _ in range(reps):
+        for _ in range(n):
             fn()
         e.record()
         torch.cuda.synchronize()
-        return a.elapsed_time(e) / reps
+        return a.elapsed_time(e) / n
 
-    res = {"single_ms": timed(lambda: comm.allgather_packed_async(pay, out=out).wait())}
+    res = {"single_ms": timed(lambda: dist.all_gather_into_tensor(out, pay, async_op=False)),
+           "single_async_wait_ms": timed(lambda: dist.all_gather_into_tensor(out, pay, async_op=True).wait())}
     if getattr(b, "xchg", None) is not None:
         x = b.xchg
         g = torch.empty_like(x.gathers[0])
@@ -585,7 +599,36 @@ def allgather_probe(run, world, reps=5):
             for h in x.send(pay, g):
                 h.wait()
         res.update(parts=x.parts, split_ms=timed(split))
+    big = torch.empty(CEILING_BYTES, dtype=torch.uint8, device=dev)
+    big_out = torch.empty(world * CEILING_BYTES, dtype=torch.uint8, device=dev)
+    res["ceiling_bytes_per_rank"] = CEILING_BYTES
+    res["ceiling_ms"] = timed(lambda: dist.all_gather_into_tensor(big_out, big, async_op=False), 3)
+    del big, big_out
+    res["issue_default"] = comm.COLLECTIVE_ISSUE
     return res
+
+
+def selection_steps(run, steps, start):
+    """The selection records of ``steps`` more steps after the timed ones (untimed: each
+    step's per-tensor records are read back, a host sync per step): branches over
+    tensor-steps, full select passes per step, the resamples by tie rule, and how often
+    the resample's multi-workgroup phases fell back — K5's global phase not co-resident
+    (k5_fallback) or recovered after a barrier timeout (k5_recovered), K5s's set path not
+    co-resident (k5s_fallback) or broken (k5s_broken): exact results either way, slower."""
+    agg = {"steps": steps, "branches": {}, "full_passes_per_step": [], "resamples": {"set": 0, "exact": 0},
+           "max_resample_candidates": 0, "k5_fallback": 0, "k5_recovered": 0, "k5s_fallback": 0, "k5s_broken": 0}
+    for i in range(steps):
+        run.step(start + i)
+        recs = run.records()
+        agg["full_passes_per_step"].append(sum(r["full_passes"] for r in recs))
+        for r in recs:
+            agg["branches"][r["branch"]] = agg["branches"].get(r["branch"], 0) + 1
+            if r["branch"] == "resample":
+                agg["resamples"][r["tie_rule"]] = agg["resamples"].get(r["tie_rule"], 0) + 1
+                agg["max_resample_candidates"] = max(agg["max_resample_candidates"], r["candidates"])
+            for key in ("k5_fallback", "k5_recovered", "k5s_fallback", "k5s_broken"):
+                agg[key] += int(r[key])
+    return agg
 
 
 def hbm_probe(reads, writes, reps=5):
@@ -730,6 +773,22 @@ def main():
     ms = {p: sum(e[p][0].elapsed_time(e[p][1]) for e in evs) / args.steps for p in timed}
     info = run.info()
     extras = {}
+    if coll and not args.no_extras and getattr(run.b, "xchg", None) is None:
+        # the step again with the single allgather issued the other way (dgc/comm.py
+        # COLLECTIVE_ISSUE): on the current stream vs on torch's collective stream + wait
+        from dgc import comm
+        mode = comm.COLLECTIVE_ISSUE
+        other = "async" if mode == "current" else "current"
+        comm.COLLECTIVE_ISSUE = other
+        try:
+            other_ms = timed_steps(run, args.steps, 2, world)
+        finally:
+            comm.COLLECTIVE_ISSUE = mode
+        extras["issue_modes"] = {
+            "default": mode, f"{mode}_ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            f"{other}_ms_per_step": round(other_ms, 4),
+            "note": "current = all_gather_into_tensor(async_op=False), run by torch on the caller's stream; async = "
+                    "async_op=True + wait(), on torch's collective stream joined by events"}
     if not args.no_extras and run.b.fill == "sparse":
         # the same steps with the reference's dense zero_() (dgc/compression.py:191) before
         # the scatter: what the persistent output's re-zero saves. The flat bucket goes on
@@ -745,6 +804,7 @@ def main():
                                 "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
                                         "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
     xgmi = allgather_probe(run, world) if coll else None
+    sel_steps = selection_steps(run, args.steps, nsteps)
     probe = hbm_probe(*run.probe_buffers())   # after the timed steps: overwrites the state
     ms_step = elapsed * 1e3 / args.steps
     full_passes = info.get("full_passes", 0)
@@ -797,18 +857,25 @@ def main():
         "phase_ms": {p: round(v, 4) for p, v in ms.items()},
         "compensate_ms_per_step": [round(e["compensate"][0].elapsed_time(e["compensate"][1]), 3) for e in evs],
         "selection": info,
+        "selection_steps": sel_steps,
     }
     if coll:
         res["collectives_per_step"] = {name: c / args.steps for name, c in counts.items()}
     if xgmi is not None and world == 1:   # --rccl-one-rank: the collective's own cost, no link traffic
         res["allgather"] = dict({"payload_bytes_per_rank": run.payload,
-                                 "note": "one rank: the RCCL collectives' cost without link traffic"}, **xgmi)
+                                 "note": "one rank: the RCCL collectives' cost without link traffic (ceiling_ms: "
+                                         "a 256 MB one-rank allgather, i.e. a device copy)"}, **xgmi)
     elif xgmi is not None:
         bus = (world - 1) * run.payload / (xgmi["single_ms"] * 1e-3) / 1e9
+        ceiling = (world - 1) * xgmi["ceiling_bytes_per_rank"] / (xgmi["ceiling_ms"] * 1e-3) / 1e9
         res["allgather"] = dict({"payload_bytes_per_rank": run.payload, "bus_GBs": bus,
                                  "peak_GBs": (world - 1) * XGMI_LINK_GBS, "frac": bus / ((world - 1) * XGMI_LINK_GBS),
-                                 "note": "one all_gather_into_tensor of the packed payload alone, after the timed "
-                                         "steps (HIP events on the compute stream around issue + wait)"}, **xgmi)
+                                 "ceiling_GBs": ceiling, "frac_of_ceiling": bus / ceiling,
+                                 "ceiling_frac_of_links": ceiling / ((world - 1) * XGMI_LINK_GBS),
+                                 "note": "bus GB/s = (W-1) x bytes per rank / time; one all_gather_into_tensor of the "
+                                         "packed payload alone after the timed steps (HIP events on the compute "
+                                         "stream around issue + completion); peak = (W-1) x 153 GB/s of xGMI links; "
+                                         "ceiling = the same collective of 256 MB per rank in this run"}, **xgmi)
     log(f"{args.workload}: {ms_step:.3f} ms/step on the GPU")
     if world == 1 and not args.no_extras:
         model = wl["model"] if wl["kind"] == "model" else args.dropin_model

@@ -171,7 +171,12 @@ typedef struct dgc_select_info {
                                  none); diagnostics of the speculative listing       */
 } dgc_select_info;
 
-enum { DGC_K5_FALLBACK = 1, DGC_K5_BROKEN = 2, DGC_K5_RECOVERED = 4 };
+/* bit 3 (DGC_K5_SET_FALLBACK): the batch engines' multi-workgroup set path (K5s)
+   found its workgroups not all resident and left the tensor to the exact replay; bit 4
+   (DGC_K5_SET_BROKEN): a K5s barrier timed out, the replay took the tensor (exact
+   either way — counted by the engines' selection records) */
+enum { DGC_K5_FALLBACK = 1, DGC_K5_BROKEN = 2, DGC_K5_RECOVERED = 4, DGC_K5_SET_FALLBACK = 8,
+       DGC_K5_SET_BROKEN = 16 };
 
 const char* dgc_last_error(void);
 const char* dgc_version(void);
@@ -499,7 +504,9 @@ int dgc_sgd_step(float* const* params, const float* const* grads, float* const* 
  * torch-CPU ops on a 16-bit tensor do — alpha rounded to the dtype; `add(alpha)` rounds
  * fl32(x + y * alpha) once in the first n - n % 32 elements of a tensor (the CPU
  * kernels' vector body) and rounds the product first in the last n % 32 (their scalar
- * tail). */
+ * tail) — the split of a ONE-thread AVX2 CPU run, which tests/golden/sgd16.* pins; the
+ * per-chunk tails of a multi-threaded run, AVX512's 64-element body and a CUDA run's
+ * single rounding are not reproduced (parity with those unpinned). */
 int dgc_sgd_step16(void* const* params, const void* const* grads, void* const* bufs, const int64_t* numels,
                    const int32_t* first, int32_t count, float lr, float momentum, float dampening,
                    float weight_decay, int32_t nesterov, int32_t dtype, void* stream);

@@ -25,7 +25,9 @@ SHAPES = [("conv.weight", (64, 3, 7, 7)), ("bn.weight", (64,)), ("bn.bias", (64,
           ("big.weight", (512, 512, 3, 3)), ("late.weight", (16, 16))]
 
 
-def _run(batch, fp16, modes, monkeypatch, dtype=torch.float32):
+def _run(batch, fp16, modes, monkeypatch, dtype=torch.float32, on_step=None):
+    """The steps ``modes`` through DistributedOptimizer(batch=...); ``on_step(opt, grads)``
+    after each synchronize(), with the gradients autograd handed over."""
     from dgc.compression import DGCCompressor
     from dgc.horovod import DistributedOptimizer
     from dgc.memory import DGCSGDMemory
@@ -56,11 +58,14 @@ def _run(batch, fp16, modes, monkeypatch, dtype=torch.float32):
                 p.grad = buf[1:].view(p.shape)   # 4-B aligned only
             else:
                 p.grad = g.clone()
+        grads = {n: p.grad.clone() for n, p in named} if on_step else None
         for p, hook in hooks:
             if p is not late:   # late.weight's hook never fires
                 hook()
         opt.synchronize()
         torch.cuda.synchronize()
+        if on_step:
+            on_step(opt, grads)
         res = {n: (p.grad.clone() if p.grad is not None else None) for n, p in named}
         st = comp.memory.state_dict()
         res.update({f"m:{n}": t.clone() for n, t in st["momentums"].items()})

@@ -199,3 +199,42 @@ def test_batched_optimizer_over_rccl(batch, fp16, rccl_one_rank, monkeypatch):
         assert w.keys() == g.keys()
         for k in w:
             assert torch.equal(dropin._bits(w[k]), dropin._bits(g[k])), (step, k)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("parts", [1, 2], ids=["payload-tail", "split-own-allgather"])
+@pytest.mark.parametrize("fp16", [False, True], ids=["wire-dtype", "wire-fp16"])
+def test_batched_optimizer_dense_wire_bytes_over_rccl(parts, fp16, rccl_one_rank, monkeypatch):
+    """batch="sparse" through RCCL: the dense tensors' wire values (compress's cast,
+    dgc/compression.py:175-177) arrive byte for byte as dgc_gather_cast wrote them — in
+    the gathered payload's tail at ``extra_off`` of every rank's ``rank_stride`` (one
+    collective), or, when the exchange splits (DGC_EXCHANGE_PARTS=2), in their own
+    allgather (``dense_gathered``) — and the weights equal the one-rank step without
+    collectives (the re-zero's alternating gather buffers included)."""
+    monkeypatch.setenv("DGC_EXCHANGE_PARTS", str(parts))
+    wire = torch.float16 if fp16 else torch.float32
+    checked = []
+
+    def on_step(opt, grads):
+        plan = opt._batched._plan
+        b = plan["batch"]
+        assert b.parts == parts and (b.extra_off is None) == (parts > 1)
+        if parts > 1:
+            rows = plan["dense_gathered"].view(1, -1)
+        else:
+            rows = b.gathered.view(1, b.rank_stride)[:, b.extra_off:]
+        for n, p, off, _ in plan["dense"]:
+            nb = p.numel() * torch.empty(0, dtype=wire).element_size()
+            ob = off * torch.empty(0, dtype=wire).element_size()
+            want = grads[n].reshape(-1).to(wire).view(torch.uint8)
+            assert torch.equal(rows[0, ob: ob + nb], want), n
+        checked.append(len(plan["dense"]))
+
+    modes = ["fresh", "fresh", "inplace", "fresh", "fresh"]
+    got = dropin._run("sparse", fp16, modes, monkeypatch, on_step=on_step)
+    assert len(checked) == len(modes) and checked[0] > 0
+    monkeypatch.setattr(rccl_one_rank, "ONE_RANK_SHORTCUT", True)
+    want = dropin._run("sparse", fp16, modes, monkeypatch)
+    for step, (w, g) in enumerate(zip(want, got)):
+        for k in w:
+            assert torch.equal(dropin._bits(w[k]), dropin._bits(g[k])), (step, k)
