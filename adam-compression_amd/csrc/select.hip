@@ -108,6 +108,8 @@ constexpr int kSpecWords = 8;                   // per-tensor speculation state 
 constexpr int kChainOneWords = 256;             // SelWS::chain: k_chain_one's words (zeroed every call) ...
 constexpr int kChainWords = kChainOneWords + 128;   // ... then k_rs_passes' (zero at rest)
 constexpr int kEmitSplit = 4;                   // k_emit workgroups per group
+constexpr int64_t kSetOneMax = kSetCoopMin;     // K5s: one workgroup up to this many candidates (DGC_SET_ONE)
+constexpr int64_t kQueueFold = 16384;           // k_nth_select emits its replay itself when every k <= this
 
 int64_t payload_layout(int64_t capacity, int vd, int id, int64_t* voff, int64_t* ioff);   // decompress.hip
 
@@ -238,6 +240,7 @@ struct Layout {
     int32_t T = 0;
     int64_t nseg = 0, ngrp = 0, nsamp = 0, ncand = 0, ngpos = 0;
     int64_t max_cand = 0;       // the largest K5 candidate capacity of a tensor
+    int64_t max_k = 0;          // the largest num_selects
     int32_t nsmall = 0;
     int32_t nwins = 0;          // tensors with a K1 sample window (their ids follow the small ones)
     int32_t nplain = 0;         // multi-block threshold tasks without a window (k_rs_reset_samples)
@@ -313,6 +316,7 @@ static void build_layout(const TensorIn* in, int32_t T, bool padded, Layout& L, 
         d.cand_cap = nth_cand_cap(d.n, d.k);
         cand += d.cand_cap;
         L.max_cand = std::max(L.max_cand, d.cand_cap);
+        L.max_k = std::max(L.max_k, d.k);
         d.gpos_off = gpos;
         gpos += 2 * (d.cand_cap / 2 + 1);
         d.idx_base = T > 1 ? d.off : 0;
@@ -1266,6 +1270,21 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
     select_pass_body<ALIGNED>(vec_flat, w, which, p, blockIdx.x);
 }
 
+// One count pass as ONE launch: the list counts (the first ncnt workgroups) beside the
+// full select pass (the rest) — a tensor takes one of the two (t_cur >= t_list or not),
+// so the two run side by side instead of one launch after the other. Only for calls
+// whose decide steps cannot leave a tensor active for a recount within the launch (the
+// multi-threshold lowering: resample on, max_iters <= kMaxLower — then a decide either
+// finishes the tensor or hands it to the lowering), so both gates read one state.
+template <bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)
+k_count_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p, int ncnt) {
+    if ((int)blockIdx.x < ncnt)
+        count_lists_body(vec_flat, w, p, blockIdx.x);
+    else
+        select_pass_body<ALIGNED>(vec_flat, w, which, p, (int64_t)blockIdx.x - ncnt);
+}
+
 // Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
 // reference's "lower" recounts, dgc/compression.py:140-148, all at once). The last
 // workgroup of the tensor picks j* = the first j whose count reaches lower*k (else
@@ -2096,6 +2115,11 @@ struct FinishArgs {
     // packed payload's header word 1, read by the W = 1 scatter (whole-granule stores)
     int64_t* order_out;
     float margin_max;   // the adaptive list margin's ceiling (kSpecMarginMax; DGC_SPEC_MARGIN_MAX for A/B runs)
+    // a tensor whose adaptation loop lowered its threshold (t < t0) lists its next call at
+    // most lowered_margin x the predicted SAMPLED threshold, so the lowered threshold
+    // 0.8 t0' is served by the lists too (0: off; lowered_all: every tensor)
+    float lowered_margin;
+    int32_t lowered_all;
 };
 
 __device__ __forceinline__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
@@ -2213,6 +2237,13 @@ __device__ __forceinline__ void sel_finish_body(const SelWS& w, const FinishArgs
             const float t0 = s.t0;
             const bool f0 = t0 == t0 && t0 > 0.f && t0 < __builtin_huge_valf();
             const float g0 = fminf(fmaxf(2.f - spec[3] / t0, 1.f), 1.5f);
+            if (f.lowered_margin > 0.f && f0 && finite) {
+                // spec[5]: calls left in the "lowers" state (4 after a lowered threshold)
+                float lw = spec[5] < __builtin_huge_valf() ? spec[5] : 0.f;
+                lw = tc < t0 ? 4.f : fmaxf(lw - 1.f, 0.f);
+                spec[5] = lw;
+                if (f.lowered_all || lw > 0.f) spec[0] = f.lowered_margin * t0 * g0;
+            }
             const float mw = wc > (uint32_t)kWinMax ? 0.985f : (s.win_keys > 0 ? 0.97f : 0.9f);
             spec[2] = f0 ? t0 * mw * g0 : __builtin_huge_valf();
             spec[3] = f0 ? t0 : __builtin_huge_valf();
@@ -2873,7 +2904,7 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
 }
 
 __global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one_max, uint32_t gmin) {
     const int t = task(w, BT_SET, (int)blockIdx.x);
     const uint32_t b = blockIdx.x - (uint32_t)w.bt[BT_SET][t];
     SelState* st = w.st + t;
@@ -2887,9 +2918,9 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o) {
     // past the registers are read from L2 on every walk, up to kSetRoundsMax per stretch
     const int rounds = (int)((n64 + kScanThreads - 1) / kScanThreads);
     uint32_t G = 1;
-    if (n64 > kSetCoopMin) {   // (then Gt >= kSetG: n64 <= cand_cap)
+    if (n64 > one_max && Gt > 1) {   // (then Gt >= kSetG: n64 <= cand_cap)
         const uint32_t want = (uint32_t)((rounds + kSetRegC - 1) / kSetRegC);
-        G = want > (uint32_t)kSetG ? (want < Gt ? want : Gt) : (uint32_t)kSetG;
+        G = want > gmin ? (want < Gt ? want : Gt) : gmin;
         G = G < Gt ? G : Gt;
     }
     const int per = (rounds + (int)G - 1) / (int)G;
@@ -2928,7 +2959,7 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G,
 // overwritten with garbage.
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
                                                             EmitOut o, int from_global, FinishArgs f,
-                                                            int force_broken) {
+                                                            int force_broken, int emit_here) {
     const int t = blockIdx.x;
     const SelState* st = w.st + t;
     __shared__ __align__(16) uint64_t smem[kK5SmemBytes / 8];
@@ -2963,6 +2994,23 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
                 g->status = (g->status & ~(uint32_t)DGC_K5_BROKEN) | (uint32_t)(DGC_K5_FALLBACK | DGC_K5_RECOVERED);
         }
         nth_element_wg(q, nc, d.k - 1, gl, gr, lq, llp, lrp, lmk, from_global && !recover ? g : nullptr);
+        if (emit_here) {
+            // the replayed order out by this workgroup (k <= kQueueFold for every tensor of
+            // the call: no k_emit_queue launch); the payload position is known, every
+            // tensor's branch and count being final before K5 runs
+            __shared__ long long obase_s;
+            __syncthreads();
+            if (threadIdx.x < kWave) {
+                const long long b = out_base(w, t);
+                if (threadIdx.x == 0) obase_s = b;
+            }
+            __syncthreads();
+            const long long ob = obase_s;
+            for (int64_t q0 = threadIdx.x; q0 < d.k; q0 += kNthThreads) {
+                const uint32_t j = (uint32_t)q[q0];
+                emit_one(o, d, ob + q0, w.cand_idx[d.cand_off + j], w.cand_val[d.cand_off + j]);
+            }
+        }
     }
     const bool idle = !(st->branch == DGC_BRANCH_RESAMPLE && (st->rs_nth == 1 || st->rs_nth == 2));
     if (idle) K5_STAMP(0);   // (profiling build: slots 0-2 are free when the replay did not run)
@@ -3093,10 +3141,24 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     // (k_count_emit) when that emit would not mask and the payload starts at slot 0
     const bool fuse = keep_lists && L.T == 1 && !L.tail_any && sync_mode == DGC_SYNC_DEVICE &&
                       (p.update_memory == 2 || p.update_memory == 0) && !std::getenv("DGC_NO_COUNT_EMIT");
+    static const bool pass_split = std::getenv("DGC_PASS_SPLIT") != nullptr;
+    const bool merge_ok = lower_fast && sync_mode == DGC_SYNC_DEVICE && !pass_split;
     auto pass = [&](int need, bool likely_lists, bool fused = false) -> int {
         // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
         // (both gated per tensor on the device); need: 1 = lists, 2 = full, 3 = either
         // each count kernel's last workgroup per tensor takes the adaptation step
+        if (need == 3 && !fused && merge_ok) {   // both in one launch (k_count_pass)
+            const int which = likely_lists ? BT_CAP16 : BT_FULL;
+            const unsigned grid = (unsigned)(L.grid[BT_CNT] + L.grid[which]);
+            if (al)
+                hipLaunchKernelGGL(k_count_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                                   (int)L.grid[BT_CNT]);
+            else
+                hipLaunchKernelGGL(k_count_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                                   (int)L.grid[BT_CNT]);
+            DGC_LAUNCHED();
+            return DGC_OK;
+        }
         if (need & 1) {
             if (fused)
                 hipLaunchKernelGGL(k_count_emit, dim3((unsigned)L.grid[BT_CNT]), dim3(kBlock), 0, s, vec, w, p, o);
@@ -3115,10 +3177,16 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
         return DGC_OK;
     };
+    static const bool lower_lists = [] {
+        const char* e = std::getenv("DGC_LOWER_LISTS");
+        return e ? std::atoi(e) != 0 : true;
+    }();
     auto lower = [&]() -> int {
         // the lists first (most lowers end within their range), then vec if needed
-        hipLaunchKernelGGL(k_lower_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w, p);
-        DGC_LAUNCHED();
+        if (lower_lists) {
+            hipLaunchKernelGGL(k_lower_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w, p);
+            DGC_LAUNCHED();
+        }
         const unsigned grid = (unsigned)L.grid[BT_CAP4];
         if (al)
             hipLaunchKernelGGL(k_lower_counts<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
@@ -3134,8 +3202,13 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         const char* e = std::getenv("DGC_SPEC_MARGIN_MAX");
         return e ? std::strtof(e, nullptr) : kSpecMarginMax;
     }();
+    static const float lowered_margin = [] {
+        const char* e = std::getenv("DGC_SPEC_LOWERED");
+        return e ? std::strtof(e, nullptr) : 0.f;
+    }();
+    static const int lowered_all = std::getenv("DGC_SPEC_LOWERED_ALL") ? 1 : 0;
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
-                         sink, 0u, order_out, margin_max};
+                         sink, 0u, order_out, margin_max, lowered_margin, lowered_all};
     bool finished = false;   // the payload count and records are written
     // one tensor, device decisions, the lowering shortcut: the lowering and the count at
     // the lowered threshold in one launch (k_chain_one); DGC_NO_CHAIN=1 (A/B runs)
@@ -3149,12 +3222,25 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     g.cand = w.cand_idx;
     g.cval = w.cand_val;
     g.ckey = w.cand_key;
+    // A/B switches (defaults measured): the one-workgroup limit of a K5s set,
+    // the replay's own emit for small k, the merged count pass, the lowering from lists
+    static const int64_t set_one_max = [] {
+        const char* e = std::getenv("DGC_SET_ONE");
+        return e ? std::max<int64_t>(std::atoll(e), 1) : kSetOneMax;
+    }();
+    static const bool queue_launch = std::getenv("DGC_QUEUE_LAUNCH") != nullptr;
+    static const uint32_t set_gmin = [] {   // the fewest workgroups of a cooperative set (DGC_SET_G)
+        const char* e = std::getenv("DGC_SET_G");
+        return (uint32_t)(e ? std::min(std::max(std::atoi(e), 2), kSetG) : kSetG);
+    }();
+    const bool emit_here = !queue_launch && L.max_k <= kQueueFold;
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
         DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order && L.grid[BT_SET] > 0) {   // K5s: an untied resample set in index order (the rest: the replay)
-            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.grid[BT_SET]), dim3(kScanThreads), 0, s, vec, w, o);
+            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.grid[BT_SET]), dim3(kScanThreads), 0, s, vec, w, o,
+                               set_one_max, set_gmin);
             DGC_LAUNCHED();
         }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
@@ -3173,11 +3259,13 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         FinishArgs f = fin;
         f.on = 1;   // k_nth_select's last workgroup finishes the call
         hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0, f,
-                           force);
+                           force, emit_here ? 1 : 0);
         DGC_LAUNCHED();
         finished = true;
-        hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
-        DGC_LAUNCHED();
+        if (!emit_here) {
+            hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
+            DGC_LAUNCHED();
+        }
         return DGC_OK;
     };
     DGC_TRY(keep_lists ? pass(3, true, fuse) : pass(2, false));

@@ -68,6 +68,9 @@ def parse():
                     help="CPU baseline (all cores), flat: elements per step (default: the whole 1B bucket)")
     ap.add_argument("--cpu-numel-1t", type=float, default=5e7, help="CPU-baseline sample (1 thread), flat")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--inputs", default="per-step", choices=["per-step", "alternating"],
+                    help="per-step: a fresh gradient per rank and step (SURVEY.md §8d, the headline); alternating: "
+                         "two buffers per rank, steps alternating between them (rounds 1-5's input model)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--rccl-one-rank", action="store_true",
                     help="N=1: exchange through a one-rank RCCL group as at N > 1 (the allgather path and its "
@@ -502,10 +505,13 @@ class DropinRun:
         self.opt.zero_grad()
 
 
-def data_note(wl, run, nsteps):
+def data_note(wl, run, nsteps, inputs="per-step"):
     per = ("a fresh gradient per rank and step, seed 0xD6C + 1000*rank + step (SURVEY.md §8d), generated in "
            "HBM before the timed region")
-    if "buffers" in wl:
+    if inputs == "alternating":
+        per = ("--inputs alternating: 2 gradient buffers per rank (seeds 0xD6C + 1000*rank + {0, 1}), steps "
+               "alternate between them (rounds 1-5's input model, not SURVEY.md §8d's)")
+    elif "buffers" in wl:
         per = (f"{wl['buffers']} gradient buffers per rank (seeds 0xD6C + 1000*rank + {{0, 1}}), steps alternate "
                f"between them: a buffer per step would need {nsteps} x {4 * run.N / 1e9:.0f} GB of HBM")
     elif run.nbuf < nsteps:
@@ -728,8 +734,9 @@ def main():
         backend = dist.get_backend()
     coll = world > 1 or one_rank
     nsteps = args.warmup + args.steps
-    run = (FlatRun(wl, rank, world, dev, args.fill, nsteps) if wl["kind"] == "flat" else
-           ModelRun(wl, rank, world, dev, args.fill, nsteps))
+    nbufs = 2 if args.inputs == "alternating" else nsteps
+    run = (FlatRun(wl, rank, world, dev, args.fill, nbufs) if wl["kind"] == "flat" else
+           ModelRun(wl, rank, world, dev, args.fill, nbufs))
 
     log(f"{args.workload}: rank {rank}/{world} set up")
     phases = ("compensate", "select", "allgather", "decompress")
@@ -799,7 +806,7 @@ def main():
             dense = timed_steps(run, args.steps, 2, world)
             run.b.fill = "sparse"
         else:
-            dense = timed_steps(ModelRun(wl, rank, world, dev, "inline", nsteps), args.steps, args.warmup, world)
+            dense = timed_steps(ModelRun(wl, rank, world, dev, "inline", nbufs), args.steps, args.warmup, world)
         extras["dense_fill"] = {"ms_per_step": round(dense, 4), "steps": args.steps,
                                 "note": "fill inline: the whole output zeroed every step (4 B/elem), as the "
                                         "reference's grad.zero_(); value/ms_per_step above use fill sparse"}
@@ -840,10 +847,10 @@ def main():
         "vs_baseline_note": "null: BASELINE.md holds no published number for this metric (the reference publishes "
                             "none); the CPU restatement of the reference timed on this host is cpu_baseline",
         "dtype": "f32",
-        "data": data_note(wl, run, nsteps),
+        "data": data_note(wl, run, nsteps, args.inputs),
         "config": dict({"workload": f"{args.workload} ({wl['config']})", "compress_ratio": wl["ratio"],
                         "nesterov": wl["nesterov"], "momentum": 0.9, "momentum_masking": True, "wire": wire,
-                        "parallelism": f"dp{world}"}, **run.config()),
+                        "parallelism": f"dp{world}", "inputs": args.inputs}, **run.config()),
         "roofline": {"kernel": k1_name, "bound": "hbm", "achieved": k1_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": k1_gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": k1_bytes, "avg_launch_ms": k1_ms,
