@@ -2115,11 +2115,6 @@ struct FinishArgs {
     // packed payload's header word 1, read by the W = 1 scatter (whole-granule stores)
     int64_t* order_out;
     float margin_max;   // the adaptive list margin's ceiling (kSpecMarginMax; DGC_SPEC_MARGIN_MAX for A/B runs)
-    // a tensor whose adaptation loop lowered its threshold (t < t0) lists its next call at
-    // most lowered_margin x the predicted SAMPLED threshold, so the lowered threshold
-    // 0.8 t0' is served by the lists too (0: off; lowered_all: every tensor)
-    float lowered_margin;
-    int32_t lowered_all;
 };
 
 __device__ __forceinline__ void sel_finish_body(const SelWS& w, const FinishArgs& f) {
@@ -2237,13 +2232,6 @@ __device__ __forceinline__ void sel_finish_body(const SelWS& w, const FinishArgs
             const float t0 = s.t0;
             const bool f0 = t0 == t0 && t0 > 0.f && t0 < __builtin_huge_valf();
             const float g0 = fminf(fmaxf(2.f - spec[3] / t0, 1.f), 1.5f);
-            if (f.lowered_margin > 0.f && f0 && finite) {
-                // spec[5]: calls left in the "lowers" state (4 after a lowered threshold)
-                float lw = spec[5] < __builtin_huge_valf() ? spec[5] : 0.f;
-                lw = tc < t0 ? 4.f : fmaxf(lw - 1.f, 0.f);
-                spec[5] = lw;
-                if (f.lowered_all || lw > 0.f) spec[0] = f.lowered_margin * t0 * g0;
-            }
             const float mw = wc > (uint32_t)kWinMax ? 0.985f : (s.win_keys > 0 ? 0.97f : 0.9f);
             spec[2] = f0 ? t0 * mw * g0 : __builtin_huge_valf();
             spec[3] = f0 ? t0 : __builtin_huge_valf();
@@ -3177,12 +3165,17 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
         return DGC_OK;
     };
-    static const bool lower_lists = [] {
+    // the lowering from the K1 lists first, then over vec if they do not reach: for one
+    // tensor (the per-tensor path; the flat bucket chains its lowering, k_chain_one). A
+    // batch goes to vec at once: on per-step gradients a lowered threshold (0.8 t0) sits
+    // below the lists almost always, and the list launch cost ResNet-50 6 us, VGG-16-BN 4
+    // (same box, 3 alternations); DGC_LOWER_LISTS=0/1 overrides
+    static const int lower_lists_env = [] {
         const char* e = std::getenv("DGC_LOWER_LISTS");
-        return e ? std::atoi(e) != 0 : true;
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
     }();
+    const bool lower_lists = lower_lists_env >= 0 ? lower_lists_env == 1 : L.T == 1;
     auto lower = [&]() -> int {
-        // the lists first (most lowers end within their range), then vec if needed
         if (lower_lists) {
             hipLaunchKernelGGL(k_lower_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w, p);
             DGC_LAUNCHED();
@@ -3202,13 +3195,8 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         const char* e = std::getenv("DGC_SPEC_MARGIN_MAX");
         return e ? std::strtof(e, nullptr) : kSpecMarginMax;
     }();
-    static const float lowered_margin = [] {
-        const char* e = std::getenv("DGC_SPEC_LOWERED");
-        return e ? std::strtof(e, nullptr) : 0.f;
-    }();
-    static const int lowered_all = std::getenv("DGC_SPEC_LOWERED_ALL") ? 1 : 0;
     const FinishArgs fin{count_out, info, margin, (int32_t)(p.update_memory == 2), (int32_t)(p.masking != 0), 0,
-                         sink, 0u, order_out, margin_max, lowered_margin, lowered_all};
+                         sink, 0u, order_out, margin_max};
     bool finished = false;   // the payload count and records are written
     // one tensor, device decisions, the lowering shortcut: the lowering and the count at
     // the lowered threshold in one launch (k_chain_one); DGC_NO_CHAIN=1 (A/B runs)

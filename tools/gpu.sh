@@ -39,16 +39,18 @@ bench)
   done
   python tools/bench_table.py "$OUT"/bench_*.json ;;
 profile)
+  # SUFFIX names a variant's files (e.g. _alternating with BENCH_ARGS="--inputs alternating")
   for wl in "$@"; do
-    CMD="bench.py --gpus 1 --steps 20 --warmup 5 --workload $wl --no-extras"
-    timeout -k 10 600 python $CMD > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err" || exit 1
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof_$wl" -o run \
-        --output-format csv -- python $CMD --no-cpu > "$OUT/bench_prof_$wl.json" 2> "$OUT/prof_$wl.err" || exit 1
-    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/$OUT/pmc_$wl" -o fetch \
-        --output-format csv -- python $CMD --no-cpu > /dev/null 2> "$OUT/pmc_fetch_$wl.err" || exit 1
-    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$GRAFT_REPO_ROOT/$OUT/pmc_$wl" -o write \
-        --output-format csv -- python $CMD --no-cpu > /dev/null 2> "$OUT/pmc_write_$wl.err" || exit 1
-    echo "profiled $wl"
+    CMD="bench.py --gpus 1 --steps 20 --warmup 5 --workload $wl --no-extras ${BENCH_ARGS:-}"
+    W="$wl${SUFFIX:-}"
+    timeout -k 10 600 python $CMD > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err" || exit 1
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof_$W" -o run \
+        --output-format csv -- python $CMD --no-cpu > "$OUT/bench_prof_$W.json" 2> "$OUT/prof_$W.err" || exit 1
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/$OUT/pmc_$W" -o fetch \
+        --output-format csv -- python $CMD --no-cpu > /dev/null 2> "$OUT/pmc_fetch_$W.err" || exit 1
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$GRAFT_REPO_ROOT/$OUT/pmc_$W" -o write \
+        --output-format csv -- python $CMD --no-cpu > /dev/null 2> "$OUT/pmc_write_$W.err" || exit 1
+    echo "profiled $W"
   done ;;
 timeline)
   for wl in "$@"; do

@@ -31,7 +31,7 @@ def main():
     L = _lib.lib()
     L.dgc_rs_prof.restype = ctypes.c_int
     L.dgc_rs_prof.argtypes = [ctypes.c_void_p]
-    run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, torch.device("cuda:0"))
+    run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, torch.device("cuda:0"), "sparse", steps)   # per-step gradients
     buf = ((ctypes.c_uint64 * 12) * 64)()
     for i in range(steps):
         run.step(i)

@@ -34,7 +34,7 @@ def main():
     L = _lib.lib()
     L.dgc_k5_prof.restype = ctypes.c_int
     L.dgc_k5_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, torch.device("cuda:0"))
+    run = bench.ModelRun(bench.WORKLOADS[wl], 0, 1, torch.device("cuda:0"), "sparse", steps)   # per-step gradients
     b = run.b
     for i in range(steps):
         torch.cuda.synchronize()
