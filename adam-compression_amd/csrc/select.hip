@@ -95,7 +95,8 @@ constexpr float kSpecCeilUp = 0.005f, kSpecCeilDown = 0.05f;
 // kSetCoopMin, kSetG up to kSetG x kSetCoopMin, up to kSetGBig beyond (VGG-16-BN's fc6) —
 // kSetRegC rounds of 1024 keys per workgroup in registers (32 spilled the radix
 // passes' registers to scratch), up to kSetRoundsMax rounds from L2 beyond.
-constexpr int kSetG = 16;
+constexpr int kSetG = 16;                       // the most workgroups of a set's minimum (DGC_SET_G)
+constexpr int kSetGDefault = 4;                 // ... and the default: a cooperative set's fewest workgroups
 constexpr int kSetGBig = 128;
 constexpr int kSetRegC = 16;
 constexpr int kSetRoundsMax = 64;
@@ -255,6 +256,18 @@ struct Layout {
 // thresholds jump), and there a 2048-block cap left the big tensors' passes
 // short of HBM rate: 8192 blocks took VGG-16-BN 0.896 -> 0.811 ms, ResNet-50 0.367 ->
 // 0.361 ms, 16384 VGG-16-BN 0.816 -> 0.805 ms, ResNet-50 unchanged (same box, tools/ab_lib.sh).
+// K5s: the fewest workgroups of a cooperative set (beyond kSetCoopMin candidates) — the
+// grid holds max(this, ceil(capacity / kSetCoopMin)) per tensor. 16 per tensor made a
+// ResNet-50 step dispatch ~430 workgroups of 1024 threads, and its biggest sets started
+// 12-14 us into the launch (tools/k5s_prof.py); DGC_SET_G overrides (2..16).
+static uint32_t set_gmin() {
+    static const uint32_t g = [] {
+        const char* e = std::getenv("DGC_SET_G");
+        return (uint32_t)(e ? std::min(std::max(std::atoi(e), 2), kSetG) : kSetGDefault);
+    }();
+    return g;
+}
+
 static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, int64_t cap_blocks) {
     const int64_t cap = std::max<int64_t>(1, ceil_div(cap_blocks * d.nseg, std::max<int64_t>(1, total_seg)));
     switch (which) {
@@ -269,7 +282,7 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, in
         case BT_SET:   // K5s: a resample set holds count(t_cur) <= cand_cap > k candidates
             if (d.k < 1 || d.cand_cap <= d.k) return 0;
             if (d.cand_cap <= kSetCoopMin) return 1;
-            return std::min<int64_t>(kSetGBig, std::max<int64_t>(kSetG, ceil_div(d.cand_cap, kSetCoopMin)));
+            return std::min<int64_t>(kSetGBig, std::max<int64_t>(set_gmin(), ceil_div(d.cand_cap, kSetCoopMin)));
         case BT_SAMP: {
             const int64_t cnt = d.samp_off < 0 ? d.n : d.S + 1;
             if (cnt <= kSmallN) return 0;   // one-workgroup threshold (k_rs_small_multi)
@@ -2906,7 +2919,7 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     // past the registers are read from L2 on every walk, up to kSetRoundsMax per stretch
     const int rounds = (int)((n64 + kScanThreads - 1) / kScanThreads);
     uint32_t G = 1;
-    if (n64 > one_max && Gt > 1) {   // (then Gt >= kSetG: n64 <= cand_cap)
+    if (n64 > one_max && Gt > 1) {   // (then Gt >= gmin: n64 <= cand_cap)
         const uint32_t want = (uint32_t)((rounds + kSetRegC - 1) / kSetRegC);
         G = want > gmin ? (want < Gt ? want : Gt) : gmin;
         G = G < Gt ? G : Gt;
@@ -3217,10 +3230,6 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         return e ? std::max<int64_t>(std::atoll(e), 1) : kSetOneMax;
     }();
     static const bool queue_launch = std::getenv("DGC_QUEUE_LAUNCH") != nullptr;
-    static const uint32_t set_gmin = [] {   // the fewest workgroups of a cooperative set (DGC_SET_G)
-        const char* e = std::getenv("DGC_SET_G");
-        return (uint32_t)(e ? std::min(std::max(std::atoi(e), 2), kSetG) : kSetG);
-    }();
     const bool emit_here = !queue_launch && L.max_k <= kQueueFold;
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
@@ -3228,7 +3237,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         DGC_TRY(launch_emit(L, vec, w, g, s));
         if (p.set_order && L.grid[BT_SET] > 0) {   // K5s: an untied resample set in index order (the rest: the replay)
             hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.grid[BT_SET]), dim3(kScanThreads), 0, s, vec, w, o,
-                               set_one_max, set_gmin);
+                               set_one_max, set_gmin());
             DGC_LAUNCHED();
         }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
