@@ -1898,8 +1898,8 @@ __device__ unsigned long long g_ce_prof[2048][6];   // tools/ce_prof.py: per-gro
 #define CE_STAMP(i) do { } while (0)
 #endif
 
-__global__ void __launch_bounds__(kBlock)
-k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
+__device__ __forceinline__ void count_emit_body(const float* __restrict__ vec_flat, const SelWS& w, const SelCfg& p,
+                                                const EmitOut& o) {
     static_assert(kBlock * kCountSegs == kGroupSegs && kCountSegs == kLstTile, "k_count_emit layout");
     SelState* st = w.st;
     if (!st->active || !(st->t_cur >= st->t_list)) return;
@@ -2107,6 +2107,24 @@ k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
     if (last_block_arrival8(st->tk8, (uint32_t)lg, (uint32_t)(w.bt[BT_CNT][1] - w.bt[BT_CNT][0])))
         decide_tensor(w, p, 0, 1);
     CE_STAMP(5);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_count_emit(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o) {
+    count_emit_body(vec_flat, w, p, o);
+}
+
+// k_count_emit beside the full select pass in ONE launch (one tensor; see k_count_pass):
+// the first ncnt workgroups count (and emit) from the lists, the rest re-list over vec
+// when the lists do not serve — one of the two does work. The merged kernel keeps the
+// select pass's occupancy (its VGPRs bound both; k_count_emit's LDS does not).
+template <bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)
+k_count_emit_pass(const float* __restrict__ vec_flat, SelWS w, SelCfg p, EmitOut o, int which, int ncnt) {
+    if ((int)blockIdx.x < ncnt)
+        count_emit_body(vec_flat, w, p, o);
+    else
+        select_pass_body<ALIGNED>(vec_flat, w, which, p, (int64_t)blockIdx.x - ncnt);
 }
 
 // Result records; the payload's total count; and every tensor's next speculative
@@ -3148,6 +3166,18 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
         // (both gated per tensor on the device); need: 1 = lists, 2 = full, 3 = either
         // each count kernel's last workgroup per tensor takes the adaptation step
+        if (need == 3 && fused && merge_ok) {   // both in one launch (k_count_emit_pass)
+            const int which = likely_lists ? BT_CAP16 : BT_FULL;
+            const unsigned grid = (unsigned)(L.grid[BT_CNT] + L.grid[which]);
+            if (al)
+                hipLaunchKernelGGL(k_count_emit_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p, o, which,
+                                   (int)L.grid[BT_CNT]);
+            else
+                hipLaunchKernelGGL(k_count_emit_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, p, o, which,
+                                   (int)L.grid[BT_CNT]);
+            DGC_LAUNCHED();
+            return DGC_OK;
+        }
         if (need == 3 && !fused && merge_ok) {   // both in one launch (k_count_pass)
             const int which = likely_lists ? BT_CAP16 : BT_FULL;
             const unsigned grid = (unsigned)(L.grid[BT_CNT] + L.grid[which]);
