@@ -986,6 +986,7 @@ struct NthG {
     uint32_t bar_count, bar_gen;   // zeroed by k_sel_init, like arrive / decide / status
     uint32_t arrive, decide;       // the residency consensus
     uint32_t status;               // DGC_K5_FALLBACK | DGC_K5_BROKEN of this call
+    uint32_t exited;               // workgroups past a GO phase's last barrier (k_nth_select's recovery)
     uint32_t bl[kNthGMax], br[kNthGMax];
 };
 
@@ -1086,10 +1087,10 @@ __device__ void nthg_prepare(uint64_t* q, NthG* g, int64_t nth) {
 // Ranges of <= min_run entries are left to the one-workgroup phase: below ~140k
 // candidates the four cross-XCD barriers per step cost more than the spread saves
 // (tools/k5ab.sh: 100k 0.28 vs 0.25 ms, 500k 0.43 vs 0.94, 1M 0.55 vs 1.44).
-__device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* lpos, uint32_t* rpos, NthG* g,
-                                 uint32_t b, uint32_t G, int64_t min_run, uint32_t G_expected) {
+// mk: kNthGMk bytes of the caller's LDS (k_nth_select lends the replay's area).
+__device__ __forceinline__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* lpos, uint32_t* rpos, NthG* g,
+                                 uint32_t b, uint32_t G, int64_t min_run, uint32_t G_expected, DGC_LDS uint8_t* mk) {
     constexpr int kB = 8;   // tiles of loads in flight per lane
-    __shared__ uint8_t mk[kNthGMk];
     __shared__ uint32_t wl[kNthWaves], wr[kNthWaves], pre_l, pre_r, tot_r, s_sh;
     __shared__ int64_t sf, sl;
     __shared__ uint32_t sP;
@@ -1251,6 +1252,7 @@ __device__ void nth_global_multi(uint64_t* q, int64_t n, int64_t nth, uint32_t* 
             nthg_prepare(q, g, nth);
         });
     }
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&g->exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // std::nth_element(q, q + nth, q + n, comp) in place, by the calling 512-thread

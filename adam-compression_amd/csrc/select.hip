@@ -172,6 +172,7 @@ struct SelState {
 // workspace is zero-filled at init; the workgroups re-zero what they used).
 struct SetG {
     uint32_t arrive, decide, bar_count, bar_gen, broken;
+    uint32_t gathered;                      // k_emit_set: the tensor's emit workgroups done with its gather
     uint32_t mn, mx;
     uint32_t cnt[kSetGBig];                 // per workgroup: its candidates >= the k-th key
     uint32_t hist0[kSetBins0], hist1[kSetBins1];   // the radix passes' merged histograms
@@ -794,9 +795,10 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         w.nthg[t].arrive = 0;
         w.nthg[t].decide = 0;
         w.nthg[t].status = 0;
+        w.nthg[t].exited = 0;
         SetG& sg = w.setg[t];
         setg_broken = sg.broken;
-        sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = 0;
+        sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = sg.gathered = 0;
         sg.mn = 0xFFFFFFFFu;
         sg.mx = 0;
         if (t == 0) *w.fin_ticket = 0;
@@ -1538,7 +1540,7 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long 
 
 // Wave-cooperative emit of one spilled segment (local ls) by re-reading vec.
 // FIRSTK: positions base + rank for |x| >= t, kept while < limit.
-__device__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long base,
+__device__ __forceinline__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long base,
                                    long long limit, long long obase, float t, const EmitOut& o, bool mask_now) {
     const int lane = threadIdx.x & 63;
     uint32_t run = 0;
@@ -1783,14 +1785,34 @@ k_chain_one(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
 
 
 
+__device__ __forceinline__ void resample_set_block(const float* __restrict__ vec_flat, const SelWS& w,
+                                                   const EmitOut& o, int bx, int64_t one_max, uint32_t gmin,
+                                                   bool wait);   // K5s, below
+
 // The few groups of a model gradient set: kEmitSplit workgroups of kGroupSegs threads
 // per group, each scanning the whole group (thread per segment) and emitting its
 // quarter with 16 waves of 16 segments — one list batch per wave, every list by a
 // wave. More waves per quarter beat k_emit's short-list threads there (measured on
 // ResNet-50: 12 vs 15 us per launch).
+//
+// SET (k_emit_set): the emit and k_resample_set in ONE launch. The workgroups from ngb
+// on are the sets' (resample_set_block); an emit workgroup that gathered a resampled
+// tensor's candidates releases its stores and counts itself in the tensor's
+// SetG::gathered, and the tensor's sets start once all of its emit workgroups have —
+// beside the other tensors' emit, one launch boundary fewer. The emit workgroups come
+// first in the grid and never wait, so a waiting set only holds a slot the emit does
+// not need (ResNet-50's whole grid, ~220 workgroups of 1024 threads, is resident at
+// once on 256 CUs; VGG-16-BN's ~680 against 512 slots, ~150 of them sets).
+template <bool SET>
 __global__ void __launch_bounds__(kGroupSegs)
-k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
-    const int t = task(w, BT_GRP, blockIdx.x);
+k_emit_wide_t(const float* __restrict__ vec_flat, SelWS w, EmitOut oa, EmitOut os, int64_t one_max, uint32_t gmin,
+              int32_t ngb) {
+    if (SET && (int)blockIdx.x >= ngb) {
+        resample_set_block(vec_flat, w, os, (int)blockIdx.x - ngb, one_max, gmin, true);
+        return;
+    }
+    const int bx = (int)blockIdx.x;
+    const int t = task(w, BT_GRP, bx);
     const SelState* st = w.st + t;
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
     if (st->spec_emitted) return;                                        // k_count_emit did
@@ -1804,7 +1826,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
     // first-k branches of an engine that defers: the next K1 zeroes what this emits
     const bool defer_here = o.defer && !k5 && !d.tail;
     const float* vec = vec_flat + d.off;
-    const int64_t lb = (int64_t)blockIdx.x - w.bt[BT_GRP][t];
+    const int64_t lb = (int64_t)bx - w.bt[BT_GRP][t];
     constexpr int split = kEmitSplit;
     const int64_t lg = lb / split;                           // group within the tensor
     const int sub = (int)(lb % split);                       // its share this workgroup emits
@@ -1857,6 +1879,7 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
                 e[q] = w.lst_off[slot];
             }
         }
+        uint32_t spilled = 0;   // (re-read after the batch: a call inside kept the loop rolled)
 #pragma unroll
         for (int q = 0; q < kEmitBatch; ++q) {
             const uint32_t L = lcn[j0 + q];
@@ -1864,13 +1887,26 @@ k_emit_wide(const float* __restrict__ vec_flat, SelWS w, EmitOut oa) {
             const int64_t ls = lseg0 + j0 + q;
             const long long ba = ga + off_a[j0 + q];
             if (L > (uint32_t)kCap) {
-                emit_reread_firstk(vec, d, ls, ba, limit, obase, tc, o, !defer_here);
+                spilled |= 1u << q;
                 continue;
             }
             const bool sel = (uint32_t)lane < L && fabsf(x[q]) >= tc;
             const uint64_t m = __ballot(sel);
             const long long pos = ba + __popcll(m & lt);
             if (sel && pos < limit) emit_one(o, d, obase + pos, ls * kSeg + e[q], x[q], !defer_here);
+        }
+        while (spilled) {   // rare: the wave re-reads the segment's 1024 elements
+            const int q = __builtin_ctz(spilled);
+            spilled &= spilled - 1;
+            emit_reread_firstk(vec, d, lseg0 + j0 + q, ga + off_a[j0 + q], limit, obase, tc, o, !defer_here);
+        }
+    }
+    if (SET && k5) {   // uniform per workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_fetch_add(&w.setg[t].gathered, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -2922,10 +2958,15 @@ __device__ __forceinline__ void resample_set_body(const float* __restrict__ vec_
     SET_STAMP(4);
 }
 
-__global__ void __launch_bounds__(kScanThreads)
-k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one_max, uint32_t gmin) {
-    const int t = task(w, BT_SET, (int)blockIdx.x);
-    const uint32_t b = blockIdx.x - (uint32_t)w.bt[BT_SET][t];
+// One workgroup of k_resample_set (bx: its index in the BT_SET grid). wait: k_emit_set,
+// whose emit workgroups gather the candidates in the same launch — the set's workgroups
+// first wait until all of the tensor's emit workgroups have counted themselves (bounded:
+// past kSetArriveTicks the tensor is left to the exact replay, recorded as a fallback).
+__device__ __forceinline__ void resample_set_block(const float* __restrict__ vec_flat, const SelWS& w,
+                                                   const EmitOut& o, int bx, int64_t one_max, uint32_t gmin,
+                                                   bool wait) {
+    const int t = task(w, BT_SET, bx);
+    const uint32_t b = (uint32_t)bx - (uint32_t)w.bt[BT_SET][t];
     SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;   // uniform per workgroup
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -2944,18 +2985,46 @@ k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t o
     }
     const int per = (rounds + (int)G - 1) / (int)G;
     if (per > kSetRoundsMax || b >= G) return;   // (past kSetRoundsMax: the replay)
+    if (wait) {
+        __shared__ int gathered;
+        if (threadIdx.x == 0) {
+            const uint32_t want = (uint32_t)(w.bt[BT_GRP][t + 1] - w.bt[BT_GRP][t]);
+            const uint64_t t0 = wall_clock64();
+            bool ok = true;
+            while (__hip_atomic_load(&w.setg[t].gathered, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                if (wall_clock64() - t0 > kSetArriveTicks) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (!ok) atomicOr(&w.nthg[t].status, (uint32_t)DGC_K5_SET_FALLBACK);
+            gathered = ok;
+        }
+        __syncthreads();
+        // (a cooperative set's other workgroups then fail the residency consensus: the replay)
+        if (!gathered) return;
+    }
     if (per > kSetRegC)
         resample_set_body<true>(vec_flat, w, o, t, b, G, per, rounds, st, d);
     else
         resample_set_body<false>(vec_flat, w, o, t, b, G, per, rounds, st, d);
 }
 
+__global__ void __launch_bounds__(kScanThreads)
+k_resample_set(const float* __restrict__ vec_flat, SelWS w, EmitOut o, int64_t one_max, uint32_t gmin) {
+    resample_set_block(vec_flat, w, o, (int)blockIdx.x, one_max, gmin, false);
+}
 
 // K5's global-memory phase by G workgroups per tensor (grid G x T, a plain launch sized
 // so all of them fit at once; a residency consensus decides whether they run it, see
-// introselect.hpp); k_nth_select goes on from the state it leaves.
+// introselect.hpp); k_nth_select goes on from the state it leaves. The A/B form
+// (DGC_NTH_SEPARATE=1): by default k_nth_select runs the phase on its own extra
+// workgroups (grid T x G), one launch fewer.
 __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G, int64_t min_run,
                                                             uint32_t G_expected) {
+    __shared__ uint8_t mk[kNthGMk];
     const int t = blockIdx.y;
     const SelState* st = w.st + t;
     if (st->branch != DGC_BRANCH_RESAMPLE || st->rs_nth != 1) return;
@@ -2963,11 +3032,16 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G,
     uint32_t* gl = w.gpos + d.gpos_off;
     uint32_t* gr = gl + d.cand_cap / 2 + 1;
     nth_global_multi(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, w.nthg + t, blockIdx.x, G, min_run,
-                     G_expected);
+                     G_expected, lds(mk));
 }
 
-// The last of the T workgroups to finish (f.on) then runs the finish of the whole call
-// (T arrivals on one ticket; nothing it writes is read by k_emit_queue).
+// Grid T x G: workgroup (t, 0) replays tensor t; with G > 1 and `global_here` the
+// tensor's G workgroups (t, 0..G-1) first run K5's global phase (nth_global_multi, its
+// stopper bytes in the replay's LDS area, which is free until the phase ends), and
+// workgroups (t, b > 0) leave after it. from_global: G > 1, the phase ran (here or in
+// k_nth_global) and the replay goes on from the state it left.
+// The last of the T workgroups (t, 0) to finish (f.on) then runs the finish of the whole
+// call (T arrivals on one ticket; nothing it writes is read by k_emit_queue).
 //
 // A global phase that BROKE (a barrier timed out after the consensus voted GO: its
 // partitions of the queue are not reliable) is recovered here, in the same call: the
@@ -2978,10 +3052,22 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G,
 // overwritten with garbage.
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
                                                             EmitOut o, int from_global, FinishArgs f,
-                                                            int force_broken, int emit_here) {
+                                                            int force_broken, int emit_here, int global_here,
+                                                            uint32_t G, int64_t min_run, uint32_t G_expected) {
     const int t = blockIdx.x;
+    const uint32_t b = blockIdx.y;
     const SelState* st = w.st + t;
     __shared__ __align__(16) uint64_t smem[kK5SmemBytes / 8];
+    static_assert(kK5SmemBytes >= (size_t)kNthGMk, "the global phase's stopper bytes fit the replay's LDS");
+    if (global_here && st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1) {   // uniform per tensor
+        const TDesc d = w.td[t];
+        uint32_t* gl = w.gpos + d.gpos_off;
+        uint32_t* gr = gl + d.cand_cap / 2 + 1;
+        nth_global_multi(w.queue + d.cand_off, st->n_cur, d.k - 1, gl, gr, w.nthg + t, b, G, min_run, G_expected,
+                         reinterpret_cast<DGC_LDS uint8_t*>(lds(smem)));
+        __syncthreads();   // (smem is the replay's from here)
+    }
+    if (b > 0) return;
     K5_STAMP(7);
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) {   // uniform per workgroup
         heap_select_wg(vec_flat, w, o, t, smem);
@@ -3003,6 +3089,13 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
                                        (uint32_t)DGC_K5_BROKEN));
         __syncthreads();
         if (recover) {
+            // a GO phase's workgroups may still be on their way out of a timed-out barrier
+            // (here, not k_nth_global): none touches the queue once it has counted itself
+            if (global_here && threadIdx.x == 0 &&
+                __hip_atomic_load(&g->decide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kNthGGo)
+                while (__hip_atomic_load(&g->exited, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < G)
+                    __builtin_amdgcn_s_sleep(2);
+            __syncthreads();
             if (force_broken)
                 for (int64_t j = threadIdx.x; j < nc; j += kNthThreads) q[j] = ~(uint64_t)j;
             __syncthreads();
@@ -3091,21 +3184,26 @@ static SelCfg cfg_of(const dgc_select_params& p) {
 // payload: stream-ordered, and in DGC_SYNC_DEVICE mode with no host synchronisation.
 // k_emit for many groups (flat buckets), k_emit_wide for few (model gradient sets).
 // DGC_EMIT_SHAPE=quarter|wide forces one (the parity tests run both at small sizes).
-static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const EmitOut& o, hipStream_t s) {
+static bool emit_is_wide(const Layout& L) {
     const char* force = std::getenv("DGC_EMIT_SHAPE");
-    const bool wide = force ? std::strcmp(force, "wide") == 0 : L.ngrp < 256;
-    if (wide)
-        hipLaunchKernelGGL(k_emit_wide, dim3((unsigned)L.grid[BT_GRP]), dim3(kGroupSegs), 0, s, vec, w, o);
+    return force ? std::strcmp(force, "wide") == 0 : L.ngrp < 256;
+}
+
+static int launch_emit(const Layout& L, const float* vec, const SelWS& w, const EmitOut& o, hipStream_t s) {
+    if (emit_is_wide(L))
+        hipLaunchKernelGGL(k_emit_wide_t<false>, dim3((unsigned)L.grid[BT_GRP]), dim3(kGroupSegs), 0, s, vec, w, o, o,
+                           (int64_t)0, 0u, (int32_t)L.grid[BT_GRP]);
     else
         hipLaunchKernelGGL(k_emit, dim3((unsigned)L.grid[BT_GRP]), dim3(kEmitSegs), 0, s, vec, w, o);
     DGC_LAUNCHED();
     return DGC_OK;
 }
 
-// Workgroups per tensor for k_nth_global: half the CUs shared among the T tensors, at
-// most kNthGMax. Its workgroups wait for each other, so all of them must be resident at
-// once: <= CUs / 2 workgroups of 8 waves and 33 KB LDS (one fits a CU) guarantee that
-// with this stream's earlier kernels done. (hipLaunchCooperativeKernel checks the same
+// Workgroups per tensor for K5's global phase (k_nth_select's extra workgroups, or
+// k_nth_global's): half the CUs shared among the T tensors, at most kNthGMax. They wait
+// for each other, so all of them must be resident at once: <= CUs / 2 workgroups of 8
+// waves (one fits a CU, with k_nth_select's ~150 KB of LDS as with k_nth_global's 33 KB)
+// guarantee that with this stream's earlier kernels done. (hipLaunchCooperativeKernel checks the same
 // but cost ~29 us per launch on MI355X: more than the phase saves below ~200k candidates.)
 // <= 1 runs the one-workgroup global phase inside k_nth_select instead; so does a call
 // whose tensors all have candidate capacities <= kNthGMinCand, and so does a tensor
@@ -3120,7 +3218,7 @@ static uint32_t nth_global_groups(int32_t T, int64_t max_cand) {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_nth_global),
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_nth_select),
                                                          kNthThreads, 0) != hipSuccess)
             per_dev = 0;
         else
@@ -3264,29 +3362,42 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
-        DGC_TRY(launch_emit(L, vec, w, g, s));
-        if (p.set_order && L.grid[BT_SET] > 0) {   // K5s: an untied resample set in index order (the rest: the replay)
-            hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.grid[BT_SET]), dim3(kScanThreads), 0, s, vec, w, o,
-                               set_one_max, set_gmin());
+        // K5s: an untied resample set in index order (the rest: the replay); with the
+        // wide emit, in its launch (k_emit_set; DGC_SET_SEPARATE=1: two launches, A/B)
+        static const bool set_separate = std::getenv("DGC_SET_SEPARATE") != nullptr;
+        const bool sets = p.set_order && L.grid[BT_SET] > 0;
+        if (sets && !set_separate && emit_is_wide(L)) {
+            hipLaunchKernelGGL(k_emit_wide_t<true>, dim3((unsigned)(L.grid[BT_GRP] + L.grid[BT_SET])),
+                               dim3(kGroupSegs), 0, s, vec, w, g, o, set_one_max, set_gmin(), (int32_t)L.grid[BT_GRP]);
             DGC_LAUNCHED();
+        } else {
+            DGC_TRY(launch_emit(L, vec, w, g, s));
+            if (sets) {
+                hipLaunchKernelGGL(k_resample_set, dim3((unsigned)L.grid[BT_SET]), dim3(kScanThreads), 0, s, vec, w,
+                                   o, set_one_max, set_gmin());
+                DGC_LAUNCHED();
+            }
         }
         const uint32_t G = nth_global_groups(L.T, L.max_cand);
-        if (G > 1) {
-            // DGC_K5_GLOBAL=multi: every range over several workgroups (parity); =abort: the
-            // kernel expects one workgroup more than launched, so the residency consensus
-            // times out and the one-workgroup replay takes over (the fallback's parity test)
-            const char* force = std::getenv("DGC_K5_GLOBAL");
-            const bool multi = force && (std::strcmp(force, "multi") == 0 || std::strcmp(force, "abort") == 0);
-            const bool abort = force && std::strcmp(force, "abort") == 0;
-            const int64_t min_run = multi ? 0 : kNthGMinCand;
+        // DGC_K5_GLOBAL=multi: every range over several workgroups (parity); =abort: the
+        // kernel expects one workgroup more than launched, so the residency consensus
+        // times out and the one-workgroup replay takes over (the fallback's parity test)
+        const char* gforce = std::getenv("DGC_K5_GLOBAL");
+        const bool multi = gforce && (std::strcmp(gforce, "multi") == 0 || std::strcmp(gforce, "abort") == 0);
+        const bool abort = gforce && std::strcmp(gforce, "abort") == 0;
+        const int64_t min_run = multi ? 0 : kNthGMinCand;
+        const uint32_t G_expected = abort ? G + 1 : G;
+        static const bool nth_separate = std::getenv("DGC_NTH_SEPARATE") != nullptr;
+        const bool global_here = G > 1 && !nth_separate;
+        if (G > 1 && !global_here) {
             hipLaunchKernelGGL(k_nth_global, dim3(G, (unsigned)L.T), dim3(kNthThreads), 0, s, w, G, min_run,
-                               abort ? G + 1 : G);
+                               G_expected);
             DGC_LAUNCHED();
         }
         FinishArgs f = fin;
         f.on = 1;   // k_nth_select's last workgroup finishes the call
-        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T), dim3(kNthThreads), 0, s, vec, w, o, G > 1 ? 1 : 0, f,
-                           force, emit_here ? 1 : 0);
+        hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T, global_here ? G : 1u), dim3(kNthThreads), 0, s, vec, w,
+                           o, G > 1 ? 1 : 0, f, force, emit_here ? 1 : 0, global_here ? 1 : 0, G, min_run, G_expected);
         DGC_LAUNCHED();
         finished = true;
         if (!emit_here) {
