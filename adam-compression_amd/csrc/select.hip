@@ -1111,6 +1111,19 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_small_multi(SelWS w, const 
 }
 
 // ------------------------------------------------------------------ count passes
+#ifdef DGC_K5_PROF
+// tools/pass_prof.py: per-workgroup stamps of the last k_count_pass (kind 0) and
+// k_lower_counts (kind 1) launch — entry, past the gate, loads done, arrival, end
+__device__ unsigned long long g_pass_prof[2][16384][6];
+#define PASS_STAMP(k, i) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 16384) g_pass_prof[k][blockIdx.x][i] = wall_clock64(); } while (0)
+// slot 5: the first iteration's loads arrived (wave 0; the wait is the profiling build's only)
+#define PASS_LOADED(k) \
+    do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); PASS_STAMP(k, 5); } while (0)
+#else
+#define PASS_STAMP(k, i) do { } while (0)
+#define PASS_LOADED(k) do { } while (0)
+#endif
 // t_cur >= t_list: counts from the lists, kCountSegs segments per thread (one group
 // per workgroup): the list counts of a thread's segments, then their first 8 entries
 // (most lists are shorter), are all in flight before any is used — one thread per
@@ -1122,7 +1135,9 @@ __device__ __forceinline__ void count_lists_body(const float* __restrict__ vec_f
                                                  int64_t bx) {
     const int t = task(w, BT_CNT, (int)bx);
     const SelState* st = w.st + t;
+    PASS_STAMP(0, 0);
     if (!st->active || !(st->t_cur >= st->t_list)) return;
+    PASS_STAMP(0, 1);
     const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
@@ -1194,11 +1209,14 @@ __device__ __forceinline__ void count_lists_body(const float* __restrict__ vec_f
         }
     }
     __syncthreads();
+    PASS_STAMP(0, 2);
     if (threadIdx.x == 0 && bsum) atomicAdd(&w.grp_cnt[d.grp0 + lseg0 / kGroupSegs], (unsigned long long)bsum);
+    PASS_STAMP(0, 3);
     // the tensor's last workgroup takes the adaptation step (no k_decide launch)
     if (last_block_arrival8(w.st[t].tk8, (uint32_t)(bx - w.bt[BT_CNT][t]),
                             (uint32_t)(w.bt[BT_CNT][t + 1] - w.bt[BT_CNT][t])))
         decide_tensor(w, p, t);
+    PASS_STAMP(0, 4);
 }
 
 __global__ void __launch_bounds__(kBlock)
@@ -1216,7 +1234,9 @@ __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_f
                                                  const SelCfg& p, int64_t bx) {
     const int t = task(w, which, (int)bx);
     const SelState* st = w.st + t;
+    PASS_STAMP(0, 0);
     if (!st->active || st->t_cur >= st->t_list) return;
+    PASS_STAMP(0, 1);
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const float tc = st->t_cur;
@@ -1236,6 +1256,7 @@ __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_f
 #pragma unroll
             for (int u = 0; u < kTiles; ++u)
                 load_tile<ALIGNED>(vec, d.n, sup * (kSuper * kSeg) + u * 256 + 4 * lane, x[u], valid[u]);
+            PASS_LOADED(0);
 #pragma unroll
             for (int sg = 0; sg < kSuper; ++sg) {
                 const int64_t ls = sup * kSuper + sg;
@@ -1274,9 +1295,12 @@ __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_f
         }
         __syncthreads();
     }
+    PASS_STAMP(0, 2);
+    PASS_STAMP(0, 3);
     // the tensor's last workgroup takes the adaptation step (no k_decide launch)
     if (last_block_arrival8(w.st[t].tk8, (uint32_t)(bx - w.bt[which][t]), (uint32_t)nb))
         decide_tensor(w, p, t);
+    PASS_STAMP(0, 4);
 }
 
 template <bool ALIGNED>
@@ -1309,7 +1333,9 @@ __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_
                                                   const SelCfg& p, int64_t bx) {
     const int t = task(w, BT_CAP4, (int)bx);
     SelState* st = w.st + t;
+    PASS_STAMP(1, 0);
     if (!st->lower_pending) return;
+    PASS_STAMP(1, 1);
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
     const float* vec = vec_flat + d.off;
     const int m = p.max_iters;
@@ -1317,40 +1343,48 @@ __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_
     th[0] = st->t_cur;
 #pragma unroll
     for (int j = 1; j <= kMaxLower; ++j) th[j] = thr_mul(th[j - 1], p.lower, p.tdtype);
-    const float tmin = th[m];
-    uint32_t c[kMaxLower + 1];
-#pragma unroll
-    for (int j = 0; j <= kMaxLower; ++j) c[j] = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ uint32_t part[kSegPerBlock4][kMaxLower + 1];
+    if (lane == 0)
+        for (int j = 1; j <= kMaxLower; ++j) part[wave][j] = 0;
+    // A wave per segment, its four tiles loaded before the first compare, then the m
+    // thresholds one after the other (a uniform loop), each compare a ballot whose
+    // popcount the scalar unit adds (per-lane "c[j] += |x| >= t_j" over all 16 slots
+    // behind a divergent |x| >= t_m branch kept the VALU busy ~5 us per workgroup after
+    // its loads: tools/pass_prof.py). Four segments per wave (a quarter of the
+    // workgroups — 6227 of them take 10 us to dispatch) was slower either way: 22 us per
+    // workgroup with per-lane counts, 16 with these.
     const int64_t nb = w.bt[BT_CAP4][t + 1] - w.bt[BT_CAP4][t];
     for (int64_t ls = (bx - w.bt[BT_CAP4][t]) * kSegPerBlock4 + wave; ls < d.nseg;
          ls += nb * kSegPerBlock4) {
-        for (int tile = 0; tile < kSegTiles; ++tile) {
-            float x[4];
-            uint32_t valid;
-            load_tile<ALIGNED>(vec, d.n, ls * kSeg + tile * 256 + 4 * lane, x, valid);
+        float xs[kSegTiles][4];
+        uint32_t vs[kSegTiles];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float a = fabsf(x[q]);
-                if (((valid >> q) & 1u) && a >= tmin) {
+        for (int u = 0; u < kSegTiles; ++u) load_tile<ALIGNED>(vec, d.n, ls * kSeg + u * 256 + 4 * lane, xs[u], vs[u]);
 #pragma unroll
-                    for (int j = 1; j <= kMaxLower; ++j) c[j] += (j <= m) && a >= th[j];
-                }
-            }
+        for (int u = 0; u < kSegTiles; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xs[u][q] = ((vs[u] >> q) & 1u) ? fabsf(xs[u][q]) : -1.f;   // (NaN: never >=)
+        PASS_LOADED(1);
+        float tj = th[0];
+        for (int j = 1; j <= m; ++j) {   // uniform
+            tj = thr_mul(tj, p.lower, p.tdtype);   // = th[j]
+            uint32_t cj = 0;
+#pragma unroll
+            for (int u = 0; u < kSegTiles; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cj += (uint32_t)__popcll(__ballot(xs[u][q] >= tj));
+            if (lane == 0) part[wave][j] += cj;
         }
     }
-    __shared__ uint32_t part[kSegPerBlock4][kMaxLower + 1];
-#pragma unroll
-    for (int j = 1; j <= kMaxLower; ++j) {
-        const uint32_t v = wave_sum(c[j]);
-        if (lane == 0) part[wave][j] = v;
-    }
     __syncthreads();
+    PASS_STAMP(1, 2);
     if (threadIdx.x >= 1 && threadIdx.x <= m) {
         const int j = threadIdx.x;
         const uint64_t v = (uint64_t)part[0][j] + part[1][j] + part[2][j] + part[3][j];
         if (v) atomicAdd(&st->lower_cnt[j], (unsigned long long)v);
     }
+    PASS_STAMP(1, 3);
     if (!last_block_arrival(&st->tickets[0], (uint32_t)nb)) return;
     if (threadIdx.x < kWave) {
         // the m counts loaded together, one lane each (a loop of dependent agent-scope
@@ -1368,6 +1402,7 @@ __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_
         st->active = 1;   // count pass + decide at t_{j*}
         }
     }
+    PASS_STAMP(1, 4);
 }
 
 template <bool ALIGNED>
@@ -1803,23 +1838,17 @@ __device__ __forceinline__ void resample_set_block(const float* __restrict__ vec
 // first in the grid and never wait, so a waiting set only holds a slot the emit does
 // not need (ResNet-50's whole grid, ~220 workgroups of 1024 threads, is resident at
 // once on 256 CUs; VGG-16-BN's ~680 against 512 slots, ~150 of them sets).
-template <bool SET>
-__global__ void __launch_bounds__(kGroupSegs)
-k_emit_wide_t(const float* __restrict__ vec_flat, SelWS w, EmitOut oa, EmitOut os, int64_t one_max, uint32_t gmin,
-              int32_t ngb) {
-    if (SET && (int)blockIdx.x >= ngb) {
-        resample_set_block(vec_flat, w, os, (int)blockIdx.x - ngb, one_max, gmin, true);
-        return;
-    }
-    const int bx = (int)blockIdx.x;
+// Returns true when the workgroup gathered a resampled tensor's candidates.
+__device__ __forceinline__ bool emit_wide_part(const float* __restrict__ vec_flat, const SelWS& w, const EmitOut& oa,
+                                               int bx) {
     const int t = task(w, BT_GRP, bx);
     const SelState* st = w.st + t;
-    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return;   // K5b emits it
-    if (st->spec_emitted) return;                                        // k_count_emit did
+    if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) return false;   // K5b emits it
+    if (st->spec_emitted) return false;                                        // k_count_emit did
     const bool k5 = st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1;
     // oa.queue set: the K5 tensors gather their candidates into the queue and the
     // others emit their payload in the same launch; unset: the K5 tensors are skipped
-    if (k5 && !oa.queue) return;
+    if (k5 && !oa.queue) return false;
     EmitOut o = oa;
     if (!k5) o.queue = nullptr;
     const TDesc d = w.td[t];   // by value: stores below cannot alias it
@@ -1901,7 +1930,18 @@ k_emit_wide_t(const float* __restrict__ vec_flat, SelWS w, EmitOut oa, EmitOut o
             emit_reread_firstk(vec, d, lseg0 + j0 + q, ga + off_a[j0 + q], limit, obase, tc, o, !defer_here);
         }
     }
-    if (SET && k5) {   // uniform per workgroup
+    return k5;
+}
+
+template <bool SET>
+__global__ void __launch_bounds__(kGroupSegs)
+k_emit_wide_t(const float* __restrict__ vec_flat, SelWS w, EmitOut oa, EmitOut os, int64_t one_max, uint32_t gmin,
+              int32_t ngb) {
+    const int bx = (int)blockIdx.x;
+    if (SET && bx >= ngb) {
+        resample_set_block(vec_flat, w, os, bx - ngb, one_max, gmin, true);
+    } else if (emit_wide_part(vec_flat, w, oa, bx) && SET) {   // uniform per workgroup
+        const int t = task(w, BT_GRP, bx);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -4053,6 +4093,11 @@ extern "C" int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt
 #ifdef DGC_K5_PROF
 extern "C" int dgc_ce_prof(void* out) {
     DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_ce_prof), sizeof(dgc::g_ce_prof)));
+    return DGC_OK;
+}
+
+extern "C" int dgc_pass_prof(void* out) {   // tools/pass_prof.py
+    DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_pass_prof), sizeof(dgc::g_pass_prof)));
     return DGC_OK;
 }
 
