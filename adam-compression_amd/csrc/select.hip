@@ -188,7 +188,7 @@ struct SelCfg {
 };
 
 // Block tables: prefix arrays [T + 1] of per-tensor workgroup counts for one launch shape.
-enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_CNT, BT_SET, BT_COUNT };
+enum { BT_K1 = 0, BT_FULL, BT_CAP16, BT_CAP4, BT_FULL8, BT_CAP8, BT_SEG, BT_GRP, BT_QUEUE, BT_SAMP, BT_CNT, BT_SET, BT_COUNT };
 
 struct SelWS {
     int32_t T;
@@ -276,6 +276,8 @@ static inline int64_t bt_blocks(int which, const TDesc& d, int64_t total_seg, in
         case BT_FULL: return ceil_div(d.nseg, (int64_t)kSegPerBlock16);
         case BT_CAP16: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock16), cap);
         case BT_CAP4: return std::min(ceil_div(d.nseg, (int64_t)kSegPerBlock4), cap);
+        case BT_FULL8: return ceil_div(d.nseg, (int64_t)(2 * kSegPerBlock4));
+        case BT_CAP8: return std::min(ceil_div(d.nseg, (int64_t)(2 * kSegPerBlock4)), cap);
         case BT_SEG: return ceil_div(d.nseg, (int64_t)kBlock);
         case BT_CNT: return ceil_div(d.nseg, (int64_t)kBlock * kCountSegs);
         case BT_GRP: return ceil_div(d.nseg, (int64_t)(kGroupSegs / kEmitSplit));
@@ -1224,14 +1226,15 @@ k_count_lists(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
     count_lists_body(vec_flat, w, p, blockIdx.x);
 }
 
-// t_cur < t_list: full select pass at t_cur — one wave per kSuper segments (16
+// t_cur < t_list: full select pass at t_cur — one wave per SUPER segments (kSuper: 16
 // float4 loads in flight per lane), re-lists every segment; seg_lcnt = seg_cnt.
 // `which` = BT_FULL (one-shot) or BT_CAP16 (grid-stride within the tensor, for a
-// launch that is most likely a gated no-op). The tensor's last workgroup then takes the
-// adaptation step (decide_tensor).
-template <bool ALIGNED>
+// launch that is most likely a gated no-op) — BT_K1 / BT_CAP4 for SUPER = 1. The
+// tensor's last workgroup then takes the adaptation step (decide_tensor).
+template <bool ALIGNED, int SUPER = kSuper>
 __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_flat, const SelWS& w, int which,
                                                  const SelCfg& p, int64_t bx) {
+    static_assert(kGroupSegs % (kSegPerBlock4 * SUPER) == 0, "a workgroup's segments lie in one group");
     const int t = task(w, which, (int)bx);
     const SelState* st = w.st + t;
     PASS_STAMP(0, 0);
@@ -1242,10 +1245,10 @@ __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_f
     const float tc = st->t_cur;
     const int64_t ntile = ceil_div(w.nseg, (int64_t)kLstTile);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int kTiles = kSuper * kSegTiles;   // 16
+    constexpr int kTiles = SUPER * kSegTiles;   // 16 for kSuper
     __shared__ uint32_t wcnt[kSegPerBlock4];
     __shared__ uint32_t wovf[kSegPerBlock4];
-    const int64_t nsuper = ceil_div(d.nseg, (int64_t)kSuper);
+    const int64_t nsuper = ceil_div(d.nseg, (int64_t)SUPER);
     const int64_t nb = w.bt[which][t + 1] - w.bt[which][t];
     for (int64_t bi = bx - w.bt[which][t]; bi * kSegPerBlock4 < nsuper; bi += nb) {
         const int64_t sup = bi * kSegPerBlock4 + wave;
@@ -1255,11 +1258,11 @@ __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_f
             uint32_t valid[kTiles];
 #pragma unroll
             for (int u = 0; u < kTiles; ++u)
-                load_tile<ALIGNED>(vec, d.n, sup * (kSuper * kSeg) + u * 256 + 4 * lane, x[u], valid[u]);
+                load_tile<ALIGNED>(vec, d.n, sup * (SUPER * kSeg) + u * 256 + 4 * lane, x[u], valid[u]);
             PASS_LOADED(0);
 #pragma unroll
-            for (int sg = 0; sg < kSuper; ++sg) {
-                const int64_t ls = sup * kSuper + sg;
+            for (int sg = 0; sg < SUPER; ++sg) {
+                const int64_t ls = sup * SUPER + sg;
                 const int64_t seg = d.seg0 + ls;
                 uint32_t c = 0;
                 uint16_t* lo = w.lst_off;
@@ -1290,7 +1293,7 @@ __device__ __forceinline__ void select_pass_body(const float* __restrict__ vec_f
         if (threadIdx.x == 0) {
             const uint32_t s = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
             const uint32_t o = wovf[0] + wovf[1] + wovf[2] + wovf[3];
-            if (s) atomicAdd(&w.grp_cnt[d.grp0 + (bi * kSegPerBlock16) / kGroupSegs], (unsigned long long)s);
+            if (s) atomicAdd(&w.grp_cnt[d.grp0 + (bi * kSegPerBlock4 * SUPER) / kGroupSegs], (unsigned long long)s);
             if (o) atomicAdd(&w.st[t].overflow, (int)o);
         }
         __syncthreads();
@@ -1315,23 +1318,24 @@ k_select_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p) 
 // whose decide steps cannot leave a tensor active for a recount within the launch (the
 // multi-threshold lowering: resample on, max_iters <= kMaxLower — then a decide either
 // finishes the tensor or hands it to the lowering), so both gates read one state.
-template <bool ALIGNED>
+template <bool ALIGNED, int SUPER>
 __global__ void __launch_bounds__(kBlock)
 k_count_pass(const float* __restrict__ vec_flat, SelWS w, int which, SelCfg p, int ncnt) {
     if ((int)blockIdx.x < ncnt)
         count_lists_body(vec_flat, w, p, blockIdx.x);
     else
-        select_pass_body<ALIGNED>(vec_flat, w, which, p, (int64_t)blockIdx.x - ncnt);
+        select_pass_body<ALIGNED, SUPER>(vec_flat, w, which, p, (int64_t)blockIdx.x - ncnt);
 }
 
 // Counts at t_j = fl32(t_{j-1} * lower), j = 1..max_iters, in ONE pass over vec (the
 // reference's "lower" recounts, dgc/compression.py:140-148, all at once). The last
 // workgroup of the tensor picks j* = the first j whose count reaches lower*k (else
 // max_iters) and arms the count pass + decide at t_{j*}.
-template <bool ALIGNED>
+template <bool ALIGNED, int SEGS = 1>
 __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_flat, const SelWS& w,
                                                   const SelCfg& p, int64_t bx) {
-    const int t = task(w, BT_CAP4, (int)bx);
+    constexpr int kWhich = SEGS == 1 ? BT_CAP4 : BT_CAP8;   // SEGS segments per wave
+    const int t = task(w, kWhich, (int)bx);
     SelState* st = w.st + t;
     PASS_STAMP(1, 0);
     if (!st->lower_pending) return;
@@ -1354,15 +1358,16 @@ __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_
     // its loads: tools/pass_prof.py). Four segments per wave (a quarter of the
     // workgroups — 6227 of them take 10 us to dispatch) was slower either way: 22 us per
     // workgroup with per-lane counts, 16 with these.
-    const int64_t nb = w.bt[BT_CAP4][t + 1] - w.bt[BT_CAP4][t];
-    for (int64_t ls = (bx - w.bt[BT_CAP4][t]) * kSegPerBlock4 + wave; ls < d.nseg;
-         ls += nb * kSegPerBlock4) {
-        float xs[kSegTiles][4];
-        uint32_t vs[kSegTiles];
+    const int64_t nb = w.bt[kWhich][t + 1] - w.bt[kWhich][t];
+    const int64_t nsup = ceil_div(d.nseg, (int64_t)SEGS);
+    constexpr int kT = SEGS * kSegTiles;
+    for (int64_t su = (bx - w.bt[kWhich][t]) * kSegPerBlock4 + wave; su < nsup; su += nb * kSegPerBlock4) {
+        float xs[kT][4];
+        uint32_t vs[kT];
 #pragma unroll
-        for (int u = 0; u < kSegTiles; ++u) load_tile<ALIGNED>(vec, d.n, ls * kSeg + u * 256 + 4 * lane, xs[u], vs[u]);
+        for (int u = 0; u < kT; ++u) load_tile<ALIGNED>(vec, d.n, su * (SEGS * kSeg) + u * 256 + 4 * lane, xs[u], vs[u]);
 #pragma unroll
-        for (int u = 0; u < kSegTiles; ++u)
+        for (int u = 0; u < kT; ++u)
 #pragma unroll
             for (int q = 0; q < 4; ++q) xs[u][q] = ((vs[u] >> q) & 1u) ? fabsf(xs[u][q]) : -1.f;   // (NaN: never >=)
         PASS_LOADED(1);
@@ -1371,7 +1376,7 @@ __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_
             tj = thr_mul(tj, p.lower, p.tdtype);   // = th[j]
             uint32_t cj = 0;
 #pragma unroll
-            for (int u = 0; u < kSegTiles; ++u)
+            for (int u = 0; u < kT; ++u)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) cj += (uint32_t)__popcll(__ballot(xs[u][q] >= tj));
             if (lane == 0) part[wave][j] += cj;
@@ -1405,10 +1410,10 @@ __device__ __forceinline__ void lower_counts_body(const float* __restrict__ vec_
     PASS_STAMP(1, 4);
 }
 
-template <bool ALIGNED>
+template <bool ALIGNED, int SEGS>
 __global__ void __launch_bounds__(kBlock)
 k_lower_counts(const float* __restrict__ vec_flat, SelWS w, SelCfg p) {
-    lower_counts_body<ALIGNED>(vec_flat, w, p, blockIdx.x);
+    lower_counts_body<ALIGNED, SEGS>(vec_flat, w, p, blockIdx.x);
 }
 
 // The "lower" recounts served by the K1 candidate lists: the counts at the first
@@ -3299,6 +3304,11 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     const bool fuse = keep_lists && L.T == 1 && !L.tail_any && sync_mode == DGC_SYNC_DEVICE &&
                       (p.update_memory == 2 || p.update_memory == 0) && !std::getenv("DGC_NO_COUNT_EMIT");
     static const bool pass_split = std::getenv("DGC_PASS_SPLIT") != nullptr;
+    static const int pass_super = [] {
+        const char* e = std::getenv("DGC_PASS_SUPER");
+        const int v = e ? std::atoi(e) : 2;
+        return v == 1 || v == 2 ? v : kSuper;
+    }();
     const bool merge_ok = lower_fast && sync_mode == DGC_SYNC_DEVICE && !pass_split;
     auto pass = [&](int need, bool likely_lists, bool fused = false) -> int {
         // one count pass at t_cur: lists when t_cur >= t_list, else the full select pass
@@ -3317,13 +3327,34 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
             return DGC_OK;
         }
         if (need == 3 && !fused && merge_ok) {   // both in one launch (k_count_pass)
-            const int which = likely_lists ? BT_CAP16 : BT_FULL;
+            // a batch's full passes: two segments per wave (DGC_PASS_SUPER=1|4: one or
+            // kSuper, A/B). Measured (tools/pass_prof.py, ResNet-50): four per wave keep
+            // a working workgroup ~9 us on its list appends after 3 us of loads, one per
+            // wave ~3 us but 6289 workgroups enter over 10.7 us (the working ones hold
+            // the slots); two: 6 us each, all entered within 3.9 us, the pass ends at 15
+            // instead of 18 us — ResNet-50 0.2269 -> 0.2235 ms, VGG-16-BN 0.6275 -> 0.6264
+            // (4 alternations; one per wave 0.2310 / 0.6282)
+            const int sup = L.T > 1 ? pass_super : kSuper;
+            const int which = sup == 1 ? (likely_lists ? BT_CAP4 : BT_K1)
+                            : sup == 2 ? (likely_lists ? BT_CAP8 : BT_FULL8) : (likely_lists ? BT_CAP16 : BT_FULL);
             const unsigned grid = (unsigned)(L.grid[BT_CNT] + L.grid[which]);
-            if (al)
-                hipLaunchKernelGGL(k_count_pass<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+            if (sup == 1 && al)
+                hipLaunchKernelGGL((k_count_pass<true, 1>), dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                                   (int)L.grid[BT_CNT]);
+            else if (sup == 1)
+                hipLaunchKernelGGL((k_count_pass<false, 1>), dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                                   (int)L.grid[BT_CNT]);
+            else if (sup == 2 && al)
+                hipLaunchKernelGGL((k_count_pass<true, 2>), dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                                   (int)L.grid[BT_CNT]);
+            else if (sup == 2)
+                hipLaunchKernelGGL((k_count_pass<false, 2>), dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                                   (int)L.grid[BT_CNT]);
+            else if (al)
+                hipLaunchKernelGGL((k_count_pass<true, kSuper>), dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
                                    (int)L.grid[BT_CNT]);
             else
-                hipLaunchKernelGGL(k_count_pass<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
+                hipLaunchKernelGGL((k_count_pass<false, kSuper>), dim3(grid), dim3(kBlock), 0, s, vec, w, which, p,
                                    (int)L.grid[BT_CNT]);
             DGC_LAUNCHED();
             return DGC_OK;
@@ -3356,16 +3387,23 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
     }();
     const bool lower_lists = lower_lists_env >= 0 ? lower_lists_env == 1 : L.T == 1;
+    static const int lower_segs = std::getenv("DGC_LOWER_SEGS") && std::atoi(std::getenv("DGC_LOWER_SEGS")) == 2 ? 2 : 1;
     auto lower = [&]() -> int {
         if (lower_lists) {
             hipLaunchKernelGGL(k_lower_lists, dim3((unsigned)L.grid[BT_SEG]), dim3(kBlock), 0, s, vec, w, p);
             DGC_LAUNCHED();
         }
-        const unsigned grid = (unsigned)L.grid[BT_CAP4];
-        if (al)
-            hipLaunchKernelGGL(k_lower_counts<true>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
+        // (DGC_LOWER_SEGS=2: two segments per wave over half the workgroups — A/B)
+        const bool two = lower_segs == 2;
+        const unsigned grid = (unsigned)L.grid[two ? BT_CAP8 : BT_CAP4];
+        if (two && al)
+            hipLaunchKernelGGL((k_lower_counts<true, 2>), dim3(grid), dim3(kBlock), 0, s, vec, w, p);
+        else if (two)
+            hipLaunchKernelGGL((k_lower_counts<false, 2>), dim3(grid), dim3(kBlock), 0, s, vec, w, p);
+        else if (al)
+            hipLaunchKernelGGL((k_lower_counts<true, 1>), dim3(grid), dim3(kBlock), 0, s, vec, w, p);
         else
-            hipLaunchKernelGGL(k_lower_counts<false>, dim3(grid), dim3(kBlock), 0, s, vec, w, p);
+            hipLaunchKernelGGL((k_lower_counts<false, 1>), dim3(grid), dim3(kBlock), 0, s, vec, w, p);
         DGC_LAUNCHED();
         return DGC_OK;
     };
