@@ -1122,9 +1122,15 @@ __device__ unsigned long long g_pass_prof[2][16384][6];
 // slot 5: the first iteration's loads arrived (wave 0; the wait is the profiling build's only)
 #define PASS_LOADED(k) \
     do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); PASS_STAMP(k, 5); } while (0)
+// tools/es_prof.py: k_emit_wide_t's workgroups — [0] entry, [1] emit: scan done / set:
+// its tensor's gather complete, [2] done
+__device__ unsigned long long g_es_prof[4096][3];
+#define ES_STAMP(i) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_es_prof[blockIdx.x][i] = wall_clock64(); } while (0)
 #else
 #define PASS_STAMP(k, i) do { } while (0)
 #define PASS_LOADED(k) do { } while (0)
+#define ES_STAMP(i) do { } while (0)
 #endif
 // t_cur >= t_list: counts from the lists, kCountSegs segments per thread (one group
 // per workgroup): the list counts of a thread's segments, then their first 8 entries
@@ -1578,15 +1584,14 @@ __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long 
     if (o.mmt) __builtin_nontemporal_store(0.f, o.mmt + d.off + li);
 }
 
-// Wave-cooperative emit of one spilled segment (local ls) by re-reading vec.
+// Wave-cooperative emit of one spilled segment (local ls) from its elements in
+// registers (xs / vs: load_segment's).
 // FIRSTK: positions base + rank for |x| >= t, kept while < limit.
-__device__ __forceinline__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d, int64_t ls, long long base,
-                                   long long limit, long long obase, float t, const EmitOut& o, bool mask_now) {
+__device__ __forceinline__ void emit_segment_firstk(const float (&xs)[kSegTiles][4], const uint32_t (&vs)[kSegTiles],
+                                                    const TDesc& d, int64_t ls, long long base, long long limit,
+                                                    long long obase, float t, const EmitOut& o, bool mask_now) {
     const int lane = threadIdx.x & 63;
     uint32_t run = 0;
-    float xs[kSegTiles][4];
-    uint32_t vs[kSegTiles];
-    load_segment(vec, d.n, ls, xs, vs);
 #pragma unroll
     for (int tile = 0; tile < kSegTiles; ++tile) {
         const float(&x)[4] = xs[tile];
@@ -1607,6 +1612,19 @@ __device__ __forceinline__ void emit_reread_firstk(const float* __restrict__ vec
         }
     }
 }
+
+// ... re-reading vec. (Two segments per call with both loads in flight made no
+// difference to ResNet-50's emit, whose spilled small tensors end ~17 us into the launch:
+// tools/es_prof.py.)
+__device__ __forceinline__ void emit_reread_firstk(const float* __restrict__ vec, const TDesc& d, int64_t ls,
+                                                   long long base, long long limit, long long obase, float t,
+                                                   const EmitOut& o, bool mask_now) {
+    float xs[kSegTiles][4];
+    uint32_t vs[kSegTiles];
+    load_segment(vec, d.n, ls, xs, vs);
+    emit_segment_firstk(xs, vs, d, ls, base, limit, obase, t, o, mask_now);
+}
+
 
 // kEmitSplit workgroups of kEmitSegs threads per group of kGroupSegs segments, one
 // thread per segment of its quarter. In-group offsets: the quarter's exclusive scan
@@ -1892,6 +1910,7 @@ __device__ __forceinline__ bool emit_wide_part(const float* __restrict__ vec_fla
         lcn[threadIdx.x] = work ? lc : kEmitSkip;
     }
     __syncthreads();
+    ES_STAMP(1);
     const long long obase = obase_s;
     const float tc = st->t_cur;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1943,6 +1962,7 @@ __global__ void __launch_bounds__(kGroupSegs)
 k_emit_wide_t(const float* __restrict__ vec_flat, SelWS w, EmitOut oa, EmitOut os, int64_t one_max, uint32_t gmin,
               int32_t ngb) {
     const int bx = (int)blockIdx.x;
+    ES_STAMP(0);
     if (SET && bx >= ngb) {
         resample_set_block(vec_flat, w, os, bx - ngb, one_max, gmin, true);
     } else if (emit_wide_part(vec_flat, w, oa, bx) && SET) {   // uniform per workgroup
@@ -1954,6 +1974,7 @@ k_emit_wide_t(const float* __restrict__ vec_flat, SelWS w, EmitOut oa, EmitOut o
             __hip_atomic_fetch_add(&w.setg[t].gathered, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    ES_STAMP(2);
 }
 
 // The first count pass of a ONE-tensor call whose lists serve t_cur (the flat
@@ -3048,6 +3069,7 @@ __device__ __forceinline__ void resample_set_block(const float* __restrict__ vec
             gathered = ok;
         }
         __syncthreads();
+        ES_STAMP(1);
         // (a cooperative set's other workgroups then fail the residency consensus: the replay)
         if (!gathered) return;
     }
@@ -4131,6 +4153,11 @@ extern "C" int dgc_batch_compress_finish(const dgc_batch_desc* batch, float* mmt
 #ifdef DGC_K5_PROF
 extern "C" int dgc_ce_prof(void* out) {
     DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_ce_prof), sizeof(dgc::g_ce_prof)));
+    return DGC_OK;
+}
+
+extern "C" int dgc_es_prof(void* out) {   // tools/es_prof.py
+    DGC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dgc::g_es_prof), sizeof(dgc::g_es_prof)));
     return DGC_OK;
 }
 
