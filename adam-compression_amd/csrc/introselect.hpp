@@ -987,6 +987,7 @@ struct NthG {
     uint32_t arrive, decide;       // the residency consensus
     uint32_t status;               // DGC_K5_FALLBACK | DGC_K5_BROKEN of this call
     uint32_t exited;               // workgroups past a GO phase's last barrier (k_nth_select's recovery)
+    uint32_t replayed;             // k_nth_select's replay of the tensor done (its extra workgroups emit it)
     uint32_t bl[kNthGMax], br[kNthGMax];
 };
 

@@ -798,6 +798,7 @@ __device__ void sel_init_tensor(const SelWS& w, int t, int keep_lists) {
         w.nthg[t].decide = 0;
         w.nthg[t].status = 0;
         w.nthg[t].exited = 0;
+        w.nthg[t].replayed = 0;
         SetG& sg = w.setg[t];
         setg_broken = sg.broken;
         sg.arrive = sg.decide = sg.bar_count = sg.bar_gen = sg.broken = sg.gathered = 0;
@@ -3117,10 +3118,17 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_global(SelWS w, uint32_t G,
 // [0, n), exact (k5_status DGC_K5_FALLBACK | DGC_K5_RECOVERED). force_broken (parity
 // tests, DGC_K5_FORCE_BROKEN=1): every replayed tensor takes that path, its queue first
 // overwritten with garbage.
+// queue_here (k > kQueueFold somewhere, and G > 1 workgroups per tensor): the extra
+// workgroups (t, 1..G-1) of a replayed tensor wait for its replay (NthG::replayed) and
+// write its k entries in the replayed order, a share each — k_emit_queue, a ~5 us
+// launch that is a no-op in every step without a replay (flat-1B, VGG-16-BN), is not
+// launched. The wait is bounded (~seconds; workgroup (t, 0) never waits on them): past
+// it the payload is incomplete and the call reports DGC_K5_BROKEN through the sink.
 __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restrict__ vec_flat, SelWS w,
                                                             EmitOut o, int from_global, FinishArgs f,
                                                             int force_broken, int emit_here, int global_here,
-                                                            uint32_t G, int64_t min_run, uint32_t G_expected) {
+                                                            uint32_t G, int64_t min_run, uint32_t G_expected,
+                                                            int queue_here) {
     const int t = blockIdx.x;
     const uint32_t b = blockIdx.y;
     const SelState* st = w.st + t;
@@ -3134,7 +3142,44 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
                          reinterpret_cast<DGC_LDS uint8_t*>(lds(smem)));
         __syncthreads();   // (smem is the replay's from here)
     }
-    if (b > 0) return;
+    if (b > 0) {
+        if (queue_here && st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 1) {   // uniform per tensor
+            NthG* g = w.nthg + t;
+            __shared__ int ready;
+            __shared__ long long qbase_s;
+            if (threadIdx.x == 0) {
+                bool done = false;
+                for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
+                    if (__hip_atomic_load(&g->replayed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        done = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (!done) {
+                    atomicOr(&g->status, (uint32_t)DGC_K5_BROKEN);
+                    raise_flag(f.sink, (int32_t)DGC_K5_BROKEN);
+                }
+                ready = done;
+            }
+            __syncthreads();
+            if (!ready) return;   // uniform
+            if (threadIdx.x < kWave) {
+                const long long ob = out_base(w, t);
+                if (threadIdx.x == 0) qbase_s = ob;
+            }
+            __syncthreads();
+            const TDesc d = w.td[t];
+            const int64_t share = ceil_div(d.k, (int64_t)(G - 1));
+            const int64_t q0 = (int64_t)(b - 1) * share, q1 = q0 + share < d.k ? q0 + share : d.k;
+            for (int64_t q = q0 + threadIdx.x; q < q1; q += kNthThreads) {
+                const uint32_t j = (uint32_t)w.queue[d.cand_off + q];
+                emit_one(o, d, qbase_s + q, w.cand_idx[d.cand_off + j], w.cand_val[d.cand_off + j]);
+            }
+        }
+        return;
+    }
     K5_STAMP(7);
     if (st->branch == DGC_BRANCH_RESAMPLE && st->rs_nth == 2) {   // uniform per workgroup
         heap_select_wg(vec_flat, w, o, t, smem);
@@ -3173,7 +3218,14 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
                 g->status = (g->status & ~(uint32_t)DGC_K5_BROKEN) | (uint32_t)(DGC_K5_FALLBACK | DGC_K5_RECOVERED);
         }
         nth_element_wg(q, nc, d.k - 1, gl, gr, lq, llp, lrp, lmk, from_global && !recover ? g : nullptr);
-        if (emit_here) {
+        if (queue_here) {   // the replayed order is in the queue: the extra workgroups emit it
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(&g->replayed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (emit_here) {
             // the replayed order out by this workgroup (k <= kQueueFold for every tensor of
             // the call: no k_emit_queue launch); the payload position is known, every
             // tensor's branch and count being final before K5 runs
@@ -3496,11 +3548,14 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         }
         FinishArgs f = fin;
         f.on = 1;   // k_nth_select's last workgroup finishes the call
+        // (DGC_QUEUE_LAUNCH=1 above: always k_emit_queue, A/B)
+        const bool queue_here = !emit_here && global_here && !queue_launch;
         hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T, global_here ? G : 1u), dim3(kNthThreads), 0, s, vec, w,
-                           o, G > 1 ? 1 : 0, f, force, emit_here ? 1 : 0, global_here ? 1 : 0, G, min_run, G_expected);
+                           o, G > 1 ? 1 : 0, f, force, emit_here ? 1 : 0, global_here ? 1 : 0, G, min_run, G_expected,
+                           queue_here ? 1 : 0);
         DGC_LAUNCHED();
         finished = true;
-        if (!emit_here) {
+        if (!emit_here && !queue_here) {
             hipLaunchKernelGGL(k_emit_queue, dim3((unsigned)L.grid[BT_QUEUE]), dim3(kBlock), 0, s, vec, w, o);
             DGC_LAUNCHED();
         }
