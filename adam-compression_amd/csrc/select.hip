@@ -1545,6 +1545,7 @@ struct EmitOut {
     int32_t defer;       // first-k branches: leave vec/mmt to the next K1 (record seg_off instead)
     float* cval;         // the K5 gather: cval[pos] = the candidate's value (null: not kept)
     uint32_t* ckey;      //   and ckey[pos] = its key
+    int32_t no_queue;    // the gather leaves queue[] unwritten (k_nth_select rebuilds it from ckey)
 };
 
 // Entries a tensor emits: the first `limit` candidates, or k after a resample.
@@ -1569,7 +1570,7 @@ __device__ __forceinline__ long long out_base(const SelWS& w, int t) {
 __device__ __forceinline__ void emit_one(const EmitOut& o, const TDesc& d, long long pos, int64_t li, float x,
                                          bool mask_now = true) {
     if (o.queue) {
-        o.queue[d.cand_off + pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
+        if (!o.no_queue) o.queue[d.cand_off + pos] = ((uint64_t)abs_key(x) << 32) | (uint64_t)(uint32_t)pos;
         o.cand[d.cand_off + pos] = li;
         if (o.cval) {
             o.cval[d.cand_off + pos] = x;
@@ -3128,7 +3129,7 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
                                                             EmitOut o, int from_global, FinishArgs f,
                                                             int force_broken, int emit_here, int global_here,
                                                             uint32_t G, int64_t min_run, uint32_t G_expected,
-                                                            int queue_here) {
+                                                            int queue_here, int rebuild_queue) {
     const int t = blockIdx.x;
     const uint32_t b = blockIdx.y;
     const SelState* st = w.st + t;
@@ -3216,6 +3217,10 @@ __global__ void __launch_bounds__(kNthThreads) k_nth_select(const float* __restr
             __syncthreads();
             if (threadIdx.x == 0)
                 g->status = (g->status & ~(uint32_t)DGC_K5_BROKEN) | (uint32_t)(DGC_K5_FALLBACK | DGC_K5_RECOVERED);
+        } else if (rebuild_queue) {   // the gather wrote no queue (an index-order engine, no global phase)
+            const DGC_GLB uint32_t* ck = glb(w.cand_key + d.cand_off);
+            for (int64_t j = threadIdx.x; j < nc; j += kNthThreads) q[j] = ((uint64_t)ck[j] << 32) | (uint64_t)j;
+            __syncthreads();
         }
         nth_element_wg(q, nc, d.k - 1, gl, gr, lq, llp, lrp, lmk, from_global && !recover ? g : nullptr);
         if (queue_here) {   // the replayed order is in the queue: the extra workgroups emit it
@@ -3514,6 +3519,14 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
     auto resample_exact = [&]() -> int {
         // nth_element path: gather candidates, replay the introselect, emit in its order.
         // The gather launch also emits every other tensor's payload (the final emit).
+        const uint32_t G = nth_global_groups(L.T, L.max_cand);
+        // An index-order engine whose replay runs on one workgroup (no global phase): the
+        // gather writes no queue — the sets read the keys, and the rare tied set that
+        // falls to the replay has k_nth_select rebuild its queue from them (one of the
+        // gather's four stores per candidate; DGC_GATHER_QUEUE=1 writes it, A/B)
+        static const bool gather_queue = std::getenv("DGC_GATHER_QUEUE") != nullptr;
+        const bool no_queue = p.set_order && G <= 1 && !gather_queue;
+        g.no_queue = no_queue ? 1 : 0;
         // K5s: an untied resample set in index order (the rest: the replay); with the
         // wide emit, in its launch (k_emit_set; DGC_SET_SEPARATE=1: two launches, A/B)
         static const bool set_separate = std::getenv("DGC_SET_SEPARATE") != nullptr;
@@ -3530,7 +3543,6 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
                 DGC_LAUNCHED();
             }
         }
-        const uint32_t G = nth_global_groups(L.T, L.max_cand);
         // DGC_K5_GLOBAL=multi: every range over several workgroups (parity); =abort: the
         // kernel expects one workgroup more than launched, so the residency consensus
         // times out and the one-workgroup replay takes over (the fallback's parity test)
@@ -3552,7 +3564,7 @@ static int select_core(float* vec, float* mmt, const SelCfg& p, const Layout& L,
         const bool queue_here = !emit_here && global_here && !queue_launch;
         hipLaunchKernelGGL(k_nth_select, dim3((unsigned)L.T, global_here ? G : 1u), dim3(kNthThreads), 0, s, vec, w,
                            o, G > 1 ? 1 : 0, f, force, emit_here ? 1 : 0, global_here ? 1 : 0, G, min_run, G_expected,
-                           queue_here ? 1 : 0);
+                           queue_here ? 1 : 0, no_queue ? 1 : 0);
         DGC_LAUNCHED();
         finished = true;
         if (!emit_here && !queue_here) {
